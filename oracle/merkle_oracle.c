@@ -1,0 +1,684 @@
+/*
+ * merkle_oracle.c -- CPU restatement of immudb's Merkle-hash path.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity oracle + timed CPU baseline).  See
+ * merkle_oracle.h for the pinning evidence and the import rule.  Each
+ * function cites the reference file:line it follows (paths relative to the
+ * immudb repository root).
+ */
+#include "merkle_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+#endif
+
+enum { OK = 0, ERR_MAX_WIDTH = 1, ERR_ILLEGAL_ARGS = 2, ERR_ILLEGAL_STATE = 3, ERR_EMPTY = 4,
+       ERR_UNEXISTENT = 5, ERR_MD_UNSUPPORTED = 6 };
+
+/* ------------------------------------------------------------------ SHA-256 */
+static const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+static const uint32_t H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                               0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+
+static void blocks_portable(uint32_t st[8], const uint8_t *p, size_t nblocks) {
+    while (nblocks--) {
+        uint32_t w[64];
+        for (int i = 0; i < 16; i++)
+            w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 |
+                   (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 64; i++) {
+            uint32_t s0 = ROR(w[i - 15], 7) ^ ROR(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            uint32_t s1 = ROR(w[i - 2], 17) ^ ROR(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+                 h = st[7];
+        for (int i = 0; i < 64; i++) {
+            uint32_t t1 = h + (ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25)) + ((e & f) ^ (~e & g)) +
+                          K256[i] + w[i];
+            uint32_t t2 = (ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+        st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+        p += 64;
+    }
+}
+
+#if defined(__x86_64__)
+/* Intel SHA extensions (sha256rnds2 / msg1 / msg2).  Same function, ~5x the
+ * portable code on one core. */
+__attribute__((target("sha,sse4.1,ssse3"))) static void blocks_shani(uint32_t st[8],
+                                                                      const uint8_t *p,
+                                                                      size_t nblocks) {
+    const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i tmp = _mm_loadu_si128((const __m128i *)&st[0]);
+    __m128i s1 = _mm_loadu_si128((const __m128i *)&st[4]);
+    tmp = _mm_shuffle_epi32(tmp, 0xB1);
+    s1 = _mm_shuffle_epi32(s1, 0x1B);
+    __m128i s0 = _mm_alignr_epi8(tmp, s1, 8);
+    s1 = _mm_blend_epi16(s1, tmp, 0xF0);
+    while (nblocks--) {
+        __m128i abef = s0, cdgh = s1, m[4];
+        for (int g = 0; g < 16; g++) {
+            __m128i w;
+            if (g < 4) {
+                m[g] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * g)), MASK);
+                w = m[g];
+            } else {
+                __m128i x = _mm_sha256msg1_epu32(m[g & 3], m[(g + 1) & 3]);
+                x = _mm_add_epi32(x, _mm_alignr_epi8(m[(g + 3) & 3], m[(g + 2) & 3], 4));
+                m[g & 3] = _mm_sha256msg2_epu32(x, m[(g + 3) & 3]);
+                w = m[g & 3];
+            }
+            __m128i msg = _mm_add_epi32(w, _mm_loadu_si128((const __m128i *)&K256[4 * g]));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, msg);
+            msg = _mm_shuffle_epi32(msg, 0x0E);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, msg);
+        }
+        s0 = _mm_add_epi32(s0, abef);
+        s1 = _mm_add_epi32(s1, cdgh);
+        p += 64;
+    }
+    tmp = _mm_shuffle_epi32(s0, 0x1B);
+    s1 = _mm_shuffle_epi32(s1, 0xB1);
+    s0 = _mm_blend_epi16(tmp, s1, 0xF0);
+    s1 = _mm_alignr_epi8(s1, tmp, 8);
+    _mm_storeu_si128((__m128i *)&st[0], s0);
+    _mm_storeu_si128((__m128i *)&st[4], s1);
+}
+
+static int detect_shani(void) {
+    unsigned a, b, c, d;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return 0;
+    int sha = (b >> 29) & 1;
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return 0;
+    int sse41 = (c >> 19) & 1, ssse3 = (c >> 9) & 1;
+    return sha && sse41 && ssse3;
+}
+#endif
+
+static int g_shani = -1;
+
+int orc_sha256_has_shani(void) {
+#if defined(__x86_64__)
+    return detect_shani();
+#else
+    return 0;
+#endif
+}
+
+void orc_sha256_use_shani(int enable) { g_shani = enable ? orc_sha256_has_shani() : 0; }
+
+static void blocks(uint32_t st[8], const uint8_t *p, size_t nblocks) {
+#if defined(__x86_64__)
+    if (g_shani < 0) g_shani = detect_shani();
+    if (g_shani) {
+        blocks_shani(st, p, nblocks);
+        return;
+    }
+#endif
+    blocks_portable(st, p, nblocks);
+}
+
+void orc_sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
+    uint32_t st[8];
+    memcpy(st, H0, sizeof st);
+    size_t full = len / 64;
+    if (full) blocks(st, msg, full);
+    uint8_t tail[128];
+    size_t rem = len - full * 64;
+    memset(tail, 0, sizeof tail);
+    if (rem) memcpy(tail, msg + full * 64, rem);
+    tail[rem] = 0x80;
+    size_t tl = (rem < 56) ? 64 : 128;
+    uint64_t bits = (uint64_t)len * 8;
+    for (int i = 0; i < 8; i++) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    blocks(st, tail, tl / 64);
+    for (int i = 0; i < 8; i++) {
+        out[4 * i] = (uint8_t)(st[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+        out[4 * i + 3] = (uint8_t)st[i];
+    }
+}
+
+/* leaf = SHA256(0x00 || d) (htree.go:79-83, ahtree.go:288-292, store leafFor) */
+static void leaf_hash(const uint8_t d[32], uint8_t out[32]) {
+    uint8_t b[33];
+    b[0] = 0;
+    memcpy(b + 1, d, 32);
+    orc_sha256(b, 33, out);
+}
+
+/* node = SHA256(0x01 || l || r) (htree.go:89-97) */
+static void node_hash(const uint8_t l[32], const uint8_t r[32], uint8_t out[32]) {
+    uint8_t b[65];
+    b[0] = 1;
+    memcpy(b + 1, l, 32);
+    memcpy(b + 33, r, 32);
+    orc_sha256(b, 65, out);
+}
+
+/* ------------------------------------------------------------ entry digest */
+int orc_entry_digest(int version, const uint8_t *key, size_t klen, const uint8_t *md,
+                     size_t mdlen, const uint8_t hval[32], uint8_t out[32]) {
+    uint8_t stackbuf[256];
+    size_t len = (version == 0) ? klen + 32 : 2 + mdlen + 2 + klen + 32;
+    uint8_t *b = len <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(len);
+    size_t i = 0;
+    if (version == 0) {
+        /* tx.go:690-701 TxEntryDigest_v1_1: key || hVal, md must be empty */
+        if (mdlen > 0) {
+            if (b != stackbuf) free(b);
+            return ERR_MD_UNSUPPORTED;
+        }
+    } else if (version == 1) {
+        /* tx.go:703-731 TxEntryDigest_v1_2: BE16 mdLen || md || BE16 kLen || key || hVal */
+        b[i++] = (uint8_t)(mdlen >> 8);
+        b[i++] = (uint8_t)mdlen;
+        if (mdlen) memcpy(b + i, md, mdlen);
+        i += mdlen;
+        b[i++] = (uint8_t)(klen >> 8);
+        b[i++] = (uint8_t)klen;
+    } else {
+        if (b != stackbuf) free(b);
+        return ERR_ILLEGAL_ARGS;
+    }
+    if (klen) memcpy(b + i, key, klen);
+    i += klen;
+    memcpy(b + i, hval, 32);
+    orc_sha256(b, len, out);
+    if (b != stackbuf) free(b);
+    return OK;
+}
+
+/* ------------------------------------------------------------------- htree */
+uint64_t orc_htree_levels_len(uint64_t n) {
+    if (n == 0) return 0;
+    uint64_t t = 0, w = n;
+    for (;;) {
+        t += w;
+        if (w == 1) break;
+        w = (w + 1) / 2;
+    }
+    return t;
+}
+
+uint64_t orc_htree_level_offset(uint64_t n, int level) {
+    uint64_t t = 0, w = n;
+    for (int l = 0; l < level; l++) {
+        t += w;
+        w = (w + 1) / 2;
+    }
+    return t;
+}
+
+/* Levels above the leaves: htree.go:85-110 (pairwise, odd last node promoted). */
+static void reduce_levels(uint8_t *lv, uint64_t n, uint8_t root[32]) {
+    uint64_t w = n, off = 0;
+    while (w > 1) {
+        uint64_t noff = off + w, wn = 0;
+        for (uint64_t i = 0; i + 1 < w; i += 2, wn++)
+            node_hash(lv + (off + i) * 32, lv + (off + i + 1) * 32, lv + (noff + wn) * 32);
+        if (w % 2 == 1) {
+            memcpy(lv + (noff + wn) * 32, lv + (off + w - 1) * 32, 32);
+            wn++;
+        }
+        off = noff;
+        w = wn;
+    }
+    memcpy(root, lv + off * 32, 32);
+}
+
+int orc_htree_build(const uint8_t *digests, uint64_t n, uint8_t *levels, uint8_t root[32]) {
+    if (n == 0) { /* htree.go:73-77 */
+        orc_sha256(NULL, 0, root);
+        return OK;
+    }
+    uint8_t *lv = levels ? levels : (uint8_t *)malloc(orc_htree_levels_len(n) * 32);
+    for (uint64_t i = 0; i < n; i++) leaf_hash(digests + i * 32, lv + i * 32);
+    reduce_levels(lv, n, root);
+    if (!levels) free(lv);
+    return OK;
+}
+
+static int bits_len64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+int orc_htree_inclusion_proof(const uint8_t *levels, uint64_t width, uint64_t i,
+                              uint8_t *terms, uint32_t *nterms) {
+    /* htree.go:121-164 */
+    *nterms = 0;
+    if (i >= width) return ERR_ILLEGAL_ARGS;
+    if (width == 1) return OK;
+    uint64_t m = i, n = width, offset = 0, l, r;
+    uint8_t tmp[64][32];
+    uint32_t cnt = 0;
+    for (;;) {
+        int d = bits_len64(n - 1);
+        uint64_t k = 1ULL << (d - 1);
+        if (m < k) {
+            l = offset + k;
+            r = offset + n - 1;
+            n = k;
+        } else {
+            l = offset;
+            r = offset + k - 1;
+            m -= k;
+            n -= k;
+            offset += k;
+        }
+        int layer = bits_len64(r - l);
+        uint64_t index = l >> layer;
+        memcpy(tmp[cnt++], levels + (orc_htree_level_offset(width, layer) + index) * 32, 32);
+        if (n < 1 || (n == 1 && m == 0)) break;
+    }
+    /* terms are prepended in Go: reverse order of discovery */
+    for (uint32_t t = 0; t < cnt; t++) memcpy(terms + t * 32, tmp[cnt - 1 - t], 32);
+    *nterms = cnt;
+    return OK;
+}
+
+int orc_htree_verify_inclusion(uint64_t leaf, uint64_t width, const uint8_t *terms,
+                               uint32_t nterms, const uint8_t digest[32], const uint8_t root[32]) {
+    /* htree.go:166-195 (a nil proof is modelled by the caller) */
+    uint8_t calc[32];
+    leaf_hash(digest, calc);
+    uint64_t i = leaf, r = width - 1;
+    for (uint32_t t = 0; t < nterms; t++) {
+        if (i % 2 == 0 && i != r)
+            node_hash(calc, terms + t * 32, calc);
+        else
+            node_hash(terms + t * 32, calc, calc);
+        i /= 2;
+        r /= 2;
+    }
+    return i == r && memcmp(calc, root, 32) == 0;
+}
+
+/* ---------------------------------------------------------- entries -> Eh */
+int orc_build_entries(int version, uint64_t n, const uint8_t *keys, const uint64_t *key_off,
+                      const uint8_t *md, const uint64_t *md_off, const uint8_t *vals,
+                      const uint64_t *val_off, const uint8_t *hval_override,
+                      const uint8_t *use_override, uint8_t *hvals_out, uint8_t *levels,
+                      uint8_t root[32]) {
+    if (n == 0) {
+        orc_sha256(NULL, 0, root);
+        return OK;
+    }
+    uint8_t *dig = (uint8_t *)malloc(n * 32);
+    int st = OK;
+    for (uint64_t i = 0; i < n && st == OK; i++) {
+        uint8_t hv[32];
+        /* immustore.go:1620-1630 */
+        if (use_override && use_override[i])
+            memcpy(hv, hval_override + i * 32, 32);
+        else
+            orc_sha256(vals + val_off[i], val_off[i + 1] - val_off[i], hv);
+        if (hvals_out) memcpy(hvals_out + i * 32, hv, 32);
+        size_t mdl = md_off ? md_off[i + 1] - md_off[i] : 0;
+        st = orc_entry_digest(version, keys + key_off[i], key_off[i + 1] - key_off[i],
+                              mdl ? md + md_off[i] : NULL, mdl, hv, dig + i * 32);
+    }
+    if (st == OK) st = orc_htree_build(dig, n, levels, root);
+    free(dig);
+    return st;
+}
+
+typedef struct {
+    int version;
+    uint64_t lo, hi;
+    const uint8_t *keys, *vals;
+    uint32_t key_len, val_len;
+    uint8_t *hvals, *lv; /* lv = leaf level base (level 0) */
+} fixed_job;
+
+static void *fixed_worker(void *arg) {
+    fixed_job *j = (fixed_job *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        uint8_t hv[32], d[32];
+        orc_sha256(j->vals + i * (uint64_t)j->val_len, j->val_len, hv);
+        if (j->hvals) memcpy(j->hvals + i * 32, hv, 32);
+        orc_entry_digest(j->version, j->keys + i * (uint64_t)j->key_len, j->key_len, NULL, 0, hv, d);
+        leaf_hash(d, j->lv + i * 32);
+    }
+    return NULL;
+}
+
+int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32_t key_len,
+                            const uint8_t *vals, uint32_t val_len, uint8_t *hvals_out,
+                            uint8_t *levels, uint8_t root[32], int nthreads) {
+    if (version != 0 && version != 1) return ERR_ILLEGAL_ARGS;
+    if (n == 0) {
+        orc_sha256(NULL, 0, root);
+        return OK;
+    }
+    uint8_t *lv = levels ? levels : (uint8_t *)malloc(orc_htree_levels_len(n) * 32);
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = (int)n;
+    /* leaf hashing split into contiguous ranges; the pairwise levels are
+     * independent of how the leaves were produced. */
+    fixed_job jobs[256];
+    pthread_t th[256];
+    if (nthreads > 256) nthreads = 256;
+    uint64_t per = (n + nthreads - 1) / nthreads;
+    int used = 0;
+    for (int t = 0; t < nthreads; t++) {
+        uint64_t lo = (uint64_t)t * per, hi = lo + per > n ? n : lo + per;
+        if (lo >= hi) break;
+        jobs[t] = (fixed_job){version, lo, hi, keys, vals, key_len, val_len, hvals_out, lv};
+        used++;
+    }
+    if (used == 1) {
+        fixed_worker(&jobs[0]);
+    } else {
+        for (int t = 0; t < used; t++) pthread_create(&th[t], NULL, fixed_worker, &jobs[t]);
+        for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
+    }
+    reduce_levels(lv, n, root);
+    if (!levels) free(lv);
+    return OK;
+}
+
+/* ------------------------------------------------------------- tx header */
+int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmdlen,
+                      uint32_t nentries, const uint8_t eh[32], uint64_t bltxid,
+                      const uint8_t blroot[32], uint8_t out[32]) {
+    /* tx.go:249-302: ts + version + (v0: BE16 nentries | v1: BE16 mdLen md BE32 nentries)
+     * + eh + blTxID + blRoot */
+    uint8_t b[8 + 2 + 2 + 256 + 4 + 32 + 8 + 32];
+    size_t i = 0;
+    for (int k = 7; k >= 0; k--) b[i++] = (uint8_t)(ts >> (8 * k));
+    b[i++] = (uint8_t)(version >> 8);
+    b[i++] = (uint8_t)version;
+    if (version == 0) {
+        if (txmdlen) return ERR_MD_UNSUPPORTED;
+        b[i++] = (uint8_t)(nentries >> 8);
+        b[i++] = (uint8_t)nentries;
+    } else if (version == 1) {
+        if (txmdlen > 256) return ERR_ILLEGAL_ARGS;
+        b[i++] = (uint8_t)(txmdlen >> 8);
+        b[i++] = (uint8_t)txmdlen;
+        if (txmdlen) memcpy(b + i, txmd, txmdlen);
+        i += txmdlen;
+        for (int k = 3; k >= 0; k--) b[i++] = (uint8_t)(nentries >> (8 * k));
+    } else {
+        return ERR_ILLEGAL_ARGS;
+    }
+    memcpy(b + i, eh, 32);
+    i += 32;
+    for (int k = 7; k >= 0; k--) b[i++] = (uint8_t)(bltxid >> (8 * k));
+    memcpy(b + i, blroot, 32);
+    i += 32;
+    orc_sha256(b, i, out);
+    return OK;
+}
+
+void orc_tx_alh(uint64_t id, const uint8_t prev_alh[32], const uint8_t inner[32], uint8_t out[32]) {
+    /* tx.go:307-319 and verification.go:32-38 (advanceLinearHash) */
+    uint8_t b[72];
+    for (int k = 7; k >= 0; k--) b[7 - k] = (uint8_t)(id >> (8 * k));
+    memcpy(b + 8, prev_alh, 32);
+    memcpy(b + 40, inner, 32);
+    orc_sha256(b, 72, out);
+}
+
+/* ------------------------------------------------------------------ ahtree */
+uint64_t orc_ahtree_nodes_upto(uint64_t n) {
+    /* ahtree.go:492-511 */
+    uint64_t o = n;
+    for (int l = 0; l < 64 && n >= (1ULL << l); l++) {
+        o += (n >> (l + 1)) << l;
+        if ((n >> l) & 1) o += n & ((1ULL << l) - 1);
+    }
+    return o;
+}
+
+uint64_t orc_ahtree_nodes_until(uint64_t n) { return n == 1 ? 0 : orc_ahtree_nodes_upto(n - 1); }
+
+static const uint8_t *aht_node(const uint8_t *dlog, uint64_t k, int l) {
+    /* ahtree.go:460-462 node(n,l) = dLog[nodesUntil(n)+l] */
+    return dlog + (orc_ahtree_nodes_until(k) + (uint64_t)l) * 32;
+}
+
+int orc_ahtree_append(uint8_t *dlog, uint64_t n_before, const uint8_t *payload, size_t plen,
+                      uint8_t root[32]) {
+    /* ahtree.go:246-322 */
+    uint64_t n = n_before + 1;
+    uint8_t *out = dlog + orc_ahtree_nodes_until(n) * 32;
+    uint8_t stackbuf[129], *b = plen + 1 <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(plen + 1);
+    b[0] = 0;
+    if (plen) memcpy(b + 1, payload, plen);
+    uint8_t h[32];
+    orc_sha256(b, plen + 1, h);
+    if (b != stackbuf) free(b);
+    memcpy(out, h, 32);
+    int cnt = 1;
+    uint64_t w = n - 1, k = n - 1;
+    for (int l = 0; w > 0; l++) {
+        if (w & 1) {
+            node_hash(aht_node(dlog, k, l), h, h);
+            memcpy(out + 32 * cnt++, h, 32);
+        }
+        k &= ~(1ULL << l);
+        w >>= 1;
+    }
+    if (root) memcpy(root, h, 32);
+    return OK;
+}
+
+int orc_ahtree_append_batch(uint8_t *dlog, uint64_t n_before, const uint8_t *payloads,
+                            uint64_t m, size_t plen) {
+    for (uint64_t i = 0; i < m; i++) orc_ahtree_append(dlog, n_before + i, payloads + i * plen, plen, NULL);
+    return OK;
+}
+
+int orc_ahtree_root_at(const uint8_t *dlog, uint64_t size, uint64_t n, uint8_t out[32]) {
+    /* ahtree.go:749-771 */
+    if (n == 0) return ERR_ILLEGAL_ARGS;
+    if (size == 0) return ERR_EMPTY;
+    if (n > size) return ERR_UNEXISTENT;
+    memcpy(out, aht_node(dlog, n, __builtin_popcountll(n - 1)), 32);
+    return OK;
+}
+
+/* proof assembly helpers: terms are prepended in Go; we build into a reversed
+ * stack and flip at the end. */
+typedef struct {
+    uint8_t t[192][32];
+    uint32_t n;
+} stack_t_;
+
+static void push_front_seq(stack_t_ *s, const uint8_t *d) { memcpy(s->t[s->n++], d, 32); }
+
+static const uint8_t *highest_node(const uint8_t *dlog, uint64_t i, int d) {
+    /* ahtree.go:653-661 */
+    int l = 0;
+    for (int r = d - 1; r >= 0; r--)
+        if ((i - 1) & (1ULL << r)) l++;
+    return aht_node(dlog, i, l);
+}
+
+/* Go inclusionProof (ahtree.go:545-577) returns p ++ proof where proof gets
+ * prepends.  Rewritten iteratively: we collect the sequence of prepended
+ * terms in "prepend order" (s) so that the final proof is reverse(s). */
+static void incl(const uint8_t *dlog, uint64_t i, uint64_t j, int height, stack_t_ *s) {
+    for (int h = height - 1; h >= 0; h--) {
+        if ((j - 1) & (1ULL << h)) {
+            uint64_t k = (j - 1) >> h << h;
+            if (i <= k) {
+                push_front_seq(s, highest_node(dlog, j, h));
+                incl(dlog, i, k, h, s);
+                return;
+            }
+            push_front_seq(s, aht_node(dlog, k, h));
+        }
+    }
+}
+
+static void cons(const uint8_t *dlog, uint64_t i, uint64_t j, int height, stack_t_ *s) {
+    /* ahtree.go:596-651 */
+    for (int h = height - 1; h >= 0; h--) {
+        if ((j - 1) & (1ULL << h)) {
+            uint64_t k = (j - 1) >> h << h;
+            if (i <= k) {
+                push_front_seq(s, highest_node(dlog, j, h));
+                if (i < k) cons(dlog, i, k, h, s);
+                if (i == k) push_front_seq(s, highest_node(dlog, i, h));
+                return;
+            }
+            push_front_seq(s, aht_node(dlog, k, h));
+            if (i == j) {
+                push_front_seq(s, highest_node(dlog, i, h));
+                return;
+            }
+        }
+    }
+}
+
+static int finish_proof(stack_t_ *s, uint8_t *terms, uint32_t *nterms) {
+    for (uint32_t t = 0; t < s->n; t++) memcpy(terms + 32 * t, s->t[s->n - 1 - t], 32);
+    *nterms = s->n;
+    return OK;
+}
+
+int orc_ahtree_inclusion_proof(const uint8_t *dlog, uint64_t size, uint64_t i, uint64_t j,
+                               uint8_t *terms, uint32_t *nterms) {
+    /* ahtree.go:525-543 */
+    *nterms = 0;
+    if (i > j) return ERR_ILLEGAL_ARGS;
+    if (j > size) return ERR_UNEXISTENT;
+    stack_t_ s;
+    s.n = 0;
+    incl(dlog, i, j, bits_len64(j - 1), &s);
+    return finish_proof(&s, terms, nterms);
+}
+
+int orc_ahtree_consistency_proof(const uint8_t *dlog, uint64_t size, uint64_t i, uint64_t j,
+                                 uint8_t *terms, uint32_t *nterms) {
+    /* ahtree.go:579-594 */
+    *nterms = 0;
+    if (i > j) return ERR_ILLEGAL_ARGS;
+    if (j > size) return ERR_UNEXISTENT;
+    stack_t_ s;
+    s.n = 0;
+    cons(dlog, i, j, bits_len64(j - 1), &s);
+    return finish_proof(&s, terms, nterms);
+}
+
+void orc_ahtree_eval_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                               const uint8_t leaf[32], uint8_t out[32]) {
+    /* ahtree/verification.go:32-56 */
+    uint64_t i1 = i - 1, j1 = j - 1;
+    uint8_t c[32];
+    memcpy(c, leaf, 32);
+    for (uint32_t t = 0; t < nterms; t++) {
+        if (i1 % 2 == 0 && i1 != j1)
+            node_hash(c, terms + 32 * t, c);
+        else
+            node_hash(terms + 32 * t, c, c);
+        i1 >>= 1;
+        j1 >>= 1;
+    }
+    memcpy(out, c, 32);
+}
+
+int orc_ahtree_verify_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                const uint8_t leaf[32], const uint8_t root[32]) {
+    /* ahtree/verification.go:21-30 */
+    if (i > j || i == 0 || (i < j && nterms == 0)) return 0;
+    uint8_t c[32];
+    orc_ahtree_eval_inclusion(terms, nterms, i, j, leaf, c);
+    return memcmp(c, root, 32) == 0;
+}
+
+int orc_ahtree_eval_consistency(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                uint8_t ci[32], uint8_t cj[32]) {
+    /* ahtree/verification.go:72-109.  Go indexes cproof[0] unguarded; we
+     * return ERR_ILLEGAL_ARGS for an empty proof instead of panicking. */
+    if (nterms == 0) return ERR_ILLEGAL_ARGS;
+    uint64_t fn = i - 1, sn = j - 1;
+    while (fn % 2 == 1) {
+        fn >>= 1;
+        sn >>= 1;
+    }
+    memcpy(ci, terms, 32);
+    memcpy(cj, terms, 32);
+    for (uint32_t t = 1; t < nterms; t++) {
+        const uint8_t *h = terms + 32 * t;
+        if (fn % 2 == 1 || fn == sn) {
+            node_hash(h, ci, ci);
+            node_hash(h, cj, cj);
+            while (fn % 2 == 0 && fn != 0) {
+                fn >>= 1;
+                sn >>= 1;
+            }
+        } else {
+            node_hash(cj, h, cj);
+        }
+        fn >>= 1;
+        sn >>= 1;
+    }
+    return OK;
+}
+
+int orc_ahtree_verify_consistency(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                  const uint8_t iroot[32], const uint8_t jroot[32]) {
+    /* ahtree/verification.go:58-70 */
+    if (i > j || i == 0 || (i < j && nterms == 0)) return 0;
+    if (i == j && nterms == 0) return memcmp(iroot, jroot, 32) == 0;
+    uint8_t ci[32], cj[32];
+    orc_ahtree_eval_consistency(terms, nterms, i, j, ci, cj);
+    return memcmp(iroot, ci, 32) == 0 && memcmp(jroot, cj, 32) == 0;
+}
+
+void orc_ahtree_eval_last_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i,
+                                    const uint8_t leaf[32], uint8_t out[32]) {
+    /* ahtree/verification.go:120-137 */
+    (void)i;
+    uint8_t r[32];
+    memcpy(r, leaf, 32);
+    for (uint32_t t = 0; t < nterms; t++) node_hash(terms + 32 * t, r, r);
+    memcpy(out, r, 32);
+}
+
+int orc_ahtree_verify_last_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i,
+                                     const uint8_t leaf[32], const uint8_t root[32]) {
+    /* ahtree/verification.go:111-118 */
+    if (i == 0) return 0;
+    uint8_t r[32];
+    orc_ahtree_eval_last_inclusion(terms, nterms, i, leaf, r);
+    return memcmp(r, root, 32) == 0;
+}
+
+/* ------------------------------------------------------------ synthetic */
+void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed) {
+    /* word w = splitmix64 output number w+1 from state `seed` (little endian) */
+    uint64_t nw = (nbytes + 7) / 8;
+    for (uint64_t w = 0; w < nw; w++) {
+        uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        z ^= z >> 31;
+        uint64_t left = nbytes - w * 8;
+        if (left >= 8)
+            memcpy(dst + w * 8, &z, 8);
+        else
+            memcpy(dst + w * 8, &z, left);
+    }
+}

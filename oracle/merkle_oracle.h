@@ -1,0 +1,110 @@
+/*
+ * merkle_oracle.h -- CPU restatement of immudb's Merkle-hash path.
+ *
+ * TEST INFRASTRUCTURE.  This is the parity oracle and the timed CPU baseline
+ * (bench.py `cpu_baseline`, kind "port").  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product library
+ * (immustore_amd/libimmustore_merkle.so) never links or calls it.
+ *
+ * Pinned by: the Go-written fixtures of the reference (tests/golden/
+ * immudb_fixtures.json: 36 stored Alh values, 42 stored values/hVal pairs and
+ * three ahtree dLog streams) and the reference's own known-answer tables
+ * (nodesUpto 1..16, empty root = SHA256(nil)).  See tests/test_oracle.py.
+ *
+ * Every function names the reference file:line it restates.  Status codes are
+ * the same as include/immustore_merkle.h (MH_*).
+ */
+#ifndef IMMUSTORE_MERKLE_ORACLE_H
+#define IMMUSTORE_MERKLE_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* FIPS 180-4 SHA-256 (Go crypto/sha256.Sum256, pinned by Go 1.18 toolchain). */
+void orc_sha256(const uint8_t *msg, size_t len, uint8_t out[32]);
+int orc_sha256_has_shani(void);
+void orc_sha256_use_shani(int enable); /* 0 = force portable code */
+
+/* embedded/store/tx.go:690-701 (v0, version 0) and :703-731 (v1, version 1).
+ * Returns 0, or 6 (MH_ERR_METADATA_UNSUPPORTED) for v0 with non-empty md. */
+int orc_entry_digest(int version, const uint8_t *key, size_t klen, const uint8_t *md,
+                     size_t mdlen, const uint8_t hval[32], uint8_t out[32]);
+
+/* Number of 32-byte nodes in the flat level-major layout: sum_l ceil(n/2^l)
+ * while the width is > 1, plus the root level (htree.go:88-107). */
+uint64_t orc_htree_levels_len(uint64_t n);
+/* Offset (in nodes) of level l inside that flat layout. */
+uint64_t orc_htree_level_offset(uint64_t n, int level);
+
+/* embedded/htree/htree.go:68-113.  levels may be NULL. */
+int orc_htree_build(const uint8_t *digests, uint64_t n, uint8_t *levels, uint8_t root[32]);
+/* embedded/htree/htree.go:121-164.  terms has room for 64 terms. */
+int orc_htree_inclusion_proof(const uint8_t *levels, uint64_t width, uint64_t i,
+                              uint8_t *terms, uint32_t *nterms);
+/* embedded/htree/htree.go:166-195.  returns 1 = verifies. */
+int orc_htree_verify_inclusion(uint64_t leaf, uint64_t width, const uint8_t *terms,
+                               uint32_t nterms, const uint8_t digest[32], const uint8_t root[32]);
+
+/* Value hash loop (embedded/store/immustore.go:1620-1630) + Tx.BuildHashTree
+ * (embedded/store/tx.go:332-355): CSR inputs (offsets have n+1 entries).
+ * md / md_off may be NULL (no KV metadata).  hval_override / use_override
+ * (IsValueTruncated) may be NULL.  hvals_out / levels may be NULL. */
+int orc_build_entries(int version, uint64_t n, const uint8_t *keys, const uint64_t *key_off,
+                      const uint8_t *md, const uint64_t *md_off, const uint8_t *vals,
+                      const uint64_t *val_off, const uint8_t *hval_override,
+                      const uint8_t *use_override, uint8_t *hvals_out, uint8_t *levels,
+                      uint8_t root[32]);
+/* Same with fixed-stride keys / values and no metadata (BASELINE C1/C2 layout).
+ * nthreads > 1 splits the leaf range into power-of-two chunks (exact by
+ * SURVEY.md finding 3). */
+int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32_t key_len,
+                            const uint8_t *vals, uint32_t val_len, uint8_t *hvals_out,
+                            uint8_t *levels, uint8_t root[32], int nthreads);
+
+/* TxHeader.innerHash / Alh: embedded/store/tx.go:249-319. */
+int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmdlen,
+                      uint32_t nentries, const uint8_t eh[32], uint64_t bltxid,
+                      const uint8_t blroot[32], uint8_t out[32]);
+void orc_tx_alh(uint64_t id, const uint8_t prev_alh[32], const uint8_t inner[32], uint8_t out[32]);
+
+/* ahtree: embedded/ahtree/ahtree.go. The dLog is a flat array of digests. */
+uint64_t orc_ahtree_nodes_upto(uint64_t n);  /* ahtree.go:492-511 */
+uint64_t orc_ahtree_nodes_until(uint64_t n); /* ahtree.go:485-490 */
+/* ahtree.go:246-373: append one payload to a tree of size n_before; dlog has
+ * room for nodesUpto(n_before+1) digests. Writes the new root to root (opt). */
+int orc_ahtree_append(uint8_t *dlog, uint64_t n_before, const uint8_t *payload, size_t plen,
+                      uint8_t root[32]);
+/* Fixed-size payload batch (syncBinaryLinking analog, immustore.go:1198-1232). */
+int orc_ahtree_append_batch(uint8_t *dlog, uint64_t n_before, const uint8_t *payloads,
+                            uint64_t m, size_t plen);
+int orc_ahtree_root_at(const uint8_t *dlog, uint64_t size, uint64_t n, uint8_t out[32]);
+int orc_ahtree_inclusion_proof(const uint8_t *dlog, uint64_t size, uint64_t i, uint64_t j,
+                               uint8_t *terms, uint32_t *nterms);
+int orc_ahtree_consistency_proof(const uint8_t *dlog, uint64_t size, uint64_t i, uint64_t j,
+                                 uint8_t *terms, uint32_t *nterms);
+/* embedded/ahtree/verification.go */
+void orc_ahtree_eval_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                               const uint8_t leaf[32], uint8_t out[32]);
+int orc_ahtree_verify_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                const uint8_t leaf[32], const uint8_t root[32]);
+int orc_ahtree_eval_consistency(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                uint8_t ci[32], uint8_t cj[32]);
+int orc_ahtree_verify_consistency(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
+                                  const uint8_t iroot[32], const uint8_t jroot[32]);
+void orc_ahtree_eval_last_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i,
+                                    const uint8_t leaf[32], uint8_t out[32]);
+int orc_ahtree_verify_last_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i,
+                                     const uint8_t leaf[32], const uint8_t root[32]);
+
+/* Deterministic synthetic input used by tests and bench (splitmix64 stream,
+ * little-endian words): identical to immustore_amd's device generator. */
+void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,285 @@
+"""ctypes binding of oracle/liboracle.so -- the CPU restatement of the path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+`cpu_baseline` leg of bench.py, always as the checker / baseline, never as the
+thing measured or shipped.  immustore_amd/ never imports this module.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+u8p = C.POINTER(C.c_uint8)
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+
+
+def _p(a, t=u8p):
+    if a is None:
+        return None
+    return a.ctypes.data_as(t)
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_sha256.argtypes = [u8p, C.c_size_t, u8p]
+        L.orc_entry_digest.argtypes = [C.c_int, u8p, C.c_size_t, u8p, C.c_size_t, u8p, u8p]
+        L.orc_htree_levels_len.restype = C.c_uint64
+        L.orc_htree_levels_len.argtypes = [C.c_uint64]
+        L.orc_htree_level_offset.restype = C.c_uint64
+        L.orc_htree_level_offset.argtypes = [C.c_uint64, C.c_int]
+        L.orc_htree_build.argtypes = [u8p, C.c_uint64, u8p, u8p]
+        L.orc_htree_inclusion_proof.argtypes = [u8p, C.c_uint64, C.c_uint64, u8p, u32p]
+        L.orc_htree_verify_inclusion.argtypes = [C.c_uint64, C.c_uint64, u8p, C.c_uint32, u8p, u8p]
+        L.orc_build_entries.argtypes = [C.c_int, C.c_uint64, u8p, u64p, u8p, u64p, u8p, u64p,
+                                        u8p, u8p, u8p, u8p, u8p]
+        L.orc_build_entries_fixed.argtypes = [C.c_int, C.c_uint64, u8p, C.c_uint32, u8p,
+                                              C.c_uint32, u8p, u8p, u8p, C.c_int]
+        L.orc_tx_inner_hash.argtypes = [C.c_uint64, C.c_int, u8p, C.c_size_t, C.c_uint32, u8p,
+                                        C.c_uint64, u8p, u8p]
+        L.orc_tx_alh.argtypes = [C.c_uint64, u8p, u8p, u8p]
+        L.orc_ahtree_nodes_upto.restype = C.c_uint64
+        L.orc_ahtree_nodes_upto.argtypes = [C.c_uint64]
+        L.orc_ahtree_nodes_until.restype = C.c_uint64
+        L.orc_ahtree_nodes_until.argtypes = [C.c_uint64]
+        L.orc_ahtree_append.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t, u8p]
+        L.orc_ahtree_append_batch.argtypes = [u8p, C.c_uint64, u8p, C.c_uint64, C.c_size_t]
+        L.orc_ahtree_root_at.argtypes = [u8p, C.c_uint64, C.c_uint64, u8p]
+        L.orc_ahtree_inclusion_proof.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]
+        L.orc_ahtree_consistency_proof.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]
+        L.orc_ahtree_eval_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_verify_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_eval_consistency.argtypes = [u8p, C.c_uint32, C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_verify_consistency.argtypes = [u8p, C.c_uint32, C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_eval_last_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_verify_last_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, u8p]
+        L.orc_fill_random.argtypes = [u8p, C.c_uint64, C.c_uint64]
+        L.orc_sha256_use_shani.argtypes = [C.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _u8(b):
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy() if not isinstance(b, np.ndarray) else b
+
+
+def sha256(b):
+    a = _u8(b)
+    out = np.zeros(32, np.uint8)
+    lib().orc_sha256(_p(a) if len(a) else None, len(a), _p(out))
+    return out.tobytes()
+
+
+def entry_digest(version, key, md, hval):
+    k, m, h = _u8(key), _u8(md), _u8(hval)
+    out = np.zeros(32, np.uint8)
+    st = lib().orc_entry_digest(version, _p(k) if len(k) else None, len(k),
+                                _p(m) if len(m) else None, len(m), _p(h), _p(out))
+    return st, out.tobytes()
+
+
+def levels_len(n):
+    return lib().orc_htree_levels_len(n)
+
+
+def level_offset(n, l):
+    return lib().orc_htree_level_offset(n, l)
+
+
+def htree_build(digests):
+    """digests: (n,32) uint8 -> (levels flat (L,32), root bytes)."""
+    d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)
+    n = d.shape[0]
+    lv = np.zeros((max(levels_len(n), 1), 32), np.uint8)
+    root = np.zeros(32, np.uint8)
+    lib().orc_htree_build(_p(d) if n else None, n, _p(lv), _p(root))
+    return lv[:levels_len(n)], root.tobytes()
+
+
+def htree_inclusion_proof(levels, width, i):
+    terms = np.zeros((64, 32), np.uint8)
+    nt = C.c_uint32(0)
+    st = lib().orc_htree_inclusion_proof(_p(np.ascontiguousarray(levels)), width, i, _p(terms),
+                                         C.byref(nt))
+    return st, terms[:nt.value].copy()
+
+
+def htree_verify_inclusion(leaf, width, terms, digest, root):
+    t = np.ascontiguousarray(terms, dtype=np.uint8).reshape(-1, 32)
+    return bool(lib().orc_htree_verify_inclusion(leaf, width, _p(t) if len(t) else None, len(t),
+                                                 _p(_u8(digest)), _p(_u8(root))))
+
+
+def build_entries_fixed(version, keys, vals, nthreads=1, want_levels=True):
+    """keys (n,klen) u8, vals (n,vlen) u8 -> (hvals, levels, root)."""
+    n = keys.shape[0]
+    hv = np.zeros((n, 32), np.uint8)
+    lv = np.zeros((max(levels_len(n), 1), 32), np.uint8) if want_levels else None
+    root = np.zeros(32, np.uint8)
+    st = lib().orc_build_entries_fixed(version, n, _p(keys), keys.shape[1], _p(vals), vals.shape[1],
+                                       _p(hv), _p(lv), _p(root), nthreads)
+    assert st == 0, st
+    return hv, (lv[:levels_len(n)] if want_levels else None), root.tobytes()
+
+
+def build_entries(version, keys, mds, vals, overrides=None):
+    """Lists of bytes -> (status, hvals, levels, root)."""
+    n = len(keys)
+
+    def csr(items):
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in items]) if n else []
+        buf = np.frombuffer(b"".join(items) + b"\0", dtype=np.uint8).copy()
+        return buf, off
+
+    kb, ko = csr(keys)
+    mb, mo = csr(mds)
+    vb, vo = csr(vals)
+    ov = use = None
+    if overrides is not None:
+        ov = np.zeros((n, 32), np.uint8)
+        use = np.zeros(n, np.uint8)
+        for i, o in enumerate(overrides):
+            if o is not None:
+                ov[i] = np.frombuffer(o, np.uint8)
+                use[i] = 1
+    hv = np.zeros((max(n, 1), 32), np.uint8)
+    lv = np.zeros((max(levels_len(n), 1), 32), np.uint8)
+    root = np.zeros(32, np.uint8)
+    st = lib().orc_build_entries(version, n, _p(kb), _p(ko, u64p), _p(mb), _p(mo, u64p), _p(vb),
+                                 _p(vo, u64p), _p(ov), _p(use), _p(hv), _p(lv), _p(root))
+    return st, hv[:n], lv[:levels_len(n)], root.tobytes()
+
+
+def tx_inner_hash(ts, version, txmd, nentries, eh, bltxid, blroot):
+    m = _u8(txmd)
+    out = np.zeros(32, np.uint8)
+    st = lib().orc_tx_inner_hash(ts, version, _p(m) if len(m) else None, len(m), nentries,
+                                 _p(_u8(eh)), bltxid, _p(_u8(blroot)), _p(out))
+    return st, out.tobytes()
+
+
+def tx_alh(txid, prev_alh, inner):
+    out = np.zeros(32, np.uint8)
+    lib().orc_tx_alh(txid, _p(_u8(prev_alh)), _p(_u8(inner)), _p(out))
+    return out.tobytes()
+
+
+def nodes_upto(n):
+    return lib().orc_ahtree_nodes_upto(n)
+
+
+def nodes_until(n):
+    return lib().orc_ahtree_nodes_until(n)
+
+
+class AHtree:
+    """Growable in-memory dLog over the oracle's ahtree functions."""
+
+    def __init__(self, cap=1024):
+        self.size = 0
+        self.dlog = np.zeros((nodes_upto(cap), 32), np.uint8)
+
+    def _grow(self, n):
+        need = nodes_upto(n)
+        if need > self.dlog.shape[0]:
+            nd = np.zeros((max(need, 2 * self.dlog.shape[0]), 32), np.uint8)
+            nd[:self.dlog.shape[0]] = self.dlog
+            self.dlog = nd
+
+    def append(self, payload):
+        p = _u8(payload)
+        self._grow(self.size + 1)
+        r = np.zeros(32, np.uint8)
+        lib().orc_ahtree_append(_p(self.dlog), self.size, _p(p) if len(p) else None, len(p), _p(r))
+        self.size += 1
+        return r.tobytes()
+
+    def append_batch(self, payloads):
+        p = np.ascontiguousarray(payloads, np.uint8)
+        m, plen = p.shape
+        self._grow(self.size + m)
+        lib().orc_ahtree_append_batch(_p(self.dlog), self.size, _p(p), m, plen)
+        self.size += m
+
+    def dlog_bytes(self):
+        return self.dlog[:nodes_upto(self.size)].tobytes()
+
+    def root_at(self, n):
+        out = np.zeros(32, np.uint8)
+        st = lib().orc_ahtree_root_at(_p(self.dlog), self.size, n, _p(out))
+        return st, out.tobytes()
+
+    def inclusion_proof(self, i, j):
+        t = np.zeros((192, 32), np.uint8)
+        nt = C.c_uint32(0)
+        st = lib().orc_ahtree_inclusion_proof(_p(self.dlog), self.size, i, j, _p(t), C.byref(nt))
+        return st, t[:nt.value].copy()
+
+    def consistency_proof(self, i, j):
+        t = np.zeros((192, 32), np.uint8)
+        nt = C.c_uint32(0)
+        st = lib().orc_ahtree_consistency_proof(_p(self.dlog), self.size, i, j, _p(t), C.byref(nt))
+        return st, t[:nt.value].copy()
+
+
+def _terms(t):
+    t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, 32)
+    return (_p(t) if len(t) else None), len(t)
+
+
+def ahtree_verify_inclusion(proof, i, j, leaf, root):
+    tp, nt = _terms(proof)
+    return bool(lib().orc_ahtree_verify_inclusion(tp, nt, i, j, _p(_u8(leaf)), _p(_u8(root))))
+
+
+def ahtree_eval_inclusion(proof, i, j, leaf):
+    tp, nt = _terms(proof)
+    out = np.zeros(32, np.uint8)
+    lib().orc_ahtree_eval_inclusion(tp, nt, i, j, _p(_u8(leaf)), _p(out))
+    return out.tobytes()
+
+
+def ahtree_verify_consistency(proof, i, j, iroot, jroot):
+    tp, nt = _terms(proof)
+    return bool(lib().orc_ahtree_verify_consistency(tp, nt, i, j, _p(_u8(iroot)), _p(_u8(jroot))))
+
+
+def ahtree_eval_consistency(proof, i, j):
+    tp, nt = _terms(proof)
+    ci = np.zeros(32, np.uint8)
+    cj = np.zeros(32, np.uint8)
+    st = lib().orc_ahtree_eval_consistency(tp, nt, i, j, _p(ci), _p(cj))
+    return st, ci.tobytes(), cj.tobytes()
+
+
+def ahtree_verify_last_inclusion(proof, i, leaf, root):
+    tp, nt = _terms(proof)
+    return bool(lib().orc_ahtree_verify_last_inclusion(tp, nt, i, _p(_u8(leaf)), _p(_u8(root))))
+
+
+def fill_random(nbytes, seed):
+    out = np.zeros(nbytes, np.uint8)
+    lib().orc_fill_random(_p(out), nbytes, seed)
+    return out
+
+
+def use_shani(enable):
+    lib().orc_sha256_use_shani(1 if enable else 0)
+
+
+def has_shani():
+    return bool(lib().orc_sha256_has_shani())
