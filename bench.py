@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's headline metric on MI355X.
+
+metric: device-resident GiB/s hashed, htree build, 1M x 1 KiB leaves.
+
+One "step" = one full htree build over one batch of entries already resident
+in HBM (BASELINE configs[1]): for every entry hVal = SHA256(value) (1 KiB),
+the v1 entry digest, the leaf hash, and every level of the tree up to the
+root (embedded/store/immustore.go:1620-1632, tx.go:332-355, htree.go:68-113),
+all by the HIP kernels of libimmustore_merkle.so through its C ABI.
+
+--gpus N (launched by torch.distributed.run, one process per GPU): every rank
+builds the subtree over its own 2^20 entries (power-of-two aligned shard of a
+global N x 2^20-leaf tree), the N subtree roots are all-gathered over RCCL and
+the top log2(N) levels are reduced on every rank (exact by
+finding 3).  Weak scaling: per-GPU work is fixed.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+N_ENTRIES = 1 << 20
+VAL_LEN = 1024
+KEY_LEN = 8
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# int32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (same lanes/clk as the
+# 157.3 TFLOPS fp32 vector peak without the FMA factor of 2).
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
+# VALU instructions per 64-byte compression of the generic compress() in the
+# gfx950 ISA of this build (counted in profiles/isa_counts_r01.txt); the
+# constant-schedule padding block (compress_kw) needs fewer.
+OPS_PER_COMP = 1399
+OPS_PER_COMP_KW = 840
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--entries", type=int, default=N_ENTRIES)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="target CPU work of the cpu_baseline sample")
+    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
+                   help="PMC-derived HBM bytes per launch of the dominant kernel (or missing)")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Oracle (C restatement, oracle/) on the host: one thread, SHA-NI if present."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    orc.use_shani(True)
+
+    def run(n):
+        vals = orc.fill_random(n * VAL_LEN, 2).reshape(n, VAL_LEN)
+        keys = np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8).reshape(n, KEY_LEN)
+        t0 = time.perf_counter()
+        orc.build_entries_fixed(1, keys, vals, nthreads=1)
+        return time.perf_counter() - t0
+
+    probe = 1 << 13
+    dt = run(probe)
+    n = int(min(N_ENTRIES, max(probe, probe * seconds / max(dt, 1e-6))))
+    n = 1 << (n.bit_length() - 1)  # power of two: an aligned subtree of the workload
+    dt = run(n)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(n * VAL_LEN / dt / 2 ** 30, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "htree build over the first %d of the 2^20 x 1 KiB entries (key BE64(i), v1, "
+                  "seed 2), single thread, SHA-NI=%s, %.2f s, CPU: %s" % (
+                      n, orc.has_shani(), dt, model),
+    }
+
+
+def main():
+    a = parse()
+    import torch
+    import immustore_amd as m
+    from immustore_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world != 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    dist = None
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    stream = torch.cuda.current_stream(dev)
+    ctx = m.Context(local, stream.cuda_stream)
+    L = N.load()
+    n = a.entries
+    # inputs resident in HBM before the timed region (synthetic, deterministic)
+    vals = torch.empty(n * VAL_LEN, dtype=torch.uint8, device=dev)
+    keys = torch.empty(n * KEY_LEN, dtype=torch.uint8, device=dev)
+    N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 2 + rank))
+    N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, rank * n))
+    nlv = m.levels_len(n)
+    levels = torch.empty(nlv * 32, dtype=torch.uint8, device=dev)
+    root = torch.empty(32, dtype=torch.uint8, device=dev)
+    if world > 1:
+        roots = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+        top_levels = torch.empty(max(m.levels_len(world), 1) * 32, dtype=torch.uint8, device=dev)
+        groot = torch.empty(32, dtype=torch.uint8, device=dev)
+
+    def step():
+        N.check(L.mh_dev_htree_build_entries_fixed(ctx.handle, 1, n, keys.data_ptr(), KEY_LEN,
+                                                   vals.data_ptr(), VAL_LEN, None,
+                                                   levels.data_ptr(), root.data_ptr()))
+        if world > 1:
+            dist.all_gather_into_tensor(roots, root)
+            N.check(L.mh_dev_htree_reduce_nodes(ctx.handle, roots.data_ptr(), world,
+                                                top_levels.data_ptr(), groot.data_ptr()))
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    ctx.set_timing(False)
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    k_ms, k_cnt = ctx.timing("entries_fixed")
+    r_ms, r_cnt = ctx.timing("reduce")
+    kern_ms = k_ms / max(k_cnt, 1)
+    lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
+    lvl_written = sum(-(-n // (1 << l)) for l in range({1: 1, 2: 2, 4: 3}[lpl]))
+    # algorithmic HBM bytes of one launch of the dominant kernel:
+    #   read value + key of every entry, write the levels the kernel owns
+    alg_bytes = n * (VAL_LEN + KEY_LEN) + 32 * lvl_written
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    comps = n * (VAL_LEN // 64 + 2) + (lvl_written - n) * 2  # + pad block below
+    valu = (comps * OPS_PER_COMP + n * OPS_PER_COMP_KW) / (kern_ms * 1e-3)
+    traffic = None
+    if os.path.exists(a.traffic_file):
+        try:
+            traffic = json.load(open(a.traffic_file)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    total_bytes = world * n * VAL_LEN
+    value = total_bytes / elapsed * a.steps / 2 ** 30
+    out = {
+        "metric": "device-resident GiB/s hashed, htree build, 1M x 1KiB leaves",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (splitmix64 values generated in HBM, keys BE64(i))",
+        "config": {"workload": "htree build (value SHA-256 + TxEntryDigest_v1_2 + leaf + all "
+                               "levels), %d x %d B entries per GPU, %d B keys" % (n, VAL_LEN, KEY_LEN),
+                   "entries_per_gpu": n, "value_len": VAL_LEN, "key_len": KEY_LEN,
+                   "parallelism": "subtree shard per GPU + RCCL all-gather of roots"
+                   if world > 1 else "single GPU", "lanes_per_leaf_group": lpl},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "k_entries_fixed",
+                     "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                     "valu": {"achieved_tops": round(valu / 1e12, 2),
+                              "peak_tops": round(VALU_PEAK_OPS / 1e12, 2),
+                              "frac": round(valu / VALU_PEAK_OPS, 4)},
+                     "reduce_ms_per_step": round(r_ms / max(a.steps, 1), 4)},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+"""ctypes binding of libimmustore_merkle.so (the C ABI in include/immustore_merkle.h).
+
+The library is built in-tree by `__graft_entry__.build()` (hipcc, gfx950 only).
+There is no fallback: if the library or a gfx950 device is missing, every
+call raises instead of silently hashing on the CPU.
+"""
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libimmustore_merkle.so")
+
+MH_OK = 0
+MH_ERR_MAX_WIDTH_EXCEEDED = 1
+MH_ERR_ILLEGAL_ARGUMENTS = 2
+MH_ERR_ILLEGAL_STATE = 3
+MH_ERR_EMPTY_TREE = 4
+MH_ERR_UNEXISTENT_DATA = 5
+MH_ERR_METADATA_UNSUPPORTED = 6
+MH_ERR_CANNOT_RESET_TO_LARGER = 7
+MH_ERR_NO_DEVICE = 8
+MH_ERR_OUT_OF_MEMORY = 9
+
+MH_AHT_INCLUSION = 0
+MH_AHT_CONSISTENCY = 1
+MH_AHT_LAST_INCLUSION = 2
+
+
+class MerkleError(Exception):
+    """Base class; `.status` holds the C status code."""
+
+    status = None
+
+    def __init__(self, status, msg=None):
+        self.status = status
+        super().__init__(msg or "status %d" % status)
+
+
+class ErrMaxWidthExceeded(MerkleError):
+    pass
+
+
+class ErrIllegalArguments(MerkleError):
+    pass
+
+
+class ErrIllegalState(MerkleError):
+    pass
+
+
+class ErrEmptyTree(MerkleError):
+    pass
+
+
+class ErrUnexistentData(MerkleError):
+    pass
+
+
+class ErrMetadataUnsupported(MerkleError):
+    pass
+
+
+class ErrCannotResetToLargerSize(MerkleError):
+    pass
+
+
+class ErrNoDevice(MerkleError):
+    pass
+
+
+class ErrOutOfMemory(MerkleError):
+    pass
+
+
+class HipError(MerkleError):
+    pass
+
+
+_ERRORS = {
+    MH_ERR_MAX_WIDTH_EXCEEDED: ErrMaxWidthExceeded,
+    MH_ERR_ILLEGAL_ARGUMENTS: ErrIllegalArguments,
+    MH_ERR_ILLEGAL_STATE: ErrIllegalState,
+    MH_ERR_EMPTY_TREE: ErrEmptyTree,
+    MH_ERR_UNEXISTENT_DATA: ErrUnexistentData,
+    MH_ERR_METADATA_UNSUPPORTED: ErrMetadataUnsupported,
+    MH_ERR_CANNOT_RESET_TO_LARGER: ErrCannotResetToLargerSize,
+    MH_ERR_NO_DEVICE: ErrNoDevice,
+    MH_ERR_OUT_OF_MEMORY: ErrOutOfMemory,
+}
+
+vp = C.c_void_p
+u8p = C.c_void_p  # raw addresses (host or device) are passed as integers
+u64 = C.c_uint64
+u32 = C.c_uint32
+i32 = C.c_int
+
+# name -> (restype, argtypes); mirrors include/immustore_merkle.h exactly.
+SIGNATURES = {
+    "mh_abi_version": (i32, []),
+    "mh_status_string": (C.c_char_p, [i32]),
+    "mh_device_count": (i32, [C.POINTER(i32)]),
+    "mh_ctx_create": (i32, [i32, vp, C.POINTER(vp)]),
+    "mh_ctx_destroy": (i32, [vp]),
+    "mh_ctx_synchronize": (i32, [vp]),
+    "mh_ctx_stream": (vp, [vp]),
+    "mh_ctx_set_timing": (i32, [vp, i32]),
+    "mh_ctx_timing": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(u64)]),
+    "mh_ctx_timing_reset": (i32, [vp]),
+    "mh_dev_alloc": (i32, [vp, u64, C.POINTER(vp)]),
+    "mh_dev_free": (i32, [vp, vp]),
+    "mh_host_alloc_pinned": (i32, [u64, C.POINTER(vp)]),
+    "mh_host_free_pinned": (i32, [vp]),
+    "mh_memcpy_h2d": (i32, [vp, vp, vp, u64]),
+    "mh_memcpy_d2h": (i32, [vp, vp, vp, u64]),
+    "mh_dev_fill_random": (i32, [vp, vp, u64, u64]),
+    "mh_dev_fill_keys_be64": (i32, [vp, vp, u64, u64]),
+    "mh_htree_levels_len": (u64, [u64]),
+    "mh_htree_level_offset": (u64, [u64, i32]),
+    "mh_htree_new": (i32, [vp, u64, C.POINTER(vp)]),
+    "mh_htree_free": (i32, [vp]),
+    "mh_htree_build_with": (i32, [vp, u8p, u64]),
+    "mh_htree_build_entries": (i32, [vp, i32, u64, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p]),
+    "mh_htree_root": (i32, [vp, u8p]),
+    "mh_htree_width": (i32, [vp, C.POINTER(u64)]),
+    "mh_htree_inclusion_proof": (i32, [vp, u64, u8p, u32, C.POINTER(u32)]),
+    "mh_htree_levels": (i32, [vp, u8p, u64]),
+    "mh_htree_levels_device": (i32, [vp, C.POINTER(vp)]),
+    "mh_htree_verify_inclusion_batch": (i32, [vp, u64, vp, vp, vp, u8p, u8p, u8p, u8p]),
+    "mh_dev_htree_build_digests": (i32, [vp, u8p, u64, u8p, u8p]),
+    "mh_dev_htree_build_entries_fixed": (i32, [vp, i32, u64, u8p, u32, u8p, u32, u8p, u8p, u8p]),
+    "mh_dev_htree_build_entries": (i32, [vp, i32, u64, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p,
+                                         u8p, u8p]),
+    "mh_dev_htree_reduce_nodes": (i32, [vp, u8p, u64, u8p, u8p]),
+    "mh_dev_sha256_batch": (i32, [vp, u8p, vp, u64, u8p]),
+    "mh_dev_htree_verify_inclusion_batch": (i32, [vp, u64, vp, vp, vp, u8p, u8p, u8p, u8p]),
+    "mh_ahtree_new": (i32, [vp, C.POINTER(vp)]),
+    "mh_ahtree_free": (i32, [vp]),
+    "mh_ahtree_append": (i32, [vp, u8p, u64, C.POINTER(u64), u8p]),
+    "mh_ahtree_append_batch": (i32, [vp, u8p, u64, u32, u8p]),
+    "mh_ahtree_size": (i32, [vp, C.POINTER(u64)]),
+    "mh_ahtree_root": (i32, [vp, C.POINTER(u64), u8p]),
+    "mh_ahtree_root_at": (i32, [vp, u64, u8p]),
+    "mh_ahtree_inclusion_proof": (i32, [vp, u64, u64, u8p, u32, C.POINTER(u32)]),
+    "mh_ahtree_consistency_proof": (i32, [vp, u64, u64, u8p, u32, C.POINTER(u32)]),
+    "mh_ahtree_reset_size": (i32, [vp, u64]),
+    "mh_ahtree_dlog": (i32, [vp, u64, u64, u8p]),
+    "mh_ahtree_dlog_device": (i32, [vp, C.POINTER(vp)]),
+    "mh_dev_ahtree_append_batch": (i32, [vp, u8p, u64, u8p, u64, u32, u8p]),
+    "mh_ahtree_nodes_upto": (u64, [u64]),
+    "mh_ahtree_verify_batch": (i32, [vp, i32, u64, vp, vp, vp, u8p, u8p, u8p, u8p, u8p]),
+    "mh_dev_ahtree_verify_batch": (i32, [vp, i32, u64, vp, vp, vp, u8p, u8p, u8p, u8p, u8p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load the library (no device access).  Raises if it was not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ErrNoDevice(MH_ERR_NO_DEVICE,
+                                  "libimmustore_merkle.so not built: run __graft_entry__.build()")
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(status):
+    if status == MH_OK:
+        return
+    msg = load().mh_status_string(status)
+    msg = msg.decode() if msg else "status %d" % status
+    if status < 0:
+        raise HipError(status, msg)
+    raise _ERRORS.get(status, MerkleError)(status, msg)

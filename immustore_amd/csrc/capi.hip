@@ -1,0 +1,1023 @@
+// capi.hip -- implementation of the C ABI declared in include/immustore_merkle.h.
+//
+// Host-side mirror of the reference's Go objects (embedded/htree.HTree,
+// embedded/ahtree.AHtree) written in C++ (the reference is compiled Go; no Go
+// toolchain exists in this image).  All hashing runs in the HIP kernels of
+// htree_kernels.hip / ahtree_kernels.hip / verify_kernels.hip; the host code
+// here only moves bytes, computes indices and reports errors.  There is no
+// CPU hashing fallback: without a usable device every entry point returns
+// MH_ERR_NO_DEVICE.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mh_internal.hpp"
+
+using namespace mh;
+
+namespace mh {
+hipError_t launch_copy_nodes(hipStream_t st, const uint8_t *src, uint64_t n, uint8_t *dst);
+}
+
+#define MH_HIP(expr)                                        \
+    do {                                                    \
+        hipError_t e_ = (expr);                             \
+        if (e_ != hipSuccess) return -(int)e_;              \
+    } while (0)
+
+static const uint8_t kEmptyRoot[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14,
+                                       0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
+                                       0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c,
+                                       0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+
+// ------------------------------------------------------------------ timing
+struct EventTimer : Timer {
+    struct Rec {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::mutex mu;
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    bool enabled = false;
+    hipEvent_t take() {
+        hipEvent_t e;
+        if (!pool.empty()) {
+            e = pool.back();
+            pool.pop_back();
+        } else {
+            hipEventCreate(&e);
+        }
+        return e;
+    }
+    void begin(const char *name, hipStream_t st) override {
+        std::lock_guard<std::mutex> g(mu);
+        Rec r;
+        r.name = name;
+        r.a = take();
+        r.b = take();
+        hipEventRecord(r.a, st);
+        recs.push_back(r);
+    }
+    void end(hipStream_t st) override {
+        std::lock_guard<std::mutex> g(mu);
+        hipEventRecord(recs.back().b, st);
+    }
+    int sum(const char *prefix, double *ms, uint64_t *cnt) {
+        std::lock_guard<std::mutex> g(mu);
+        double tot = 0;
+        uint64_t c = 0;
+        size_t pl = prefix ? strlen(prefix) : 0;
+        for (auto &r : recs) {
+            if (pl && r.name.compare(0, pl, prefix) != 0) continue;
+            hipError_t e = hipEventSynchronize(r.b);
+            if (e != hipSuccess) return -(int)e;
+            float x = 0;
+            hipEventElapsedTime(&x, r.a, r.b);
+            tot += x;
+            c++;
+        }
+        if (ms) *ms = tot;
+        if (cnt) *cnt = c;
+        return MH_OK;
+    }
+    void reset() {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto &r : recs) {
+            hipEventSynchronize(r.b);
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
+        recs.clear();
+    }
+    ~EventTimer() {
+        for (auto &r : recs) {
+            hipEventDestroy(r.a);
+            hipEventDestroy(r.b);
+        }
+        for (auto e : pool) hipEventDestroy(e);
+    }
+};
+
+// ------------------------------------------------------------------ buffers
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t c = std::max<uint64_t>(bytes + 64, 256);
+        hipError_t e = hipMalloc(&p, c);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    template <class T>
+    T *as() const {
+        return reinterpret_cast<T *>(p);
+    }
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+};
+
+struct mh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    EventTimer timer;
+    std::mutex mu;  // guards scratch for mh_dev_* calls
+    DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs;
+    Timer *tm() { return timer.enabled ? &timer : nullptr; }
+};
+
+struct mh_htree {
+    mh_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t max_width = 0;
+    uint64_t width = 0;
+    uint8_t root[32];
+    DevBuf levels, in_a, in_b, in_c, off_a, off_b, off_c, ov, use, hv, msgoff, msgs, digests;
+    void *pinned = nullptr;
+    uint64_t pinned_cap = 0;
+    LevelGeom geom;
+};
+
+struct mh_ahtree {
+    mh_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t size = 0;
+    DevBuf dlog, in, roots, idx, out;
+};
+
+// ------------------------------------------------------------------ misc
+extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
+
+extern "C" const char *mh_status_string(int st) {
+    switch (st) {
+        case MH_OK: return "ok";
+        case MH_ERR_MAX_WIDTH_EXCEEDED: return "htree: max width exceeded";
+        case MH_ERR_ILLEGAL_ARGUMENTS: return "illegal arguments";
+        case MH_ERR_ILLEGAL_STATE: return "htree: illegal state";
+        case MH_ERR_EMPTY_TREE: return "ahtree: empty tree";
+        case MH_ERR_UNEXISTENT_DATA: return "ahtree: attempt to read unexistent data";
+        case MH_ERR_METADATA_UNSUPPORTED: return "metadata is unsupported when in 1.1 compatibility mode";
+        case MH_ERR_CANNOT_RESET_TO_LARGER: return "ahtree: can not reset the tree to a larger size";
+        case MH_ERR_NO_DEVICE: return "no usable gfx950 device";
+        case MH_ERR_OUT_OF_MEMORY: return "out of device memory";
+        default: return st < 0 ? hipGetErrorString((hipError_t)(-st)) : "unknown status";
+    }
+}
+
+extern "C" int mh_device_count(int *count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return MH_ERR_NO_DEVICE;
+    }
+    *count = n;
+    return MH_OK;
+}
+
+static int map_alloc(hipError_t e) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return MH_ERR_OUT_OF_MEMORY;
+    return e == hipSuccess ? MH_OK : -(int)e;
+}
+
+// ------------------------------------------------------------------ context
+extern "C" int mh_ctx_create(int device_ordinal, void *hip_stream, mh_ctx **out) {
+    if (!out) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return MH_ERR_NO_DEVICE;
+    if (device_ordinal < 0 || device_ordinal >= n) return MH_ERR_ILLEGAL_ARGUMENTS;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) return MH_ERR_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MH_ERR_NO_DEVICE;
+    MH_HIP(hipSetDevice(device_ordinal));
+    mh_ctx *c = new (std::nothrow) mh_ctx();
+    if (!c) return MH_ERR_OUT_OF_MEMORY;
+    c->device = device_ordinal;
+    if (hip_stream) {
+        c->stream = (hipStream_t)hip_stream;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete c;
+            return -(int)e;
+        }
+        c->own_stream = true;
+    }
+    *out = c;
+    return MH_OK;
+}
+
+extern "C" int mh_ctx_destroy(mh_ctx *c) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    if (c->own_stream) hipStreamDestroy(c->stream);
+    delete c;
+    return MH_OK;
+}
+
+extern "C" int mh_ctx_synchronize(mh_ctx *c) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    MH_HIP(hipStreamSynchronize(c->stream));
+    return MH_OK;
+}
+
+extern "C" void *mh_ctx_stream(mh_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" int mh_ctx_set_timing(mh_ctx *c, int enable) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    c->timer.enabled = enable != 0;
+    return MH_OK;
+}
+
+extern "C" int mh_ctx_timing(mh_ctx *c, const char *prefix, double *total_ms, uint64_t *launches) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    return c->timer.sum(prefix, total_ms, launches);
+}
+
+extern "C" int mh_ctx_timing_reset(mh_ctx *c) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    c->timer.reset();
+    return MH_OK;
+}
+
+extern "C" int mh_dev_alloc(mh_ctx *c, uint64_t bytes, void **dptr) {
+    if (!c || !dptr) return MH_ERR_ILLEGAL_ARGUMENTS;
+    hipSetDevice(c->device);
+    return map_alloc(hipMalloc(dptr, std::max<uint64_t>(bytes, 1)));
+}
+
+extern "C" int mh_dev_free(mh_ctx *c, void *dptr) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    MH_HIP(hipFree(dptr));
+    return MH_OK;
+}
+
+extern "C" int mh_host_alloc_pinned(uint64_t bytes, void **hptr) {
+    if (!hptr) return MH_ERR_ILLEGAL_ARGUMENTS;
+    return map_alloc(hipHostMalloc(hptr, std::max<uint64_t>(bytes, 1), hipHostMallocDefault));
+}
+
+extern "C" int mh_host_free_pinned(void *hptr) {
+    MH_HIP(hipHostFree(hptr));
+    return MH_OK;
+}
+
+extern "C" int mh_memcpy_h2d(mh_ctx *c, void *dst, const void *src, uint64_t bytes) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!bytes) return MH_OK;
+    MH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_memcpy_d2h(mh_ctx *c, void *dst, const void *src, uint64_t bytes) {
+    if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!bytes) return MH_OK;
+    MH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_fill_random(mh_ctx *c, void *dptr, uint64_t nbytes, uint64_t seed) {
+    if (!c || (!dptr && nbytes)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!nbytes) return MH_OK;
+    MH_HIP(launch_fill_random(c->stream, (uint8_t *)dptr, nbytes, seed));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_fill_keys_be64(mh_ctx *c, void *dptr, uint64_t n, uint64_t first) {
+    if (!c || (!dptr && n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (((uintptr_t)dptr) & 7) return MH_ERR_ILLEGAL_ARGUMENTS;
+    MH_HIP(launch_fill_keys_be64(c->stream, (uint8_t *)dptr, n, first));
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ htree core
+extern "C" uint64_t mh_htree_levels_len(uint64_t n) {
+    LevelGeom g;
+    g.init(n);
+    return g.total;
+}
+
+extern "C" uint64_t mh_htree_level_offset(uint64_t n, int level) {
+    LevelGeom g;
+    g.init(n);
+    if (level < 0 || level >= kMaxLevels) return 0;
+    if (level >= g.nlevels) return g.total;
+    return g.off[level];
+}
+
+static int write_root(hipStream_t st, const LevelGeom &g, uint8_t *levels, uint8_t *root) {
+    if (!root) return MH_OK;
+    if (g.n == 0) {
+        MH_HIP(hipMemcpyAsync(root, kEmptyRoot, 32, hipMemcpyHostToDevice, st));
+        return MH_OK;
+    }
+    MH_HIP(hipMemcpyAsync(root, levels + g.off[g.nlevels - 1] * 32, 32, hipMemcpyDeviceToDevice, st));
+    return MH_OK;
+}
+
+// Fused fixed-stride path (device pointers, stream st).
+static int build_fixed(hipStream_t st, Timer *tm, int version, uint64_t n, const uint8_t *keys,
+                       uint32_t key_len, const uint8_t *vals, uint32_t val_len, uint8_t *hvals_out,
+                       uint8_t *levels, const LevelGeom &g) {
+    int done = 0;
+    MH_HIP(launch_entries_fixed(st, tm, version, n, keys, key_len, vals, val_len, hvals_out, levels,
+                                g, &done));
+    MH_HIP(launch_reduce(st, tm, levels, g, done));
+    return MH_OK;
+}
+
+static int build_digests(hipStream_t st, Timer *tm, const uint8_t *digests, uint64_t n,
+                         uint8_t *levels, const LevelGeom &g) {
+    int done = 0;
+    MH_HIP(launch_leaves_from_digests(st, tm, digests, n, levels, g, &done));
+    MH_HIP(launch_reduce(st, tm, levels, g, done));
+    return MH_OK;
+}
+
+// General CSR path.  msg_total = sum of digest message lengths (host known).
+static int build_csr(hipStream_t st, Timer *tm, int version, uint64_t n, const uint8_t *keys,
+                     const uint64_t *key_off, const uint8_t *md, const uint64_t *md_off,
+                     const uint8_t *vals, const uint64_t *val_off, const uint8_t *ov,
+                     const uint8_t *use, uint8_t *hvals, uint64_t *msg_off, uint8_t *msgs,
+                     uint8_t *digests, uint8_t *levels, const LevelGeom &g) {
+    MH_HIP(launch_sha256_csr(st, tm, vals, val_off, n, ov, use, hvals));
+    MH_HIP(launch_msg_offsets(st, tm, version, n, key_off, md_off, msg_off));
+    MH_HIP(launch_digest_assemble(st, tm, version, n, keys, key_off, md, md_off, hvals, msg_off, msgs,
+                                  nullptr));
+    MH_HIP(launch_sha256_csr(st, tm, msgs, msg_off, n, nullptr, nullptr, digests));
+    return build_digests(st, tm, digests, n, levels, g);
+}
+
+extern "C" int mh_dev_htree_build_digests(mh_ctx *c, const uint8_t *digests, uint64_t n,
+                                          uint8_t *levels, uint8_t *root) {
+    if (!c || (n && (!digests || !levels))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (((uintptr_t)digests & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    LevelGeom g;
+    g.init(n);
+    if (n) {
+        int st = build_digests(c->stream, c->tm(), digests, n, levels, g);
+        if (st) return st;
+    }
+    return write_root(c->stream, g, levels, root);
+}
+
+extern "C" int mh_dev_htree_build_entries_fixed(mh_ctx *c, int version, uint64_t n,
+                                                const uint8_t *keys, uint32_t key_len,
+                                                const uint8_t *vals, uint32_t val_len,
+                                                uint8_t *hvals_out, uint8_t *levels, uint8_t *root) {
+    if (!c || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n && (!levels || (!keys && key_len) || (!vals && val_len))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (((uintptr_t)levels & 15) || ((uintptr_t)hvals_out & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    LevelGeom g;
+    g.init(n);
+    if (n) {
+        if (entries_fixed_supported(version, keys, key_len, vals, val_len)) {
+            int st = build_fixed(c->stream, c->tm(), version, n, keys, key_len, vals, val_len,
+                                 hvals_out, levels, g);
+            if (st) return st;
+        } else {
+            // odd shapes: general CSR path over generated offsets
+            std::lock_guard<std::mutex> lk(c->mu);
+            MH_HIP(c->s_offs.ensure(2 * (n + 1) * sizeof(uint64_t)));
+            uint64_t *koff = c->s_offs.as<uint64_t>(), *voff = koff + (n + 1);
+            MH_HIP(launch_iota_offsets(c->stream, koff, n, key_len));
+            MH_HIP(launch_iota_offsets(c->stream, voff, n, val_len));
+            uint64_t msg_total = n * ((uint64_t)key_len + (version == 1 ? 36 : 32));
+            MH_HIP(c->s_hvals.ensure(n * 32));
+            MH_HIP(c->s_msgoff.ensure((n + 1) * 8));
+            MH_HIP(c->s_msgs.ensure(msg_total));
+            MH_HIP(c->s_digests.ensure(n * 32));
+            uint8_t *hv = hvals_out ? hvals_out : c->s_hvals.as<uint8_t>();
+            int st = build_csr(c->stream, c->tm(), version, n, keys, koff, nullptr, nullptr, vals,
+                               voff, nullptr, nullptr, hv, c->s_msgoff.as<uint64_t>(),
+                               c->s_msgs.as<uint8_t>(), c->s_digests.as<uint8_t>(), levels, g);
+            if (st) return st;
+        }
+    }
+    return write_root(c->stream, g, levels, root);
+}
+
+extern "C" int mh_dev_htree_build_entries(mh_ctx *c, int version, uint64_t n, const uint8_t *keys,
+                                          const uint64_t *key_off, const uint8_t *md,
+                                          const uint64_t *md_off, const uint8_t *vals,
+                                          const uint64_t *val_off, const uint8_t *hval_override,
+                                          const uint8_t *use_override, uint8_t *hvals_out,
+                                          uint8_t *levels, uint8_t *root) {
+    if (!c || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n && (!levels || !key_off || !val_off)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    LevelGeom g;
+    g.init(n);
+    if (n) {
+        // bounds of the CSR arrays (one small D2H): sizes the message scratch
+        // and rejects v0 + KV metadata up front (tx.go:691-693).
+        uint64_t kb[2], mb[2] = {0, 0};
+        MH_HIP(hipMemcpyAsync(&kb[0], key_off, 8, hipMemcpyDeviceToHost, c->stream));
+        MH_HIP(hipMemcpyAsync(&kb[1], key_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+        if (md_off) {
+            MH_HIP(hipMemcpyAsync(&mb[0], md_off, 8, hipMemcpyDeviceToHost, c->stream));
+            MH_HIP(hipMemcpyAsync(&mb[1], md_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+        }
+        MH_HIP(hipStreamSynchronize(c->stream));
+        if (version == 0 && mb[1] != mb[0]) return MH_ERR_METADATA_UNSUPPORTED;
+        const uint64_t msg_total = (kb[1] - kb[0]) + (mb[1] - mb[0]) + n * (version == 1 ? 36 : 32);
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(c->s_hvals.ensure(n * 32));
+        MH_HIP(c->s_msgoff.ensure((n + 1) * 8));
+        MH_HIP(c->s_msgs.ensure(msg_total));
+        MH_HIP(c->s_digests.ensure(n * 32));
+        uint8_t *hv = hvals_out ? hvals_out : c->s_hvals.as<uint8_t>();
+        int st = build_csr(c->stream, c->tm(), version, n, keys, key_off, md, md_off, vals, val_off,
+                           hval_override, use_override, hv, c->s_msgoff.as<uint64_t>(),
+                           c->s_msgs.as<uint8_t>(), c->s_digests.as<uint8_t>(), levels, g);
+        if (st) return st;
+    }
+    return write_root(c->stream, g, levels, root);
+}
+
+extern "C" int mh_dev_htree_reduce_nodes(mh_ctx *c, const uint8_t *nodes, uint64_t w,
+                                         uint8_t *levels, uint8_t *root) {
+    if (!c || (w && (!nodes || !levels))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (((uintptr_t)nodes & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    LevelGeom g;
+    g.init(w);
+    if (w) {
+        MH_HIP(launch_copy_nodes(c->stream, nodes, w, levels));
+        MH_HIP(launch_reduce(c->stream, c->tm(), levels, g, 0));
+    }
+    return write_root(c->stream, g, levels, root);
+}
+
+extern "C" int mh_dev_sha256_batch(mh_ctx *c, const uint8_t *buf, const uint64_t *off, uint64_t n,
+                                   uint8_t *out) {
+    if (!c || (n && (!off || !out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    MH_HIP(launch_sha256_csr(c->stream, c->tm(), buf, off, n, nullptr, nullptr, out));
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ htree handle
+extern "C" int mh_htree_new(mh_ctx *c, uint64_t max_width, mh_htree **out) {
+    if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *out = nullptr;
+    hipSetDevice(c->device);
+    mh_htree *t = new (std::nothrow) mh_htree();
+    if (!t) return MH_ERR_OUT_OF_MEMORY;
+    t->ctx = c;
+    t->max_width = max_width;
+    memcpy(t->root, kEmptyRoot, 32);
+    hipError_t e = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete t;
+        return -(int)e;
+    }
+    if (max_width) {
+        e = t->levels.ensure(mh_htree_levels_len(max_width) * 32);
+        if (e != hipSuccess) {
+            hipStreamDestroy(t->stream);
+            delete t;
+            return map_alloc(e);
+        }
+    }
+    *out = t;
+    return MH_OK;
+}
+
+extern "C" int mh_htree_free(mh_htree *t) {
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    hipStreamSynchronize(t->stream);
+    hipStreamDestroy(t->stream);
+    if (t->pinned) hipHostFree(t->pinned);
+    delete t;
+    return MH_OK;
+}
+
+static int stage_h2d(mh_htree *t, DevBuf &dst, const void *src, uint64_t bytes) {
+    MH_HIP(dst.ensure(bytes));
+    if (bytes) MH_HIP(hipMemcpyAsync(dst.p, src, bytes, hipMemcpyHostToDevice, t->stream));
+    return MH_OK;
+}
+
+static int finish_build(mh_htree *t, uint64_t n) {
+    t->geom.init(n);
+    t->width = n;
+    if (n == 0) {
+        memcpy(t->root, kEmptyRoot, 32);
+        return MH_OK;
+    }
+    MH_HIP(hipMemcpyAsync(t->root, t->levels.as<uint8_t>() + t->geom.off[t->geom.nlevels - 1] * 32, 32,
+                          hipMemcpyDeviceToHost, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_htree_build_with(mh_htree *t, const uint8_t *digests, uint64_t n) {
+    if (!t || (n && !digests)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n > t->max_width) return MH_ERR_MAX_WIDTH_EXCEEDED;  // htree.go:69-71
+    if (n == 0) return finish_build(t, 0);                    // htree.go:73-77
+    hipSetDevice(t->ctx->device);
+    int st = stage_h2d(t, t->in_a, digests, n * 32);
+    if (st) return st;
+    LevelGeom g;
+    g.init(n);
+    st = build_digests(t->stream, t->ctx->tm(), t->in_a.as<uint8_t>(), n, t->levels.as<uint8_t>(), g);
+    if (st) return st;
+    return finish_build(t, n);
+}
+
+static bool is_progression(const uint64_t *off, uint64_t n, uint64_t *stride) {
+    if (!off) return false;
+    if (off[0] != 0) return false;
+    const uint64_t s = n ? off[1] - off[0] : 0;
+    for (uint64_t i = 1; i <= n; i++)
+        if (off[i] - off[i - 1] != s) return false;
+    *stride = s;
+    return true;
+}
+
+extern "C" int mh_htree_build_entries(mh_htree *t, int version, uint64_t n, const uint8_t *keys,
+                                      const uint64_t *key_off, const uint8_t *md,
+                                      const uint64_t *md_off, const uint8_t *vals,
+                                      const uint64_t *val_off, const uint8_t *hval_override,
+                                      const uint8_t *use_override, uint8_t *hvals_out) {
+    if (!t || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n && (!key_off || !val_off)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n > t->max_width) return MH_ERR_MAX_WIDTH_EXCEEDED;
+    const uint64_t md_bytes = md_off && n ? md_off[n] - md_off[0] : 0;
+    if (version == 0 && md_bytes) return MH_ERR_METADATA_UNSUPPORTED;  // tx.go:691-693
+    if (n == 0) return finish_build(t, 0);
+    hipSetDevice(t->ctx->device);
+    Timer *tm = t->ctx->tm();
+    const uint64_t kbytes = key_off[n] - key_off[0], vbytes = val_off[n] - val_off[0];
+    LevelGeom g;
+    g.init(n);
+    int st;
+    bool any_override = false;
+    if (use_override)
+        for (uint64_t i = 0; i < n && !any_override; i++) any_override = use_override[i] != 0;
+    uint64_t kstride = 0, vstride = 0;
+    uint8_t *hv_dev = nullptr;
+    MH_HIP(t->hv.ensure(n * 32));
+    hv_dev = t->hv.as<uint8_t>();
+    if (!md_bytes && !any_override && is_progression(key_off, n, &kstride) &&
+        is_progression(val_off, n, &vstride) && kstride <= 0xffffffffull &&
+        vstride <= 0xffffffffull) {
+        // uniform shapes: fused kernel (same as BASELINE C1/C2)
+        if ((st = stage_h2d(t, t->in_a, keys, kbytes))) return st;
+        if ((st = stage_h2d(t, t->in_b, vals, vbytes))) return st;
+        if (entries_fixed_supported(version, t->in_a.as<uint8_t>(), (uint32_t)kstride,
+                                    t->in_b.as<uint8_t>(), (uint32_t)vstride)) {
+            st = build_fixed(t->stream, tm, version, n, t->in_a.as<uint8_t>(), (uint32_t)kstride,
+                             t->in_b.as<uint8_t>(), (uint32_t)vstride, hv_dev,
+                             t->levels.as<uint8_t>(), g);
+            if (st) return st;
+            goto done;
+        }
+    }
+    {
+        // general CSR path: rebase offsets to 0 and stage everything
+        std::vector<uint64_t> ko(n + 1), vo(n + 1), mo;
+        for (uint64_t i = 0; i <= n; i++) {
+            ko[i] = key_off[i] - key_off[0];
+            vo[i] = val_off[i] - val_off[0];
+        }
+        if ((st = stage_h2d(t, t->in_a, keys ? keys + key_off[0] : nullptr, kbytes))) return st;
+        if ((st = stage_h2d(t, t->in_b, vals ? vals + val_off[0] : nullptr, vbytes))) return st;
+        if ((st = stage_h2d(t, t->off_a, ko.data(), (n + 1) * 8))) return st;
+        if ((st = stage_h2d(t, t->off_b, vo.data(), (n + 1) * 8))) return st;
+        uint64_t *mo_dev = nullptr;
+        if (md_off) {
+            mo.resize(n + 1);
+            for (uint64_t i = 0; i <= n; i++) mo[i] = md_off[i] - md_off[0];
+            if ((st = stage_h2d(t, t->in_c, md ? md + md_off[0] : nullptr, md_bytes))) return st;
+            if ((st = stage_h2d(t, t->off_c, mo.data(), (n + 1) * 8))) return st;
+            mo_dev = t->off_c.as<uint64_t>();
+        }
+        const uint8_t *ovd = nullptr, *used = nullptr;
+        if (any_override) {
+            if ((st = stage_h2d(t, t->ov, hval_override, n * 32))) return st;
+            if ((st = stage_h2d(t, t->use, use_override, n))) return st;
+            ovd = t->ov.as<uint8_t>();
+            used = t->use.as<uint8_t>();
+        }
+        const uint64_t msg_total = kbytes + md_bytes + n * (version == 1 ? 36 : 32);
+        MH_HIP(t->msgoff.ensure((n + 1) * 8));
+        MH_HIP(t->msgs.ensure(msg_total));
+        MH_HIP(t->digests.ensure(n * 32));
+        st = build_csr(t->stream, tm, version, n, t->in_a.as<uint8_t>(), t->off_a.as<uint64_t>(),
+                       md_off ? t->in_c.as<uint8_t>() : nullptr, mo_dev, t->in_b.as<uint8_t>(),
+                       t->off_b.as<uint64_t>(), ovd, used, hv_dev, t->msgoff.as<uint64_t>(),
+                       t->msgs.as<uint8_t>(), t->digests.as<uint8_t>(), t->levels.as<uint8_t>(), g);
+        if (st) return st;
+    }
+done:
+    if (hvals_out) MH_HIP(hipMemcpyAsync(hvals_out, hv_dev, n * 32, hipMemcpyDeviceToHost, t->stream));
+    return finish_build(t, n);
+}
+
+extern "C" int mh_htree_root(mh_htree *t, uint8_t root[32]) {
+    if (!t || !root) return MH_ERR_ILLEGAL_ARGUMENTS;
+    memcpy(root, t->root, 32);
+    return MH_OK;
+}
+
+extern "C" int mh_htree_width(mh_htree *t, uint64_t *width) {
+    if (!t || !width) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *width = t->width;
+    return MH_OK;
+}
+
+static int bits_len64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+extern "C" int mh_htree_inclusion_proof(mh_htree *t, uint64_t i, uint8_t *terms, uint32_t cap,
+                                        uint32_t *nterms) {
+    // htree.go:121-164: index walk on the host, terms gathered from HBM.
+    if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *nterms = 0;
+    if (i >= t->width) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (t->width == 1) return MH_OK;
+    uint64_t m = i, n = t->width, offset = 0, l, r;
+    uint64_t idx[64];
+    uint32_t cnt = 0;
+    for (;;) {
+        const int d = bits_len64(n - 1);
+        const uint64_t k = 1ull << (d - 1);
+        if (m < k) {
+            l = offset + k;
+            r = offset + n - 1;
+            n = k;
+        } else {
+            l = offset;
+            r = offset + k - 1;
+            m -= k;
+            n -= k;
+            offset += k;
+        }
+        const int layer = bits_len64(r - l);
+        idx[cnt++] = t->geom.off[layer] + (l >> layer);
+        if (n < 1 || (n == 1 && m == 0)) break;
+    }
+    if (cnt > cap || !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
+    // Go prepends each term: output is the reverse discovery order
+    for (uint32_t k = 0; k < cnt; k++)
+        MH_HIP(hipMemcpyAsync(terms + 32 * k, t->levels.as<uint8_t>() + idx[cnt - 1 - k] * 32, 32,
+                              hipMemcpyDeviceToHost, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    *nterms = cnt;
+    return MH_OK;
+}
+
+extern "C" int mh_htree_levels(mh_htree *t, uint8_t *out, uint64_t cap_nodes) {
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    const uint64_t total = mh_htree_levels_len(t->width);
+    if (cap_nodes < total || (total && !out)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!total) return MH_OK;
+    MH_HIP(hipMemcpyAsync(out, t->levels.p, total * 32, hipMemcpyDeviceToHost, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_htree_levels_device(mh_htree *t, const uint8_t **dptr) {
+    if (!t || !dptr) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *dptr = t->levels.as<uint8_t>();
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ verification
+extern "C" int mh_dev_htree_verify_inclusion_batch(mh_ctx *c, uint64_t np, const uint64_t *leaf,
+                                                   const uint64_t *width, const uint64_t *term_off,
+                                                   const uint8_t *terms, const uint8_t *digests,
+                                                   const uint8_t *roots, uint8_t *ok) {
+    if (!c || (np && (!leaf || !width || !term_off || !digests || !roots || !ok)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!np) return MH_OK;
+    MH_HIP(launch_htree_verify(c->stream, c->tm(), np, leaf, width, term_off, terms, digests, roots,
+                               ok));
+    return MH_OK;
+}
+
+// host wrapper: stage, run on the context stream, copy back
+extern "C" int mh_htree_verify_inclusion_batch(mh_ctx *c, uint64_t np, const uint64_t *leaf,
+                                               const uint64_t *width, const uint64_t *term_off,
+                                               const uint8_t *terms, const uint8_t *digests,
+                                               const uint8_t *roots, uint8_t *ok) {
+    if (!c || (np && (!leaf || !width || !term_off || !digests || !roots || !ok)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!np) return MH_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    const uint64_t nterms = term_off[np] - term_off[0];
+    std::vector<uint64_t> to(np + 1);
+    for (uint64_t p = 0; p <= np; p++) to[p] = term_off[p] - term_off[0];
+    // layout in one scratch buffer: leaf | width | off | digests | roots | terms | ok
+    const uint64_t b_leaf = 0, b_width = b_leaf + np * 8, b_off = b_width + np * 8,
+                   b_dig = (b_off + (np + 1) * 8 + 15) & ~15ull, b_root = b_dig + np * 32,
+                   b_terms = b_root + np * 32, b_ok = b_terms + nterms * 32,
+                   total = b_ok + np + 16;
+    MH_HIP(c->s_msgs.ensure(total));
+    uint8_t *base = c->s_msgs.as<uint8_t>();
+    hipStream_t st = c->stream;
+    MH_HIP(hipMemcpyAsync(base + b_leaf, leaf, np * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_width, width, np * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_off, to.data(), (np + 1) * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_dig, digests, np * 32, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_root, roots, np * 32, hipMemcpyHostToDevice, st));
+    if (nterms)
+        MH_HIP(hipMemcpyAsync(base + b_terms, terms + term_off[0] * 32, nterms * 32,
+                              hipMemcpyHostToDevice, st));
+    MH_HIP(launch_htree_verify(st, c->tm(), np, (const uint64_t *)(base + b_leaf),
+                               (const uint64_t *)(base + b_width), (const uint64_t *)(base + b_off),
+                               base + b_terms, base + b_dig, base + b_root, base + b_ok));
+    MH_HIP(hipMemcpyAsync(ok, base + b_ok, np, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_ahtree_verify_batch(mh_ctx *c, int kind, uint64_t np, const uint64_t *i,
+                                          const uint64_t *j, const uint64_t *term_off,
+                                          const uint8_t *terms, const uint8_t *a, const uint8_t *b,
+                                          uint8_t *ok, uint8_t *eval_out) {
+    if (!c || kind < 0 || kind > 2) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (np && (!i || !j || !term_off || !a || !b || !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!np) return MH_OK;
+    MH_HIP(launch_ahtree_verify(c->stream, c->tm(), kind, np, i, j, term_off, terms, a, b, ok,
+                                eval_out));
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_verify_batch(mh_ctx *c, int kind, uint64_t np, const uint64_t *i,
+                                      const uint64_t *j, const uint64_t *term_off,
+                                      const uint8_t *terms, const uint8_t *a, const uint8_t *b,
+                                      uint8_t *ok, uint8_t *eval_out) {
+    if (!c || kind < 0 || kind > 2) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (np && (!i || !j || !term_off || !a || !b || !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!np) return MH_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    const uint64_t nterms = term_off[np] - term_off[0];
+    std::vector<uint64_t> to(np + 1);
+    for (uint64_t p = 0; p <= np; p++) to[p] = term_off[p] - term_off[0];
+    const uint64_t eval_w = kind == MH_AHT_CONSISTENCY ? 64 : 32;
+    const uint64_t b_i = 0, b_j = np * 8, b_off = 2 * np * 8,
+                   b_a = (b_off + (np + 1) * 8 + 15) & ~15ull, b_b = b_a + np * 32,
+                   b_terms = b_b + np * 32, b_eval = b_terms + nterms * 32,
+                   b_ok = b_eval + (eval_out ? np * eval_w : 0), total = b_ok + np + 16;
+    MH_HIP(c->s_msgs.ensure(total));
+    uint8_t *base = c->s_msgs.as<uint8_t>();
+    hipStream_t st = c->stream;
+    MH_HIP(hipMemcpyAsync(base + b_i, i, np * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_j, j, np * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_off, to.data(), (np + 1) * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_a, a, np * 32, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_b, b, np * 32, hipMemcpyHostToDevice, st));
+    if (nterms)
+        MH_HIP(hipMemcpyAsync(base + b_terms, terms + term_off[0] * 32, nterms * 32,
+                              hipMemcpyHostToDevice, st));
+    MH_HIP(launch_ahtree_verify(st, c->tm(), kind, np, (const uint64_t *)(base + b_i),
+                                (const uint64_t *)(base + b_j), (const uint64_t *)(base + b_off),
+                                base + b_terms, base + b_a, base + b_b, base + b_ok,
+                                eval_out ? base + b_eval : nullptr));
+    MH_HIP(hipMemcpyAsync(ok, base + b_ok, np, hipMemcpyDeviceToHost, st));
+    if (eval_out)
+        MH_HIP(hipMemcpyAsync(eval_out, base + b_eval, np * eval_w, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ ahtree
+extern "C" uint64_t mh_ahtree_nodes_upto(uint64_t n) { return ahtree_nodes_upto(n); }
+
+extern "C" int mh_dev_ahtree_append_batch(mh_ctx *c, uint8_t *dlog, uint64_t n0,
+                                          const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                          uint8_t *roots_out) {
+    if (!c || (m && (!dlog || (!payloads && plen)))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m) return MH_OK;
+    MH_HIP(launch_ahtree_append(c->stream, c->tm(), dlog, n0, payloads, m, plen, roots_out));
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_new(mh_ctx *c, mh_ahtree **out) {
+    if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *out = nullptr;
+    hipSetDevice(c->device);
+    mh_ahtree *t = new (std::nothrow) mh_ahtree();
+    if (!t) return MH_ERR_OUT_OF_MEMORY;
+    t->ctx = c;
+    hipError_t e = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete t;
+        return -(int)e;
+    }
+    *out = t;
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_free(mh_ahtree *t) {
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    hipStreamSynchronize(t->stream);
+    hipStreamDestroy(t->stream);
+    delete t;
+    return MH_OK;
+}
+
+static int aht_reserve(mh_ahtree *t, uint64_t new_size) {
+    const uint64_t need = ahtree_nodes_upto(new_size) * 32;
+    if (need <= t->dlog.cap && t->dlog.p) return MH_OK;
+    uint64_t cap = std::max<uint64_t>(need, t->dlog.cap * 2);
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) {
+        cap = need;  // retry exact
+        e = hipMalloc(&p, cap);
+        if (e != hipSuccess) return map_alloc(e);
+    }
+    const uint64_t used = ahtree_nodes_upto(t->size) * 32;
+    if (used) MH_HIP(hipMemcpyAsync(p, t->dlog.p, used, hipMemcpyDeviceToDevice, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    if (t->dlog.p) hipFree(t->dlog.p);
+    t->dlog.p = p;
+    t->dlog.cap = cap;
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m,
+                                      uint32_t plen, uint8_t *roots_out) {
+    if (!t || (m && !payloads && plen)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m) return MH_OK;
+    hipSetDevice(t->ctx->device);
+    int st = aht_reserve(t, t->size + m);
+    if (st) return st;
+    MH_HIP(t->in.ensure((uint64_t)m * plen));
+    if (plen) MH_HIP(hipMemcpyAsync(t->in.p, payloads, (uint64_t)m * plen, hipMemcpyHostToDevice, t->stream));
+    uint8_t *rd = nullptr;
+    if (roots_out) {
+        MH_HIP(t->roots.ensure(m * 32));
+        rd = t->roots.as<uint8_t>();
+    }
+    MH_HIP(launch_ahtree_append(t->stream, t->ctx->tm(), t->dlog.as<uint8_t>(), t->size,
+                                t->in.as<uint8_t>(), m, plen, rd));
+    if (roots_out) MH_HIP(hipMemcpyAsync(roots_out, rd, m * 32, hipMemcpyDeviceToHost, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    t->size += m;
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_append(mh_ahtree *t, const uint8_t *payload, uint64_t plen, uint64_t *n,
+                                uint8_t h[32]) {
+    // ahtree.go:246-373 (d == nil -> ErrIllegalArguments, ahtree.go:258-261)
+    if (!t || (!payload && plen)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!payload) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (plen > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
+    uint8_t root[32];
+    int st = mh_ahtree_append_batch(t, payload, 1, (uint32_t)plen, root);
+    if (st) return st;
+    if (n) *n = t->size;
+    if (h) memcpy(h, root, 32);
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_size(mh_ahtree *t, uint64_t *size) {
+    if (!t || !size) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *size = t->size;
+    return MH_OK;
+}
+
+static int aht_read_nodes(mh_ahtree *t, const uint64_t *idx, uint32_t cnt, uint8_t *out) {
+    for (uint32_t k = 0; k < cnt; k++)
+        MH_HIP(hipMemcpyAsync(out + 32 * k, t->dlog.as<uint8_t>() + idx[k] * 32, 32,
+                              hipMemcpyDeviceToHost, t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_root_at(mh_ahtree *t, uint64_t n, uint8_t root[32]) {
+    // ahtree.go:749-771
+    if (!t || !root) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n == 0) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (t->size == 0) return MH_ERR_EMPTY_TREE;
+    if (n > t->size) return MH_ERR_UNEXISTENT_DATA;
+    const uint64_t idx = ahtree_nodes_until(n) + (uint64_t)__builtin_popcountll(n - 1);
+    return aht_read_nodes(t, &idx, 1, root);
+}
+
+extern "C" int mh_ahtree_root(mh_ahtree *t, uint64_t *n, uint8_t root[32]) {
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (t->size == 0) return MH_ERR_EMPTY_TREE;  // ahtree.go:731-734
+    if (n) *n = t->size;
+    return mh_ahtree_root_at(t, t->size, root);
+}
+
+// Proof index walks: ahtree.go:545-577 / 596-661, node(k,l) = nodesUntil(k)+l.
+static uint64_t aht_node_idx(uint64_t k, int l) { return ahtree_nodes_until(k) + (uint64_t)l; }
+
+static uint64_t aht_highest(uint64_t i, int d) {
+    int l = 0;
+    for (int r = d - 1; r >= 0; r--)
+        if ((i - 1) & (1ull << r)) l++;
+    return aht_node_idx(i, l);
+}
+
+static void aht_incl(uint64_t i, uint64_t j, int height, std::vector<uint64_t> &s) {
+    for (int h = height - 1; h >= 0; h--) {
+        if ((j - 1) & (1ull << h)) {
+            const uint64_t k = (j - 1) >> h << h;
+            if (i <= k) {
+                s.push_back(aht_highest(j, h));
+                aht_incl(i, k, h, s);
+                return;
+            }
+            s.push_back(aht_node_idx(k, h));
+        }
+    }
+}
+
+static void aht_cons(uint64_t i, uint64_t j, int height, std::vector<uint64_t> &s) {
+    for (int h = height - 1; h >= 0; h--) {
+        if ((j - 1) & (1ull << h)) {
+            const uint64_t k = (j - 1) >> h << h;
+            if (i <= k) {
+                s.push_back(aht_highest(j, h));
+                if (i < k) aht_cons(i, k, h, s);
+                if (i == k) s.push_back(aht_highest(i, h));
+                return;
+            }
+            s.push_back(aht_node_idx(k, h));
+            if (i == j) {
+                s.push_back(aht_highest(i, h));
+                return;
+            }
+        }
+    }
+}
+
+static int aht_emit(mh_ahtree *t, std::vector<uint64_t> &s, uint8_t *terms, uint32_t cap,
+                    uint32_t *nterms) {
+    std::reverse(s.begin(), s.end());  // Go prepends every term
+    if (s.size() > cap || (!terms && !s.empty())) return MH_ERR_ILLEGAL_ARGUMENTS;
+    int st = aht_read_nodes(t, s.data(), (uint32_t)s.size(), terms);
+    if (st) return st;
+    *nterms = (uint32_t)s.size();
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_inclusion_proof(mh_ahtree *t, uint64_t i, uint64_t j, uint8_t *terms,
+                                         uint32_t cap, uint32_t *nterms) {
+    if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *nterms = 0;
+    if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;    // ahtree.go:534-536
+    if (j > t->size) return MH_ERR_UNEXISTENT_DATA;  // ahtree.go:538-540
+    std::vector<uint64_t> s;
+    aht_incl(i, j, bits_len64(j - 1), s);
+    return aht_emit(t, s, terms, cap, nterms);
+}
+
+extern "C" int mh_ahtree_consistency_proof(mh_ahtree *t, uint64_t i, uint64_t j, uint8_t *terms,
+                                           uint32_t cap, uint32_t *nterms) {
+    if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *nterms = 0;
+    if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (j > t->size) return MH_ERR_UNEXISTENT_DATA;
+    std::vector<uint64_t> s;
+    aht_cons(i, j, bits_len64(j - 1), s);
+    return aht_emit(t, s, terms, cap, nterms);
+}
+
+extern "C" int mh_ahtree_reset_size(mh_ahtree *t, uint64_t new_size) {
+    // ahtree.go:375-458 (file-size checks belong to the Go appendables)
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (new_size > t->size) return MH_ERR_CANNOT_RESET_TO_LARGER;
+    t->size = new_size;
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_dlog(mh_ahtree *t, uint64_t first, uint64_t count, uint8_t *out) {
+    if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+    const uint64_t total = ahtree_nodes_upto(t->size);
+    if (first > total || count > total - first) return MH_ERR_UNEXISTENT_DATA;
+    if (!count) return MH_OK;
+    if (!out) return MH_ERR_ILLEGAL_ARGUMENTS;
+    MH_HIP(hipMemcpyAsync(out, t->dlog.as<uint8_t>() + first * 32, count * 32, hipMemcpyDeviceToHost,
+                          t->stream));
+    MH_HIP(hipStreamSynchronize(t->stream));
+    return MH_OK;
+}
+
+extern "C" int mh_ahtree_dlog_device(mh_ahtree *t, const uint8_t **dptr) {
+    if (!t || !dptr) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *dptr = t->dlog.as<uint8_t>();
+    return MH_OK;
+}

@@ -1,0 +1,99 @@
+// digest_io.hpp -- device-side byte <-> SHA word movement shared by the
+// kernel translation units.
+#pragma once
+#include "sha256_cdna.hpp"
+
+namespace mh {
+
+// ------------------------------------------------------------------ device helpers
+__device__ __forceinline__ void load_digest(const uint8_t *p, uint32_t w[8]) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(p);
+    const uint4 b = *reinterpret_cast<const uint4 *>(p + 16);
+    w[0] = bswap(a.x); w[1] = bswap(a.y); w[2] = bswap(a.z); w[3] = bswap(a.w);
+    w[4] = bswap(b.x); w[5] = bswap(b.y); w[6] = bswap(b.z); w[7] = bswap(b.w);
+}
+
+__device__ __forceinline__ void store_digest(uint8_t *p, const uint32_t w[8]) {
+    uint4 a, b;
+    a.x = bswap(w[0]); a.y = bswap(w[1]); a.z = bswap(w[2]); a.w = bswap(w[3]);
+    b.x = bswap(w[4]); b.y = bswap(w[5]); b.z = bswap(w[6]); b.w = bswap(w[7]);
+    *reinterpret_cast<uint4 *>(p) = a;
+    *reinterpret_cast<uint4 *>(p + 16) = b;
+}
+
+__device__ __forceinline__ void copy8(uint32_t d[8], const uint32_t s[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) d[j] = s[j];
+}
+
+
+// ============================================================================
+// Generic SHA-256 over one per-lane byte range of any alignment and length,
+// optionally preceded by one prefix byte (pre >= 0): SHA256(pre || p[0:len]).
+// Used by the general CSR path (values, entry-digest messages) and by ahtree
+// leaves of arbitrary payload size (ahtree.go:288-292).
+// ============================================================================
+__device__ __forceinline__ uint32_t ld_guard(const uint32_t *p, const uint8_t *lo,
+                                             const uint8_t *hi) {
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(p);
+    return (b + 4 > lo && b < hi) ? *p : 0u;
+}
+
+__device__ inline void sha256_bytes(const uint8_t *p, uint64_t len, int pre, uint32_t out[8]) {
+    State s;
+    s.init();
+    const uint64_t L = len + (pre >= 0 ? 1 : 0);   // virtual message length
+    const uint8_t *q = p - (pre >= 0 ? 1 : 0);       // virtual byte 0 address
+    const uint32_t al = (uint32_t)((uintptr_t)q & 3);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(q - al);
+    const uint8_t *end = p + len;
+    const uint64_t nfull = L >> 6;
+    for (uint64_t b = 0; b < nfull; b++) {
+        const uint32_t *qq = base + b * 16;
+        uint32_t d[17], w[16];
+        if (b == 0 && pre >= 0) {
+#pragma unroll
+            for (int j = 0; j < 17; j++) d[j] = ld_guard(qq + j, p, end);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) d[j] = qq[j];
+            d[16] = al ? ld_guard(qq + 16, p, end) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        if (b == 0 && pre >= 0) w[0] = (w[0] & 0x00ffffffu) | ((uint32_t)pre << 24);
+        compress(s, w);
+    }
+    const uint32_t rem = (uint32_t)(L - nfull * 64);
+    const uint32_t *qq = base + nfull * 16;
+    uint32_t d[17], w[32];
+#pragma unroll
+    for (int j = 0; j < 17; j++) d[j] = ld_guard(qq + j, p, end);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t x = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        const int v = (int)rem - 4 * j;  // valid bytes in this word
+        const uint32_t m = v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu << (32 - 8 * v)));
+        x &= m;
+        if (v >= 0 && v < 4) x |= 0x80u << (24 - 8 * v);
+        w[j] = x;
+    }
+    if (nfull == 0 && pre >= 0) w[0] = (w[0] & 0x00ffffffu) | ((uint32_t)pre << 24);
+#pragma unroll
+    for (int j = 16; j < 32; j++) w[j] = 0;
+    const uint64_t bits = L * 8;
+    if (rem < 56) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(s, w);
+    } else {
+        w[30] = (uint32_t)(bits >> 32);
+        w[31] = (uint32_t)bits;
+        compress(s, w);
+        compress(s, w + 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[j] = s.h[j];
+}
+
+}  // namespace mh

@@ -1,0 +1,104 @@
+// mh_internal.hpp -- shared declarations between the kernel translation units
+// and the C-ABI implementation (capi.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/immustore_merkle.h"
+
+namespace mh {
+
+constexpr int kMaxLevels = 66;
+
+// Level-major flat layout of an htree of width n (embedded/htree/htree.go:
+// levels[l] holds ceil(n/2^l) used nodes; promoted odd nodes are copied up).
+struct LevelGeom {
+    uint64_t n = 0;
+    int nlevels = 0;                // number of levels incl. root level
+    uint64_t off[kMaxLevels] = {};  // offset (in 32-byte nodes) of level l
+    uint64_t width[kMaxLevels] = {};
+    uint64_t total = 0;             // total nodes
+    void init(uint64_t n_);
+};
+
+// Kernel arguments passed by value (fits in the 4 KB kernarg segment).
+struct LevelArgs {
+    uint64_t off[kMaxLevels];
+    uint64_t width[kMaxLevels];
+};
+
+struct KWTable {
+    uint32_t kw[64];
+};
+
+// Compute K[t]+W[t] of the padding block of a message of `len` bytes whose
+// length is a multiple of 64 (constant schedule: 0x80, zeros, bit length).
+void pad_block_kw(uint64_t len, KWTable *out);
+
+// ---------------------------------------------------------------- launchers
+// All return hipError_t (hipSuccess == 0) and enqueue on `st`.
+// Per-kernel timing hook (ctx-level); may be null.
+struct Timer {
+    virtual void begin(const char *name, hipStream_t st) = 0;
+    virtual void end(hipStream_t st) = 0;
+    virtual ~Timer() {}
+};
+
+hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t n,
+                                const uint8_t *keys, uint32_t key_len, const uint8_t *vals,
+                                uint32_t val_len, uint8_t *hvals_out, uint8_t *levels,
+                                const LevelGeom &g, int *lanes_levels_done);
+bool entries_fixed_supported(int version, const uint8_t *keys, uint32_t key_len,
+                             const uint8_t *vals, uint32_t val_len);
+
+hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
+                             uint64_t n, const uint8_t *override32, const uint8_t *use_override,
+                             uint8_t *out32);
+hipError_t launch_sha256_fixed(hipStream_t st, Timer *tm, const uint8_t *buf, uint64_t stride,
+                               uint64_t len, uint64_t n, uint8_t *out32);
+
+// Assemble entry-digest messages (tx.go:690-731) into `msgs` at msg_off.
+// err_flag (device int) is set to MH_ERR_METADATA_UNSUPPORTED for v0 + md.
+hipError_t launch_digest_assemble(hipStream_t st, Timer *tm, int version, uint64_t n,
+                                  const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
+                                  const uint64_t *md_off, const uint8_t *hvals,
+                                  const uint64_t *msg_off, uint8_t *msgs, int *err_flag);
+hipError_t launch_msg_offsets(hipStream_t st, Timer *tm, int version, uint64_t n,
+                              const uint64_t *key_off, const uint64_t *md_off, uint64_t *msg_off);
+
+// Leaves from digests (htree.go:79-83) + in-lane levels up to log2(LPL).
+hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *digests,
+                                      uint64_t n, uint8_t *levels, const LevelGeom &g,
+                                      int *levels_done);
+// Copy nodes into level 0 (no leaf hashing): used for reducing subtree roots.
+// Reduce levels [from, top] in place (htree.go:85-110).
+hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const LevelGeom &g,
+                         int from_level);
+
+// Generic helpers
+hipError_t launch_fill_random(hipStream_t st, uint8_t *dst, uint64_t nbytes, uint64_t seed);
+hipError_t launch_fill_keys_be64(hipStream_t st, uint8_t *dst, uint64_t n, uint64_t first);
+hipError_t launch_iota_offsets(hipStream_t st, uint64_t *off, uint64_t n, uint64_t stride);
+hipError_t launch_gather_nodes(hipStream_t st, const uint8_t *src, const uint64_t *idx, uint64_t n,
+                               uint8_t *dst);
+
+// ---- verification (embedded/htree/htree.go:166-195, ahtree/verification.go)
+hipError_t launch_htree_verify(hipStream_t st, Timer *tm, uint64_t np, const uint64_t *leaf,
+                               const uint64_t *width, const uint64_t *term_off,
+                               const uint8_t *terms, const uint8_t *digests, const uint8_t *roots,
+                               uint8_t *ok);
+hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np,
+                                const uint64_t *i, const uint64_t *j, const uint64_t *term_off,
+                                const uint8_t *terms, const uint8_t *a, const uint8_t *b,
+                                uint8_t *ok, uint8_t *eval_out);
+
+// ---- ahtree batch append (embedded/ahtree/ahtree.go:246-373)
+hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                uint8_t *roots_out);
+
+// host-side index math shared with the C API
+uint64_t ahtree_nodes_upto(uint64_t n);
+uint64_t ahtree_nodes_until(uint64_t n);
+
+}  // namespace mh

@@ -1,0 +1,457 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden data.  Bit-exact everywhere (integer/byte work).
+
+Run on the MI355X box:  python -m pytest tests -m gpu -x -q
+"""
+import hashlib
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from gpu_util import DevBuf
+
+pytestmark = pytest.mark.gpu
+
+
+def H(b):
+    return hashlib.sha256(b).digest()
+
+
+@pytest.fixture(scope="module")
+def m():
+    import torch  # noqa: F401  (load the HIP runtime the way the bench does)
+    import immustore_amd as m
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return m
+
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["1", "2", "4"])
+def lpl(request):
+    old = os.environ.get("MH_LPL")
+    os.environ["MH_LPL"] = request.param
+    yield int(request.param)
+    if old is None:
+        del os.environ["MH_LPL"]
+    else:
+        os.environ["MH_LPL"] = old
+
+
+# ------------------------------------------------------------------ SHA-256
+def test_sha256_batch_any_alignment(m, ctx):
+    from immustore_amd import _native as N
+    rng = np.random.default_rng(11)
+    lens = list(range(0, 140)) + [255, 256, 257, 1000, 1023, 1024, 1025, 4096, 5000]
+    # random gaps make every start alignment mod 4 / mod 16 appear
+    offs, pos = [], 0
+    for L in lens:
+        pos += int(rng.integers(0, 7))
+        offs.append((pos, pos + L))
+        pos += L
+    buf = rng.integers(0, 256, pos + 3, dtype=np.uint8)
+    # CSR needs contiguous ranges: build [start_i, end_i) as off[i], off[i+1] pairs by
+    # hashing every range through its own 2-entry offset table
+    d_buf = DevBuf.from_host(ctx, buf)
+    for (a, b) in offs:
+        off = np.array([a, b], np.uint64)
+        d_off = DevBuf.from_host(ctx, off)
+        d_out = DevBuf(ctx, 32)
+        N.check(N.load().mh_dev_sha256_batch(ctx.handle, d_buf.ptr, d_off.ptr, 1, d_out.ptr))
+        assert d_out.to_host().tobytes() == H(buf[a:b].tobytes()), (a, b)
+    # and one big batch over contiguous ranges
+    cuts = np.sort(rng.integers(0, pos, 500)).astype(np.uint64)
+    cuts[0] = 0
+    d_off = DevBuf.from_host(ctx, cuts)
+    d_out = DevBuf(ctx, 32 * (len(cuts) - 1))
+    N.check(N.load().mh_dev_sha256_batch(ctx.handle, d_buf.ptr, d_off.ptr, len(cuts) - 1, d_out.ptr))
+    got = d_out.to_host().reshape(-1, 32)
+    for i in range(len(cuts) - 1):
+        assert got[i].tobytes() == H(buf[int(cuts[i]):int(cuts[i + 1])].tobytes())
+
+
+# ------------------------------------------------------------------ htree
+def test_htree_build_with_golden(m, ctx, synthetic, lpl):
+    for case in synthetic["htree"]:
+        w = case["width"]
+        digs = [H(struct.pack(">Q", i)) for i in range(w)]
+        t = m.HTree(max(w, 1), ctx)
+        t.build_with(digs)
+        assert t.root().hex() == case["root"], w
+        lv = t.levels()
+        assert lv.shape[0] == case["levels_len"]
+        assert H(lv.tobytes()).hex() == case["levels_sha256"], w
+        for pr in case.get("proofs", []):
+            p = t.inclusion_proof(pr["leaf"])
+            assert [x.hex() for x in p.terms] == pr["terms"]
+        t.close()
+
+
+def test_htree_errors(m, ctx):
+    # embedded/htree/htree_test.go:27-87
+    t = m.HTree(0, ctx)
+    with pytest.raises(m.ErrMaxWidthExceeded):
+        t.build_with([H(b"")])
+    t.build_with([])
+    assert t.root() == H(b"")
+    t = m.HTree(1000, ctx)
+    digs = [H(struct.pack(">Q", i)) for i in range(1000)]
+    t.build_with(digs)
+    root = t.root()
+    proofs = [t.inclusion_proof(i) for i in range(1000)]
+    assert m.verify_inclusion_batch(proofs, digs, [root] * 1000).all()
+    assert not m.verify_inclusion_batch(proofs, [H(d) for d in digs], [root] * 1000).any()
+    assert not m.verify_inclusion_batch(proofs, digs, [H(root)] * 1000).any()
+    stripped = [m.InclusionProof(p.leaf, p.width, []) for p in proofs]
+    assert not m.verify_inclusion_batch(stripped, digs, [root] * 1000).any()
+    assert not m.verify_inclusion(None, digs[0], root)
+    t.build_with([])
+    assert t.root() == H(b"")
+    with pytest.raises(m.ErrMaxWidthExceeded):
+        t.build_with([b"\0" * 32] * 1001)
+    with pytest.raises(m.ErrIllegalArguments):
+        t.inclusion_proof(1000)
+
+
+def test_htree_random_widths_vs_oracle(m, ctx, orc, lpl):
+    rng = np.random.default_rng(5)
+    for w in [1, 2, 3, 4, 5, 6, 7, 8, 9, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025,
+              4095, 4097, 65535, 65537, 262145, 1048577]:
+        d = rng.integers(0, 256, (w, 32), dtype=np.uint8)
+        t = m.HTree(w, ctx)
+        t.build_with(d)
+        lv, root = orc.htree_build(d)
+        assert t.root() == root, w
+        assert np.array_equal(t.levels(), lv), w
+        t.close()
+
+
+# ------------------------------------------------------------ entries (fused)
+def _fixed_inputs(orc, n, klen, vlen, seed):
+    vals = orc.fill_random(n * vlen, seed).reshape(n, vlen) if vlen else np.zeros((n, 0), np.uint8)
+    keys = orc.fill_random(n * klen, seed + 1000).reshape(n, klen) if klen else np.zeros((n, 0), np.uint8)
+    return keys, vals
+
+
+def _dev_build_fixed(m, ctx, version, keys, vals):
+    from immustore_amd import _native as N
+    n, klen = keys.shape
+    vlen = vals.shape[1]
+    dk = DevBuf.from_host(ctx, keys if keys.size else np.zeros(16, np.uint8))
+    dv = DevBuf.from_host(ctx, vals if vals.size else np.zeros(16, np.uint8))
+    dl = DevBuf(ctx, max(m.levels_len(n), 1) * 32)
+    dh = DevBuf(ctx, max(n, 1) * 32)
+    dr = DevBuf(ctx, 32)
+    N.check(N.load().mh_dev_htree_build_entries_fixed(ctx.handle, version, n, dk.ptr, klen, dv.ptr,
+                                                       vlen, dh.ptr, dl.ptr, dr.ptr))
+    ctx.synchronize()
+    return (dh.to_host().reshape(-1, 32)[:n], dl.to_host().reshape(-1, 32)[:m.levels_len(n)],
+            dr.to_host().tobytes())
+
+
+def test_c1_plumbing_config(m, ctx, orc, synthetic, lpl):
+    # BASELINE configs[0]: 1024 x 256 B, key = BE64(i), v1, seed 1
+    c1 = synthetic["c1"]
+    vals = orc.fill_random(1024 * 256, 1).reshape(1024, 256)
+    keys = np.frombuffer(b"".join(struct.pack(">Q", i) for i in range(1024)), np.uint8).reshape(1024, 8)
+    hv, lv, root = _dev_build_fixed(m, ctx, 1, keys, vals)
+    assert root.hex() == c1["eh"]
+    assert H(lv.tobytes()).hex() == c1["levels_sha256"]
+    for i in (0, 1, 511, 1023):
+        assert hv[i].tobytes() == H(vals[i].tobytes())
+
+
+@pytest.mark.parametrize("version,klen", [(1, 0), (1, 4), (1, 8), (1, 12), (1, 16), (0, 0), (0, 8),
+                                          (0, 20)])
+def test_entries_fixed_shapes(m, ctx, orc, lpl, version, klen):
+    for vlen in (0, 16, 48, 64, 80, 112, 128, 192, 1024, 1040):
+        for n in (1, 2, 3, 5, 63, 64, 65, 255, 257, 1000):
+            keys, vals = _fixed_inputs(orc, n, klen, vlen, 7 + vlen + n)
+            hv, lv, root = _dev_build_fixed(m, ctx, version, keys, vals)
+            ohv, olv, oroot = orc.build_entries_fixed(version, keys, vals)
+            assert root == oroot, (version, klen, vlen, n)
+            assert np.array_equal(hv, ohv), (version, klen, vlen, n)
+            assert np.array_equal(lv, olv), (version, klen, vlen, n)
+
+
+def test_entries_fixed_odd_shapes_use_general_path(m, ctx, orc):
+    # shapes outside the fused kernel's preconditions (unaligned stride,
+    # long keys) go through the generic CSR kernels -- same answer
+    for version, klen, vlen in [(1, 3, 17), (1, 33, 100), (0, 1, 1), (1, 64, 63), (0, 100, 5)]:
+        for n in (1, 7, 300):
+            keys, vals = _fixed_inputs(orc, n, klen, vlen, 99)
+            hv, lv, root = _dev_build_fixed(m, ctx, version, keys, vals)
+            ohv, olv, oroot = orc.build_entries_fixed(version, keys, vals)
+            assert root == oroot and np.array_equal(lv, olv) and np.array_equal(hv, ohv)
+
+
+def test_entries_csr_md_override(m, ctx, orc, synthetic):
+    ents = synthetic["entries"]
+    keys = [bytes.fromhex(e["key"]) for e in ents]
+    mds = [bytes.fromhex(e["md"]) for e in ents]
+    vals = [bytes.fromhex(e["value"]) for e in ents]
+    eh, hv, lv = m.build_hash_tree(1, keys, vals, mds, ctx=ctx)
+    digs = np.stack([np.frombuffer(bytes.fromhex(e["digest_v1"]), np.uint8) for e in ents])
+    olv, oroot = orc.htree_build(digs)
+    assert eh == oroot and np.array_equal(lv, olv)
+    assert [h.tobytes().hex() for h in hv] == [e["hval"] for e in ents]
+    with pytest.raises(m.ErrMetadataUnsupported):
+        m.build_hash_tree(0, keys, vals, mds, ctx=ctx)
+    # IsValueTruncated: override hVal, value absent (immustore.go:1624-1626)
+    ov = [bytes.fromhex(e["hval"]) if i % 3 == 0 else None for i, e in enumerate(ents)]
+    vals2 = [b"" if o else v for o, v in zip(ov, vals)]
+    eh2, hv2, _ = m.build_hash_tree(1, keys, vals2, mds, hval_overrides=ov, ctx=ctx)
+    assert eh2 == eh and np.array_equal(hv2, hv)
+    # v0 without metadata
+    nomd = [i for i, e in enumerate(ents) if not e["md"]]
+    eh0, _, _ = m.build_hash_tree(0, [keys[i] for i in nomd], [vals[i] for i in nomd], ctx=ctx)
+    d0 = np.stack([np.frombuffer(bytes.fromhex(ents[i]["digest_v0"]), np.uint8) for i in nomd])
+    assert eh0 == orc.htree_build(d0)[1]
+
+
+def test_entries_csr_random_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 17, 300, 2049):
+        keys = [rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8).tobytes() for _ in range(n)]
+        mds = [rng.integers(0, 256, int(rng.integers(0, 12)), dtype=np.uint8).tobytes() for _ in range(n)]
+        vals = [rng.integers(0, 256, int(rng.integers(0, 700)), dtype=np.uint8).tobytes() for _ in range(n)]
+        eh, hv, lv = m.build_hash_tree(1, keys, vals, mds, ctx=ctx)
+        st, ohv, olv, oroot = orc.build_entries(1, keys, mds, vals)
+        assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
+
+
+def test_go_fixtures_alh_chain_on_gpu(m, ctx, orc, fixtures):
+    """Eh computed on the GPU -> innerHash/Alh (oracle) == Alh stored by Go."""
+    for name, fx in fixtures.items():
+        prev = H(b"")
+        for tx in fx["txs"]:
+            h = tx["header"]
+            ents = tx["entries"]
+            keys = [bytes.fromhex(e["key"]) for e in ents]
+            mds = [bytes.fromhex(e["md"]) for e in ents]
+            # values where the vLog holds them, otherwise the stored hVal as override
+            vals = [bytes.fromhex(e.get("value", "")) for e in ents]
+            ov = [None if "value" in e else bytes.fromhex(e["hval"]) for e in ents]
+            eh, hv, _ = m.build_hash_tree(h["version"], keys, vals, mds, hval_overrides=ov, ctx=ctx)
+            assert [x.tobytes().hex() for x in hv] == [e["hval"] for e in ents]
+            st, inner = orc.tx_inner_hash(h["ts"], h["version"], bytes.fromhex(h["md"]),
+                                          h["nentries"], eh, h["bltxid"], bytes.fromhex(h["blroot"]))
+            alh = orc.tx_alh(h["id"], prev, inner)
+            assert alh.hex() == h["alh"], (name, h["id"])
+            prev = alh
+
+
+def test_c2_full_size_vs_oracle(m, ctx, orc):
+    """BASELINE configs[1] at full size: 2^20 x 1 KiB, key = BE64(i), v1."""
+    n, vlen = 1 << 20, 1024
+    vals = orc.fill_random(n * vlen, 2).reshape(n, vlen)
+    keys = np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8).reshape(n, 8)
+    hv, lv, root = _dev_build_fixed(m, ctx, 1, keys, vals)
+    ohv, olv, oroot = orc.build_entries_fixed(1, keys, vals, nthreads=min(16, os.cpu_count() or 1))
+    assert root == oroot
+    assert np.array_equal(lv, olv)
+    assert np.array_equal(hv, ohv)
+
+
+def test_reduce_nodes_matches_sharded_build(m, ctx, orc):
+    """Finding 3: subtree roots of power-of-two shards + top levels == full root."""
+    from immustore_amd import _native as N
+    rng = np.random.default_rng(8)
+    for n, shard in [(1000, 128), (1 << 14, 1 << 11), (5000, 1024), (4097, 512)]:
+        d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        roots = [orc.htree_build(d[i:i + shard])[1] for i in range(0, n, shard)]
+        w = len(roots)
+        dn = DevBuf.from_host(ctx, np.frombuffer(b"".join(roots), np.uint8))
+        dl = DevBuf(ctx, m.levels_len(w) * 32)
+        dr = DevBuf(ctx, 32)
+        N.check(N.load().mh_dev_htree_reduce_nodes(ctx.handle, dn.ptr, w, dl.ptr, dr.ptr))
+        assert dr.to_host().tobytes() == orc.htree_build(d)[1]
+
+
+# ------------------------------------------------------------------ ahtree
+def test_ahtree_golden_small(m, ctx, synthetic):
+    a = synthetic["ahtree"]
+    t = m.AHtree(ctx)
+    for i in range(1, 301):
+        n, r = t.append(bytes([i & 0xFF]))
+        assert n == i and r.hex() == a["roots"][i - 1]
+    # rest in one batch of 1-byte payloads
+    p = np.array([[i & 0xFF] for i in range(301, a["n"] + 1)], np.uint8)
+    roots = t.append_batch(p, with_roots=True)
+    assert [x.tobytes().hex() for x in roots] == a["roots"][300:]
+    assert H(t.dlog()).hex() == a["dlog_sha256"]
+    for i in (1, 2, 17, 1024, 1100):
+        assert t.root_at(i).hex() == a["roots"][i - 1]
+    with pytest.raises(m.ErrIllegalArguments):
+        t.root_at(0)
+    with pytest.raises(m.ErrUnexistentData):
+        t.root_at(1101)
+    with pytest.raises(m.ErrEmptyTree):
+        m.AHtree(ctx).root()
+    with pytest.raises(m.ErrIllegalArguments):
+        t.append(None)
+    for pr in synthetic["ahtree_proofs"]:
+        i, j = pr["i"], pr["j"]
+        assert [x.hex() for x in t.inclusion_proof(i, j)] == pr["iproof"]
+        assert [x.hex() for x in t.consistency_proof(i, j)] == pr["cproof"]
+    with pytest.raises(m.ErrIllegalArguments):
+        t.inclusion_proof(2, 1)
+    with pytest.raises(m.ErrIllegalArguments):
+        t.consistency_proof(2, 1)
+
+
+def test_ahtree_go_fixture_dlogs(m, ctx, fixtures):
+    for name, fx in fixtures.items():
+        pay = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
+        t = m.AHtree(ctx)
+        t.append_batch(pay)
+        assert t.dlog() == bytes.fromhex(fx["aht_dlog"]), name
+        # one at a time as the store does (immustore.go:1939-1946)
+        t2 = m.AHtree(ctx)
+        for p in pay:
+            t2.append(p.tobytes())
+        assert t2.dlog() == bytes.fromhex(fx["aht_dlog"]), name
+
+
+def test_ahtree_random_batches_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(21)
+    t = m.AHtree(ctx)
+    o = orc.AHtree()
+    total = 0
+    for bs in [1, 1, 2, 3, 7, 64, 1, 1000, 4096, 5, 33333, 1, 2]:
+        p = rng.integers(0, 256, (bs, 32), dtype=np.uint8)
+        roots = t.append_batch(p, with_roots=True)
+        o.append_batch(p)
+        total += bs
+        assert t.size() == total
+        assert t.dlog() == o.dlog_bytes()
+        assert roots[-1].tobytes() == o.root_at(total)[1]
+    # reset and re-append (ResetSize, ahtree.go:375-458)
+    t.reset_size(total - 10)
+    with pytest.raises(m.ErrCannotResetToLargerSize):
+        t.reset_size(total + 1)
+    o2 = orc.AHtree()
+    # rebuild oracle to the same prefix then the same suffix
+    t.append_batch(np.zeros((10, 32), np.uint8))
+    assert t.root_at(total - 10) == o.root_at(total - 10)[1]
+    # variable-size payloads (generic leaf path)
+    t3 = m.AHtree(ctx)
+    for ln in [0, 1, 31, 32, 33, 55, 56, 63, 64, 100, 1000]:
+        pp = rng.integers(0, 256, (5, ln), dtype=np.uint8) if ln else np.zeros((5, 0), np.uint8)
+        t3.append_batch(pp)
+        for row in pp:
+            o2.append(row.tobytes())
+    assert t3.dlog() == o2.dlog_bytes()
+
+
+def test_ahtree_large_recurrence(m, ctx, orc):
+    """10^6 appends: sampled appends re-derived from the dLog's own nodes
+    (ahtree.go:296-322) with the oracle's SHA-256, plus a 2^17 prefix vs oracle."""
+    rng = np.random.default_rng(4)
+    M = 10 ** 6
+    pay = orc.fill_random(32 * M, 3).reshape(M, 32)
+    t = m.AHtree(ctx)
+    t.append_batch(pay[: 1 << 17])
+    o = orc.AHtree(1 << 17)
+    o.append_batch(pay[: 1 << 17])
+    assert t.dlog() == o.dlog_bytes()
+    t.append_batch(pay[1 << 17:])
+    dl = np.frombuffer(t.dlog(), np.uint8).reshape(-1, 32)
+    assert dl.shape[0] == orc.nodes_upto(M)
+
+    def node(k, l):
+        return dl[orc.nodes_until(k) + l].tobytes()
+
+    for n in list(rng.integers(1, M + 1, 3000)) + [M, M - 1, 1 << 19, (1 << 19) + 1]:
+        n = int(n)
+        h = H(b"\x00" + pay[n - 1].tobytes())
+        base = orc.nodes_until(n)
+        assert dl[base].tobytes() == h
+        w, k, l, cnt = n - 1, n - 1, 0, 1
+        while w > 0:
+            if w & 1:
+                h = H(b"\x01" + node(k, l) + h)
+                assert dl[base + cnt].tobytes() == h, (n, l)
+                cnt += 1
+            k &= ~(1 << l)
+            w >>= 1
+            l += 1
+
+
+def test_ahtree_verify_batch_vs_oracle(m, ctx, orc):
+    from immustore_amd import _native as N
+    rng = np.random.default_rng(9)
+    o = orc.AHtree()
+    pay = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    o.append_batch(pay)
+    inc, cons, last, exp_i, exp_c, exp_l = [], [], [], [], [], []
+    for _ in range(600):
+        j = int(rng.integers(1, 701))
+        i = int(rng.integers(1, j + 1))
+        _, ip = o.inclusion_proof(i, j)
+        _, cp = o.consistency_proof(i, j)
+        ip = [x.tobytes() for x in ip]
+        cp = [x.tobytes() for x in cp]
+        leaf = H(b"\x00" + pay[i - 1].tobytes())
+        jr = o.root_at(j)[1]
+        ir = o.root_at(i)[1]
+        if rng.random() < 0.2 and ip:
+            k = int(rng.integers(0, len(ip)))
+            ip[k] = bytes([ip[k][0] ^ 1]) + ip[k][1:]
+        if rng.random() < 0.2 and cp:
+            k = int(rng.integers(0, len(cp)))
+            cp[k] = bytes([cp[k][0] ^ 1]) + cp[k][1:]
+        ii = i if rng.random() > 0.05 else 0
+        inc.append((ip, ii, j, leaf, jr))
+        exp_i.append(orc.ahtree_verify_inclusion(ip, ii, j, leaf, jr))
+        cons.append((cp, i, j, ir, jr))
+        exp_c.append(orc.ahtree_verify_consistency(cp, i, j, ir, jr))
+        _, lp = o.inclusion_proof(i, j)
+        lp = [x.tobytes() for x in lp]
+        last.append((lp, i, j, leaf, ir))
+        exp_l.append(orc.ahtree_verify_last_inclusion(lp, i, leaf, ir))
+    assert list(m.ahtree_verify_batch(N.MH_AHT_INCLUSION, inc, ctx)[0]) == exp_i
+    assert list(m.ahtree_verify_batch(N.MH_AHT_CONSISTENCY, cons, ctx)[0]) == exp_c
+    assert list(m.ahtree_verify_batch(N.MH_AHT_LAST_INCLUSION, last, ctx)[0]) == exp_l
+    assert any(exp_i) and not all(exp_i) and any(exp_c) and not all(exp_c) and any(exp_l)
+    # verification_test.go:26-32 edge cases
+    z = H(b"")
+    assert not m.ahtree_verify_inclusion([], 1, 10, z, z, ctx)
+    assert not m.ahtree_verify_inclusion([], 10, 1, z, z, ctx)
+    assert not m.ahtree_verify_consistency([], 1, 10, z, z, ctx)
+    assert not m.ahtree_verify_consistency([], 10, 1, z, z, ctx)
+    assert m.ahtree_verify_consistency([], 5, 5, z, z, ctx)
+
+
+def test_htree_verify_batch_c5_shape(m, ctx, orc):
+    """BASELINE configs[4] shape at reduced count: depth-24 proofs over a
+    2^24-leaf tree would need 512 MiB of levels on the host oracle; use a
+    2^16-leaf tree (depth 16) and 20k proofs with 10 % tampered."""
+    rng = np.random.default_rng(5)
+    w = 1 << 16
+    d = rng.integers(0, 256, (w, 32), dtype=np.uint8)
+    lv, root = orc.htree_build(d)
+    P = 20000
+    idx = rng.integers(0, w, P)
+    proofs, digs, exp = [], [], []
+    for i in idx:
+        _, terms = orc.htree_inclusion_proof(lv, w, int(i))
+        terms = [x.tobytes() for x in terms]
+        dg = d[i].tobytes()
+        if rng.random() < 0.1:
+            k = int(rng.integers(0, len(terms)))
+            terms[k] = bytes([terms[k][0] ^ 0x80]) + terms[k][1:]
+        proofs.append(m.InclusionProof(int(i), w, terms))
+        digs.append(dg)
+        exp.append(orc.htree_verify_inclusion(int(i), w, terms, dg, root))
+    got = m.verify_inclusion_batch(proofs, digs, [root] * P, ctx)
+    assert list(got) == exp
+    assert 0.85 < np.mean(exp) < 0.95
