@@ -38,8 +38,8 @@ VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 # VALU instructions per 64-byte compression of the generic compress() in the
 # gfx950 ISA of this build (counted in profiles/isa_counts_r01.txt); the
 # constant-schedule padding block (compress_kw) needs fewer.
-OPS_PER_COMP = 1399
-OPS_PER_COMP_KW = 840
+OPS_PER_COMP = 1388
+OPS_PER_COMP_KW = 901
 
 
 def parse():

@@ -397,6 +397,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
         if (on) compress(s, w);
 
         // ---------------------------------------------------------- transition
+        bool entry_done = false;
         if (op == OP_VALUE) {
             if (++b < nfull) continue;
             b = 0;
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
         } else if (op == OP_LEAF) {
             if (i < c) store_digest(levels + idx * 32, s.h);  // level 0 offset is 0
             if (LPL == 1) break;
+            entry_done = true;
             if ((i & 1) == 0) {
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
@@ -451,8 +453,9 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
             }
             if (LPL == 4 && i == 3 && c > 0) store_node(levels, la, 2, first >> 2, A);
             if (LPL == 2 || i == LPL - 1) break;
+            entry_done = true;
         }
-        if (op == OP_LEAF || op == OP_NODE2) {
+        if (entry_done) {
             // next entry of the group
             if (++i >= LPL) break;
             s.init();

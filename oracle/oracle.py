@@ -11,6 +11,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
+_KEEP = []
 
 u8p = C.POINTER(C.c_uint8)
 u64p = C.POINTER(C.c_uint64)
@@ -118,9 +119,9 @@ def htree_inclusion_proof(levels, width, i):
 
 
 def htree_verify_inclusion(leaf, width, terms, digest, root):
-    t = np.ascontiguousarray(terms, dtype=np.uint8).reshape(-1, 32)
-    return bool(lib().orc_htree_verify_inclusion(leaf, width, _p(t) if len(t) else None, len(t),
-                                                 _p(_u8(digest)), _p(_u8(root))))
+    tp, nt = _terms(terms)
+    return bool(lib().orc_htree_verify_inclusion(leaf, width, tp, nt, _p(_u8(digest)),
+                                                 _p(_u8(root))))
 
 
 def build_entries_fixed(version, keys, vals, nthreads=1, want_levels=True):
@@ -237,7 +238,13 @@ class AHtree:
 
 
 def _terms(t):
+    if not isinstance(t, np.ndarray):
+        t = np.frombuffer(b"".join(bytes(x) for x in t), dtype=np.uint8) if len(t) else \
+            np.zeros((0, 32), np.uint8)
     t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, 32)
+    _KEEP.append(t)  # keep alive until the call returns
+    if len(_KEEP) > 64:
+        del _KEEP[:32]
     return (_p(t) if len(t) else None), len(t)
 
 
