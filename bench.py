@@ -40,6 +40,13 @@ VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 # constant-schedule padding block (compress_kw) needs fewer.
 OPS_PER_COMP = 1388
 OPS_PER_COMP_KW = 901
+# Measured SHA-256 compression ceiling of this chip with this round function:
+# tools/microbench_sha.hip, registers only, >= 2 waves/SIMD (profiles/
+# microbench_r01.txt).  v_alignbit_b32 / v_add3_u32 / v_perm_b32 issue at
+# about half the rate of v_add_u32 / v_bitop3_b32 on gfx950
+# (tools/microbench_valu.hip), so the nominal VALU peak above over-states
+# what a SHA-256 round can reach.
+SHA_PEAK_GCOMPS = 30.9
 
 
 def parse():
@@ -98,6 +105,7 @@ def main():
     import torch
     import immustore_amd as m
     from immustore_amd import _native as N
+    from immustore_amd import sharding
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -124,7 +132,6 @@ def main():
     levels = torch.empty(nlv * 32, dtype=torch.uint8, device=dev)
     root = torch.empty(32, dtype=torch.uint8, device=dev)
     if world > 1:
-        roots = torch.empty(world * 32, dtype=torch.uint8, device=dev)
         top_levels = torch.empty(max(m.levels_len(world), 1) * 32, dtype=torch.uint8, device=dev)
         groot = torch.empty(32, dtype=torch.uint8, device=dev)
 
@@ -133,8 +140,10 @@ def main():
                                                    vals.data_ptr(), VAL_LEN, None,
                                                    levels.data_ptr(), root.data_ptr()))
         if world > 1:
-            dist.all_gather_into_tensor(roots, root)
-            N.check(L.mh_dev_htree_reduce_nodes(ctx.handle, roots.data_ptr(), world,
+            # 32 B per rank over RCCL, then the top log2(world) levels locally
+            # (immustore_amd/sharding.py; exact by SURVEY.md finding 3)
+            g = sharding.allgather_roots(root, world)
+            N.check(L.mh_dev_htree_reduce_nodes(ctx.handle, g.data_ptr(), world,
                                                 top_levels.data_ptr(), groot.data_ptr()))
 
     for _ in range(a.warmup):
@@ -164,13 +173,21 @@ def main():
     r_ms, r_cnt = ctx.timing("reduce")
     kern_ms = k_ms / max(k_cnt, 1)
     lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
-    lvl_written = sum(-(-n // (1 << l)) for l in range({1: 1, 2: 2, 4: 3}[lpl]))
+    # levels written by one launch of the dominant kernel: the lanes' groups
+    # up to level log2(lpl), then each workgroup's subtree 8 levels higher
+    top = min({1: 0, 2: 1, 4: 2}[lpl] + 8, max(m.levels_len(n) and (n - 1).bit_length(), 0))
+    widths = [-(-n // (1 << l)) for l in range(top + 1)]
+    nodes_written = sum(widths)
     # algorithmic HBM bytes of one launch of the dominant kernel:
-    #   read value + key of every entry, write the levels the kernel owns
-    alg_bytes = n * (VAL_LEN + KEY_LEN) + 32 * lvl_written
+    #   read value + key of every entry, write every level node it produces
+    alg_bytes = n * (VAL_LEN + KEY_LEN) + 32 * nodes_written
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    comps = n * (VAL_LEN // 64 + 2) + (lvl_written - n) * 2  # + pad block below
-    valu = (comps * OPS_PER_COMP + n * OPS_PER_COMP_KW) / (kern_ms * 1e-3)
+    # compressions: 16 value blocks + digest + leaf per entry (generic),
+    # the constant padding block (compress_kw), 2 per inner node
+    node_hashes = nodes_written - n
+    valu = (n * (VAL_LEN // 64 + 2) * OPS_PER_COMP + n * OPS_PER_COMP_KW +
+            2 * node_hashes * OPS_PER_COMP) / (kern_ms * 1e-3)
+    comp_rate = (n * (VAL_LEN // 64 + 3) + 2 * node_hashes) / (kern_ms * 1e-3)
     traffic = None
     if os.path.exists(a.traffic_file):
         try:
@@ -205,6 +222,9 @@ def main():
                      "valu": {"achieved_tops": round(valu / 1e12, 2),
                               "peak_tops": round(VALU_PEAK_OPS / 1e12, 2),
                               "frac": round(valu / VALU_PEAK_OPS, 4)},
+                     "sha": {"gcomp_per_s": round(comp_rate / 1e9, 2),
+                             "peak_gcomp_per_s": SHA_PEAK_GCOMPS,
+                             "frac": round(comp_rate / 1e9 / SHA_PEAK_GCOMPS, 4)},
                      "reduce_ms_per_step": round(r_ms / max(a.steps, 1), 4)},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

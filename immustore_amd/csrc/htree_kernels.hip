@@ -72,15 +72,17 @@ void pad_block_kw(uint64_t len, KWTable *out) {
     for (int t = 0; t < 64; t++) out->kw[t] = K[t] + w[t];
 }
 
-// Offsets / widths of levels 0..2 (the levels an in-lane group writes).
+// Offsets / widths of levels 0..10: the levels a leaf workgroup writes (its
+// lanes' groups up to level log2(LPL), then its subtree up to 8 more levels).
+constexpr int kLaneLevels = 11;
 struct LaneLevels {
-    uint64_t off[3];
-    uint64_t width[3];
+    uint64_t off[kLaneLevels];
+    uint64_t width[kLaneLevels];
 };
 
 static LaneLevels lane_levels(const LevelGeom &g) {
     LaneLevels a;
-    for (int l = 0; l < 3; l++) {
+    for (int l = 0; l < kLaneLevels; l++) {
         a.off[l] = l < g.nlevels ? g.off[l] : 0;
         a.width[l] = l < g.nlevels ? g.width[l] : 0;
     }
@@ -292,18 +294,19 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     const uint64_t wave_slot0 = ((uint64_t)blockIdx.x * (kFixedThreads / 64) + wave) * 64;
     const uint64_t first = (wave_slot0 + lane) * LPL;
     const int c = first < n ? (int)min<uint64_t>(LPL, n - first) : 0;
-    if (wave_slot0 * LPL >= n) return;  // whole wave idle (wave-uniform)
+    const bool wave_busy = wave_slot0 * LPL < n;  // wave-uniform
 
     const uint32_t nfull = val_len >> 6;
     const uint32_t rem = val_len & 63;  // 0, 16, 32 or 48 (fast-path precondition)
     const uint32_t nsteps2 = nfull >> 1;
     const uint32_t units = nsteps2 + (nfull & 1);
     const int kw4 = key_len >> 2;
-    if (units) dma_issue(vals, val_len, wave_slot0, LPL, 0, n, 0, nsteps2 > 0, lds, lane);
-
     State s;
     s.init();
     uint32_t A[8], B[8], ny7 = 0;
+    if (wave_busy) {
+    if (units) dma_issue(vals, val_len, wave_slot0, LPL, 0, n, 0, nsteps2 > 0, lds, lane);
+
     int i = 0;         // entry of the lane group (uniform)
     uint32_t b = 0;    // value block (uniform)
     int node = 0;      // node step of the group after leaf i (uniform)
@@ -463,6 +466,43 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
             if (!nfull && !rem && i < c) compress_kw(s, kw_lds);
         }
     }
+    }  // wave_busy
+
+    // -------------------------------------------------------- workgroup subtree
+    // The workgroup's 256 lane-group nodes (level L0 = log2 LPL) are reduced
+    // in LDS to up to 8 more levels (htree.go:85-110), writing every level.
+    constexpr int L0 = LPL == 4 ? 2 : (LPL == 2 ? 1 : 0);
+    const int t = threadIdx.x;
+    uint32_t(*buf)[kFixedThreads][9] = reinterpret_cast<uint32_t(*)[kFixedThreads][9]>(smem);
+    __syncthreads();  // every wave is done with its staging area
+#pragma unroll
+    for (int j = 0; j < 8; j++) buf[0][t][j] = LPL == 1 ? s.h[j] : A[j];
+    int cur = 0;
+#pragma unroll 1
+    for (int st = 1; st <= 8; st++) {
+        __syncthreads();
+        const int active = kFixedThreads >> st;
+        const int l = L0 + st;
+        if (t < active) {
+            const uint64_t q = (uint64_t)blockIdx.x * active + t;
+            if (q < la.width[l]) {
+                uint32_t lft[8], rgt[8], out[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) lft[j] = buf[cur][2 * t][j];
+                if (2 * q + 1 < la.width[l - 1]) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) rgt[j] = buf[cur][2 * t + 1][j];
+                    node_hash(lft, rgt, out);
+                } else {
+                    copy8(out, lft);
+                }
+                store_digest(levels + (la.off[l] + q) * 32, out);
+#pragma unroll
+                for (int j = 0; j < 8; j++) buf[cur ^ 1][t][j] = out[j];
+            }
+        }
+        cur ^= 1;
+    }
 }
 
 // ============================================================================
@@ -502,13 +542,14 @@ __global__ void k_copy_nodes(const uint8_t *__restrict__ src, uint64_t n, uint8_
 // intermediate levels in LDS and writing every level to HBM (levels are
 // needed for InclusionProof, htree.go:158).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_reduce(uint8_t *__restrict__ levels, LevelArgs la, int l0,
-                                                int nsteps) {
-    __shared__ uint32_t buf[2][256][9];  // +1 word pad: conflict-free 2t / 2t+1 reads
+template <int T>
+__global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, LevelArgs la, int l0,
+                                              int nsteps) {
+    __shared__ uint32_t buf[2][T][9];  // +1 word pad: conflict-free 2t / 2t+1 reads
     const int t = threadIdx.x;
     const uint64_t blk = blockIdx.x;
     {
-        const uint64_t q = blk * 256 + t;
+        const uint64_t q = blk * T + t;
         if (q < la.width[l0 + 1]) {
             uint32_t lft[8], rgt[8], out[8];
             load_digest(levels + (la.off[l0] + 2 * q) * 32, lft);
@@ -526,7 +567,7 @@ __global__ __launch_bounds__(256) void k_reduce(uint8_t *__restrict__ levels, Le
     int cur = 0;
     for (int s = 2; s <= nsteps; s++) {
         __syncthreads();
-        const int active = 256 >> (s - 1);
+        const int active = T >> (s - 1);
         const int l = l0 + s;
         if (t < active) {
             const uint64_t q = blk * active + t;
@@ -710,7 +751,7 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
             hipLaunchKernelGGL(k_entries_fixed<1>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
                                val_len, keys, key_len, version, n, hvals_out, levels, la);
     }
-    *levels_done = std::min(lpl == 4 ? 2 : lpl == 2 ? 1 : 0, g.nlevels - 1);
+    *levels_done = std::min((lpl == 4 ? 2 : lpl == 2 ? 1 : 0) + 8, g.nlevels - 1);
     return hipGetLastError();
 }
 
@@ -738,14 +779,23 @@ hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *
 
 hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const LevelGeom &g,
                          int from_level) {
+    // Each launch: a workgroup of T threads turns 2T nodes into log2(2T)
+    // levels.  The last (top) launch uses 512 threads = 10 levels, so a
+    // 2^20-leaf tree whose leaf kernel stopped at level 10 needs one launch.
     LevelArgs la = level_args(g);
     int cur = from_level;
     while (cur < g.nlevels - 1) {
-        const int steps = std::min(9, g.nlevels - 1 - cur);
-        const unsigned grid = grid_for(g.width[cur + 1], 256);
+        const int left = g.nlevels - 1 - cur;
         TimerScope ts(tm, "reduce", st);
-        hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);
-        cur += steps;
+        if (left <= 10 && g.width[cur] <= 1024) {
+            hipLaunchKernelGGL(k_reduce<512>, dim3(1), dim3(512), 0, st, levels, la, cur, left);
+            cur += left;
+        } else {
+            const int steps = std::min(9, left);
+            const unsigned grid = grid_for(g.width[cur + 1], 256);
+            hipLaunchKernelGGL(k_reduce<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);
+            cur += steps;
+        }
     }
     return hipGetLastError();
 }
