@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--entries", type=int, default=N_ENTRIES)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="independent builds in flight on separate streams (1 = sequential)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU work of the cpu_baseline sample")
     p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
@@ -113,69 +115,121 @@ def main():
     if a.gpus != world and world != 1:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
     dist = None
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; MH_DIST_BACKEND=gloo rehearses several ranks on
+    # fewer GPUs (device = local rank modulo the visible devices)
+    backend = os.environ.get("MH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend != "gloo" and world > 1 and local >= ndev:
+        raise SystemExit("rank %d has no GPU (%d visible)" % (local, ndev))
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    local = dev.index
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
-    stream = torch.cuda.current_stream(dev)
-    ctx = m.Context(local, stream.cuda_stream)
+    # D builds in flight (--inflight), each on its own HIP stream with its own
+    # level buffers: the latency-bound top of one tree overlaps the leaf
+    # hashing of the next, as concurrent commits do in immudb (up to
+    # MaxConcurrency precommits, embedded/store/options.go:35).  D = 1 is
+    # strictly sequential.
+    D = max(1, a.inflight)
+    streams = [torch.cuda.current_stream(dev)] if D == 1 else \
+        [torch.cuda.Stream(dev) for _ in range(D)]
+    ctxs = [m.Context(local, s.cuda_stream) for s in streams]
+    ctx = ctxs[0]
     L = N.load()
     n = a.entries
     # inputs resident in HBM before the timed region (synthetic, deterministic)
     vals = torch.empty(n * VAL_LEN, dtype=torch.uint8, device=dev)
     keys = torch.empty(n * KEY_LEN, dtype=torch.uint8, device=dev)
-    N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 2 + rank))
-    N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, rank * n))
+    with torch.cuda.stream(streams[0]):
+        N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 2 + rank))
+        N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, rank * n))
+    torch.cuda.synchronize(dev)
     nlv = m.levels_len(n)
-    levels = torch.empty(nlv * 32, dtype=torch.uint8, device=dev)
-    root = torch.empty(32, dtype=torch.uint8, device=dev)
-    if world > 1:
-        top_levels = torch.empty(max(m.levels_len(world), 1) * 32, dtype=torch.uint8, device=dev)
-        groot = torch.empty(32, dtype=torch.uint8, device=dev)
+    levels = [torch.empty(nlv * 32, dtype=torch.uint8, device=dev) for _ in range(D)]
+    root = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(D)]
+    top_levels = [torch.empty(max(m.levels_len(world), 1) * 32, dtype=torch.uint8, device=dev)
+                  for _ in range(D)]
+    groot = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(D)]
 
-    def step():
-        N.check(L.mh_dev_htree_build_entries_fixed(ctx.handle, 1, n, keys.data_ptr(), KEY_LEN,
-                                                   vals.data_ptr(), VAL_LEN, None,
-                                                   levels.data_ptr(), root.data_ptr()))
+    # collectives of all in-flight builds go through ONE stream, in issue
+    # order, so every rank runs its RCCL kernels in the same order
+    comm = torch.cuda.Stream(dev) if (world > 1 and D > 1) else streams[0]
+    comm_ctx = ctx if comm is streams[0] else m.Context(local, comm.cuda_stream)
+
+    def step(k):
+        j = k % D
+        with torch.cuda.stream(streams[j]):
+            N.check(L.mh_dev_htree_build_entries_fixed(ctxs[j].handle, 1, n, keys.data_ptr(),
+                                                       KEY_LEN, vals.data_ptr(), VAL_LEN, None,
+                                                       levels[j].data_ptr(), root[j].data_ptr()))
         if world > 1:
             # 32 B per rank over RCCL, then the top log2(world) levels locally
             # (immustore_amd/sharding.py; exact by SURVEY.md finding 3)
-            g = sharding.allgather_roots(root, world)
-            N.check(L.mh_dev_htree_reduce_nodes(ctx.handle, g.data_ptr(), world,
-                                                top_levels.data_ptr(), groot.data_ptr()))
+            comm.wait_stream(streams[j])
+            with torch.cuda.stream(comm):
+                g = sharding.allgather_roots(root[j], world)
+                N.check(L.mh_dev_htree_reduce_nodes(comm_ctx.handle, g.data_ptr(), world,
+                                                    top_levels[j].data_ptr(), groot[j].data_ptr()))
+            streams[j].wait_stream(comm)
 
-    for _ in range(a.warmup):
-        step()
+    for k in range(a.warmup):
+        step(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ctx.timing_reset()
-    ctx.set_timing(True)
+    for c in ctxs:
+        c.timing_reset()
+        c.set_timing(True)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for k in range(a.steps):
+        step(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    ctx.set_timing(False)
+    for c in ctxs:
+        c.set_timing(False)
     elapsed = t1 - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    k_ms0, k_cnt0 = ctxs[0].timing("entries_fixed")
+    r_ms0 = ctxs[0].timing("reduce")[0]
+    # isolated launches (outside the timed region): one build at a time on
+    # one stream, for the dominant kernel's exclusive duration
+    iso_ms = None
+    if D > 1:
+        ctxs[0].timing_reset()
+        ctxs[0].set_timing(True)
+        for k in range(5):
+            step(0)
+            torch.cuda.synchronize(dev)
+        ctxs[0].set_timing(False)
+        ims, icnt = ctxs[0].timing("entries_fixed")
+        iso_ms = ims / max(icnt, 1)
+    # every build's root must be the same tree root (same input each step)
+    r0 = root[0].cpu()
+    assert all(torch.equal(r0, r.cpu()) for r in root), "in-flight builds disagree"
 
-    k_ms, k_cnt = ctx.timing("entries_fixed")
-    r_ms, r_cnt = ctx.timing("reduce")
+    k_ms = sum(c.timing("entries_fixed")[0] for c in ctxs[1:]) + k_ms0
+    k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
+    r_ms = sum(c.timing("reduce")[0] for c in ctxs[1:]) + r_ms0
     kern_ms = k_ms / max(k_cnt, 1)
     lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
     # levels written by one launch of the dominant kernel: the lanes' groups
     # up to level log2(lpl), then each workgroup's subtree 8 levels higher
-    top = min({1: 0, 2: 1, 4: 2}[lpl] + 8, max(m.levels_len(n) and (n - 1).bit_length(), 0))
+    wgl = int(os.environ.get("MH_WG_LEVELS", "8"))
+    top = min({1: 0, 2: 1, 4: 2}[lpl] + wgl, max(m.levels_len(n) and (n - 1).bit_length(), 0))
     widths = [-(-n // (1 << l)) for l in range(top + 1)]
     nodes_written = sum(widths)
     # algorithmic HBM bytes of one launch of the dominant kernel:
@@ -214,7 +268,8 @@ def main():
                                "levels), %d x %d B entries per GPU, %d B keys" % (n, VAL_LEN, KEY_LEN),
                    "entries_per_gpu": n, "value_len": VAL_LEN, "key_len": KEY_LEN,
                    "parallelism": "subtree shard per GPU + RCCL all-gather of roots"
-                   if world > 1 else "single GPU", "lanes_per_leaf_group": lpl},
+                   if world > 1 else "single GPU", "lanes_per_leaf_group": lpl,
+                   "builds_in_flight": D, "wg_subtree_levels": wgl},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": "k_entries_fixed",
@@ -225,7 +280,14 @@ def main():
                      "sha": {"gcomp_per_s": round(comp_rate / 1e9, 2),
                              "peak_gcomp_per_s": SHA_PEAK_GCOMPS,
                              "frac": round(comp_rate / 1e9 / SHA_PEAK_GCOMPS, 4)},
-                     "reduce_ms_per_step": round(r_ms / max(a.steps, 1), 4)},
+                     "reduce_ms_per_step": round(r_ms / max(a.steps, 1), 4),
+                     "note": "kernel_ms: mean launch duration over the timed region (builds "
+                             "in flight overlap, so it includes sharing the GPU)",
+                     "isolated_kernel_ms": round(iso_ms, 4) if iso_ms else None,
+                     "isolated_frac": round(alg_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                     if iso_ms else None,
+                     "isolated_sha_frac": round(comp_rate * kern_ms / iso_ms / 1e9 /
+                                                SHA_PEAK_GCOMPS, 4) if iso_ms else None},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
@@ -233,7 +295,10 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    if comm_ctx is not ctx:
+        comm_ctx.close()
+    for c in ctxs:
+        c.close()
     if dist:
         dist.destroy_process_group()
 

@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libimmustore_merkle.so")
+LIB_PATH = os.environ.get("MH_LIB_PATH") or os.path.join(_HERE, "libimmustore_merkle.so")
 
 MH_OK = 0
 MH_ERR_MAX_WIDTH_EXCEEDED = 1

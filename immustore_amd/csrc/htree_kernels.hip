@@ -265,7 +265,7 @@ template <int LPL>
 __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     const uint8_t *__restrict__ vals, uint32_t val_len, const uint8_t *__restrict__ keys,
     uint32_t key_len, int version, uint64_t n, uint8_t *__restrict__ hvals_out,
-    uint8_t *__restrict__ levels, LaneLevels la) {
+    uint8_t *__restrict__ levels, LaneLevels la, int wg_levels) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -315,22 +315,39 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     for (;;) {
         const uint64_t idx = first + i;
         bool on = i < c;
-        uint32_t w[16];
         if (op == OP_VALUE) {
-            const uint32_t u = b >> 1;
-            const bool two = u < nsteps2;
-            const int h = two ? (int)(b & 1) : 0;
-            lds_block(lds, lane, two, h, w);
-            if (!two || h == 1) {
-                // this unit is fully in registers: start the next DMA
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (u + 1 < units)
-                    dma_issue(vals, val_len, wave_slot0, LPL, i, n, (u + 1) * 128,
-                              (u + 1) < nsteps2, lds, lane);
-                else if (i + 1 < LPL)
-                    dma_issue(vals, val_len, wave_slot0, LPL, i + 1, n, 0, nsteps2 > 0, lds, lane);
+            // tight loop over the value's full blocks: its own compress site,
+            // no state-machine dispatch per block
+#pragma unroll 1
+            for (; b < nfull; b++) {
+                const uint32_t u = b >> 1;
+                const bool two = u < nsteps2;
+                const int h = two ? (int)(b & 1) : 0;
+                uint32_t w[16];
+                lds_block(lds, lane, two, h, w);
+                if (!two || h == 1) {
+                    // this unit is fully in registers: start the next DMA
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (u + 1 < units)
+                        dma_issue(vals, val_len, wave_slot0, LPL, i, n, (u + 1) * 128,
+                                  (u + 1) < nsteps2, lds, lane);
+                    else if (i + 1 < LPL)
+                        dma_issue(vals, val_len, wave_slot0, LPL, i + 1, n, 0, nsteps2 > 0, lds,
+                                  lane);
+                }
+                if (on) compress(s, w);
             }
-        } else if (op == OP_TAIL) {
+            b = 0;
+            if (rem) {
+                op = OP_TAIL;
+            } else {
+                if (on) compress_kw(s, kw_lds);
+                op = OP_DIGEST;
+            }
+            continue;
+        }
+        uint32_t w[16];
+        if (op == OP_TAIL) {
             // rem data bytes (16/32/48, dword aligned) + 0x80 + 64-bit length
             const uint32_t rw = rem >> 2;
             const uint32_t *tp =
@@ -401,16 +418,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
 
         // ---------------------------------------------------------- transition
         bool entry_done = false;
-        if (op == OP_VALUE) {
-            if (++b < nfull) continue;
-            b = 0;
-            if (rem) {
-                op = OP_TAIL;
-                continue;
-            }
-            if (i < c) compress_kw(s, kw_lds);
-            op = OP_DIGEST;
-        } else if (op == OP_TAIL) {
+        if (op == OP_TAIL) {
             op = OP_DIGEST;
         } else if (op == OP_DIGEST) {
             op = OP_LEAF;
@@ -472,6 +480,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     // The workgroup's 256 lane-group nodes (level L0 = log2 LPL) are reduced
     // in LDS to up to 8 more levels (htree.go:85-110), writing every level.
     constexpr int L0 = LPL == 4 ? 2 : (LPL == 2 ? 1 : 0);
+    if (wg_levels == 0) return;  // launch-uniform
     const int t = threadIdx.x;
     uint32_t(*buf)[kFixedThreads][9] = reinterpret_cast<uint32_t(*)[kFixedThreads][9]>(smem);
     __syncthreads();  // every wave is done with its staging area
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     for (int j = 0; j < 8; j++) buf[0][t][j] = LPL == 1 ? s.h[j] : A[j];
     int cur = 0;
 #pragma unroll 1
-    for (int st = 1; st <= 8; st++) {
+    for (int st = 1; st <= wg_levels; st++) {
         __syncthreads();
         const int active = kFixedThreads >> st;
         const int l = L0 + st;
@@ -739,19 +748,24 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
     const uint64_t lanes = (n + lpl - 1) / lpl;
     const unsigned grid = grid_for(lanes, kFixedThreads);
     const size_t lds = (kFixedThreads / 64) * kWaveLds + 256;
+    // levels each leaf workgroup reduces in LDS after its lanes (0..8); 0
+    // leaves the whole upper tree to k_reduce, which a concurrent build on
+    // another stream can overlap (MH_WG_LEVELS overrides).
+    int wgl = 8;
+    if (const char *e = getenv("MH_WG_LEVELS")) wgl = std::max(0, std::min(8, atoi(e)));
     {
         TimerScope ts(tm, "entries_fixed", st);
         if (lpl == 4)
             hipLaunchKernelGGL(k_entries_fixed<4>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
         else if (lpl == 2)
             hipLaunchKernelGGL(k_entries_fixed<2>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
         else
             hipLaunchKernelGGL(k_entries_fixed<1>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
     }
-    *levels_done = std::min((lpl == 4 ? 2 : lpl == 2 ? 1 : 0) + 8, g.nlevels - 1);
+    *levels_done = std::min((lpl == 4 ? 2 : lpl == 2 ? 1 : 0) + wgl, g.nlevels - 1);
     return hipGetLastError();
 }
 

@@ -33,6 +33,12 @@ def allgather_roots(root, world: int):
     rank's device: RCCL for cuda tensors, gloo for cpu tensors)."""
     import torch
     import torch.distributed as dist
+    if root.is_cuda and dist.get_backend() == "gloo":
+        # rehearsal of the multi-rank path with gloo (several ranks sharing
+        # one GPU): stage the 32 bytes through the host
+        out = torch.empty(world * 32, dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, root.contiguous().view(32).cpu())
+        return out.to(root.device)
     out = torch.empty(world * 32, dtype=torch.uint8, device=root.device)
     dist.all_gather_into_tensor(out, root.contiguous().view(32))
     return out
