@@ -17,6 +17,7 @@
 // which reproduces the reference's dLog byte stream exactly (tests compare it
 // with Go's tree/00000000.sha fixtures and with the oracle).
 #include <algorithm>
+#include <cstdlib>
 
 #include "digest_io.hpp"
 #include "mh_internal.hpp"
@@ -112,14 +113,177 @@ __global__ __launch_bounds__(256) void k_aht_spine(uint8_t *__restrict__ dlog, u
     if (roots_out) store_digest(roots_out + i * 32, h);
 }
 
+// ---------------------------------------------------------------------------
+// Table-driven variants (sha256_cdna.hpp node_hash_tab): every workgroup
+// builds the 256 node-tail schedules in LDS once and then runs a grid-stride
+// loop, so the table cost is amortised over many node hashes.
+
+__global__ __launch_bounds__(512) void k_aht_perfect_t(uint8_t *__restrict__ dlog, int l,
+                                                       uint64_t j0, uint64_t cnt) {
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    const uint64_t half = 1ull << (l - 1);
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = (j0 + t + 1) << l;
+        uint32_t a[8], b[8], o[8];
+        load_digest(dlog + (dev_nodes_until(e - half) + (uint64_t)(l - 1)) * 32, a);
+        const uint64_t ue = dev_nodes_until(e);
+        load_digest(dlog + (ue + (uint64_t)(l - 1)) * 32, b);
+        node_hash_tab(a, b, o, tab);
+        store_digest(dlog + (ue + (uint64_t)l) * 32, o);
+    }
+}
+
+// Spine with balanced lanes.  The chain of n has popcount(n-1) - tz(n) steps:
+// the low 7 bits of n-1 (r) contribute len(r) = popcount(r) - trailing_ones(r)
+// steps (0..6, 321 in total over r = 0..127), the higher bits B = (n-1) >> 7
+// are shared by the 128 n of an aligned block and give popcount(B) steps each.
+// One wave takes one aligned block; lane L runs the chains of TWO n of it,
+// r = pr.ra[L] then r = pr.rb[L], paired so that len(ra) + len(rb) <= 6
+// (longest with shortest).  All lanes of a wave then do 5..6 + 2 popcount(B)
+// hash steps, against up to 6 + popcount(B) with 1 chain per lane, where the
+// low-bit part idles most of the wave (~40 % of the lanes' time at 10^7).
+// The B-part reads (node(k, l), l >= 7) are wave-uniform broadcast loads.
+struct SpinePairs {
+    uint8_t ra[64], rb[64];
+};
+
+// Blocks are handed out through a work queue (one atomic per wave and block):
+// a block's work varies with popcount(B), and a static grid-stride split left
+// the longest wave ~15 % behind the average.  amdgpu_waves_per_eu(6) caps the
+// kernel at 80 VGPRs so three 512-thread workgroups (the LDS limit with the
+// 53 KB table) fit per CU, 6 waves per SIMD.
+template <bool PREFETCH>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k_aht_spine_pairs(uint8_t *__restrict__ dlog,
+                                                            uint64_t n0, uint64_t m,
+                                                            uint8_t *__restrict__ roots_out,
+                                                            SpinePairs pr, uint64_t blk0,
+                                                            uint64_t nblk,
+                                                            uint32_t *__restrict__ work_ctr) {
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    const int lane = threadIdx.x & 63;
+    const uint64_t nlast = n0 + m;
+    const uint32_t ra = pr.ra[lane], rb = pr.rb[lane];
+    for (;;) {
+        uint32_t got = 0;
+        if (lane == 0) got = atomicAdd(work_ctr, 1u);
+        const uint64_t bi = __builtin_amdgcn_readfirstlane(got);
+        if (bi >= nblk) break;
+        const uint64_t base = (blk0 + bi) << 7;  // n - 1 of r = 0 (wave-uniform)
+        // S(base + x) = S(base) + x * popcount(B) + S(x) for x <= 128: the
+        // per-lane index math only walks the 7 low bits
+        const uint64_t sb = popsum_below(base);
+        const uint32_t pcb = (uint32_t)__builtin_popcountll(base);
+        const uint64_t nA = base + ra + 1, nB = base + rb + 1;
+        const bool vA = nA > n0 && nA <= nlast, vB = nB > n0 && nB <= nlast;
+        bool second = !vA, done = !(vA || vB);
+        uint32_t r = vA ? ra : rb;
+        uint64_t n = 0, un = 0, rest = 0, sk = 0;
+        int t = 0;
+        uint32_t h[8], left[8];
+#define MH_SPINE_SETUP()                                                                          \
+    do {                                                                                          \
+        n = base + r + 1;                                                                         \
+        const int t0_ = __builtin_ctzll(n);                                                       \
+        un = (n - 1) + sb + (uint64_t)(r + 1) * pcb + popsum_below(r + 1) -                       \
+             (pcb + (uint32_t)__builtin_popcount(r));                                             \
+        load_digest(dlog + (un + (uint64_t)t0_) * 32, h);                                         \
+        if (r != 127) {                                                                           \
+            const uint32_t rr_ = (r >> (t0_ + 1)) << (t0_ + 1);                                   \
+            rest = base + rr_;                                                                    \
+            sk = sb + (uint64_t)rr_ * pcb + popsum_below(rr_);                                    \
+        } else {                                                                                  \
+            rest = t0_ + 1 < 64 ? ((n - 1) >> (t0_ + 1)) << (t0_ + 1) : 0;                        \
+            sk = popsum_below(rest);                                                              \
+        }                                                                                         \
+        t = t0_;                                                                                  \
+        if (PREFETCH && rest)                                                                     \
+            load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)__builtin_ctzll(rest)) * 32,   \
+                        left);                                                                    \
+    } while (0)
+        if (!done) MH_SPINE_SETUP();
+        for (;;) {
+            while (!done && rest == 0) {
+                if (roots_out) store_digest(roots_out + (n - n0 - 1) * 32, h);
+                if (!second && vB) {
+                    second = true;
+                    r = rb;
+                    MH_SPINE_SETUP();
+                } else {
+                    done = true;
+                }
+            }
+            if (done) break;
+            // drop the lowest set bit l of rest (rank popcount(rest) from the
+            // top) and prefetch the next step's left node before hashing
+            const int l = __builtin_ctzll(rest);
+            if (!PREFETCH) load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)l) * 32, left);
+            sk -= (l ? ((uint64_t)l << (l - 1)) : 0) +
+                  ((uint64_t)(__builtin_popcountll(rest) - 1) << l);
+            rest &= rest - 1;
+            uint32_t nxt[8];
+            if (PREFETCH && rest)
+                load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)__builtin_ctzll(rest)) * 32,
+                            nxt);
+            node_hash_tab(left, h, h, tab);
+            t++;
+            store_digest(dlog + (un + (uint64_t)t) * 32, h);
+            if (PREFETCH) copy8(left, nxt);
+        }
+#undef MH_SPINE_SETUP
+    }
+}
+
+static SpinePairs make_spine_pairs() {
+    int len[128], ord[128];
+    for (int r = 0; r < 128; r++) {
+        int to = 0;
+        while ((r >> to) & 1) to++;
+        len[r] = __builtin_popcount(r) - to;
+        ord[r] = r;
+    }
+    std::stable_sort(ord, ord + 128, [&](int x, int y) { return len[x] < len[y]; });
+    SpinePairs p;
+    for (int i = 0; i < 64; i++) {
+        p.ra[i] = (uint8_t)ord[127 - i];  // long chain first, short one second
+        p.rb[i] = (uint8_t)ord[i];
+    }
+    return p;
+}
+
+// Resident workgroups for a grid-stride kernel with the node table in LDS.
+static unsigned resident_grid(const void *kern, int block, uint64_t work_items) {
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, kNodeTabBytes) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const uint64_t need = (work_items + block - 1) / block;
+    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu;
+    return (unsigned)std::max<uint64_t>(1, std::min(need, cap));
+}
+
+static bool use_node_table() {
+    static const bool on = [] {
+        const char *e = getenv("MH_NODE_TABLE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static inline unsigned grid_for(uint64_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }
 
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out) {
+                                uint8_t *roots_out, uint32_t *work_ctr) {
     if (!m) return hipSuccess;
+    const bool tab = use_node_table();
     if (tm) tm->begin("aht_leaves", st);
     hipLaunchKernelGGL(k_aht_leaves, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, payloads,
                        m, plen);
@@ -130,12 +294,40 @@ hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64
         const uint64_t j0 = n0 >> l;             // first j with (j+1)*2^l > n0
         const uint64_t j1 = n_end >> l;          // one past the last j with (j+1)*2^l <= n_end
         if (j1 <= j0) continue;
-        hipLaunchKernelGGL(k_aht_perfect, dim3(grid_for(j1 - j0, 256)), dim3(256), 0, st, dlog, l,
-                           j0, j1 - j0);
+        if (tab)
+            hipLaunchKernelGGL(k_aht_perfect_t,
+                               dim3(resident_grid((const void *)k_aht_perfect_t, 512, j1 - j0)),
+                               dim3(512), kNodeTabBytes, st, dlog, l, j0, j1 - j0);
+        else
+            hipLaunchKernelGGL(k_aht_perfect, dim3(grid_for(j1 - j0, 256)), dim3(256), 0, st, dlog,
+                               l, j0, j1 - j0);
     }
     if (tm) tm->end(st);
     if (tm) tm->begin("aht_spine", st);
-    hipLaunchKernelGGL(k_aht_spine, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, m, roots_out);
+    if (tab) {
+        static const SpinePairs pairs = make_spine_pairs();
+        if (hipError_t e = hipMemsetAsync(work_ctr, 0, sizeof(uint32_t), st)) return e;
+        const uint64_t blk0 = n0 >> 7, nblk = ((n_end - 1) >> 7) - blk0 + 1;
+        static const bool pf = [] {
+            const char *e = getenv("MH_SPINE_PREFETCH");  // A/B knob, default off
+            return e && e[0] == '1';
+        }();
+        if (pf)
+            hipLaunchKernelGGL(
+                k_aht_spine_pairs<true>,
+                dim3(resident_grid((const void *)k_aht_spine_pairs<true>, 512, nblk * 64)),
+                dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
+                work_ctr);
+        else
+            hipLaunchKernelGGL(
+                k_aht_spine_pairs<false>,
+                dim3(resident_grid((const void *)k_aht_spine_pairs<false>, 512, nblk * 64)),
+                dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
+                work_ctr);
+    } else {
+        hipLaunchKernelGGL(k_aht_spine, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, m,
+                           roots_out);
+    }
     if (tm) tm->end(st);
     return hipGetLastError();
 }

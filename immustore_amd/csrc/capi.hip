@@ -133,7 +133,7 @@ struct mh_ctx {
     bool own_stream = false;
     EventTimer timer;
     std::mutex mu;  // guards scratch for mh_dev_* calls
-    DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs;
+    DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs, s_ctr;
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
 };
 
@@ -153,7 +153,7 @@ struct mh_ahtree {
     mh_ctx *ctx = nullptr;
     hipStream_t stream = nullptr;
     uint64_t size = 0;
-    DevBuf dlog, in, roots, idx, out;
+    DevBuf dlog, in, roots, idx, out, ctr;
 };
 
 // ------------------------------------------------------------------ misc
@@ -806,7 +806,13 @@ extern "C" int mh_dev_ahtree_append_batch(mh_ctx *c, uint8_t *dlog, uint64_t n0,
     if (!c || (m && (!dlog || (!payloads && plen)))) return MH_ERR_ILLEGAL_ARGUMENTS;
     if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
     if (!m) return MH_OK;
-    MH_HIP(launch_ahtree_append(c->stream, c->tm(), dlog, n0, payloads, m, plen, roots_out));
+    hipSetDevice(c->device);
+    // the work-queue counter is ctx scratch: reset + launch are enqueued
+    // under the lock so concurrent callers on this ctx never share one
+    std::lock_guard<std::mutex> lk(c->mu);
+    MH_HIP(c->s_ctr.ensure(256));
+    MH_HIP(launch_ahtree_append(c->stream, c->tm(), dlog, n0, payloads, m, plen, roots_out,
+                                c->s_ctr.as<uint32_t>()));
     return MH_OK;
 }
 
@@ -868,8 +874,9 @@ extern "C" int mh_ahtree_append_batch(mh_ahtree *t, const uint8_t *payloads, uin
         MH_HIP(t->roots.ensure(m * 32));
         rd = t->roots.as<uint8_t>();
     }
+    MH_HIP(t->ctr.ensure(256));
     MH_HIP(launch_ahtree_append(t->stream, t->ctx->tm(), t->dlog.as<uint8_t>(), t->size,
-                                t->in.as<uint8_t>(), m, plen, rd));
+                                t->in.as<uint8_t>(), m, plen, rd, t->ctr.as<uint32_t>()));
     if (roots_out) MH_HIP(hipMemcpyAsync(roots_out, rd, m * 32, hipMemcpyDeviceToHost, t->stream));
     MH_HIP(hipStreamSynchronize(t->stream));
     t->size += m;

@@ -93,9 +93,11 @@ hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np
                                 uint8_t *ok, uint8_t *eval_out);
 
 // ---- ahtree batch append (embedded/ahtree/ahtree.go:246-373)
+// work_ctr: 4 bytes of device memory private to this launch's stream order
+// (the spine kernel's work queue; reset on `st` before the launch).
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out);
+                                uint8_t *roots_out, uint32_t *work_ctr);
 
 // host-side index math shared with the C API
 uint64_t ahtree_nodes_upto(uint64_t n);

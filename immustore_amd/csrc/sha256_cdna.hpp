@@ -103,8 +103,6 @@ struct State {
 
 // Compress one block whose 16 message words are in w[] (values, may be
 // compile-time constants after inlining: the compiler folds the schedule).
-// Compress one block whose 16 message words are in w[] (values, may be
-// compile-time constants after inlining: the compiler folds the schedule).
 __device__ __forceinline__ void compress(State &s, const uint32_t win[16]) {
     uint32_t w[16];
 #pragma unroll
@@ -189,6 +187,115 @@ __device__ __forceinline__ void node_hash(const uint32_t l[8], const uint32_t r[
     for (int j = 1; j < 15; j++) w[j] = 0;
     w[15] = 65u * 8u;
     compress(s, w);
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[j] = s.h[j];
+}
+
+// ---------------------------------------------------------------------------
+// Node hashes against a per-workgroup schedule table.
+//
+// The second block of a node hash (65-byte message) is
+//   W0 = r[31] << 24 | 0x80 << 16,  W1..W14 = 0,  W15 = 520,
+// so its whole message schedule is a function of ONE byte, r[31].  A
+// workgroup that hashes many nodes builds the 256 possible schedules once in
+// LDS (K[t] + W[t] for t = 16..63; rounds 0..15 fold to immediates) and the
+// block then runs like compress_kw: no schedule expansion, 12 ds_read_b128
+// per block instead of ~490 VALU ops (about 17 % of a node hash).  Rows are
+// padded to 52 words (13 x 16 B) so rows of different lanes spread over the
+// LDS bank groups.
+constexpr int kNodeTabStride = 52;
+constexpr int kNodeTabWords = 256 * kNodeTabStride;
+constexpr int kNodeTabBytes = kNodeTabWords * 4;
+
+// The table is a compile-time constant (constexpr schedule expansion); every
+// workgroup copies it from global memory (L2 resident after the first
+// touch) into LDS.
+struct alignas(16) NodeTab {
+    uint32_t w[kNodeTabWords];
+};
+
+constexpr NodeTab make_node_tab() {
+    constexpr uint32_t K[64] = {
+        0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+        0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+        0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+        0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+        0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+        0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+        0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+        0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+        0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+        0xc67178f2u};
+    NodeTab t{};
+    for (uint32_t v = 0; v < 256; v++) {
+        uint32_t w[64] = {};
+        w[0] = (v << 24) | 0x00800000u;
+        w[15] = 65u * 8u;
+        for (int i = 16; i < 64; i++) {
+            const uint32_t x = w[i - 15], y = w[i - 2];
+            const uint32_t s0 = ((x >> 7) | (x << 25)) ^ ((x >> 18) | (x << 14)) ^ (x >> 3);
+            const uint32_t s1 = ((y >> 17) | (y << 15)) ^ ((y >> 19) | (y << 13)) ^ (y >> 10);
+            w[i] = s1 + w[i - 7] + s0 + w[i - 16];
+            t.w[v * kNodeTabStride + (i - 16)] = w[i] + K[i];
+        }
+    }
+    return t;
+}
+
+__device__ static const NodeTab g_node_tab = make_node_tab();
+
+__device__ __forceinline__ void node_tab_init(uint32_t *tab) {
+    const uint4 *src = (const uint4 *)g_node_tab.w;
+    uint4 *dst = (uint4 *)tab;
+    for (int i = threadIdx.x; i < kNodeTabWords / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+#define MH_ROUNDS8(k0, k1, k2, k3, k4, k5, k6, k7)                                                \
+    do {                                                                                          \
+        MH_ROUND(a, b, c, d, e, f, g, h, k0);                                                     \
+        MH_ROUND(h, a, b, c, d, e, f, g, k1);                                                     \
+        MH_ROUND(g, h, a, b, c, d, e, f, k2);                                                     \
+        MH_ROUND(f, g, h, a, b, c, d, e, k3);                                                     \
+        MH_ROUND(e, f, g, h, a, b, c, d, k4);                                                     \
+        MH_ROUND(d, e, f, g, h, a, b, c, k5);                                                     \
+        MH_ROUND(c, d, e, f, g, h, a, b, k6);                                                     \
+        MH_ROUND(b, c, d, e, f, g, h, a, k7);                                                     \
+    } while (0)
+
+// Second block of SHA256(0x01 || l || r) given r's last word.
+__device__ __forceinline__ void compress_node_tail(State &s, uint32_t r7,
+                                                   const uint32_t *__restrict__ tab) {
+    const uint4 *row = (const uint4 *)(tab + (r7 & 0xffu) * kNodeTabStride);
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6],
+             h = s.h[7];
+    MH_ROUNDS8(MH_K(0) + ((r7 << 24) | 0x00800000u), MH_K(1), MH_K(2), MH_K(3), MH_K(4), MH_K(5),
+               MH_K(6), MH_K(7));
+    MH_ROUNDS8(MH_K(8), MH_K(9), MH_K(10), MH_K(11), MH_K(12), MH_K(13), MH_K(14),
+               MH_K(15) + 65u * 8u);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint4 x = row[2 * q], y = row[2 * q + 1];
+        MH_ROUNDS8(x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w);
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+// node = SHA256(0x01 || l || r) with the second block from the LDS table.
+__device__ __forceinline__ void node_hash_tab(const uint32_t l[8], const uint32_t r[8],
+                                              uint32_t out[8], const uint32_t *__restrict__ tab) {
+    uint32_t w[16];
+    w[0] = 0x01000000u | (l[0] >> 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[j] = __builtin_amdgcn_alignbit(l[j - 1], l[j], 8);
+    w[8] = __builtin_amdgcn_alignbit(l[7], r[0], 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[8 + j] = __builtin_amdgcn_alignbit(r[j - 1], r[j], 8);
+    State s;
+    s.init();
+    compress(s, w);
+    compress_node_tail(s, r[7], tab);
 #pragma unroll
     for (int j = 0; j < 8; j++) out[j] = s.h[j];
 }

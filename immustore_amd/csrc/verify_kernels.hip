@@ -6,6 +6,8 @@
 //   ahtree.VerifyLastInclusion / EvalLastInclusion   ahtree/verification.go:111-137
 // The left/right choice of every step is a per-lane select of the operands
 // of ONE node_hash call, so lanes of a wave never diverge on it.
+#include <algorithm>
+
 #include "digest_io.hpp"
 #include "mh_internal.hpp"
 
@@ -18,15 +20,19 @@ __device__ __forceinline__ bool eq8(const uint32_t a[8], const uint32_t b[8]) {
     return x == 0;
 }
 
-__global__ __launch_bounds__(256) void k_htree_verify(uint64_t np, const uint64_t *__restrict__ leaf,
+// Both kernels run grid-stride over the proofs with 512-thread workgroups that
+// first build the node-tail schedule table in LDS (sha256_cdna.hpp).
+__global__ __launch_bounds__(512) void k_htree_verify(uint64_t np, const uint64_t *__restrict__ leaf,
                                                       const uint64_t *__restrict__ width,
                                                       const uint64_t *__restrict__ term_off,
                                                       const uint8_t *__restrict__ terms,
                                                       const uint8_t *__restrict__ digests,
                                                       const uint8_t *__restrict__ roots,
                                                       uint8_t *__restrict__ ok) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= np) return;
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
+         p += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t d[8], calc[8], root[8];
     load_digest(digests + p * 32, d);
     leaf_hash(d, calc);
@@ -41,15 +47,21 @@ __global__ __launch_bounds__(256) void k_htree_verify(uint64_t np, const uint64_
             l[j] = calc_left ? calc[j] : term[j];
             rr[j] = calc_left ? term[j] : calc[j];
         }
-        node_hash(l, rr, calc);
+        node_hash_tab(l, rr, calc, tab);
         i >>= 1;
         r >>= 1;
     }
     load_digest(roots + p * 32, root);
     ok[p] = (i == r) && eq8(calc, root);
+    }
 }
 
-__global__ __launch_bounds__(256) void k_ahtree_verify(int kind, uint64_t np,
+// One node hash per loop iteration for all three kinds (a single inlined
+// compression site keeps the kernel at full occupancy).  A consistency step
+// over term h is up to two hashes: "A" (ci = H(h, ci), only when the first
+// tree's path turns here) and "B" (cj = H(h, cj) or H(cj, h)); `phase`
+// walks them in order.
+__global__ __launch_bounds__(512) void k_ahtree_verify(int kind, uint64_t np,
                                                        const uint64_t *__restrict__ vi,
                                                        const uint64_t *__restrict__ vj,
                                                        const uint64_t *__restrict__ term_off,
@@ -58,102 +70,132 @@ __global__ __launch_bounds__(256) void k_ahtree_verify(int kind, uint64_t np,
                                                        const uint8_t *__restrict__ vb,
                                                        uint8_t *__restrict__ ok,
                                                        uint8_t *__restrict__ eval_out) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= np) return;
-    const uint64_t i = vi[p], j = vj[p];
-    const uint64_t t0 = term_off[p], t1 = term_off[p + 1], len = t1 - t0;
-    uint32_t a[8], b[8];
-    load_digest(va + p * 32, a);
-    load_digest(vb + p * 32, b);
-    bool res = false;
-    if (kind == MH_AHT_INCLUSION) {
-        // verification.go:21-56
-        uint32_t c[8];
-        copy8(c, a);
-        if (!(i > j || i == 0 || (i < j && len == 0))) {
-            uint64_t i1 = i - 1, j1 = j - 1;
-            for (uint64_t t = t0; t < t1; t++) {
-                uint32_t h[8], l[8], r[8];
-                load_digest(terms + t * 32, h);
-                const bool c_left = (i1 % 2 == 0) && (i1 != j1);
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    l[k] = c_left ? c[k] : h[k];
-                    r[k] = c_left ? h[k] : c[k];
-                }
-                node_hash(l, r, c);
-                i1 >>= 1;
-                j1 >>= 1;
-            }
-            res = eq8(c, b);
-        }
-        if (eval_out) store_digest(eval_out + p * 32, c);
-    } else if (kind == MH_AHT_LAST_INCLUSION) {
-        // verification.go:111-137 (every term is a left sibling)
-        uint32_t c[8];
-        copy8(c, a);
-        for (uint64_t t = t0; t < t1; t++) {
-            uint32_t h[8];
-            load_digest(terms + t * 32, h);
-            node_hash(h, c, c);
-        }
-        res = (i != 0) && eq8(c, b);
-        if (eval_out) store_digest(eval_out + p * 32, c);
-    } else {
-        // verification.go:58-109
-        uint32_t ci[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cj[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (i > j || i == 0 || (i < j && len == 0)) {
-            res = false;
-        } else if (i == j && len == 0) {
-            res = eq8(a, b);
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    const bool cons = kind == MH_AHT_CONSISTENCY;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = vi[p], j = vj[p];
+        const uint64_t t0 = term_off[p], t1 = term_off[p + 1], len = t1 - t0;
+        uint32_t c[8], cj[8];
+        // verification.go:22-24 / :59-61: argument checks shared by inclusion
+        // and consistency; last inclusion only needs i != 0 (:112-114)
+        const bool bad = i > j || i == 0 || (i < j && len == 0);
+        uint64_t x = i - 1, y = j - 1;  // i1/j1 (inclusion) or fn/sn (consistency)
+        uint64_t t = t0;
+        bool run;
+        if (kind == MH_AHT_INCLUSION) {
+            load_digest(va + p * 32, c);
+            run = !bad;
+        } else if (kind == MH_AHT_LAST_INCLUSION) {
+            load_digest(va + p * 32, c);
+            run = true;
         } else {
-            uint64_t fn = i - 1, sn = j - 1;
-            while (fn % 2 == 1) {
-                fn >>= 1;
-                sn >>= 1;
-            }
-            load_digest(terms + t0 * 32, ci);
-            copy8(cj, ci);
-            for (uint64_t t = t0 + 1; t < t1; t++) {
-                uint32_t h[8], l[8], r[8];
-                load_digest(terms + t * 32, h);
-                const bool both = (fn % 2 == 1) || (fn == sn);
-                if (both) node_hash(h, ci, ci);
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    l[k] = both ? h[k] : cj[k];
-                    r[k] = both ? cj[k] : h[k];
+            for (int k = 0; k < 8; k++) c[k] = cj[k] = 0;
+            run = !bad && !(i == j && len == 0);
+            if (run) {
+                while (x % 2 == 1) {  // verification.go:71-74
+                    x >>= 1;
+                    y >>= 1;
                 }
-                node_hash(l, r, cj);
-                if (both) {
-                    while (fn % 2 == 0 && fn != 0) {
-                        fn >>= 1;
-                        sn >>= 1;
-                    }
-                }
-                fn >>= 1;
-                sn >>= 1;
+                load_digest(terms + t0 * 32, c);  // ci = cj = proof[0]
+                copy8(cj, c);
+                t = t0 + 1;
             }
-            res = eq8(a, ci) && eq8(b, cj);
         }
+        int phase = 0;
+        while (run && t < t1) {
+            uint32_t h[8], L[8], R[8], o[8];
+            load_digest(terms + t * 32, h);
+            bool h_left, to_c;
+            const bool both = (x % 2 == 1) || (x == y);
+            if (!cons) {
+                // inclusion: calc is the left operand iff i1 even and i1 != j1
+                // (verification.go:37-45); last inclusion: always H(h, calc)
+                h_left = kind == MH_AHT_LAST_INCLUSION || !((x % 2 == 0) && (x != y));
+                to_c = true;
+            } else {
+                if (phase == 0 && !both) phase = 1;
+                to_c = phase == 0;  // A: ci = H(h, ci)
+                h_left = to_c || both;  // B: H(h, cj) if both else H(cj, h)
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t cur = to_c ? c[k] : cj[k];
+                L[k] = h_left ? h[k] : cur;
+                R[k] = h_left ? cur : h[k];
+            }
+            node_hash_tab(L, R, o, tab);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                c[k] = to_c ? o[k] : c[k];
+                cj[k] = to_c ? cj[k] : o[k];
+            }
+            if (cons && phase == 0) {
+                phase = 1;  // same term, hash B next
+                continue;
+            }
+            if (cons && both) {  // verification.go:95-100
+                while (x % 2 == 0 && x != 0) {
+                    x >>= 1;
+                    y >>= 1;
+                }
+            }
+            x >>= 1;
+            y >>= 1;
+            t++;
+            phase = 0;
+        }
+        uint32_t a[8], b[8];
+        load_digest(va + p * 32, a);
+        load_digest(vb + p * 32, b);
+        bool res;
+        if (kind == MH_AHT_INCLUSION)
+            res = !bad && eq8(c, b);
+        else if (kind == MH_AHT_LAST_INCLUSION)
+            res = i != 0 && eq8(c, b);
+        else if (bad)
+            res = false;
+        else if (i == j && len == 0)
+            res = eq8(a, b);  // verification.go:63-65
+        else
+            res = eq8(a, c) && eq8(b, cj);
         if (eval_out) {
-            store_digest(eval_out + p * 64, ci);
-            store_digest(eval_out + p * 64 + 32, cj);
+            if (cons) {
+                store_digest(eval_out + p * 64, c);
+                store_digest(eval_out + p * 64 + 32, cj);
+            } else {
+                store_digest(eval_out + p * 32, c);
+            }
         }
+        ok[p] = res ? 1 : 0;
     }
-    ok[p] = res ? 1 : 0;
 }
 
-static inline unsigned grid_for(uint64_t threads, unsigned block) {
-    return (unsigned)((threads + block - 1) / block);
+static unsigned resident_grid(const void *kern, int block, uint64_t work_items) {
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, kNodeTabBytes) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const uint64_t need = (work_items + block - 1) / block;
+    // a few resident waves of workgroups: the table build is amortised, the
+    // tail of uneven proof lengths still balances
+    const uint64_t cap = (uint64_t)cus * (uint64_t)per_cu * 4;
+    return (unsigned)std::max<uint64_t>(1, std::min(need, cap));
 }
 
 hipError_t launch_htree_verify(hipStream_t st, Timer *tm, uint64_t np, const uint64_t *leaf,
                                const uint64_t *width, const uint64_t *term_off,
                                const uint8_t *terms, const uint8_t *digests, const uint8_t *roots,
                                uint8_t *ok) {
+    if (!np) return hipSuccess;
     if (tm) tm->begin("htree_verify", st);
-    hipLaunchKernelGGL(k_htree_verify, dim3(grid_for(np, 256)), dim3(256), 0, st, np, leaf, width,
+    hipLaunchKernelGGL(k_htree_verify, dim3(resident_grid((const void *)k_htree_verify, 512, np)),
+                       dim3(512), kNodeTabBytes, st, np, leaf, width,
                        term_off, terms, digests, roots, ok);
     if (tm) tm->end(st);
     return hipGetLastError();
@@ -163,8 +205,10 @@ hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np
                                 const uint64_t *i, const uint64_t *j, const uint64_t *term_off,
                                 const uint8_t *terms, const uint8_t *a, const uint8_t *b,
                                 uint8_t *ok, uint8_t *eval_out) {
+    if (!np) return hipSuccess;
     if (tm) tm->begin("ahtree_verify", st);
-    hipLaunchKernelGGL(k_ahtree_verify, dim3(grid_for(np, 256)), dim3(256), 0, st, kind, np, i, j,
+    hipLaunchKernelGGL(k_ahtree_verify, dim3(resident_grid((const void *)k_ahtree_verify, 512, np)),
+                       dim3(512), kNodeTabBytes, st, kind, np, i, j,
                        term_off, terms, a, b, ok, eval_out);
     if (tm) tm->end(st);
     return hipGetLastError();
