@@ -15,5 +15,8 @@ from .merkle import (Context, default_context, device_count, HTree, InclusionPro
                      nodes_upto, levels_len, level_offset, ahtree_verify_inclusion,
                      ahtree_eval_inclusion, ahtree_verify_consistency, ahtree_eval_consistency,
                      ahtree_verify_last_inclusion, ahtree_verify_batch, build_hash_tree)
+from . import txlayer
+from .txlayer import (TX_HEADER, tx_alh_batch, htree_build_many, verify_linear_proof_batch,
+                      verify_dual_proof_v2_batch, VerifyDualProofV2, txlog_validate)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -21,6 +21,15 @@ MH_ERR_METADATA_UNSUPPORTED = 6
 MH_ERR_CANNOT_RESET_TO_LARGER = 7
 MH_ERR_NO_DEVICE = 8
 MH_ERR_OUT_OF_MEMORY = 9
+MH_ERR_SOURCE_TX_NEWER = 10
+MH_ERR_UNEXPECTED_LINKING = 11
+MH_ERR_INCLUSION_NOT_VALID = 12
+MH_ERR_CONSISTENCY_NOT_VALID = 13
+MH_ERR_CORRUPTED_DATA = 14
+MH_ERR_CORRUPTED_MAX_ENTRIES = 15
+MH_ERR_CORRUPTED_MAX_KEYLEN = 16
+MH_ERR_CORRUPTED_UNKNOWN_VERSION = 17
+MH_ERR_TRUNCATED = 18
 
 MH_AHT_INCLUSION = 0
 MH_AHT_CONSISTENCY = 1
@@ -73,6 +82,46 @@ class ErrOutOfMemory(MerkleError):
     pass
 
 
+class ErrSourceTxNewerThanTargetTx(ErrIllegalArguments):
+    pass
+
+
+class ErrUnexpectedLinkingError(MerkleError):
+    pass
+
+
+class ErrInclusionProofNotValid(MerkleError):
+    pass
+
+
+class ErrConsistencyProofNotValid(MerkleError):
+    pass
+
+
+class ErrCorruptedData(MerkleError):
+    pass
+
+
+class ErrCorruptedTxData(MerkleError):
+    pass
+
+
+class ErrCorruptedTxDataMaxTxEntriesExceeded(ErrCorruptedTxData):
+    pass
+
+
+class ErrCorruptedTxDataMaxKeyLenExceeded(ErrCorruptedTxData):
+    pass
+
+
+class ErrCorruptedTxDataUnknownHeaderVersion(ErrCorruptedTxData):
+    pass
+
+
+class ErrUnexpectedEOF(MerkleError):
+    pass
+
+
 class HipError(MerkleError):
     pass
 
@@ -87,6 +136,15 @@ _ERRORS = {
     MH_ERR_CANNOT_RESET_TO_LARGER: ErrCannotResetToLargerSize,
     MH_ERR_NO_DEVICE: ErrNoDevice,
     MH_ERR_OUT_OF_MEMORY: ErrOutOfMemory,
+    MH_ERR_SOURCE_TX_NEWER: ErrSourceTxNewerThanTargetTx,
+    MH_ERR_UNEXPECTED_LINKING: ErrUnexpectedLinkingError,
+    MH_ERR_INCLUSION_NOT_VALID: ErrInclusionProofNotValid,
+    MH_ERR_CONSISTENCY_NOT_VALID: ErrConsistencyProofNotValid,
+    MH_ERR_CORRUPTED_DATA: ErrCorruptedData,
+    MH_ERR_CORRUPTED_MAX_ENTRIES: ErrCorruptedTxDataMaxTxEntriesExceeded,
+    MH_ERR_CORRUPTED_MAX_KEYLEN: ErrCorruptedTxDataMaxKeyLenExceeded,
+    MH_ERR_CORRUPTED_UNKNOWN_VERSION: ErrCorruptedTxDataUnknownHeaderVersion,
+    MH_ERR_TRUNCATED: ErrUnexpectedEOF,
 }
 
 vp = C.c_void_p
@@ -150,6 +208,14 @@ SIGNATURES = {
     "mh_ahtree_nodes_upto": (u64, [u64]),
     "mh_ahtree_verify_batch": (i32, [vp, i32, u64, vp, vp, vp, u8p, u8p, u8p, u8p, u8p]),
     "mh_dev_ahtree_verify_batch": (i32, [vp, i32, u64, vp, vp, vp, u8p, u8p, u8p, u8p, u8p]),
+    "mh_tx_alh_batch": (i32, [vp, u64, vp, u8p, u64, u8p, u8p]),
+    "mh_dev_tx_alh_batch": (i32, [vp, u64, vp, u8p, u8p, u8p, u8p, u8p]),
+    "mh_htree_build_many": (i32, [vp, u64, vp, u8p, u8p]),
+    "mh_verify_linear_proof_batch": (i32, [vp, u64, vp, vp, vp, u8p, vp, vp, u8p, u8p, u8p]),
+    "mh_verify_dual_proof_v2_batch": (i32, [vp, u64, vp, vp, u8p, u64, vp, u8p, vp, u8p, vp, vp,
+                                            u8p, u8p, vp]),
+    "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
+                                u8p, vp]),
 }
 
 _lib = None

@@ -16,145 +16,12 @@
 #include <string>
 #include <vector>
 
-#include "mh_internal.hpp"
+#include "capi_internal.hpp"
 
-using namespace mh;
 
 namespace mh {
 hipError_t launch_copy_nodes(hipStream_t st, const uint8_t *src, uint64_t n, uint8_t *dst);
 }
-
-#define MH_HIP(expr)                                        \
-    do {                                                    \
-        hipError_t e_ = (expr);                             \
-        if (e_ != hipSuccess) return -(int)e_;              \
-    } while (0)
-
-static const uint8_t kEmptyRoot[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14,
-                                       0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
-                                       0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c,
-                                       0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
-
-// ------------------------------------------------------------------ timing
-struct EventTimer : Timer {
-    struct Rec {
-        std::string name;
-        hipEvent_t a, b;
-    };
-    std::mutex mu;
-    std::vector<Rec> recs;
-    std::vector<hipEvent_t> pool;
-    bool enabled = false;
-    hipEvent_t take() {
-        hipEvent_t e;
-        if (!pool.empty()) {
-            e = pool.back();
-            pool.pop_back();
-        } else {
-            hipEventCreate(&e);
-        }
-        return e;
-    }
-    void begin(const char *name, hipStream_t st) override {
-        std::lock_guard<std::mutex> g(mu);
-        Rec r;
-        r.name = name;
-        r.a = take();
-        r.b = take();
-        hipEventRecord(r.a, st);
-        recs.push_back(r);
-    }
-    void end(hipStream_t st) override {
-        std::lock_guard<std::mutex> g(mu);
-        hipEventRecord(recs.back().b, st);
-    }
-    int sum(const char *prefix, double *ms, uint64_t *cnt) {
-        std::lock_guard<std::mutex> g(mu);
-        double tot = 0;
-        uint64_t c = 0;
-        size_t pl = prefix ? strlen(prefix) : 0;
-        for (auto &r : recs) {
-            if (pl && r.name.compare(0, pl, prefix) != 0) continue;
-            hipError_t e = hipEventSynchronize(r.b);
-            if (e != hipSuccess) return -(int)e;
-            float x = 0;
-            hipEventElapsedTime(&x, r.a, r.b);
-            tot += x;
-            c++;
-        }
-        if (ms) *ms = tot;
-        if (cnt) *cnt = c;
-        return MH_OK;
-    }
-    void reset() {
-        std::lock_guard<std::mutex> g(mu);
-        for (auto &r : recs) {
-            hipEventSynchronize(r.b);
-            pool.push_back(r.a);
-            pool.push_back(r.b);
-        }
-        recs.clear();
-    }
-    ~EventTimer() {
-        for (auto &r : recs) {
-            hipEventDestroy(r.a);
-            hipEventDestroy(r.b);
-        }
-        for (auto e : pool) hipEventDestroy(e);
-    }
-};
-
-// ------------------------------------------------------------------ buffers
-struct DevBuf {
-    void *p = nullptr;
-    uint64_t cap = 0;
-    hipError_t ensure(uint64_t bytes) {
-        if (bytes <= cap && p) return hipSuccess;
-        if (p) hipFree(p);
-        p = nullptr;
-        cap = 0;
-        uint64_t c = std::max<uint64_t>(bytes + 64, 256);
-        hipError_t e = hipMalloc(&p, c);
-        if (e == hipSuccess) cap = c;
-        return e;
-    }
-    template <class T>
-    T *as() const {
-        return reinterpret_cast<T *>(p);
-    }
-    ~DevBuf() {
-        if (p) hipFree(p);
-    }
-};
-
-struct mh_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    EventTimer timer;
-    std::mutex mu;  // guards scratch for mh_dev_* calls
-    DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs, s_ctr;
-    Timer *tm() { return timer.enabled ? &timer : nullptr; }
-};
-
-struct mh_htree {
-    mh_ctx *ctx = nullptr;
-    hipStream_t stream = nullptr;
-    uint64_t max_width = 0;
-    uint64_t width = 0;
-    uint8_t root[32];
-    DevBuf levels, in_a, in_b, in_c, off_a, off_b, off_c, ov, use, hv, msgoff, msgs, digests;
-    void *pinned = nullptr;
-    uint64_t pinned_cap = 0;
-    LevelGeom geom;
-};
-
-struct mh_ahtree {
-    mh_ctx *ctx = nullptr;
-    hipStream_t stream = nullptr;
-    uint64_t size = 0;
-    DevBuf dlog, in, roots, idx, out, ctr;
-};
 
 // ------------------------------------------------------------------ misc
 extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
@@ -171,6 +38,17 @@ extern "C" const char *mh_status_string(int st) {
         case MH_ERR_CANNOT_RESET_TO_LARGER: return "ahtree: can not reset the tree to a larger size";
         case MH_ERR_NO_DEVICE: return "no usable gfx950 device";
         case MH_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case MH_ERR_SOURCE_TX_NEWER: return "illegal arguments: source tx is newer than target tx";
+        case MH_ERR_UNEXPECTED_LINKING:
+            return "internal inconsistency between linear and binary linking";
+        case MH_ERR_INCLUSION_NOT_VALID: return "inclusion proof does NOT validate";
+        case MH_ERR_CONSISTENCY_NOT_VALID: return "consistency proof does NOT validate";
+        case MH_ERR_CORRUPTED_DATA: return "data is corrupted";
+        case MH_ERR_CORRUPTED_MAX_ENTRIES:
+            return "tx data is corrupted: maximum number of TX entries exceeded";
+        case MH_ERR_CORRUPTED_MAX_KEYLEN: return "tx data is corrupted: maximum key length exceeded";
+        case MH_ERR_CORRUPTED_UNKNOWN_VERSION: return "tx data is corrupted: unknown TX header version";
+        case MH_ERR_TRUNCATED: return "unexpected EOF";
         default: return st < 0 ? hipGetErrorString((hipError_t)(-st)) : "unknown status";
     }
 }

@@ -1,0 +1,478 @@
+// capi_tx.hip -- C ABI of the transaction layer (include/immustore_merkle.h,
+// "tx layer" section): header Alh (a7), linear and dual proofs (a13), tx-log
+// read-path validation (a14) and many-tree htree builds (a3 over many txs).
+//
+// Host code here parses records, lays out device buffers and combines
+// per-proof verdicts; every SHA-256 runs in tx_kernels.hip / verify_kernels.hip
+// / htree_kernels.hip.
+#include <cstring>
+#include <vector>
+
+#include "capi_internal.hpp"
+
+namespace {
+
+// Sub-allocations of one device scratch buffer (256-byte aligned).
+struct Layout {
+    uint64_t total = 0;
+    uint64_t add(uint64_t bytes) {
+        const uint64_t o = total;
+        total = (total + bytes + 255) & ~255ull;
+        return o;
+    }
+};
+
+// Header preconditions shared by every entry point that hashes headers.
+int check_header(const mh_tx_header &h, uint64_t md_blob_len, bool have_blob) {
+    if (h.version > 1) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (h.md_len) {
+        if (h.version == 0) return MH_ERR_METADATA_UNSUPPORTED;
+        if (h.md_len > MH_MAX_TX_METADATA_LEN || !have_blob) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((uint64_t)h.md_off + h.md_len > md_blob_len) return MH_ERR_ILLEGAL_ARGUMENTS;
+    }
+    return MH_OK;
+}
+
+// ---------------------------------------------------------------- many trees
+// Level plan of a batch of htrees (htree.go:85-110 per tree): level 0 are the
+// leaves of all trees back to back, every further level appends the nodes of
+// the trees that still have more than one node.
+struct TreePlan {
+    std::vector<uint64_t> cur, prev, prevw;  // items, grouped by level
+    struct Level {
+        uint64_t base, nodes, item0, nitems;
+    };
+    std::vector<Level> levels;
+    std::vector<uint64_t> root_idx;  // per tree: node index of the root, ~0 = empty tree
+    uint64_t total_nodes = 0;
+
+    void build(uint64_t ntrees, const uint64_t *leaf_off) {
+        const uint64_t o0 = leaf_off[0];
+        root_idx.assign(ntrees, ~0ull);
+        struct Act {
+            uint64_t t, base, w;
+        };
+        std::vector<Act> act, nxt;
+        for (uint64_t t = 0; t < ntrees; t++) {
+            const uint64_t w = leaf_off[t + 1] - leaf_off[t];
+            if (w == 1) root_idx[t] = leaf_off[t] - o0;
+            if (w > 1) act.push_back({t, leaf_off[t] - o0, w});
+        }
+        uint64_t next = leaf_off[ntrees] - o0;
+        while (!act.empty()) {
+            Level L{next, 0, cur.size(), act.size()};
+            nxt.clear();
+            for (const Act &a : act) {
+                const uint64_t cw = (a.w + 1) / 2;
+                cur.push_back(next);
+                prev.push_back(a.base);
+                prevw.push_back(a.w);
+                if (cw == 1)
+                    root_idx[a.t] = next;
+                else
+                    nxt.push_back({a.t, next, cw});
+                next += cw;
+                L.nodes += cw;
+            }
+            levels.push_back(L);
+            act.swap(nxt);
+        }
+        total_nodes = next;
+    }
+};
+
+// Leaves + levels + roots of a planned batch on `st`.  d_digests: E x 32 on
+// the device; d_roots: ntrees x 32.  Uses the ctx's s_tree scratch.
+int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,
+                  const uint8_t *d_digests, uint8_t *d_roots) {
+    Layout L;
+    const uint64_t nitems = P.cur.size();
+    const uint64_t b_nodes = L.add(std::max<uint64_t>(P.total_nodes, 1) * 32);
+    const uint64_t b_cur = L.add(nitems * 8), b_prev = L.add(nitems * 8),
+                   b_prevw = L.add(nitems * 8), b_root = L.add(ntrees * 8);
+    MH_HIP(c->s_tree.ensure(L.total));
+    uint8_t *base = c->s_tree.as<uint8_t>();
+    uint8_t *nodes = base + b_nodes;
+    if (nitems) {
+        MH_HIP(hipMemcpyAsync(base + b_cur, P.cur.data(), nitems * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_prev, P.prev.data(), nitems * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_prevw, P.prevw.data(), nitems * 8, hipMemcpyHostToDevice,
+                              st));
+    }
+    MH_HIP(hipMemcpyAsync(base + b_root, P.root_idx.data(), ntrees * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_leaf_for(st, c->tm(), nleaves, d_digests, nodes));  // htree.go:79-83
+    for (const auto &lv : P.levels)
+        MH_HIP(launch_seg_level(st, c->tm(), lv.nodes, lv.base, (uint32_t)lv.nitems,
+                                (const uint64_t *)(base + b_cur) + lv.item0,
+                                (const uint64_t *)(base + b_prev) + lv.item0,
+                                (const uint64_t *)(base + b_prevw) + lv.item0, nodes));
+    MH_HIP(launch_gather32(st, ntrees, nodes, (const uint64_t *)(base + b_root), d_roots));
+    return MH_OK;
+}
+
+uint64_t be_at(const uint8_t *p, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ a7
+extern "C" int mh_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
+                               const uint8_t *md_blob, uint64_t md_blob_len, uint8_t *inner_out,
+                               uint8_t *alh_out) {
+    if (!c || (n && (!hdrs || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    for (uint64_t k = 0; k < n; k++)
+        if (int e = check_header(hdrs[k], md_blob_len, md_blob != nullptr)) return e;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    Layout L;
+    const uint64_t b_h = L.add(n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
+                   b_s = L.add(n * kTxInnerStride), b_in = L.add(n * 32), b_a = L.add(n * 32);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base + b_h, hdrs, n * sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
+    if (md_blob && md_blob_len)
+        MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_tx_alh(st, c->tm(), n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
+                         base + b_s, nullptr, nullptr, base + b_in, base + b_a, nullptr));
+    if (inner_out) MH_HIP(hipMemcpyAsync(inner_out, base + b_in, n * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(alh_out, base + b_a, n * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
+                                   const uint8_t *md_blob, const uint8_t *eh, uint8_t *scratch,
+                                   uint8_t *inner_out, uint8_t *alh_out) {
+    if (!c || (n && (!hdrs || !scratch || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    hipSetDevice(c->device);
+    MH_HIP(launch_tx_alh(c->stream, c->tm(), n, hdrs, md_blob, eh, scratch, nullptr, nullptr,
+                         inner_out, alh_out, nullptr));
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ a3 x many
+extern "C" int mh_htree_build_many(mh_ctx *c, uint64_t ntrees, const uint64_t *leaf_off,
+                                   const uint8_t *digests, uint8_t *roots) {
+    if (!c || (ntrees && (!leaf_off || !roots))) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!ntrees) return MH_OK;
+    for (uint64_t t = 0; t < ntrees; t++)
+        if (leaf_off[t + 1] < leaf_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
+    const uint64_t E = leaf_off[ntrees] - leaf_off[0];
+    if (E && !digests) return MH_ERR_ILLEGAL_ARGUMENTS;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    TreePlan P;
+    P.build(ntrees, leaf_off);
+    Layout L;
+    const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_r = L.add(ntrees * 32);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    if (E)
+        MH_HIP(hipMemcpyAsync(base + b_d, digests + leaf_off[0] * 32, E * 32,
+                              hipMemcpyHostToDevice, st));
+    if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
+    MH_HIP(hipMemcpyAsync(roots, base + b_r, ntrees * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ a13
+extern "C" int mh_verify_linear_proof_batch(mh_ctx *c, uint64_t n, const uint64_t *proof_src,
+                                            const uint64_t *proof_tgt, const uint64_t *term_off,
+                                            const uint8_t *terms, const uint64_t *src,
+                                            const uint64_t *tgt, const uint8_t *src_alh,
+                                            const uint8_t *tgt_alh, uint8_t *ok) {
+    if (!c || (n && (!proof_src || !proof_tgt || !term_off || !src || !tgt || !src_alh ||
+                     !tgt_alh || !ok)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    const uint64_t nterms = term_off[n] - term_off[0];
+    if (nterms && !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    std::vector<uint64_t> to(n + 1);
+    for (uint64_t p = 0; p <= n; p++) to[p] = term_off[p] - term_off[0];
+    Layout L;
+    const uint64_t b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_s = L.add(n * 8),
+                   b_t = L.add(n * 8), b_off = L.add((n + 1) * 8), b_terms = L.add(nterms * 32),
+                   b_sa = L.add(n * 32), b_ta = L.add(n * 32), b_ok = L.add(n);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base + b_ps, proof_src, n * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_pt, proof_tgt, n * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_s, src, n * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_t, tgt, n * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_off, to.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (nterms)
+        MH_HIP(hipMemcpyAsync(base + b_terms, terms + term_off[0] * 32, nterms * 32,
+                              hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_sa, src_alh, n * 32, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_ta, tgt_alh, n * 32, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_linear_verify(st, c->tm(), n, (const uint64_t *)(base + b_ps),
+                                (const uint64_t *)(base + b_pt), (const uint64_t *)(base + b_s),
+                                (const uint64_t *)(base + b_t), (const uint64_t *)(base + b_off),
+                                base + b_terms, base + b_sa, base + b_ta, base + b_ok));
+    MH_HIP(hipMemcpyAsync(ok, base + b_ok, n, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_header *sh,
+                                             const mh_tx_header *th, const uint8_t *md_blob,
+                                             uint64_t md_blob_len, const uint64_t *incl_off,
+                                             const uint8_t *incl_terms, const uint64_t *cons_off,
+                                             const uint8_t *cons_terms, const uint64_t *src,
+                                             const uint64_t *tgt, const uint8_t *src_alh,
+                                             const uint8_t *tgt_alh, int32_t *status) {
+    if (!c || (n && (!sh || !th || !incl_off || !cons_off || !src || !tgt || !src_alh ||
+                     !tgt_alh || !status)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
+    if ((ni && !incl_terms) || (nc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    // verification.go:305-316: argument checks on the host, headers that
+    // cannot be hashed (unknown version, bad md) fail as ErrIllegalArguments
+    std::vector<mh_tx_header> hh(2 * n);
+    std::vector<uint8_t> expect(2 * n * 32);
+    for (uint64_t p = 0; p < n; p++) {
+        int32_t s = MH_OK;
+        if (sh[p].id == 0 || sh[p].id != src[p] || th[p].id != tgt[p])
+            s = MH_ERR_ILLEGAL_ARGUMENTS;
+        else if (src[p] > tgt[p])
+            s = MH_ERR_SOURCE_TX_NEWER;
+        else if (check_header(sh[p], md_blob_len, md_blob != nullptr) ||
+                 check_header(th[p], md_blob_len, md_blob != nullptr))
+            s = MH_ERR_ILLEGAL_ARGUMENTS;
+        status[p] = s;
+        hh[p] = sh[p];
+        hh[n + p] = th[p];
+        if (s != MH_OK) {  // keep the kernel's reads inside md_blob; result unused
+            hh[p].version = hh[n + p].version = 1;
+            hh[p].md_len = hh[n + p].md_len = 0;
+        }
+        memcpy(&expect[p * 32], src_alh + p * 32, 32);
+        memcpy(&expect[(n + p) * 32], tgt_alh + p * 32, 32);
+    }
+    std::vector<uint64_t> io(n + 1), co(n + 1), ii(n), ij(n), ci(n);
+    std::vector<uint8_t> sel(n), sbl(n * 32), tbl(n * 32);
+    for (uint64_t p = 0; p <= n; p++) {
+        io[p] = incl_off[p] - incl_off[0];
+        co[p] = cons_off[p] - cons_off[0];
+    }
+    for (uint64_t p = 0; p < n; p++) {
+        ii[p] = src[p];                                    // verification.go:342-348
+        ij[p] = th[p].bl_tx_id;
+        sel[p] = src[p] == 1;                              // :354-370
+        ci[p] = src[p] == 1 ? src[p] : sh[p].bl_tx_id;
+        memcpy(&sbl[p * 32], sh[p].bl_root, 32);
+        memcpy(&tbl[p * 32], th[p].bl_root, 32);
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    Layout L;
+    const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
+                   b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
+                   b_st = L.add(2 * n * 4), b_leaf = L.add(n * 32), b_sbl = L.add(n * 32),
+                   b_tbl = L.add(n * 32), b_ca = L.add(n * 32), b_sel = L.add(n),
+                   b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
+                   b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8), b_it = L.add(ni * 32),
+                   b_ct = L.add(nc * 32), b_oki = L.add(n), b_okc = L.add(n);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
+                     : hipSuccess;
+    };
+    MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
+    if (md_blob) MH_HIP(h2d(b_md, md_blob, md_blob_len));
+    MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
+    MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
+    MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
+    MH_HIP(h2d(b_sel, sel.data(), n));
+    MH_HIP(h2d(b_ii, ii.data(), n * 8));
+    MH_HIP(h2d(b_ij, ij.data(), n * 8));
+    MH_HIP(h2d(b_ci, ci.data(), n * 8));
+    MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
+    MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
+    if (ni) MH_HIP(h2d(b_it, incl_terms + incl_off[0] * 32, ni * 32));
+    if (nc) MH_HIP(h2d(b_ct, cons_terms + cons_off[0] * 32, nc * 32));
+    // Alh of both headers vs the given ones (verification.go:318-326)
+    MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, (const MhTxHeader *)(base + b_h), base + b_md,
+                         nullptr, base + b_s, base + b_x, nullptr, nullptr, nullptr,
+                         (int32_t *)(base + b_st)));
+    // leafFor(sourceAlh) (verification.go:346), then the two ahtree proofs
+    MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
+    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
+                                (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
+                                base + b_it, base + b_leaf, base + b_tbl, base + b_oki, nullptr));
+    MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
+    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
+                                (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
+                                (const uint64_t *)(base + b_co), base + b_ct, base + b_ca,
+                                base + b_tbl, base + b_okc, nullptr));
+    std::vector<int32_t> ast(2 * n);
+    std::vector<uint8_t> oki(n), okc(n);
+    MH_HIP(hipMemcpyAsync(ast.data(), base + b_st, 2 * n * 4, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(oki.data(), base + b_oki, n, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(okc.data(), base + b_okc, n, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    for (uint64_t p = 0; p < n; p++) {
+        if (status[p] != MH_OK) continue;
+        if (ast[p] != MH_OK || ast[n + p] != MH_OK) {
+            status[p] = MH_ERR_ILLEGAL_ARGUMENTS;
+        } else if (sh[p].id - 1 != sh[p].bl_tx_id || th[p].id - 1 != th[p].bl_tx_id) {
+            status[p] = MH_ERR_UNEXPECTED_LINKING;  // :328-330
+        } else if (src[p] == tgt[p]) {
+            status[p] = MH_OK;  // :332-334
+        } else if (!oki[p]) {
+            status[p] = MH_ERR_INCLUSION_NOT_VALID;
+        } else if (!okc[p]) {
+            status[p] = MH_ERR_CONSISTENCY_NOT_VALID;
+        }
+    }
+    return MH_OK;
+}
+
+// ------------------------------------------------------------------ a14
+extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                                 uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
+                                 uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
+                                 int32_t *status_out) {
+    if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    // ---- host parse (tx.go:419-603): structure only, no hashing
+    std::vector<mh_tx_header> H;
+    std::vector<uint64_t> alh_pos, leaf_off{0}, rec_off, msg_off{0};
+    std::vector<uint8_t> ver;
+    uint64_t p = 0;
+    int rc = MH_OK;
+    while (H.size() < max_txs) {
+        const uint64_t p0 = p;
+        if (p + 8 > len) break;
+        mh_tx_header h;
+        memset(&h, 0, sizeof h);
+        h.id = be_at(buf + p, 8);
+        if (h.id == 0) break;  // preallocated tail, read as EOF (tx.go:427-430)
+        if (p + 90 > len) { rc = MH_ERR_TRUNCATED; break; }
+        h.ts = (int64_t)be_at(buf + p + 8, 8);
+        h.bl_tx_id = be_at(buf + p + 16, 8);
+        memcpy(h.bl_root, buf + p + 24, 32);
+        memcpy(h.prev_alh, buf + p + 56, 32);
+        h.version = (uint32_t)be_at(buf + p + 88, 2);
+        p += 90;
+        if (h.version == 0) {
+            if (p + 2 > len) { rc = MH_ERR_TRUNCATED; break; }
+            h.nentries = (uint32_t)be_at(buf + p, 2);
+            p += 2;
+        } else if (h.version == 1) {
+            if (p + 2 > len) { rc = MH_ERR_TRUNCATED; break; }
+            h.md_len = (uint32_t)be_at(buf + p, 2);
+            p += 2;
+            if (h.md_len > MH_MAX_TX_METADATA_LEN) { rc = MH_ERR_CORRUPTED_DATA; break; }
+            if (p + h.md_len + 4 > len) { rc = MH_ERR_TRUNCATED; break; }
+            h.md_off = (uint32_t)p;
+            if (p > 0xffffffffull) { rc = MH_ERR_ILLEGAL_ARGUMENTS; break; }
+            p += h.md_len;
+            h.nentries = (uint32_t)be_at(buf + p, 4);
+            p += 4;
+        } else {
+            rc = MH_ERR_CORRUPTED_UNKNOWN_VERSION;
+            break;
+        }
+        if (h.nentries > max_entries) { rc = MH_ERR_CORRUPTED_MAX_ENTRIES; break; }
+        const size_t e0 = rec_off.size();
+        int bad = MH_OK;
+        for (uint32_t e = 0; e < h.nentries; e++) {
+            const uint64_t q = p;
+            if (p + 2 > len) { bad = MH_ERR_TRUNCATED; break; }
+            const uint64_t ml = be_at(buf + p, 2);
+            if (ml > MH_MAX_KV_METADATA_LEN) { bad = MH_ERR_CORRUPTED_DATA; break; }
+            if (p + 2 + ml + 2 > len) { bad = MH_ERR_TRUNCATED; break; }
+            const uint64_t kl = be_at(buf + p + 2 + ml, 2);
+            if (kl > max_key_len) { bad = MH_ERR_CORRUPTED_MAX_KEYLEN; break; }
+            if (p + 4 + ml + kl + 12 + 32 > len) { bad = MH_ERR_TRUNCATED; break; }
+            p += 4 + ml + kl + 12 + 32;
+            rec_off.push_back(q);
+            ver.push_back((uint8_t)h.version);
+            msg_off.push_back(msg_off.back() + (h.version == 1 ? 4 + ml + kl : kl) + 32);
+        }
+        if (bad == MH_OK && p + 32 > len) bad = MH_ERR_TRUNCATED;
+        if (bad != MH_OK) {
+            rc = bad;
+            rec_off.resize(e0);
+            ver.resize(e0);
+            msg_off.resize(e0 + 1);
+            p = p0;
+            break;
+        }
+        alh_pos.push_back(p);
+        p += 32;
+        leaf_off.push_back(rec_off.size());
+        H.push_back(h);
+        (void)p0;
+    }
+    if (rc != MH_OK) {
+        // p was left inside the failing record by the header-level breaks
+        uint64_t last_end = alh_pos.empty() ? 0 : alh_pos.back() + 32;
+        p = last_end;
+    }
+    const uint64_t ntx = H.size(), E = rec_off.size();
+    if (ntx_out) *ntx_out = ntx;
+    if (consumed_out) *consumed_out = p;
+    if (!ntx) return rc;
+    // ---- device: digests, trees, Alh
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    TreePlan P;
+    P.build(ntx, leaf_off.data());
+    const uint64_t used = p;  // bytes of buf covered by the parsed records
+    Layout L;
+    const uint64_t b_buf = L.add(used), b_rec = L.add(E * 8), b_ver = L.add(E),
+                   b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_off.back()),
+                   b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_h = L.add(ntx * sizeof(mh_tx_header)),
+                   b_ap = L.add(ntx * 8), b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride),
+                   b_a = L.add(ntx * 32), b_st = L.add(ntx * 4);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base + b_buf, buf, used, hipMemcpyHostToDevice, st));
+    if (E) {
+        MH_HIP(hipMemcpyAsync(base + b_rec, rec_off.data(), E * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_ver, ver.data(), E, hipMemcpyHostToDevice, st));
+    }
+    MH_HIP(hipMemcpyAsync(base + b_mo, msg_off.data(), (E + 1) * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(base + b_h, H.data(), ntx * sizeof(mh_tx_header), hipMemcpyHostToDevice,
+                          st));
+    MH_HIP(hipMemcpyAsync(base + b_ap, alh_pos.data(), ntx * 8, hipMemcpyHostToDevice, st));
+    // entry digests (tx.go:578-585 -> 690-731)
+    MH_HIP(launch_txe_assemble(st, c->tm(), E, base + b_buf, (const uint64_t *)(base + b_rec),
+                               base + b_ver, (const uint64_t *)(base + b_mo), base + b_msg));
+    MH_HIP(launch_sha256_csr(st, c->tm(), base + b_msg, (const uint64_t *)(base + b_mo), E,
+                             nullptr, nullptr, base + b_dig));
+    // one htree per tx (tx.go:617-621)
+    if (int e = run_tree_plan(c, st, P, ntx, E, base + b_dig, base + b_eh)) return e;
+    // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
+    MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), base + b_buf,
+                         base + b_eh, base + b_s, base + b_buf, (const uint64_t *)(base + b_ap),
+                         nullptr, base + b_a, (int32_t *)(base + b_st)));
+    std::vector<uint8_t> eh(hdrs_out ? ntx * 32 : 0);
+    if (status_out)
+        MH_HIP(hipMemcpyAsync(status_out, base + b_st, ntx * 4, hipMemcpyDeviceToHost, st));
+    if (alh_out) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
+    if (hdrs_out) MH_HIP(hipMemcpyAsync(eh.data(), base + b_eh, ntx * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    if (hdrs_out)
+        for (uint64_t k = 0; k < ntx; k++) {
+            hdrs_out[k] = H[k];
+            memcpy(hdrs_out[k].eh, &eh[k * 32], 32);
+        }
+    return rc;
+}

@@ -707,16 +707,6 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }
 
-struct TimerScope {
-    Timer *tm;
-    hipStream_t st;
-    TimerScope(Timer *t, const char *name, hipStream_t s) : tm(t), st(s) {
-        if (tm) tm->begin(name, st);
-    }
-    ~TimerScope() {
-        if (tm) tm->end(st);
-    }
-};
 
 static int choose_lpl(uint64_t n) {
     if (const char *e = getenv("MH_LPL")) {

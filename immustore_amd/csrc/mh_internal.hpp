@@ -44,6 +44,17 @@ struct Timer {
     virtual ~Timer() {}
 };
 
+struct TimerScope {
+    Timer *tm;
+    hipStream_t st;
+    TimerScope(Timer *t, const char *name, hipStream_t s) : tm(t), st(s) {
+        if (tm) tm->begin(name, st);
+    }
+    ~TimerScope() {
+        if (tm) tm->end(st);
+    }
+};
+
 hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t n,
                                 const uint8_t *keys, uint32_t key_len, const uint8_t *vals,
                                 uint32_t val_len, uint8_t *hvals_out, uint8_t *levels,
@@ -103,4 +114,29 @@ hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64
 uint64_t ahtree_nodes_upto(uint64_t n);
 uint64_t ahtree_nodes_until(uint64_t n);
 
+
+// ---------------------------------------------------------------- tx layer
+typedef mh_tx_header MhTxHeader;
+constexpr uint64_t kTxInnerStride = 384;  // >= 8+2+2+268+4+32+8+32 (tx.go:249-302)
+
+hipError_t launch_tx_alh(hipStream_t st, Timer *tm, uint64_t n, const MhTxHeader *hdrs,
+                         const uint8_t *md_blob, const uint8_t *eh_src, uint8_t *scratch,
+                         const uint8_t *expect, const uint64_t *expect_off, uint8_t *inner_out,
+                         uint8_t *alh_out, int32_t *status);
+hipError_t launch_leaf_for(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *in, uint8_t *out);
+hipError_t launch_select32(hipStream_t st, uint64_t n, const uint8_t *sel, const uint8_t *x,
+                           const uint8_t *y, uint8_t *out);
+hipError_t launch_linear_verify(hipStream_t st, Timer *tm, uint64_t n, const uint64_t *psrc,
+                                const uint64_t *ptgt, const uint64_t *src, const uint64_t *tgt,
+                                const uint64_t *term_off, const uint8_t *terms,
+                                const uint8_t *src_alh, const uint8_t *tgt_alh, uint8_t *ok);
+hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
+                               const uint64_t *rec_off, const uint8_t *ver,
+                               const uint64_t *msg_off, uint8_t *msgs);
+hipError_t launch_seg_level(hipStream_t st, Timer *tm, uint64_t nnodes, uint64_t level_base,
+                            uint32_t nitems, const uint64_t *cur_base, const uint64_t *prev_base,
+                            const uint64_t *prev_w, uint8_t *nodes);
+// idx[p] == ~0 writes SHA256(nil) (the empty tree's root, htree.go:73-77)
+hipError_t launch_gather32(hipStream_t st, uint64_t n, const uint8_t *src, const uint64_t *idx,
+                           uint8_t *out);
 }  // namespace mh

@@ -1,0 +1,315 @@
+// tx_kernels.hip -- the transaction layer around the Merkle path on CDNA4.
+//
+//   TxHeader.innerHash / Alh             embedded/store/tx.go:249-319        (a7)
+//   advanceLinearHash / VerifyLinearProof embedded/store/verification.go:32-64 (a13)
+//   leafFor                              embedded/store/verification.go:237-242
+//   many small htrees at once            htree.BuildWith (htree.go:68-113) per tx,
+//                                        for the read path (tx.go:605-630, a14)
+//                                        and for concurrent BuildHashTree calls
+//                                        (tx.go:332-355, immustore.go:1632)
+//   entry-digest messages from raw tx-log records (tx.go:520-588 + 690-731)
+//
+// Everything is one message (or one chain) per lane; the per-tx work is a few
+// compressions, so these kernels are latency/occupancy shaped rather than
+// roofline shaped, and they exist so that no hashing of this layer runs on
+// the host.
+#include <algorithm>
+
+#include "digest_io.hpp"
+#include "mh_internal.hpp"
+
+namespace mh {
+
+static inline unsigned grid_for(uint64_t threads, unsigned block) {
+    return (unsigned)((threads + block - 1) / block);
+}
+
+__device__ __forceinline__ uint32_t ld_be32_aligned(const uint8_t *p) {
+    return bswap(*reinterpret_cast<const uint32_t *>(p));
+}
+
+// SHA256(BE64 id || prev[8 words] || inner[8 words]): 72 bytes, two blocks
+// (tx.go:307-319, verification.go:32-38).
+__device__ __forceinline__ void alh_hash(uint64_t id, const uint32_t prev[8],
+                                         const uint32_t inner[8], uint32_t out[8]) {
+    uint32_t w[16];
+    w[0] = (uint32_t)(id >> 32);
+    w[1] = (uint32_t)id;
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[2 + j] = prev[j];
+#pragma unroll
+    for (int j = 0; j < 6; j++) w[10 + j] = inner[j];
+    State s;
+    s.init();
+    compress(s, w);
+    w[0] = inner[6];
+    w[1] = inner[7];
+    w[2] = 0x80000000u;
+#pragma unroll
+    for (int j = 3; j < 15; j++) w[j] = 0;
+    w[15] = 72u * 8u;
+    compress(s, w);
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[j] = s.h[j];
+}
+
+__device__ __forceinline__ void put_be(uint8_t *&o, uint64_t v, int n) {
+    for (int k = n - 1; k >= 0; k--) *o++ = (uint8_t)(v >> (8 * k));
+}
+
+// One header per lane: innerHash (message assembled in the lane's scratch
+// slot, <= 356 bytes) then Alh.  eh_src (nullable) replaces hdrs[p].eh;
+// expect (nullable) turns the Alh into a pass / MH_ERR_CORRUPTED_DATA status.
+__global__ __launch_bounds__(256) void k_tx_alh(uint64_t n, const MhTxHeader *__restrict__ hdrs,
+                                                const uint8_t *__restrict__ md_blob,
+                                                const uint8_t *__restrict__ eh_src,
+                                                uint8_t *__restrict__ scratch,
+                                                const uint8_t *__restrict__ expect,
+                                                const uint64_t *__restrict__ expect_off,
+                                                uint8_t *__restrict__ inner_out,
+                                                uint8_t *__restrict__ alh_out,
+                                                int32_t *__restrict__ status) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const MhTxHeader &h = hdrs[p];
+    uint8_t *msg = scratch + p * kTxInnerStride;
+    uint8_t *o = msg;
+    put_be(o, (uint64_t)h.ts, 8);
+    put_be(o, h.version, 2);
+    if (h.version == 0) {
+        put_be(o, h.nentries, 2);
+    } else {
+        put_be(o, h.md_len, 2);
+        const uint8_t *md = md_blob + h.md_off;
+        for (uint32_t k = 0; k < h.md_len; k++) *o++ = md[k];
+        put_be(o, h.nentries, 4);
+    }
+    const uint8_t *eh = eh_src ? eh_src + p * 32 : h.eh;
+    for (int k = 0; k < 32; k++) *o++ = eh[k];
+    put_be(o, h.bl_tx_id, 8);
+    for (int k = 0; k < 32; k++) *o++ = h.bl_root[k];
+    uint32_t inner[8], prev[8], a[8];
+    sha256_bytes(msg, (uint64_t)(o - msg), -1, inner);
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = ld_be32_aligned(h.prev_alh + 4 * j);
+    alh_hash(h.id, prev, inner, a);
+    if (inner_out) store_digest(inner_out + p * 32, inner);
+    if (alh_out) store_digest(alh_out + p * 32, a);
+    if (status) {
+        const uint8_t *e = expect + (expect_off ? expect_off[p] : p * 32);
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t v = ((uint32_t)e[4 * j] << 24) | ((uint32_t)e[4 * j + 1] << 16) |
+                               ((uint32_t)e[4 * j + 2] << 8) | e[4 * j + 3];
+            x |= v ^ a[j];
+        }
+        status[p] = x ? MH_ERR_CORRUPTED_DATA : MH_OK;
+    }
+}
+
+// leafFor(d) = SHA256(0x00 || d)  (verification.go:237-242, ahtree.go:288-292)
+__global__ __launch_bounds__(256) void k_leaf_for(uint64_t n, const uint8_t *__restrict__ in,
+                                                  uint8_t *__restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    uint32_t d[8], h[8];
+    load_digest(in + p * 32, d);
+    leaf_hash(d, h);
+    store_digest(out + p * 32, h);
+}
+
+__global__ __launch_bounds__(256) void k_select32(uint64_t n, const uint8_t *__restrict__ sel,
+                                                  const uint8_t *__restrict__ x,
+                                                  const uint8_t *__restrict__ y,
+                                                  uint8_t *__restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint4 *s = reinterpret_cast<const uint4 *>((sel[p] ? x : y) + p * 32);
+    uint4 *d = reinterpret_cast<uint4 *>(out + p * 32);
+    d[0] = s[0];
+    d[1] = s[1];
+}
+
+// VerifyLinearProof (verification.go:40-64), one proof per lane.
+__global__ __launch_bounds__(256) void k_linear_verify(
+    uint64_t n, const uint64_t *__restrict__ psrc, const uint64_t *__restrict__ ptgt,
+    const uint64_t *__restrict__ src, const uint64_t *__restrict__ tgt,
+    const uint64_t *__restrict__ term_off, const uint8_t *__restrict__ terms,
+    const uint8_t *__restrict__ src_alh, const uint8_t *__restrict__ tgt_alh,
+    uint8_t *__restrict__ ok) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t s = psrc[p], t = ptgt[p], t0 = term_off[p], t1 = term_off[p + 1];
+    bool res = s == src[p] && t == tgt[p] && s != 0 && s <= t && t1 > t0 && (t1 - t0) == t - s + 1;
+    uint32_t c[8], x[8];
+    if (res) {
+        load_digest(terms + t0 * 32, c);
+        load_digest(src_alh + p * 32, x);
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) d |= c[j] ^ x[j];
+        res = d == 0;
+    }
+    if (res) {
+        for (uint64_t i = 1; i < t1 - t0; i++) {
+            uint32_t term[8];
+            load_digest(terms + (t0 + i) * 32, term);
+            alh_hash(s + i, c, term, c);
+        }
+        load_digest(tgt_alh + p * 32, x);
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) d |= c[j] ^ x[j];
+        res = d == 0;
+    }
+    ok[p] = res ? 1 : 0;
+}
+
+// Entry-digest messages straight from raw tx-log entry records
+// (tx.go:520-588): a record at rec is  BE16 mdLen | md | BE16 kLen | key |
+// BE32 vLen | BE64 vOff | hVal.  v1 message = record[0 : 4+md+key] || hVal,
+// v0 message = key || hVal (tx.go:690-731).
+__global__ __launch_bounds__(256) void k_txe_assemble(uint64_t n, const uint8_t *__restrict__ buf,
+                                                      const uint64_t *__restrict__ rec_off,
+                                                      const uint8_t *__restrict__ ver,
+                                                      const uint64_t *__restrict__ msg_off,
+                                                      uint8_t *__restrict__ msgs) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint8_t *r = buf + rec_off[e];
+    const uint32_t ml = ((uint32_t)r[0] << 8) | r[1];
+    const uint32_t kl = ((uint32_t)r[2 + ml] << 8) | r[3 + ml];
+    uint8_t *o = msgs + msg_off[e];
+    const uint8_t *src = ver[e] == 1 ? r : r + 4 + ml;
+    const uint32_t head = ver[e] == 1 ? 4 + ml + kl : kl;
+    for (uint32_t k = 0; k < head; k++) *o++ = src[k];
+    const uint8_t *hv = r + 4 + ml + kl + 12;
+    for (int k = 0; k < 32; k++) *o++ = hv[k];
+}
+
+// ---------------------------------------------------------------- many trees
+// Level l of a batch of independent htrees.  Item k describes one tree that
+// still has > 1 node at level l-1: its nodes at level l are written at
+// cur_base[k] .. cur_base[k] + ceil(prev_w[k] / 2), its level-(l-1) nodes
+// live at prev_base[k].  Thread i finds its item by binary search over
+// cur_base (sorted) and pairs (or promotes) exactly as htree.go:85-110.
+__global__ __launch_bounds__(256) void k_seg_level(uint64_t nnodes, uint64_t level_base,
+                                                   uint32_t nitems,
+                                                   const uint64_t *__restrict__ cur_base,
+                                                   const uint64_t *__restrict__ prev_base,
+                                                   const uint64_t *__restrict__ prev_w,
+                                                   uint8_t *__restrict__ nodes) {
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnodes;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = level_base + i;
+        uint32_t lo = 0, hi = nitems - 1;
+        while (lo < hi) {  // last k with cur_base[k] <= g
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (cur_base[mid] <= g)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const uint64_t j = g - cur_base[lo];
+        const uint64_t lpos = prev_base[lo] + 2 * j;
+        uint32_t a[8], o[8];
+        load_digest(nodes + lpos * 32, a);
+        if (2 * j + 1 < prev_w[lo]) {
+            uint32_t b[8];
+            load_digest(nodes + (lpos + 1) * 32, b);
+            node_hash_tab(a, b, o, tab);
+        } else {
+            copy8(o, a);
+        }
+        store_digest(nodes + g * 32, o);
+    }
+}
+
+__device__ __constant__ static const uint8_t kEmptyRootDev[32] = {
+    0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
+    0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+
+__global__ __launch_bounds__(256) void k_gather32(uint64_t n, const uint8_t *__restrict__ src,
+                                                  const uint64_t *__restrict__ idx,
+                                                  uint8_t *__restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t k = idx[p];
+    const uint4 *s = reinterpret_cast<const uint4 *>(k == ~0ull ? kEmptyRootDev : src + k * 32);
+    uint4 *d = reinterpret_cast<uint4 *>(out + p * 32);
+    d[0] = s[0];
+    d[1] = s[1];
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_tx_alh(hipStream_t st, Timer *tm, uint64_t n, const MhTxHeader *hdrs,
+                         const uint8_t *md_blob, const uint8_t *eh_src, uint8_t *scratch,
+                         const uint8_t *expect, const uint64_t *expect_off, uint8_t *inner_out,
+                         uint8_t *alh_out, int32_t *status) {
+    if (!n) return hipSuccess;
+    TimerScope ts(tm, "tx_alh", st);
+    hipLaunchKernelGGL(k_tx_alh, dim3(grid_for(n, 256)), dim3(256), 0, st, n, hdrs, md_blob,
+                       eh_src, scratch, expect, expect_off, inner_out, alh_out, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_for(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *in, uint8_t *out) {
+    if (!n) return hipSuccess;
+    TimerScope ts(tm, "leaf_for", st);
+    hipLaunchKernelGGL(k_leaf_for, dim3(grid_for(n, 256)), dim3(256), 0, st, n, in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_select32(hipStream_t st, uint64_t n, const uint8_t *sel, const uint8_t *x,
+                           const uint8_t *y, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_select32, dim3(grid_for(n, 256)), dim3(256), 0, st, n, sel, x, y, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_linear_verify(hipStream_t st, Timer *tm, uint64_t n, const uint64_t *psrc,
+                                const uint64_t *ptgt, const uint64_t *src, const uint64_t *tgt,
+                                const uint64_t *term_off, const uint8_t *terms,
+                                const uint8_t *src_alh, const uint8_t *tgt_alh, uint8_t *ok) {
+    if (!n) return hipSuccess;
+    TimerScope ts(tm, "linear_verify", st);
+    hipLaunchKernelGGL(k_linear_verify, dim3(grid_for(n, 256)), dim3(256), 0, st, n, psrc, ptgt,
+                       src, tgt, term_off, terms, src_alh, tgt_alh, ok);
+    return hipGetLastError();
+}
+
+hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
+                               const uint64_t *rec_off, const uint8_t *ver,
+                               const uint64_t *msg_off, uint8_t *msgs) {
+    if (!n) return hipSuccess;
+    TimerScope ts(tm, "txe_assemble", st);
+    hipLaunchKernelGGL(k_txe_assemble, dim3(grid_for(n, 256)), dim3(256), 0, st, n, buf, rec_off,
+                       ver, msg_off, msgs);
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_level(hipStream_t st, Timer *tm, uint64_t nnodes, uint64_t level_base,
+                            uint32_t nitems, const uint64_t *cur_base, const uint64_t *prev_base,
+                            const uint64_t *prev_w, uint8_t *nodes) {
+    if (!nnodes || !nitems) return hipSuccess;
+    TimerScope ts(tm, "seg_level", st);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(nnodes, 256), (uint64_t)cus * 8);
+    hipLaunchKernelGGL(k_seg_level, dim3(grid), dim3(256), kNodeTabBytes, st, nnodes, level_base,
+                       nitems, cur_base, prev_base, prev_w, nodes);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather32(hipStream_t st, uint64_t n, const uint8_t *src, const uint64_t *idx,
+                           uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_gather32, dim3(grid_for(n, 256)), dim3(256), 0, st, n, src, idx, out);
+    return hipGetLastError();
+}
+
+}  // namespace mh

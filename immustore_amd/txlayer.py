@@ -1,0 +1,159 @@
+"""Python mirror of the transaction layer around the Merkle path (embedded/store).
+
+  TxHeader.Alh / innerHash         tx.go:249-319          -> tx_alh_batch
+  Tx.BuildHashTree over many txs   tx.go:332-355          -> htree_build_many
+  VerifyLinearProof                verification.go:40-64  -> verify_linear_proof_batch
+  VerifyDualProofV2                verification.go:304-372 -> verify_dual_proof_v2_batch
+  Tx.readFrom (read-path check)    tx.go:388-630          -> txlog_validate
+
+Headers travel as a numpy structured array of TX_HEADER (the C struct
+mh_tx_header); metadata bytes live in a side blob addressed by md_off.
+All hashing runs in libimmustore_merkle.so's HIP kernels.
+"""
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .merkle import Context, _addr, _u8, default_context
+
+TX_HEADER = np.dtype([("id", "<u8"), ("ts", "<i8"), ("bl_tx_id", "<u8"), ("bl_root", "u1", 32),
+                      ("prev_alh", "u1", 32), ("eh", "u1", 32), ("version", "<u4"),
+                      ("nentries", "<u4"), ("md_len", "<u4"), ("md_off", "<u4")])
+assert TX_HEADER.itemsize == 136
+
+# TxReader limits (store options: MaxTxEntries, MaxKeyLen; options.go)
+DEFAULT_MAX_TX_ENTRIES = 1 << 10
+DEFAULT_MAX_KEY_LEN = 1 << 10
+
+
+def _ctx(ctx: Optional[Context]) -> Context:
+    return ctx or default_context()
+
+
+def _hdrs(h) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(h, TX_HEADER).reshape(-1))
+
+
+def _blob(b) -> Tuple[Optional[np.ndarray], int]:
+    if b is None or len(b) == 0:
+        return None, 0
+    a = _u8(b)
+    return a, a.size
+
+
+def _terms_csr(lists):
+    off = np.zeros(len(lists) + 1, np.uint64)
+    for k, t in enumerate(lists):
+        off[k + 1] = off[k] + len(t)
+    flat = b"".join(bytes(x) for t in lists for x in t)
+    arr = np.frombuffer(flat, np.uint8).copy() if flat else np.zeros(32, np.uint8)
+    return off, arr
+
+
+def _d32(xs, n) -> np.ndarray:
+    if isinstance(xs, np.ndarray):
+        a = np.ascontiguousarray(xs, np.uint8).reshape(-1, 32)
+    else:
+        a = np.frombuffer(b"".join(bytes(x) for x in xs), np.uint8).reshape(-1, 32).copy() \
+            if n else np.zeros((0, 32), np.uint8)
+    assert a.shape[0] == n
+    return a
+
+
+def tx_alh_batch(hdrs, md_blob=b"", ctx: Optional[Context] = None):
+    """-> (inner[n,32], alh[n,32]) for every header (TxHeader.Alh, tx.go:307)."""
+    h = _hdrs(hdrs)
+    n = h.size
+    inner = np.zeros((max(n, 1), 32), np.uint8)
+    alh = np.zeros((max(n, 1), 32), np.uint8)
+    mb, ml = _blob(md_blob)
+    N.check(N.load().mh_tx_alh_batch(_ctx(ctx).handle, n, _addr(h), _addr(mb), ml, _addr(inner),
+                                     _addr(alh)))
+    return inner[:n], alh[:n]
+
+
+def htree_build_many(trees: Sequence, ctx: Optional[Context] = None) -> np.ndarray:
+    """One htree root per digest list (width 0 -> SHA256(nil))."""
+    off = np.zeros(len(trees) + 1, np.uint64)
+    for k, t in enumerate(trees):
+        off[k + 1] = off[k] + len(t)
+    flat = b"".join(bytes(d) for t in trees for d in t)
+    d = np.frombuffer(flat, np.uint8).copy() if flat else None
+    roots = np.zeros((max(len(trees), 1), 32), np.uint8)
+    N.check(N.load().mh_htree_build_many(_ctx(ctx).handle, len(trees), _addr(off), _addr(d),
+                                         _addr(roots)))
+    return roots[:len(trees)]
+
+
+def verify_linear_proof_batch(proofs, ctx: Optional[Context] = None) -> np.ndarray:
+    """proofs: sequence of (proof_src, proof_tgt, terms, src, tgt, src_alh, tgt_alh)."""
+    n = len(proofs)
+    if n == 0:
+        return np.zeros(0, bool)
+    ps = np.array([p[0] for p in proofs], np.uint64)
+    pt = np.array([p[1] for p in proofs], np.uint64)
+    off, terms = _terms_csr([p[2] for p in proofs])
+    s = np.array([p[3] for p in proofs], np.uint64)
+    t = np.array([p[4] for p in proofs], np.uint64)
+    sa = _d32([p[5] for p in proofs], n)
+    ta = _d32([p[6] for p in proofs], n)
+    ok = np.zeros(n, np.uint8)
+    N.check(N.load().mh_verify_linear_proof_batch(_ctx(ctx).handle, n, _addr(ps), _addr(pt),
+                                                  _addr(off), _addr(terms), _addr(s), _addr(t),
+                                                  _addr(sa), _addr(ta), _addr(ok)))
+    return ok.astype(bool)
+
+
+def verify_dual_proof_v2_batch(src_hdrs, tgt_hdrs, md_blob, incl, cons, src, tgt, src_alh,
+                               tgt_alh, ctx: Optional[Context] = None) -> np.ndarray:
+    """status[n] (0 = verifies, else the MH_ERR_* of the Go error)."""
+    sh, th = _hdrs(src_hdrs), _hdrs(tgt_hdrs)
+    n = sh.size
+    if n == 0:
+        return np.zeros(0, np.int32)
+    mb, ml = _blob(md_blob)
+    io, it = _terms_csr(incl)
+    co, ct = _terms_csr(cons)
+    s = np.asarray(src, np.uint64)
+    t = np.asarray(tgt, np.uint64)
+    sa, ta = _d32(src_alh, n), _d32(tgt_alh, n)
+    st = np.zeros(n, np.int32)
+    N.check(N.load().mh_verify_dual_proof_v2_batch(
+        _ctx(ctx).handle, n, _addr(sh), _addr(th), _addr(mb), ml, _addr(io), _addr(it),
+        _addr(co), _addr(ct), _addr(s), _addr(t), _addr(sa), _addr(ta), _addr(st)))
+    return st
+
+
+def VerifyDualProofV2(src_hdr, tgt_hdr, md_blob, incl, cons, src, tgt, src_alh, tgt_alh,
+                      ctx: Optional[Context] = None) -> None:
+    """Go-shaped single proof: raises the Go error, returns None on success."""
+    st = verify_dual_proof_v2_batch([src_hdr], [tgt_hdr], md_blob, [incl], [cons], [src], [tgt],
+                                    [src_alh], [tgt_alh], ctx)
+    N.check(int(st[0]))
+
+
+def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
+                   max_key_len: int = DEFAULT_MAX_KEY_LEN, max_txs: Optional[int] = None,
+                   ctx: Optional[Context] = None):
+    """-> (status, ntx, consumed, hdrs[ntx] TX_HEADER (Eh rebuilt), alh[ntx,32], per_tx[ntx])
+
+    status is the structural error that stopped parsing (0 at a clean end);
+    per_tx[k] is 0 or MH_ERR_CORRUPTED_DATA (ALH mismatch)."""
+    b = _u8(buf)
+    cap = max(1, len(b) // 90 + 1)
+    if max_txs is not None:
+        cap = max(1, min(cap, max_txs))
+    hd = np.zeros(cap, TX_HEADER)
+    alh = np.zeros((cap, 32), np.uint8)
+    sts = np.zeros(cap, np.int32)
+    ntx, used = C.c_uint64(0), C.c_uint64(0)
+    rc = N.load().mh_txlog_validate(_ctx(ctx).handle, _addr(b) if b.size else None, b.size,
+                                    max_entries, max_key_len,
+                                    cap if max_txs is None else min(cap, max_txs), C.byref(ntx),
+                                    C.byref(used), _addr(hd), _addr(alh), _addr(sts))
+    if rc < 0:
+        N.check(rc)
+    k = ntx.value
+    return rc, k, used.value, hd[:k].copy(), alh[:k].copy(), sts[:k].copy()

@@ -44,6 +44,19 @@ extern "C" {
 #define MH_ERR_CANNOT_RESET_TO_LARGER 7 /* ahtree.ErrCannotResetToLargerSize ahtree.go:45 */
 #define MH_ERR_NO_DEVICE 8           /* no usable gfx950 device / library not initialised */
 #define MH_ERR_OUT_OF_MEMORY 9
+/* transaction layer (embedded/store) */
+#define MH_ERR_SOURCE_TX_NEWER 10       /* store.ErrSourceTxNewerThanTargetTx immustore.go:101 */
+#define MH_ERR_UNEXPECTED_LINKING 11    /* store.ErrUnexpectedLinkingError immustore.go:53 */
+#define MH_ERR_INCLUSION_NOT_VALID 12   /* "inclusion proof does NOT validate" verification.go:349 */
+#define MH_ERR_CONSISTENCY_NOT_VALID 13 /* "consistency proof does NOT validate" verification.go:368 */
+#define MH_ERR_CORRUPTED_DATA 14        /* store.ErrCorruptedData immustore.go:77 (ALH mismatch, tx.go:625) */
+#define MH_ERR_CORRUPTED_MAX_ENTRIES 15 /* ErrCorruptedTxDataMaxTxEntriesExceeded immustore.go:72 */
+#define MH_ERR_CORRUPTED_MAX_KEYLEN 16  /* ErrCorruptedTxDataMaxKeyLenExceeded immustore.go:75 */
+#define MH_ERR_CORRUPTED_UNKNOWN_VERSION 17 /* ErrCorruptedTxDataUnknownHeaderVersion immustore.go:74 */
+#define MH_ERR_TRUNCATED 18             /* record cut short (io.ErrUnexpectedEOF from the reader) */
+
+#define MH_MAX_TX_METADATA_LEN 268 /* maxTxMetadataLen tx_metadata.go:36-39 */
+#define MH_MAX_KV_METADATA_LEN 11  /* maxKVMetadataLen kv_metadata.go:41-43 */
 
 /* ahtree verification kinds (embedded/ahtree/verification.go) */
 #define MH_AHT_INCLUSION 0      /* VerifyInclusion      verification.go:21 */
@@ -51,6 +64,22 @@ extern "C" {
 #define MH_AHT_LAST_INCLUSION 2 /* VerifyLastInclusion  verification.go:111 */
 
 typedef struct mh_ctx mh_ctx;
+
+/* TxHeader (embedded/store/tx.go:103-117) as a plain C struct.  md_len bytes of
+ * TxMetadata.Bytes() (version 1 only) live at md_blob + md_off, md_blob being
+ * the buffer passed next to the headers.  136 bytes, 8-byte aligned. */
+typedef struct mh_tx_header {
+    uint64_t id;
+    int64_t ts;
+    uint64_t bl_tx_id;
+    uint8_t bl_root[32];
+    uint8_t prev_alh[32];
+    uint8_t eh[32];
+    uint32_t version; /* 0 or 1 (TxHeader.Version) */
+    uint32_t nentries;
+    uint32_t md_len;
+    uint32_t md_off;
+} mh_tx_header;
 typedef struct mh_htree mh_htree;
 typedef struct mh_ahtree mh_ahtree;
 
@@ -198,6 +227,71 @@ int mh_dev_ahtree_verify_batch(mh_ctx *ctx, int kind, uint64_t nproofs, const ui
                                const uint64_t *j, const uint64_t *term_off, const uint8_t *terms,
                                const uint8_t *a, const uint8_t *b, uint8_t *ok,
                                uint8_t *eval_out);
+
+/* ---------------------------------------------------------------- tx layer
+ * SURVEY.md 8(a) a7 (header hashes), a13 (linear / dual proofs), a14 (tx-log
+ * read-path validation) and a3 for many trees at once.  Hashing runs on the
+ * device; the host side parses records and combines verdicts. */
+
+/* TxHeader.Alh for n headers (tx.go:249-319: innerHash then
+ * SHA256(BE64 id || prevAlh || innerHash)).  inner_out may be NULL.
+ * Replaces per-header hdr.Alh() calls (tx.go:307, verification.go:141-150,
+ * 317-325).  MH_ERR_ILLEGAL_ARGUMENTS: version not 0/1, md on a v0 header or
+ * md_len > MH_MAX_TX_METADATA_LEN, md outside md_blob. */
+int mh_tx_alh_batch(mh_ctx *ctx, uint64_t n, const mh_tx_header *hdrs, const uint8_t *md_blob,
+                    uint64_t md_blob_len, uint8_t *inner_out, uint8_t *alh_out);
+/* Device variant: hdrs / md_blob / outputs in device memory; eh (nullable,
+ * n x 32) replaces hdrs[k].eh (e.g. Eh just built on the device).  scratch:
+ * n * 384 bytes of device memory.  Arguments are not validated. */
+int mh_dev_tx_alh_batch(mh_ctx *ctx, uint64_t n, const mh_tx_header *hdrs, const uint8_t *md_blob,
+                        const uint8_t *eh, uint8_t *scratch, uint8_t *inner_out, uint8_t *alh_out);
+
+/* Many independent htrees in one pass (Tx.BuildHashTree tx.go:332-355 over
+ * many txs, e.g. the MaxConcurrency concurrent commits at immustore.go:1632):
+ * tree t is digests[leaf_off[t] .. leaf_off[t+1]) and gets roots[t]
+ * (width 0 -> SHA256(nil), htree.go:73-77).  leaf_off has ntrees + 1 entries. */
+int mh_htree_build_many(mh_ctx *ctx, uint64_t ntrees, const uint64_t *leaf_off,
+                        const uint8_t *digests, uint8_t *roots);
+
+/* VerifyLinearProof (verification.go:40-64) for n proofs: proof p has
+ * SourceTxID proof_src[p], TargetTxID proof_tgt[p] and terms
+ * terms[term_off[p] .. term_off[p+1]); it is checked against src[p], tgt[p],
+ * src_alh[p], tgt_alh[p].  ok[p] = 1 iff it verifies. */
+int mh_verify_linear_proof_batch(mh_ctx *ctx, uint64_t n, const uint64_t *proof_src,
+                                 const uint64_t *proof_tgt, const uint64_t *term_off,
+                                 const uint8_t *terms, const uint64_t *src, const uint64_t *tgt,
+                                 const uint8_t *src_alh, const uint8_t *tgt_alh, uint8_t *ok);
+
+/* VerifyDualProofV2 (verification.go:304-372) for n proofs.  Proof p:
+ * src_hdr[p], tgt_hdr[p] (md in md_blob), InclusionProof terms
+ * incl_terms[incl_off[p] .. incl_off[p+1]), ConsistencyProof terms
+ * cons_terms[cons_off[p] ..), checked against src[p], tgt[p], src_alh[p],
+ * tgt_alh[p].  status[p] = MH_OK or the Go error: MH_ERR_ILLEGAL_ARGUMENTS,
+ * MH_ERR_SOURCE_TX_NEWER, MH_ERR_UNEXPECTED_LINKING,
+ * MH_ERR_INCLUSION_NOT_VALID, MH_ERR_CONSISTENCY_NOT_VALID. */
+int mh_verify_dual_proof_v2_batch(mh_ctx *ctx, uint64_t n, const mh_tx_header *src_hdr,
+                                  const mh_tx_header *tgt_hdr, const uint8_t *md_blob,
+                                  uint64_t md_blob_len, const uint64_t *incl_off,
+                                  const uint8_t *incl_terms, const uint64_t *cons_off,
+                                  const uint8_t *cons_terms, const uint64_t *src,
+                                  const uint64_t *tgt, const uint8_t *src_alh,
+                                  const uint8_t *tgt_alh, int32_t *status);
+
+/* Tx-log read path (Tx.readFrom tx.go:388-630: readHeader, readEntry,
+ * buildAndValidateHtree) over buf = back-to-back tx records as written by
+ * immustore.go:1812-1924.  Parses up to max_txs records, stopping at id 0 (a
+ * preallocated tail) or at the first structural error, which is returned
+ * (MH_ERR_CORRUPTED_* / MH_ERR_TRUNCATED) with *consumed = that record's
+ * offset; then, on the device, rebuilds every entry digest, every tx's htree
+ * (Eh) and Alh and compares it with the stored one: status[k] = MH_OK or
+ * MH_ERR_CORRUPTED_DATA ("ALH mismatch", tx.go:625).  Optional outputs
+ * (capacity max_txs): hdrs (md_off relative to buf, eh = rebuilt Eh) and
+ * alh (recomputed).  KV / tx metadata are hashed as stored; the reference
+ * re-serializes its parsed attributes, which gives the same bytes for every
+ * record it writes. */
+int mh_txlog_validate(mh_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                      uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx, uint64_t *consumed,
+                      mh_tx_header *hdrs, uint8_t *alh, int32_t *status);
 
 #ifdef __cplusplus
 }

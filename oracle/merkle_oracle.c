@@ -18,7 +18,10 @@
 #endif
 
 enum { OK = 0, ERR_MAX_WIDTH = 1, ERR_ILLEGAL_ARGS = 2, ERR_ILLEGAL_STATE = 3, ERR_EMPTY = 4,
-       ERR_UNEXISTENT = 5, ERR_MD_UNSUPPORTED = 6 };
+       ERR_UNEXISTENT = 5, ERR_MD_UNSUPPORTED = 6, ERR_SOURCE_TX_NEWER = 10,
+       ERR_UNEXPECTED_LINKING = 11, ERR_INCLUSION_NOT_VALID = 12, ERR_CONSISTENCY_NOT_VALID = 13,
+       ERR_CORRUPTED_DATA = 14, ERR_CORRUPTED_MAX_ENTRIES = 15, ERR_CORRUPTED_MAX_KEYLEN = 16,
+       ERR_CORRUPTED_UNKNOWN_VERSION = 17, ERR_TRUNCATED = 18 };
 
 /* ------------------------------------------------------------------ SHA-256 */
 static const uint32_t K256[64] = {
@@ -401,7 +404,7 @@ int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmd
                       const uint8_t blroot[32], uint8_t out[32]) {
     /* tx.go:249-302: ts + version + (v0: BE16 nentries | v1: BE16 mdLen md BE32 nentries)
      * + eh + blTxID + blRoot */
-    uint8_t b[8 + 2 + 2 + 256 + 4 + 32 + 8 + 32];
+    uint8_t b[8 + 2 + 2 + 268 + 4 + 32 + 8 + 32];
     size_t i = 0;
     for (int k = 7; k >= 0; k--) b[i++] = (uint8_t)(ts >> (8 * k));
     b[i++] = (uint8_t)(version >> 8);
@@ -411,7 +414,7 @@ int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmd
         b[i++] = (uint8_t)(nentries >> 8);
         b[i++] = (uint8_t)nentries;
     } else if (version == 1) {
-        if (txmdlen > 256) return ERR_ILLEGAL_ARGS;
+        if (txmdlen > 268) return ERR_ILLEGAL_ARGS; /* maxTxMetadataLen, tx_metadata.go:36-39 */
         b[i++] = (uint8_t)(txmdlen >> 8);
         b[i++] = (uint8_t)txmdlen;
         if (txmdlen) memcpy(b + i, txmd, txmdlen);
@@ -681,4 +684,165 @@ void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed) {
         else
             memcpy(dst + w * 8, &z, left);
     }
+}
+
+/* ------------------------------------------------------------------ tx layer */
+int orc_tx_header_alh(const orc_tx_header *h, const uint8_t *md_blob, uint8_t inner[32],
+                      uint8_t alh[32]) {
+    /* TxHeader.Alh, tx.go:307-319 over innerHash, tx.go:249-302 */
+    uint8_t in[32];
+    int st = orc_tx_inner_hash((uint64_t)h->ts, (int)h->version,
+                               h->md_len ? md_blob + h->md_off : NULL, h->md_len, h->nentries,
+                               h->eh, h->bl_tx_id, h->bl_root, in);
+    if (st) return st;
+    if (inner) memcpy(inner, in, 32);
+    orc_tx_alh(h->id, h->prev_alh, in, alh);
+    return OK;
+}
+
+int orc_verify_linear_proof(uint64_t p_src, uint64_t p_tgt, const uint8_t *terms, uint32_t nterms,
+                            uint64_t src, uint64_t tgt, const uint8_t src_alh[32],
+                            const uint8_t tgt_alh[32]) {
+    /* store/verification.go:40-64 */
+    if (p_src != src || p_tgt != tgt) return 0;
+    if (p_src == 0 || p_src > p_tgt || nterms == 0 || memcmp(src_alh, terms, 32) != 0) return 0;
+    if ((uint64_t)nterms != tgt - src + 1) return 0;
+    uint8_t c[32];
+    memcpy(c, terms, 32);
+    for (uint32_t i = 1; i < nterms; i++) orc_tx_alh(p_src + i, c, terms + 32 * (size_t)i, c);
+    return memcmp(tgt_alh, c, 32) == 0;
+}
+
+static void leaf_for(const uint8_t d[32], uint8_t out[32]) { leaf_hash(d, out); }
+
+int orc_verify_linear_advance_proof(int has_proof, const uint8_t *lin_terms, uint32_t nlin,
+                                    const uint8_t *incl_terms, const uint32_t *incl_off,
+                                    uint32_t nincl, uint64_t start, uint64_t end,
+                                    const uint8_t end_alh[32], const uint8_t root[32],
+                                    uint64_t size) {
+    /* store/verification.go:66-125 */
+    if (end < start) return 0;
+    if (end <= start + 1) return 1;
+    if (!has_proof || (uint64_t)nlin != end - start || (uint64_t)nincl != end - start - 1) return 0;
+    uint8_t c[32], lf[32];
+    memcpy(c, lin_terms, 32);
+    for (uint64_t tx = start + 1; tx < end; tx++) {
+        const uint64_t k = tx - start - 1;
+        leaf_for(c, lf);
+        if (!orc_ahtree_verify_inclusion(incl_terms + 32 * (size_t)incl_off[k],
+                                         incl_off[k + 1] - incl_off[k], tx, size, lf, root))
+            return 0;
+        orc_tx_alh(tx + 1, c, lin_terms + 32 * (size_t)(tx - start), c);
+    }
+    return memcmp(c, end_alh, 32) == 0;
+}
+
+int orc_verify_dual_proof_v2(const orc_tx_header *sh, const orc_tx_header *th,
+                             const uint8_t *md_blob, const uint8_t *incl, uint32_t nincl,
+                             const uint8_t *cons, uint32_t ncons, uint64_t src, uint64_t tgt,
+                             const uint8_t src_alh[32], const uint8_t tgt_alh[32]) {
+    /* store/verification.go:304-372 */
+    if (!sh || !th || sh->id == 0 || sh->id != src || th->id != tgt) return ERR_ILLEGAL_ARGS;
+    if (src > tgt) return ERR_SOURCE_TX_NEWER;
+    uint8_t a[32];
+    if (orc_tx_header_alh(sh, md_blob, NULL, a) || memcmp(a, src_alh, 32)) return ERR_ILLEGAL_ARGS;
+    if (orc_tx_header_alh(th, md_blob, NULL, a) || memcmp(a, tgt_alh, 32)) return ERR_ILLEGAL_ARGS;
+    if (sh->id - 1 != sh->bl_tx_id || th->id - 1 != th->bl_tx_id) return ERR_UNEXPECTED_LINKING;
+    if (src == tgt) return OK;
+    uint8_t lf[32];
+    leaf_for(src_alh, lf);
+    if (!orc_ahtree_verify_inclusion(incl, nincl, src, th->bl_tx_id, lf, th->bl_root))
+        return ERR_INCLUSION_NOT_VALID;
+    int ok;
+    if (src == 1)
+        ok = orc_ahtree_verify_consistency(cons, ncons, src, th->bl_tx_id, lf, th->bl_root);
+    else
+        ok = orc_ahtree_verify_consistency(cons, ncons, sh->bl_tx_id, th->bl_tx_id, sh->bl_root,
+                                           th->bl_root);
+    return ok ? OK : ERR_CONSISTENCY_NOT_VALID;
+}
+
+/* ---- tx log records (immustore.go:1812-1924 writer, tx.go:388-630 reader) */
+static int rd(uint64_t len, uint64_t *p, uint64_t n) {
+    if (*p + n > len) return 0;
+    *p += n;
+    return 1;
+}
+static uint64_t be(const uint8_t *b, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | b[i];
+    return v;
+}
+
+int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                       uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
+                       uint64_t *consumed_out, uint8_t *alh_out, int32_t *status_out) {
+    uint64_t p = 0, ntx = 0;
+    int rc = OK;
+    uint8_t *digs = (uint8_t *)malloc((size_t)(max_entries ? max_entries : 1) * 32);
+    uint8_t *lv = (uint8_t *)malloc((size_t)orc_htree_levels_len(max_entries ? max_entries : 1) * 32);
+    while (ntx < max_txs) {
+        const uint64_t p0 = p;
+        orc_tx_header h;
+        memset(&h, 0, sizeof h);
+        uint8_t txmd[268];
+        /* readHeader, tx.go:419-518 */
+        if (p + 8 > len) break;
+        h.id = be(buf + p, 8);
+        if (h.id == 0) break; /* preallocated tail reads as EOF */
+        p += 8;
+        if (!rd(len, &p, 16 + 64 + 2)) { rc = ERR_TRUNCATED; p = p0; break; }
+        h.ts = (int64_t)be(buf + p0 + 8, 8);
+        h.bl_tx_id = be(buf + p0 + 16, 8);
+        memcpy(h.bl_root, buf + p0 + 24, 32);
+        memcpy(h.prev_alh, buf + p0 + 56, 32);
+        h.version = (uint32_t)be(buf + p0 + 88, 2);
+        if (h.version == 0) {
+            if (!rd(len, &p, 2)) { rc = ERR_TRUNCATED; p = p0; break; }
+            h.nentries = (uint32_t)be(buf + p - 2, 2);
+        } else if (h.version == 1) {
+            if (!rd(len, &p, 2)) { rc = ERR_TRUNCATED; p = p0; break; }
+            h.md_len = (uint32_t)be(buf + p - 2, 2);
+            if (h.md_len > 268) { rc = ERR_CORRUPTED_DATA; p = p0; break; }
+            if (!rd(len, &p, h.md_len)) { rc = ERR_TRUNCATED; p = p0; break; }
+            memcpy(txmd, buf + p - h.md_len, h.md_len);
+            if (!rd(len, &p, 4)) { rc = ERR_TRUNCATED; p = p0; break; }
+            h.nentries = (uint32_t)be(buf + p - 4, 4);
+        } else {
+            rc = ERR_CORRUPTED_UNKNOWN_VERSION;
+            p = p0;
+            break;
+        }
+        if (h.nentries > max_entries) { rc = ERR_CORRUPTED_MAX_ENTRIES; p = p0; break; }
+        /* readEntry, tx.go:520-588 */
+        int bad = 0;
+        for (uint32_t e = 0; e < h.nentries && !bad; e++) {
+            uint64_t q = p;
+            if (!rd(len, &p, 2)) { bad = ERR_TRUNCATED; break; }
+            const uint64_t ml = be(buf + q, 2);
+            if (ml > 11) { bad = ERR_CORRUPTED_DATA; break; } /* maxKVMetadataLen */
+            if (!rd(len, &p, ml + 2)) { bad = ERR_TRUNCATED; break; }
+            const uint64_t kl = be(buf + p - 2, 2);
+            if (kl > max_key_len) { bad = ERR_CORRUPTED_MAX_KEYLEN; break; }
+            if (!rd(len, &p, kl + 4 + 8 + 32)) { bad = ERR_TRUNCATED; break; }
+            const uint8_t *md = buf + q + 2, *key = buf + q + 4 + ml, *hv = buf + p - 32;
+            int st = orc_entry_digest((int)h.version, key, kl, md, ml, hv, digs + 32 * (size_t)e);
+            if (st) { bad = st; break; }
+        }
+        if (bad) { rc = bad; p = p0; break; }
+        /* buildAndValidateHtree, tx.go:605-630 */
+        if (!rd(len, &p, 32)) { rc = ERR_TRUNCATED; p = p0; break; }
+        orc_htree_build(digs, h.nentries, lv, h.eh);
+        uint8_t a[32];
+        orc_tx_header_alh(&h, txmd, NULL, a);
+        /* the md blob for orc_tx_header_alh is txmd itself at offset 0 */
+        if (alh_out) memcpy(alh_out + 32 * ntx, a, 32);
+        if (status_out) status_out[ntx] = memcmp(a, buf + p - 32, 32) ? ERR_CORRUPTED_DATA : OK;
+        ntx++;
+    }
+    free(digs);
+    free(lv);
+    if (ntx_out) *ntx_out = ntx;
+    if (consumed_out) *consumed_out = p;
+    return rc;
 }

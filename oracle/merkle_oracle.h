@@ -71,6 +71,52 @@ int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmd
                       const uint8_t blroot[32], uint8_t out[32]);
 void orc_tx_alh(uint64_t id, const uint8_t prev_alh[32], const uint8_t inner[32], uint8_t out[32]);
 
+/* Transaction header (embedded/store/tx.go:103-117), same layout as
+ * include/immustore_merkle.h mh_tx_header.  md_len bytes of TxMetadata.Bytes()
+ * live at md_blob + md_off (v1 only). */
+typedef struct orc_tx_header {
+    uint64_t id;
+    int64_t ts;
+    uint64_t bl_tx_id;
+    uint8_t bl_root[32];
+    uint8_t prev_alh[32];
+    uint8_t eh[32];
+    uint32_t version;
+    uint32_t nentries;
+    uint32_t md_len;
+    uint32_t md_off;
+} orc_tx_header;
+
+/* tx.go:249-319 on a header struct; inner may be NULL. */
+int orc_tx_header_alh(const orc_tx_header *h, const uint8_t *md_blob, uint8_t inner[32],
+                      uint8_t alh[32]);
+/* store/verification.go:40-64 (VerifyLinearProof); returns 1 = verifies. */
+int orc_verify_linear_proof(uint64_t p_src, uint64_t p_tgt, const uint8_t *terms, uint32_t nterms,
+                            uint64_t src, uint64_t tgt, const uint8_t src_alh[32],
+                            const uint8_t tgt_alh[32]);
+/* store/verification.go:66-125 (VerifyLinearAdvanceProof); incl_off has
+ * nincl + 1 entries (term offsets of each nested inclusion proof). */
+int orc_verify_linear_advance_proof(int has_proof, const uint8_t *lin_terms, uint32_t nlin,
+                                    const uint8_t *incl_terms, const uint32_t *incl_off,
+                                    uint32_t nincl, uint64_t start, uint64_t end,
+                                    const uint8_t end_alh[32], const uint8_t root[32],
+                                    uint64_t size);
+/* store/verification.go:304-372 (VerifyDualProofV2): MH_OK or the status of
+ * the Go error (2 ErrIllegalArguments, 10 ErrSourceTxNewerThanTargetTx,
+ * 11 ErrUnexpectedLinkingError, 12 inclusion / 13 consistency not valid). */
+int orc_verify_dual_proof_v2(const orc_tx_header *sh, const orc_tx_header *th,
+                             const uint8_t *md_blob, const uint8_t *incl, uint32_t nincl,
+                             const uint8_t *cons, uint32_t ncons, uint64_t src, uint64_t tgt,
+                             const uint8_t src_alh[32], const uint8_t tgt_alh[32]);
+/* Tx log read path (tx.go:388-630: readHeader, readEntry, buildAndValidateHtree)
+ * over a buffer of back-to-back tx records (immustore.go:1812-1924).  Stops at
+ * id 0 (preallocated tail), at max_txs, or at the first structural error
+ * (returned; *consumed_out = offset of the failing record).  Per parsed tx:
+ * the recomputed Alh and status 0 / 14 (ALH mismatch, ErrCorruptedData). */
+int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                       uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
+                       uint64_t *consumed_out, uint8_t *alh_out, int32_t *status_out);
+
 /* ahtree: embedded/ahtree/ahtree.go. The dLog is a flat array of digests. */
 uint64_t orc_ahtree_nodes_upto(uint64_t n);  /* ahtree.go:492-511 */
 uint64_t orc_ahtree_nodes_until(uint64_t n); /* ahtree.go:485-490 */

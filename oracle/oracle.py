@@ -68,6 +68,16 @@ def lib():
         L.orc_ahtree_eval_last_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, u8p]
         L.orc_ahtree_verify_last_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, u8p]
         L.orc_fill_random.argtypes = [u8p, C.c_uint64, C.c_uint64]
+        L.orc_tx_header_alh.argtypes = [u8p, u8p, u8p, u8p]
+        L.orc_verify_linear_proof.argtypes = [C.c_uint64, C.c_uint64, u8p, C.c_uint32, C.c_uint64,
+                                              C.c_uint64, u8p, u8p]
+        L.orc_verify_linear_advance_proof.argtypes = [C.c_int, u8p, C.c_uint32, u8p, u32p,
+                                                      C.c_uint32, C.c_uint64, C.c_uint64, u8p,
+                                                      u8p, C.c_uint64]
+        L.orc_verify_dual_proof_v2.argtypes = [u8p, u8p, u8p, u8p, C.c_uint32, u8p, C.c_uint32,
+                                               C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_txlog_validate.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
+                                         u64p, u64p, u8p, C.POINTER(C.c_int32)]
         L.orc_sha256_use_shani.argtypes = [C.c_int]
         _LIB = L
     return _LIB
@@ -290,3 +300,68 @@ def use_shani(enable):
 
 def has_shani():
     return bool(lib().orc_sha256_has_shani())
+
+
+# ---------------------------------------------------------------- tx layer
+# Same layout as orc_tx_header / include/immustore_merkle.h mh_tx_header.
+TX_HEADER = np.dtype([("id", "<u8"), ("ts", "<i8"), ("bl_tx_id", "<u8"), ("bl_root", "u1", 32),
+                      ("prev_alh", "u1", 32), ("eh", "u1", 32), ("version", "<u4"),
+                      ("nentries", "<u4"), ("md_len", "<u4"), ("md_off", "<u4")])
+assert TX_HEADER.itemsize == 136
+
+
+def tx_header_alh(hdr, md_blob=b""):
+    """hdr: a TX_HEADER record (np.void or 1-element array)."""
+    h = np.ascontiguousarray(np.asarray(hdr, TX_HEADER).reshape(1))
+    mb = _u8(md_blob) if len(md_blob) else np.zeros(1, np.uint8)
+    inner, alh = np.zeros(32, np.uint8), np.zeros(32, np.uint8)
+    st = lib().orc_tx_header_alh(_p(h.view(np.uint8)), _p(mb), _p(inner), _p(alh))
+    return st, inner.tobytes(), alh.tobytes()
+
+
+def verify_linear_proof(p_src, p_tgt, terms, src, tgt, src_alh, tgt_alh):
+    tp, nt = _terms(terms)
+    return bool(lib().orc_verify_linear_proof(p_src, p_tgt, tp, nt, src, tgt,
+                                              _p(_u8(src_alh)), _p(_u8(tgt_alh))))
+
+
+def verify_linear_advance_proof(proof, start, end, end_alh, root, size):
+    """proof: None or (linear_terms, [inclusion_terms, ...])."""
+    if proof is None:
+        z = np.zeros((1, 32), np.uint8)
+        return bool(lib().orc_verify_linear_advance_proof(0, _p(z), 0, _p(z), None, 0, start, end,
+                                                          _p(_u8(end_alh)), _p(_u8(root)), size))
+    lin, incs = proof
+    lp, nl = _terms(lin)
+    off = np.zeros(len(incs) + 1, np.uint32)
+    for k, ip in enumerate(incs):
+        off[k + 1] = off[k] + len(ip)
+    ip_, _ = _terms([x for ip in incs for x in ip])
+    return bool(lib().orc_verify_linear_advance_proof(1, lp, nl, ip_, _p(off, u32p), len(incs),
+                                                      start, end, _p(_u8(end_alh)),
+                                                      _p(_u8(root)), size))
+
+
+def verify_dual_proof_v2(sh, th, md_blob, incl, cons, src, tgt, src_alh, tgt_alh):
+    a = np.ascontiguousarray(np.asarray(sh, TX_HEADER).reshape(1))
+    b = np.ascontiguousarray(np.asarray(th, TX_HEADER).reshape(1))
+    mb = _u8(md_blob) if len(md_blob) else np.zeros(1, np.uint8)
+    ip_, ni = _terms(incl)
+    cp_, nc = _terms(cons)
+    return lib().orc_verify_dual_proof_v2(_p(a.view(np.uint8)), _p(b.view(np.uint8)), _p(mb),
+                                          ip_, ni, cp_, nc, src, tgt,
+                                          _p(_u8(src_alh)), _p(_u8(tgt_alh)))
+
+
+def txlog_validate(buf, max_entries=1024, max_key_len=1024, max_txs=1 << 40):
+    """-> (status, ntx, consumed, alh[ntx,32], per_tx_status[ntx])"""
+    b = _u8(buf) if len(buf) else np.zeros(1, np.uint8)
+    cap = max(1, min(max_txs, len(buf) // 90 + 1))
+    alh = np.zeros((cap, 32), np.uint8)
+    sts = np.zeros(cap, np.int32)
+    ntx, used = C.c_uint64(0), C.c_uint64(0)
+    st = lib().orc_txlog_validate(_p(b), len(buf), max_entries, max_key_len, min(max_txs, cap),
+                                  C.byref(ntx), C.byref(used), _p(alh),
+                                  sts.ctypes.data_as(C.POINTER(C.c_int32)))
+    n = ntx.value
+    return st, n, used.value, alh[:n].copy(), sts[:n].copy()

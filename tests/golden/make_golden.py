@@ -338,8 +338,34 @@ def fixture_store(root):
     ours = b"".join(aht.dlog)
     assert ours[:len(dlog)] == dlog, "dLog mismatch"
     assert n_aht == nodes_upto(len(payloads))
+    # raw tx-log records (data file of the reference's test store) for the
+    # read-path validation tests, and dual / linear proofs built the way
+    # ImmuStore.DualProofV2 / LinearProof build them (immustore.go:2356-2387,
+    # :2471-2510) from this store's own headers and dLog
+    raw = read_appendable(os.path.join(root, "tx/00000000.tx"))
+    hdrs = [t["header"] for t in txs]
+    dual, linear = [], []
+    for s_ in range(1, len(hdrs) + 1):
+        for t_ in range(s_, len(hdrs) + 1):
+            sh, th = hdrs[s_ - 1], hdrs[t_ - 1]
+            if sh["bltxid"] != s_ - 1 or th["bltxid"] != t_ - 1:
+                continue
+            case = {"src": s_, "tgt": t_, "incl": [], "cons": []}
+            if s_ < t_:
+                case["incl"] = [x.hex() for x in aht.inclusion_proof(s_, th["bltxid"])]
+                case["cons"] = [x.hex() for x in aht.consistency_proof(max(1, sh["bltxid"]),
+                                                                       th["bltxid"])]
+            dual.append(case)
+            terms = [sh["alh"]] + [inner_hash(hdrs[k - 1]).hex() for k in range(s_ + 1, t_ + 1)]
+            c = bytes.fromhex(terms[0])
+            for k in range(1, len(terms)):
+                c = sha(struct.pack(">Q", s_ + k) + c + bytes.fromhex(terms[k]))
+            assert c.hex() == th["alh"]
+            if (t_ - s_) % 7 == 0 or t_ == len(hdrs):
+                linear.append({"src": s_, "tgt": t_, "terms": terms})
     return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(), "n_values": sum(
-        1 for t in txs for e in t["entries"] if "value" in e)}
+        1 for t in txs for e in t["entries"] if "value" in e), "txlog": raw.hex(),
+        "dual_v2": dual, "linear": linear}
 
 
 # ---------------------------------------------------------------- synthetic

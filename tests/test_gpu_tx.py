@@ -1,0 +1,233 @@
+"""GPU parity of the tx layer (SURVEY.md 8(a) a7, a13, a14 and a3 over many
+trees) through the C ABI, against the reference's Go-written stores
+(tests/golden/immudb_fixtures.json: raw tx logs, stored Alh, DualProofV2 and
+linear proofs built from the stores' own dLog) and the oracle on synthetic
+logs.  Bit-exact digests and identical statuses.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from tx_util import headers_from_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def m():
+    import torch  # noqa: F401
+    import immustore_amd as m
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return m
+
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+def test_tx_alh_batch_fixture_headers(m, ctx, fixtures):
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        inner, alh = m.tx_alh_batch(recs, blob, ctx)
+        assert [a.tobytes() for a in alh] == alhs, name
+
+
+def test_tx_alh_batch_synthetic_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(7)
+    n = 3000
+    recs = np.zeros(n, m.TX_HEADER)
+    blob = bytearray()
+    for k in range(n):
+        r = recs[k]
+        r["id"] = int(rng.integers(1, 1 << 62))
+        r["ts"] = int(rng.integers(-(1 << 62), 1 << 62))
+        r["bl_tx_id"] = int(rng.integers(0, 1 << 62))
+        for f in ("bl_root", "prev_alh", "eh"):
+            r[f] = rng.integers(0, 256, 32, dtype=np.uint8)
+        r["version"] = k % 2
+        r["nentries"] = int(rng.integers(0, 1 << 31))
+        if r["version"] == 1:
+            ml = [0, 1, 9, 12, 100, 268][k % 6]
+            r["md_len"], r["md_off"] = ml, len(blob)
+            blob += rng.integers(0, 256, ml, dtype=np.uint8).tobytes()
+        else:
+            r["nentries"] &= 0xFFFF
+    inner, alh = m.tx_alh_batch(recs, bytes(blob), ctx)
+    for k in range(0, n, 7):
+        st, oi, oa = orc.tx_header_alh(recs[k], bytes(blob))
+        assert st == 0 and inner[k].tobytes() == oi and alh[k].tobytes() == oa, k
+    bad = recs[:2].copy()
+    bad[0]["version"] = 2
+    with pytest.raises(m.ErrIllegalArguments):
+        m.tx_alh_batch(bad, bytes(blob), ctx)
+    bad = recs[:2].copy()
+    bad[0]["version"], bad[0]["md_len"] = 0, 3
+    with pytest.raises(m.ErrMetadataUnsupported):
+        m.tx_alh_batch(bad, bytes(blob), ctx)
+
+
+def test_htree_build_many_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(8)
+    widths = [0, 1, 2, 3, 4, 5, 7, 8, 9, 16, 17, 31, 33, 100, 1000, 1024, 1025, 1, 1, 0, 2] + \
+        list(rng.integers(1, 300, 400))
+    trees = [rng.integers(0, 256, (w, 32), dtype=np.uint8) for w in widths]
+    roots = m.htree_build_many(trees, ctx)
+    for t, r in zip(trees, roots):
+        assert r.tobytes() == orc.htree_build(t)[1]
+
+
+def test_txlog_validate_fixture_stores(m, ctx, fixtures):
+    for name, fx in fixtures.items():
+        raw = bytes.fromhex(fx["txlog"])
+        rc, n, used, hdrs, alh, sts = m.txlog_validate(raw, ctx=ctx)
+        assert rc == 0 and n == len(fx["txs"]) and used <= len(raw)
+        assert list(sts) == [0] * n
+        assert [a.tobytes().hex() for a in alh] == [t["header"]["alh"] for t in fx["txs"]]
+        assert [h["eh"].tobytes().hex() for h in hdrs] == [t["header"]["eh"] for t in fx["txs"]]
+        assert [int(h["id"]) for h in hdrs] == [t["header"]["id"] for t in fx["txs"]]
+
+
+def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True):
+    """Tx records in the immustore.go:1812-1924 layout with a valid Alh chain
+    (the stored alh of each record is the oracle's Alh over its own fields)."""
+    out = bytearray()
+    prev = orc.sha256(b"")
+    for k in range(ntx):
+        ver = int(rng.integers(0, 2)) if version_mix else 1
+        ne = int(rng.integers(0, max_entries + 1)) if k % 5 else int(rng.integers(1, 3))
+        txmd = b"" if ver == 0 else bytes(rng.integers(0, 256, [0, 0, 3, 268][k % 4], dtype=np.uint8))
+        ents, digs = bytearray(), []
+        for e in range(ne):
+            md = b"" if ver == 0 else [b"", b"\x00", b"\x01" + struct.pack(">Q", e), b"\x02",
+                                       b"\x00\x01" + struct.pack(">Q", k) + b"\x02"][(k + e) % 5]
+            key = bytes(rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8))
+            hv = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+            ents += struct.pack(">H", len(md)) + md + struct.pack(">H", len(key)) + key
+            ents += struct.pack(">IQ", int(rng.integers(0, 1 << 20)), int(rng.integers(0, 1 << 40)))
+            ents += hv
+            digs.append(orc.entry_digest(ver, key, md, hv)[1])
+        eh = orc.htree_build(np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))[1] if ne \
+            else orc.sha256(b"")
+        ts, bl = int(rng.integers(0, 1 << 40)), int(rng.integers(0, k + 1))
+        blroot = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        st, inner = orc.tx_inner_hash(ts, ver, txmd, ne, eh, bl, blroot)
+        assert st == 0
+        alh = orc.tx_alh(k + 1, prev, inner)
+        hdr = struct.pack(">QQQ", k + 1, ts, bl) + blroot + prev + struct.pack(">H", ver)
+        hdr += struct.pack(">H", ne) if ver == 0 else struct.pack(">H", len(txmd)) + txmd + \
+            struct.pack(">I", ne)
+        out += hdr + ents + alh
+        prev = alh
+    return bytes(out)
+
+
+def test_txlog_validate_synthetic_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(11)
+    raw = _synthetic_txlog(rng, 300, orc)
+    rc, n, used, hdrs, alh, sts = m.txlog_validate(raw, ctx=ctx)
+    o = orc.txlog_validate(raw)
+    assert (rc, n, used) == (o[0], o[1], o[2]) == (0, 300, len(raw))
+    assert np.array_equal(alh, o[3]) and list(sts) == list(o[4]) == [0] * 300
+    # corrupt a few hVals / stored alhs / a header field: per-tx statuses match
+    bad = bytearray(raw)
+    rng2 = np.random.default_rng(3)
+    for pos in rng2.integers(0, len(raw), 40):
+        bad[int(pos)] ^= 0x10
+    r1 = m.txlog_validate(bytes(bad), ctx=ctx)
+    r2 = orc.txlog_validate(bytes(bad))
+    assert (r1[0], r1[1], r1[2]) == (r2[0], r2[1], r2[2])
+    assert list(r1[5]) == list(r2[4])
+    assert np.array_equal(r1[4], r2[3])
+    # structural errors and limits agree
+    for kw in ({"max_entries": 5}, {"max_key_len": 10}, {"max_txs": 17}):
+        a = m.txlog_validate(raw, ctx=ctx, **kw)
+        b = orc.txlog_validate(raw, **kw)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]) and list(a[5]) == list(b[4]), kw
+    for cut in (1, 50, 91, len(raw) // 2, len(raw) - 1):
+        a = m.txlog_validate(raw[:cut], ctx=ctx)
+        b = orc.txlog_validate(raw[:cut])
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), cut
+
+
+def test_dual_proof_v2_fixture_cases(m, ctx, orc, fixtures):
+    seen = set()
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        S, T, I, Cn, SA, TA, exp = [], [], [], [], [], [], []
+
+        def add(s, t, incl, cons, sa, ta, sh=None, th=None):
+            S.append(s)
+            T.append(t)
+            I.append(incl)
+            Cn.append(cons)
+            SA.append(sa)
+            TA.append(ta)
+            sh_ = recs[s - 1] if sh is None else sh
+            th_ = recs[t - 1] if th is None else th
+            exp.append(orc.verify_dual_proof_v2(sh_, th_, blob, incl, cons, s, t, sa, ta))
+            return sh_, th_
+
+        SH, TH = [], []
+        for c in fx["dual_v2"]:
+            s, t = c["src"], c["tgt"]
+            incl = [bytes.fromhex(x) for x in c["incl"]]
+            cons = [bytes.fromhex(x) for x in c["cons"]]
+            for variant in range(4):
+                ii, cc, sa = list(incl), list(cons), alhs[s - 1]
+                if variant == 1 and ii:
+                    ii[0] = bytes([ii[0][0] ^ 1]) + ii[0][1:]
+                if variant == 2 and cc:
+                    cc[-1] = bytes([cc[-1][0] ^ 1]) + cc[-1][1:]
+                if variant == 3:
+                    sa = bytes(32)
+                a, b = add(s, t, ii, cc, sa, alhs[t - 1])
+                SH.append(a)
+                TH.append(b)
+        st = m.verify_dual_proof_v2_batch(np.array(SH), np.array(TH), blob, I, Cn, S, T, SA, TA,
+                                          ctx)
+        assert list(st) == exp, name
+        seen |= set(exp)
+    assert {0, 2, 12, 13} <= seen
+    # Go-shaped wrapper raises the Go error
+    fx = fixtures["long_linear_proof"]
+    recs, blob, alhs = headers_from_fixture(fx["txs"])
+    c = [x for x in fx["dual_v2"] if x["src"] < x["tgt"]][0]
+    s, t = c["src"], c["tgt"]
+    incl = [bytes.fromhex(x) for x in c["incl"]]
+    cons = [bytes.fromhex(x) for x in c["cons"]]
+    m.VerifyDualProofV2(recs[s - 1], recs[t - 1], blob, incl, cons, s, t, alhs[s - 1],
+                        alhs[t - 1], ctx)
+    with pytest.raises(m._native.ErrSourceTxNewerThanTargetTx):
+        m.VerifyDualProofV2(recs[t - 1], recs[s - 1], blob, incl, cons, t, s, alhs[t - 1],
+                            alhs[s - 1], ctx)
+
+
+def test_linear_proofs_fixture_and_random(m, ctx, orc, fixtures):
+    items, exp = [], []
+    for name, fx in fixtures.items():
+        alhs = [bytes.fromhex(t["header"]["alh"]) for t in fx["txs"]]
+        for c in fx["linear"]:
+            s, t = c["src"], c["tgt"]
+            terms = [bytes.fromhex(x) for x in c["terms"]]
+            for v in range(3):
+                tt = list(terms)
+                tgt = t
+                if v == 1 and len(tt) > 1:
+                    tt[-1] = bytes([tt[-1][0] ^ 2]) + tt[-1][1:]
+                if v == 2:
+                    tgt = t + 1
+                items.append((s, t, tt, s, tgt, alhs[s - 1], alhs[t - 1]))
+                exp.append(orc.verify_linear_proof(s, t, tt, s, tgt, alhs[s - 1], alhs[t - 1]))
+    z = bytes(32)
+    for it in [(0, 1, [z], 0, 1, z, z), (2, 1, [z], 2, 1, z, z), (1, 1, [], 1, 1, z, z),
+               (1, 1, [z], 1, 1, z, z)]:
+        items.append(it)
+        exp.append(orc.verify_linear_proof(*it))
+    got = m.verify_linear_proof_batch(items, ctx)
+    assert list(got) == exp
+    assert any(exp) and not all(exp)

@@ -1,0 +1,144 @@
+"""Oracle restatement of the tx layer against
+the reference's Go-written test stores: every stored Alh, the raw tx-log
+records, and DualProofV2 / linear proofs built from the stores' own headers
+and dLog (tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from tx_util import headers_from_fixture
+
+
+def test_header_alh_matches_stored(orc, fixtures):
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        for k in range(len(recs)):
+            st, _, a = orc.tx_header_alh(recs[k], blob)
+            assert st == 0 and a == alhs[k], (name, k)
+
+
+def test_txlog_validate_fixture_stores(orc, fixtures):
+    for name, fx in fixtures.items():
+        raw = bytes.fromhex(fx["txlog"])
+        st, n, used, alh, sts = orc.txlog_validate(raw)
+        assert st == 0 and n == len(fx["txs"]), name
+        assert all(s == 0 for s in sts)
+        assert [a.tobytes().hex() for a in alh] == [t["header"]["alh"] for t in fx["txs"]]
+
+
+def _record_spans(raw):
+    """byte offset of every tx record (walks the same format)."""
+    import struct
+    p, spans = 0, []
+    while p + 8 <= len(raw) and struct.unpack(">Q", raw[p:p + 8])[0]:
+        s = p
+        p += 8 + 16 + 64
+        ver = struct.unpack(">H", raw[p:p + 2])[0]
+        p += 2
+        if ver == 0:
+            ne = struct.unpack(">H", raw[p:p + 2])[0]
+            p += 2
+        else:
+            ml = struct.unpack(">H", raw[p:p + 2])[0]
+            p += 2 + ml
+            ne = struct.unpack(">I", raw[p:p + 4])[0]
+            p += 4
+        for _ in range(ne):
+            ml = struct.unpack(">H", raw[p:p + 2])[0]
+            p += 2 + ml
+            kl = struct.unpack(">H", raw[p:p + 2])[0]
+            p += 2 + kl + 12 + 32
+        p += 32
+        spans.append((s, p))
+    return spans
+
+
+def test_txlog_validate_detects_corruption(orc, fixtures):
+    raw = bytes.fromhex(fixtures["long_linear_proof"]["txlog"])
+    spans = _record_spans(raw)
+    assert len(spans) == len(fixtures["long_linear_proof"]["txs"])
+    # flip one bit of tx 5's last stored hVal (just before its stored alh)
+    s, e = spans[4]
+    bad = bytearray(raw)
+    bad[e - 32 - 1] ^= 1
+    st, n, _, _, sts = orc.txlog_validate(bytes(bad))
+    assert st == 0 and n == len(spans)
+    assert [k for k, x in enumerate(sts) if x] == [4] and sts[4] == 14
+    # stored alh flipped: same per-tx status
+    bad = bytearray(raw)
+    bad[e - 1] ^= 0x80
+    assert list(orc.txlog_validate(bytes(bad))[4]).count(14) == 1
+    # unknown header version -> structural error at that record
+    bad = bytearray(raw)
+    bad[s + 88:s + 90] = b"\x00\x07"
+    st, n, used, _, _ = orc.txlog_validate(bytes(bad))
+    assert st == 17 and n == 4 and used == s
+    # too many entries for the reader's limit
+    st, n, _, _, _ = orc.txlog_validate(raw, max_entries=0)
+    assert st == 15 and n == 0
+    # key longer than MaxKeyLen
+    st, n, _, _, _ = orc.txlog_validate(raw, max_key_len=3)
+    assert st == 16 and n == 0
+    # truncated record
+    st, n, used, _, _ = orc.txlog_validate(raw[:e - 5])
+    assert st == 18 and n == 4 and used == s
+    # preallocated zero tail ends the log cleanly
+    st, n, _, _, _ = orc.txlog_validate(raw + b"\0" * 64)
+    assert st == 0 and n == len(spans)
+    assert orc.txlog_validate(raw, max_txs=3)[1] == 3
+
+
+def test_dual_proof_v2_fixture_cases(orc, fixtures):
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        for c in fx["dual_v2"]:
+            s, t = c["src"], c["tgt"]
+            incl = [bytes.fromhex(x) for x in c["incl"]]
+            cons = [bytes.fromhex(x) for x in c["cons"]]
+            args = (recs[s - 1], recs[t - 1], blob, incl, cons, s, t, alhs[s - 1], alhs[t - 1])
+            assert orc.verify_dual_proof_v2(*args) == 0, (name, s, t)
+            if incl:
+                bad = [bytes([incl[0][0] ^ 1]) + incl[0][1:]] + incl[1:]
+                assert orc.verify_dual_proof_v2(recs[s - 1], recs[t - 1], blob, bad, cons, s, t,
+                                                alhs[s - 1], alhs[t - 1]) == 12
+            if cons:
+                bad = cons[:-1] + [bytes([cons[-1][0] ^ 1]) + cons[-1][1:]]
+                assert orc.verify_dual_proof_v2(recs[s - 1], recs[t - 1], blob, incl, bad, s, t,
+                                                alhs[s - 1], alhs[t - 1]) == 13
+            # wrong source alh, swapped ids, mismatching header ids
+            assert orc.verify_dual_proof_v2(recs[s - 1], recs[t - 1], blob, incl, cons, s, t,
+                                            alhs[t - 1] if s != t else b"\0" * 32,
+                                            alhs[t - 1]) == 2
+            if s < t:
+                assert orc.verify_dual_proof_v2(recs[t - 1], recs[s - 1], blob, incl, cons, t, s,
+                                                alhs[t - 1], alhs[s - 1]) == 10
+            assert orc.verify_dual_proof_v2(recs[s - 1], recs[t - 1], blob, incl, cons, s + 1, t,
+                                            alhs[s - 1], alhs[t - 1]) == 2
+
+
+def test_linear_proofs_fixture_cases(orc, fixtures):
+    for name, fx in fixtures.items():
+        alhs = [bytes.fromhex(t["header"]["alh"]) for t in fx["txs"]]
+        for c in fx["linear"]:
+            s, t = c["src"], c["tgt"]
+            terms = [bytes.fromhex(x) for x in c["terms"]]
+            assert orc.verify_linear_proof(s, t, terms, s, t, alhs[s - 1], alhs[t - 1])
+            assert not orc.verify_linear_proof(s, t, terms, s, t + 1, alhs[s - 1], alhs[t - 1])
+            assert not orc.verify_linear_proof(s, t, terms[:-1], s, t, alhs[s - 1], alhs[t - 1]) or \
+                len(terms) == 1
+            if len(terms) > 1:
+                bad = terms[:1] + [bytes([terms[1][0] ^ 4]) + terms[1][1:]] + terms[2:]
+                assert not orc.verify_linear_proof(s, t, bad, s, t, alhs[s - 1], alhs[t - 1])
+        # verification.go:43-49 edge rules
+        assert not orc.verify_linear_proof(0, 1, [alhs[0]], 0, 1, alhs[0], alhs[0])
+        assert not orc.verify_linear_proof(2, 1, [alhs[0]], 2, 1, alhs[0], alhs[0])
+        assert not orc.verify_linear_proof(1, 1, [], 1, 1, alhs[0], alhs[0])
+        assert orc.verify_linear_proof(1, 1, [alhs[0]], 1, 1, alhs[0], alhs[0])
+
+
+def test_linear_advance_proof_edges(orc):
+    z = b"\0" * 32
+    # verification.go:90-104: end < start false, end <= start+1 true, nil proof false
+    assert not orc.verify_linear_advance_proof(None, 5, 4, z, z, 10)
+    assert orc.verify_linear_advance_proof(None, 5, 6, z, z, 10)
+    assert not orc.verify_linear_advance_proof(None, 5, 7, z, z, 10)
+    assert not orc.verify_linear_advance_proof(([z, z], []), 5, 7, z, z, 10)
