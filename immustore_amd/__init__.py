@@ -17,6 +17,7 @@ from .merkle import (Context, default_context, device_count, HTree, InclusionPro
                      ahtree_verify_last_inclusion, ahtree_verify_batch, build_hash_tree)
 from . import txlayer
 from .txlayer import (TX_HEADER, tx_alh_batch, htree_build_many, verify_linear_proof_batch,
-                      verify_dual_proof_v2_batch, VerifyDualProofV2, txlog_validate)
+                      verify_dual_proof_v2_batch, VerifyDualProofV2, verify_dual_proof_batch,
+                      txlog_validate)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

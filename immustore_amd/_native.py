@@ -214,6 +214,7 @@ SIGNATURES = {
     "mh_verify_linear_proof_batch": (i32, [vp, u64, vp, vp, vp, u8p, vp, vp, u8p, u8p, u8p]),
     "mh_verify_dual_proof_v2_batch": (i32, [vp, u64, vp, vp, u8p, u64, vp, u8p, vp, u8p, vp, vp,
                                             u8p, u8p, vp]),
+    "mh_verify_dual_proof_batch": (i32, [vp, vp, u8p]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
                                 u8p, vp]),
 }

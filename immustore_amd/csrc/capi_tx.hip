@@ -342,6 +342,227 @@ extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_
     return MH_OK;
 }
 
+extern "C" int mh_verify_dual_proof_batch(mh_ctx *c, const mh_dual_proof_batch *B, uint8_t *ok) {
+    if (!c || !B || (B->n && !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    const uint64_t n = B->n;
+    if (!n) return MH_OK;
+    if (!B->src_hdr || !B->tgt_hdr || !B->incl_off || !B->cons_off || !B->target_bl_tx_alh ||
+        !B->last_off || !B->has_linear || !B->linear_src || !B->linear_tgt || !B->linear_off ||
+        !B->has_advance || !B->advance_off || !B->advance_incl_first || !B->advance_incl_off ||
+        !B->src || !B->tgt || !B->src_alh || !B->tgt_alh)
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    const mh_tx_header *sh = B->src_hdr, *th = B->tgt_hdr;
+    const uint64_t ni = B->incl_off[n] - B->incl_off[0], nc = B->cons_off[n] - B->cons_off[0],
+                   nl = B->last_off[n] - B->last_off[0], nlin = B->linear_off[n] - B->linear_off[0],
+                   nadv = B->advance_off[n] - B->advance_off[0],
+                   Q = B->advance_incl_first[n] - B->advance_incl_first[0],
+                   nq = Q ? B->advance_incl_off[B->advance_incl_first[n]] -
+                                B->advance_incl_off[B->advance_incl_first[0]]
+                          : 0;
+    if ((ni && !B->incl_terms) || (nc && !B->cons_terms) || (nl && !B->last_terms) ||
+        (nlin && !B->linear_terms) || (nadv && !B->advance_terms) ||
+        (nq && !B->advance_incl_terms))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    const uint64_t q0 = B->advance_incl_first[0], qt0 = Q ? B->advance_incl_off[q0] : 0;
+
+    // ---- host side: argument checks and per-check operands (verification.go:128-235)
+    std::vector<uint8_t> alive(n, 1), adv_state(n, 0);  // 0 run chain, 1 true, 2 false
+    std::vector<mh_tx_header> hh(2 * n);
+    std::vector<uint8_t> expect(2 * n * 32), lin_sa(n * 32), end_alh(n * 32), sbl(n * 32),
+        tbl(n * 32);
+    std::vector<uint64_t> ii(n), ij(n), ci(n), li(n), ls(n), lt(n), lo(n + 1), io(n + 1),
+        co(n + 1), lso(n + 1);
+    std::vector<uint64_t> a_start, a_cnt, a_t0, a_first, a_idx;
+    std::vector<uint8_t> a_end;
+    for (uint64_t p = 0; p <= n; p++) {
+        io[p] = B->incl_off[p] - B->incl_off[0];
+        co[p] = B->cons_off[p] - B->cons_off[0];
+        lso[p] = B->last_off[p] - B->last_off[0];
+        lo[p] = B->linear_off[p] - B->linear_off[0];
+    }
+    for (uint64_t p = 0; p < n; p++) {
+        const uint64_t src = B->src[p], tgt = B->tgt[p];
+        if (sh[p].id != src || th[p].id != tgt || sh[p].id == 0 || sh[p].id > th[p].id ||
+            check_header(sh[p], B->md_blob_len, B->md_blob != nullptr) ||
+            check_header(th[p], B->md_blob_len, B->md_blob != nullptr))
+            alive[p] = 0;
+        hh[p] = sh[p];
+        hh[n + p] = th[p];
+        if (!alive[p]) {
+            hh[p].version = hh[n + p].version = 1;
+            hh[p].md_len = hh[n + p].md_len = 0;
+        }
+        memcpy(&expect[p * 32], B->src_alh + p * 32, 32);
+        memcpy(&expect[(n + p) * 32], B->tgt_alh + p * 32, 32);
+        memcpy(&sbl[p * 32], sh[p].bl_root, 32);
+        memcpy(&tbl[p * 32], th[p].bl_root, 32);
+        const uint64_t tbl_id = th[p].bl_tx_id;
+        ii[p] = src;
+        ij[p] = tbl_id;
+        ci[p] = sh[p].bl_tx_id;
+        li[p] = tbl_id;
+        const bool a_branch = src < tbl_id;  // verification.go:195 vs :214
+        ls[p] = a_branch ? tbl_id : src;
+        lt[p] = tgt;
+        memcpy(&lin_sa[p * 32], a_branch ? B->target_bl_tx_alh + p * 32 : B->src_alh + p * 32, 32);
+        const uint64_t start = sh[p].bl_tx_id, end = a_branch ? src : tbl_id;
+        memcpy(&end_alh[p * 32], a_branch ? B->src_alh + p * 32 : B->target_bl_tx_alh + p * 32, 32);
+        // VerifyLinearAdvanceProof preconditions (verification.go:90-104)
+        const uint64_t f0 = B->advance_incl_first[p], f1 = B->advance_incl_first[p + 1];
+        if (end < start) {
+            adv_state[p] = 2;
+        } else if (end <= start + 1) {
+            adv_state[p] = 1;
+        } else if (!B->has_advance[p] ||
+                   B->advance_off[p + 1] - B->advance_off[p] != end - start ||
+                   f1 - f0 != end - start - 1) {
+            adv_state[p] = 2;
+        } else {
+            adv_state[p] = 0;
+            a_idx.push_back(p);
+            a_start.push_back(start);
+            a_cnt.push_back(end - start - 1);
+            a_t0.push_back(B->advance_off[p] - B->advance_off[0]);
+            a_first.push_back(f0 - q0);
+            a_end.insert(a_end.end(), &end_alh[p * 32], &end_alh[p * 32] + 32);
+        }
+    }
+    // nested inclusion proofs (every q; those of proofs not run are ignored)
+    std::vector<uint64_t> qi(std::max<uint64_t>(Q, 1)), qj(std::max<uint64_t>(Q, 1)),
+        qo(Q + 1);
+    std::vector<uint8_t> qroot(std::max<uint64_t>(Q, 1) * 32);
+    for (uint64_t q = 0; q <= Q; q++) qo[q] = B->advance_incl_off[q0 + q] - qt0;
+    for (uint64_t k = 0; k < a_idx.size(); k++) {
+        const uint64_t p = a_idx[k];
+        for (uint64_t x = 0; x < a_cnt[k]; x++) {
+            const uint64_t q = a_first[k] + x;
+            qi[q] = a_start[k] + 1 + x;  // txID, verification.go:108-114
+            qj[q] = th[p].bl_tx_id;
+            memcpy(&qroot[q * 32], th[p].bl_root, 32);
+        }
+    }
+    const uint64_t na = a_idx.size();
+
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    Layout L;
+    const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(B->md_blob_len),
+                   b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
+                   b_ast = L.add(2 * n * 4), b_tba = L.add(n * 32), b_lfa = L.add(n * 32),
+                   b_lft = L.add(n * 32), b_sbl = L.add(n * 32), b_tbl = L.add(n * 32),
+                   b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
+                   b_li = L.add(n * 8), b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8),
+                   b_lso = L.add((n + 1) * 8), b_it = L.add(ni * 32), b_ct = L.add(nc * 32),
+                   b_lt = L.add(nl * 32), b_oki = L.add(n), b_okc = L.add(n), b_okl = L.add(n),
+                   b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_ls = L.add(n * 8),
+                   b_ltg = L.add(n * 8), b_lo = L.add((n + 1) * 8), b_lterm = L.add(nlin * 32),
+                   b_lsa = L.add(n * 32), b_ta = L.add(n * 32), b_oklin = L.add(n),
+                   b_ast0 = L.add(na * 8), b_acnt = L.add(na * 8), b_at0 = L.add(na * 8),
+                   b_afirst = L.add(na * 8), b_aend = L.add(na * 32), b_aterm = L.add(nadv * 32),
+                   b_aok = L.add(na), b_qsrc = L.add(Q * 32), b_qleaf = L.add(Q * 32),
+                   b_qi = L.add(Q * 8), b_qj = L.add(Q * 8), b_qo = L.add((Q + 1) * 8),
+                   b_qroot = L.add(Q * 32), b_qterm = L.add(nq * 32), b_qok = L.add(Q);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
+                     : hipSuccess;
+    };
+    auto U = [&](uint64_t off) { return (const uint64_t *)(base + off); };
+    MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
+    if (B->md_blob) MH_HIP(h2d(b_md, B->md_blob, B->md_blob_len));
+    MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
+    MH_HIP(h2d(b_tba, B->target_bl_tx_alh, n * 32));
+    MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
+    MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
+    MH_HIP(h2d(b_ii, ii.data(), n * 8));
+    MH_HIP(h2d(b_ij, ij.data(), n * 8));
+    MH_HIP(h2d(b_ci, ci.data(), n * 8));
+    MH_HIP(h2d(b_li, li.data(), n * 8));
+    MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
+    MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
+    MH_HIP(h2d(b_lso, lso.data(), (n + 1) * 8));
+    MH_HIP(h2d(b_it, ni ? B->incl_terms + B->incl_off[0] * 32 : nullptr, ni * 32));
+    MH_HIP(h2d(b_ct, nc ? B->cons_terms + B->cons_off[0] * 32 : nullptr, nc * 32));
+    MH_HIP(h2d(b_lt, nl ? B->last_terms + B->last_off[0] * 32 : nullptr, nl * 32));
+    MH_HIP(h2d(b_ps, B->linear_src, n * 8));
+    MH_HIP(h2d(b_pt, B->linear_tgt, n * 8));
+    MH_HIP(h2d(b_ls, ls.data(), n * 8));
+    MH_HIP(h2d(b_ltg, lt.data(), n * 8));
+    MH_HIP(h2d(b_lo, lo.data(), (n + 1) * 8));
+    MH_HIP(h2d(b_lterm, nlin ? B->linear_terms + B->linear_off[0] * 32 : nullptr, nlin * 32));
+    MH_HIP(h2d(b_lsa, lin_sa.data(), n * 32));
+    MH_HIP(h2d(b_ta, B->tgt_alh, n * 32));
+    MH_HIP(h2d(b_ast0, a_start.data(), na * 8));
+    MH_HIP(h2d(b_acnt, a_cnt.data(), na * 8));
+    MH_HIP(h2d(b_at0, a_t0.data(), na * 8));
+    MH_HIP(h2d(b_afirst, a_first.data(), na * 8));
+    MH_HIP(h2d(b_aend, a_end.data(), na * 32));
+    MH_HIP(h2d(b_aterm, nadv ? B->advance_terms + B->advance_off[0] * 32 : nullptr, nadv * 32));
+    MH_HIP(h2d(b_qi, qi.data(), Q * 8));
+    MH_HIP(h2d(b_qj, qj.data(), Q * 8));
+    MH_HIP(h2d(b_qo, qo.data(), (Q + 1) * 8));
+    MH_HIP(h2d(b_qroot, qroot.data(), Q * 32));
+    MH_HIP(h2d(b_qterm, nq ? B->advance_incl_terms + qt0 * 32 : nullptr, nq * 32));
+    Timer *tm = c->tm();
+    // header Alh (verification.go:141-150)
+    MH_HIP(launch_tx_alh(st, tm, 2 * n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
+                         base + b_s, base + b_x, nullptr, nullptr, nullptr,
+                         (int32_t *)(base + b_ast)));
+    // inclusion / consistency / last inclusion (verification.go:152-190)
+    MH_HIP(launch_leaf_for(st, tm, n, base + b_x, base + b_lfa));
+    MH_HIP(launch_leaf_for(st, tm, n, base + b_tba, base + b_lft));
+    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, n, U(b_ii), U(b_ij), U(b_io),
+                                base + b_it, base + b_lfa, base + b_tbl, base + b_oki, nullptr));
+    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_CONSISTENCY, n, U(b_ci), U(b_ij), U(b_co),
+                                base + b_ct, base + b_sbl, base + b_tbl, base + b_okc, nullptr));
+    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_LAST_INCLUSION, n, U(b_li), U(b_li), U(b_lso),
+                                base + b_lt, base + b_lft, base + b_tbl, base + b_okl, nullptr));
+    // linear proof (verification.go:195-197 / :214-216)
+    MH_HIP(launch_linear_verify(st, tm, n, U(b_ps), U(b_pt), U(b_ls), U(b_ltg), U(b_lo),
+                                base + b_lterm, base + b_lsa, base + b_ta, base + b_oklin));
+    // linear advance proofs: chain, then the nested inclusion proofs
+    MH_HIP(launch_advance_chain(st, tm, na, U(b_ast0), U(b_acnt), U(b_at0), base + b_aterm,
+                                U(b_afirst), base + b_aend, base + b_qsrc, base + b_aok));
+    MH_HIP(launch_leaf_for(st, tm, Q, base + b_qsrc, base + b_qleaf));
+    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, Q, U(b_qi), U(b_qj), U(b_qo),
+                                base + b_qterm, base + b_qleaf, base + b_qroot, base + b_qok,
+                                nullptr));
+    std::vector<int32_t> ast(2 * n);
+    std::vector<uint8_t> oki(n), okc(n), okl(n), oklin(n), aok(std::max<uint64_t>(na, 1)),
+        qok(std::max<uint64_t>(Q, 1));
+    auto d2h = [&](void *dst, uint64_t off, uint64_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, base + off, bytes, hipMemcpyDeviceToHost, st)
+                     : hipSuccess;
+    };
+    MH_HIP(d2h(ast.data(), b_ast, 2 * n * 4));
+    MH_HIP(d2h(oki.data(), b_oki, n));
+    MH_HIP(d2h(okc.data(), b_okc, n));
+    MH_HIP(d2h(okl.data(), b_okl, n));
+    MH_HIP(d2h(oklin.data(), b_oklin, n));
+    MH_HIP(d2h(aok.data(), b_aok, na));
+    MH_HIP(d2h(qok.data(), b_qok, Q));
+    MH_HIP(hipStreamSynchronize(st));
+    std::vector<uint8_t> adv_ok(n, 0);
+    for (uint64_t k = 0; k < na; k++) {
+        bool all = aok[k] != 0;
+        for (uint64_t x = 0; x < a_cnt[k] && all; x++) all = qok[a_first[k] + x] != 0;
+        adv_ok[a_idx[k]] = all;
+    }
+    for (uint64_t p = 0; p < n; p++) {
+        const uint64_t src = B->src[p], tbl_id = th[p].bl_tx_id;
+        bool r = alive[p] && ast[p] == MH_OK && ast[n + p] == MH_OK;
+        if (r && src < tbl_id) r = oki[p];
+        if (r && sh[p].bl_tx_id > 0) r = okc[p];
+        if (r && tbl_id > 0) r = okl[p];
+        if (r) r = B->has_linear[p] && oklin[p];
+        if (r) r = adv_state[p] == 1 || (adv_state[p] == 0 && adv_ok[p]);
+        ok[p] = r ? 1 : 0;
+    }
+    return MH_OK;
+}
+
 // ------------------------------------------------------------------ a14
 extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                                  uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,

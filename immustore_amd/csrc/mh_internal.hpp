@@ -130,6 +130,10 @@ hipError_t launch_linear_verify(hipStream_t st, Timer *tm, uint64_t n, const uin
                                 const uint64_t *ptgt, const uint64_t *src, const uint64_t *tgt,
                                 const uint64_t *term_off, const uint8_t *terms,
                                 const uint8_t *src_alh, const uint8_t *tgt_alh, uint8_t *ok);
+hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uint64_t *start,
+                                const uint64_t *cnt, const uint64_t *term_off,
+                                const uint8_t *terms, const uint64_t *first,
+                                const uint8_t *end_alh, uint8_t *leaves_src, uint8_t *ok);
 hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
                                const uint64_t *rec_off, const uint8_t *ver,
                                const uint64_t *msg_off, uint8_t *msgs);

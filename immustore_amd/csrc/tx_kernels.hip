@@ -166,6 +166,35 @@ __global__ __launch_bounds__(256) void k_linear_verify(
     ok[p] = res ? 1 : 0;
 }
 
+// VerifyLinearAdvanceProof chain (verification.go:106-121) for proofs that
+// passed the host-side length checks: calc starts at terms[0] (Alh of
+// start+1); before every advance the current calc is written to
+// leaves_src[first + k] (its leafFor must be included in the target tree at
+// index start+1+k), then calc = advanceLinearHash(calc, start+2+k, terms[k+1]).
+// ok[p] = (final calc == end_alh[p]).
+__global__ __launch_bounds__(256) void k_advance_chain(
+    uint64_t n, const uint64_t *__restrict__ start, const uint64_t *__restrict__ cnt,
+    const uint64_t *__restrict__ term_off, const uint8_t *__restrict__ terms,
+    const uint64_t *__restrict__ first, const uint8_t *__restrict__ end_alh,
+    uint8_t *__restrict__ leaves_src, uint8_t *__restrict__ ok) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t t0 = term_off[p], c0 = cnt[p], s = start[p], f = first[p];
+    uint32_t c[8], x[8];
+    load_digest(terms + t0 * 32, c);
+    for (uint64_t k = 0; k < c0; k++) {
+        store_digest(leaves_src + (f + k) * 32, c);
+        uint32_t term[8];
+        load_digest(terms + (t0 + k + 1) * 32, term);
+        alh_hash(s + 2 + k, c, term, c);
+    }
+    load_digest(end_alh + p * 32, x);
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) d |= c[j] ^ x[j];
+    ok[p] = d == 0;
+}
+
 // Entry-digest messages straight from raw tx-log entry records
 // (tx.go:520-588): a record at rec is  BE16 mdLen | md | BE16 kLen | key |
 // BE32 vLen | BE64 vOff | hVal.  v1 message = record[0 : 4+md+key] || hVal,
@@ -278,6 +307,17 @@ hipError_t launch_linear_verify(hipStream_t st, Timer *tm, uint64_t n, const uin
     TimerScope ts(tm, "linear_verify", st);
     hipLaunchKernelGGL(k_linear_verify, dim3(grid_for(n, 256)), dim3(256), 0, st, n, psrc, ptgt,
                        src, tgt, term_off, terms, src_alh, tgt_alh, ok);
+    return hipGetLastError();
+}
+
+hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uint64_t *start,
+                                const uint64_t *cnt, const uint64_t *term_off,
+                                const uint8_t *terms, const uint64_t *first,
+                                const uint8_t *end_alh, uint8_t *leaves_src, uint8_t *ok) {
+    if (!n) return hipSuccess;
+    TimerScope ts(tm, "advance_chain", st);
+    hipLaunchKernelGGL(k_advance_chain, dim3(grid_for(n, 256)), dim3(256), 0, st, n, start, cnt,
+                       term_off, terms, first, end_alh, leaves_src, ok);
     return hipGetLastError();
 }
 

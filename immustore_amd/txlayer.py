@@ -4,6 +4,8 @@
   Tx.BuildHashTree over many txs   tx.go:332-355          -> htree_build_many
   VerifyLinearProof                verification.go:40-64  -> verify_linear_proof_batch
   VerifyDualProofV2                verification.go:304-372 -> verify_dual_proof_v2_batch
+  VerifyDualProof (v1, with linear / linear-advance parts)
+                                   verification.go:127-235 -> verify_dual_proof_batch
   Tx.readFrom (read-path check)    tx.go:388-630          -> txlog_validate
 
 Headers travel as a numpy structured array of TX_HEADER (the C struct
@@ -132,6 +134,67 @@ def VerifyDualProofV2(src_hdr, tgt_hdr, md_blob, incl, cons, src, tgt, src_alh, 
     st = verify_dual_proof_v2_batch([src_hdr], [tgt_hdr], md_blob, [incl], [cons], [src], [tgt],
                                     [src_alh], [tgt_alh], ctx)
     N.check(int(st[0]))
+
+
+class _DualProofBatch(C.Structure):
+    """mirror of mh_dual_proof_batch (include/immustore_merkle.h)"""
+    _fields_ = [("n", C.c_uint64), ("src_hdr", C.c_void_p), ("tgt_hdr", C.c_void_p),
+                ("md_blob", C.c_void_p), ("md_blob_len", C.c_uint64),
+                ("incl_off", C.c_void_p), ("incl_terms", C.c_void_p),
+                ("cons_off", C.c_void_p), ("cons_terms", C.c_void_p),
+                ("target_bl_tx_alh", C.c_void_p), ("last_off", C.c_void_p),
+                ("last_terms", C.c_void_p), ("has_linear", C.c_void_p),
+                ("linear_src", C.c_void_p), ("linear_tgt", C.c_void_p),
+                ("linear_off", C.c_void_p), ("linear_terms", C.c_void_p),
+                ("has_advance", C.c_void_p), ("advance_off", C.c_void_p),
+                ("advance_terms", C.c_void_p), ("advance_incl_first", C.c_void_p),
+                ("advance_incl_off", C.c_void_p), ("advance_incl_terms", C.c_void_p),
+                ("src", C.c_void_p), ("tgt", C.c_void_p), ("src_alh", C.c_void_p),
+                ("tgt_alh", C.c_void_p)]
+
+
+def verify_dual_proof_batch(src_hdrs, tgt_hdrs, md_blob, incl, cons, target_bl_tx_alh, last,
+                            linear, advance, src, tgt, src_alh, tgt_alh,
+                            ctx: Optional[Context] = None) -> np.ndarray:
+    """VerifyDualProof (v1, verification.go:127-235) over n proofs -> ok[n] (bool).
+
+    linear[p]: None (nil proof) or (SourceTxID, TargetTxID, terms);
+    advance[p]: None or (LinearProofTerms, [InclusionProofs...])."""
+    sh, th = _hdrs(src_hdrs), _hdrs(tgt_hdrs)
+    n = sh.size
+    if n == 0:
+        return np.zeros(0, bool)
+    keep = []
+
+    def k(a):
+        keep.append(a)
+        return _addr(a)
+
+    mb, ml = _blob(md_blob)
+    io, it = _terms_csr(incl)
+    co, ct = _terms_csr(cons)
+    lo, lt = _terms_csr(last)
+    has_lin = np.array([x is not None for x in linear], np.uint8)
+    lsrc = np.array([x[0] if x is not None else 0 for x in linear], np.uint64)
+    ltgt = np.array([x[1] if x is not None else 0 for x in linear], np.uint64)
+    lno, lnt = _terms_csr([x[2] if x is not None else [] for x in linear])
+    has_adv = np.array([x is not None for x in advance], np.uint8)
+    ao, at = _terms_csr([x[0] if x is not None else [] for x in advance])
+    nested = [x[1] if x is not None else [] for x in advance]
+    first = np.zeros(n + 1, np.uint64)
+    for p, ns in enumerate(nested):
+        first[p + 1] = first[p] + len(ns)
+    qo, qt = _terms_csr([ip for ns in nested for ip in ns])
+    s_ = np.asarray(src, np.uint64)
+    t_ = np.asarray(tgt, np.uint64)
+    sa, ta, tba = _d32(src_alh, n), _d32(tgt_alh, n), _d32(target_bl_tx_alh, n)
+    b = _DualProofBatch(n, k(sh), k(th), k(mb) if mb is not None else None, ml, k(io), k(it),
+                        k(co), k(ct), k(tba), k(lo), k(lt), k(has_lin), k(lsrc), k(ltgt), k(lno),
+                        k(lnt), k(has_adv), k(ao), k(at), k(first), k(qo), k(qt), k(s_), k(t_),
+                        k(sa), k(ta))
+    ok = np.zeros(n, np.uint8)
+    N.check(N.load().mh_verify_dual_proof_batch(_ctx(ctx).handle, C.byref(b), _addr(ok)))
+    return ok.astype(bool)
 
 
 def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,

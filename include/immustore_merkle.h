@@ -277,6 +277,45 @@ int mh_verify_dual_proof_v2_batch(mh_ctx *ctx, uint64_t n, const mh_tx_header *s
                                   const uint64_t *tgt, const uint8_t *src_alh,
                                   const uint8_t *tgt_alh, int32_t *status);
 
+/* VerifyDualProof (verification.go:127-235: v1 proofs with linear and
+ * linear-advance parts) for n proofs, all arrays host memory, term lists as
+ * CSR (x_off has n + 1 entries, terms x_terms[x_off[p] .. x_off[p+1])).
+ * The linear-advance inclusion proofs of proof p are nested proofs
+ * advance_incl_first[p] .. advance_incl_first[p+1]) whose terms are
+ * advance_incl_terms[advance_incl_off[q] .. advance_incl_off[q+1]).
+ * has_linear / has_advance = 0 stand for Go's nil proofs.  ok[p] = 1 iff the
+ * proof verifies (the Go function returns bool). */
+typedef struct mh_dual_proof_batch {
+    uint64_t n;
+    const mh_tx_header *src_hdr;
+    const mh_tx_header *tgt_hdr;
+    const uint8_t *md_blob;
+    uint64_t md_blob_len;
+    const uint64_t *incl_off;
+    const uint8_t *incl_terms;
+    const uint64_t *cons_off;
+    const uint8_t *cons_terms;
+    const uint8_t *target_bl_tx_alh; /* n x 32 (DualProof.TargetBlTxAlh) */
+    const uint64_t *last_off;
+    const uint8_t *last_terms;
+    const uint8_t *has_linear;
+    const uint64_t *linear_src; /* LinearProof.SourceTxID */
+    const uint64_t *linear_tgt; /* LinearProof.TargetTxID */
+    const uint64_t *linear_off;
+    const uint8_t *linear_terms;
+    const uint8_t *has_advance;
+    const uint64_t *advance_off;
+    const uint8_t *advance_terms;
+    const uint64_t *advance_incl_first;
+    const uint64_t *advance_incl_off;
+    const uint8_t *advance_incl_terms;
+    const uint64_t *src;
+    const uint64_t *tgt;
+    const uint8_t *src_alh;
+    const uint8_t *tgt_alh;
+} mh_dual_proof_batch;
+int mh_verify_dual_proof_batch(mh_ctx *ctx, const mh_dual_proof_batch *b, uint8_t *ok);
+
 /* Tx-log read path (Tx.readFrom tx.go:388-630: readHeader, readEntry,
  * buildAndValidateHtree) over buf = back-to-back tx records as written by
  * immustore.go:1812-1924.  Parses up to max_txs records, stopping at id 0 (a

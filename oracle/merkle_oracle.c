@@ -762,6 +762,48 @@ int orc_verify_dual_proof_v2(const orc_tx_header *sh, const orc_tx_header *th,
     return ok ? OK : ERR_CONSISTENCY_NOT_VALID;
 }
 
+int orc_verify_dual_proof(const orc_tx_header *sh, const orc_tx_header *th,
+                          const uint8_t *md_blob, const uint8_t *incl, uint32_t nincl,
+                          const uint8_t *cons, uint32_t ncons, const uint8_t tbl_alh[32],
+                          const uint8_t *last, uint32_t nlast, int has_lin, uint64_t lin_src,
+                          uint64_t lin_tgt, const uint8_t *lin, uint32_t nlin, int has_lap,
+                          const uint8_t *lap_terms, uint32_t nlap, const uint8_t *lap_incl,
+                          const uint32_t *lap_incl_off, uint32_t nlap_incl, uint64_t src,
+                          uint64_t tgt, const uint8_t src_alh[32], const uint8_t tgt_alh[32]) {
+    /* store/verification.go:127-235 */
+    if (!sh || !th || sh->id != src || th->id != tgt) return 0;
+    if (sh->id == 0 || sh->id > th->id) return 0;
+    uint8_t a[32], lf[32];
+    if (orc_tx_header_alh(sh, md_blob, NULL, a) || memcmp(a, src_alh, 32)) return 0;
+    if (orc_tx_header_alh(th, md_blob, NULL, a) || memcmp(a, tgt_alh, 32)) return 0;
+    if (src < th->bl_tx_id) {
+        leaf_for(src_alh, lf);
+        if (!orc_ahtree_verify_inclusion(incl, nincl, src, th->bl_tx_id, lf, th->bl_root)) return 0;
+    }
+    if (sh->bl_tx_id > 0 &&
+        !orc_ahtree_verify_consistency(cons, ncons, sh->bl_tx_id, th->bl_tx_id, sh->bl_root,
+                                       th->bl_root))
+        return 0;
+    if (th->bl_tx_id > 0) {
+        leaf_for(tbl_alh, lf);
+        if (!orc_ahtree_verify_last_inclusion(last, nlast, th->bl_tx_id, lf, th->bl_root)) return 0;
+    }
+    if (src < th->bl_tx_id) {
+        if (!has_lin || !orc_verify_linear_proof(lin_src, lin_tgt, lin, nlin, th->bl_tx_id, tgt,
+                                                 tbl_alh, tgt_alh))
+            return 0;
+        return orc_verify_linear_advance_proof(has_lap, lap_terms, nlap, lap_incl, lap_incl_off,
+                                               nlap_incl, sh->bl_tx_id, src, src_alh, th->bl_root,
+                                               th->bl_tx_id);
+    }
+    if (!has_lin ||
+        !orc_verify_linear_proof(lin_src, lin_tgt, lin, nlin, src, tgt, src_alh, tgt_alh))
+        return 0;
+    return orc_verify_linear_advance_proof(has_lap, lap_terms, nlap, lap_incl, lap_incl_off,
+                                           nlap_incl, sh->bl_tx_id, th->bl_tx_id, tbl_alh,
+                                           th->bl_root, th->bl_tx_id);
+}
+
 /* ---- tx log records (immustore.go:1812-1924 writer, tx.go:388-630 reader) */
 static int rd(uint64_t len, uint64_t *p, uint64_t n) {
     if (*p + n > len) return 0;

@@ -108,6 +108,16 @@ int orc_verify_dual_proof_v2(const orc_tx_header *sh, const orc_tx_header *th,
                              const uint8_t *md_blob, const uint8_t *incl, uint32_t nincl,
                              const uint8_t *cons, uint32_t ncons, uint64_t src, uint64_t tgt,
                              const uint8_t src_alh[32], const uint8_t tgt_alh[32]);
+/* store/verification.go:127-235 (VerifyDualProof, v1 proofs with linear and
+ * linear-advance parts); returns 1 = verifies. */
+int orc_verify_dual_proof(const orc_tx_header *sh, const orc_tx_header *th,
+                          const uint8_t *md_blob, const uint8_t *incl, uint32_t nincl,
+                          const uint8_t *cons, uint32_t ncons, const uint8_t tbl_alh[32],
+                          const uint8_t *last, uint32_t nlast, int has_lin, uint64_t lin_src,
+                          uint64_t lin_tgt, const uint8_t *lin, uint32_t nlin, int has_lap,
+                          const uint8_t *lap_terms, uint32_t nlap, const uint8_t *lap_incl,
+                          const uint32_t *lap_incl_off, uint32_t nlap_incl, uint64_t src,
+                          uint64_t tgt, const uint8_t src_alh[32], const uint8_t tgt_alh[32]);
 /* Tx log read path (tx.go:388-630: readHeader, readEntry, buildAndValidateHtree)
  * over a buffer of back-to-back tx records (immustore.go:1812-1924).  Stops at
  * id 0 (preallocated tail), at max_txs, or at the first structural error

@@ -76,6 +76,10 @@ def lib():
                                                       u8p, C.c_uint64]
         L.orc_verify_dual_proof_v2.argtypes = [u8p, u8p, u8p, u8p, C.c_uint32, u8p, C.c_uint32,
                                                C.c_uint64, C.c_uint64, u8p, u8p]
+        L.orc_verify_dual_proof.argtypes = [u8p, u8p, u8p, u8p, C.c_uint32, u8p, C.c_uint32, u8p,
+                                            u8p, C.c_uint32, C.c_int, C.c_uint64, C.c_uint64, u8p,
+                                            C.c_uint32, C.c_int, u8p, C.c_uint32, u8p, u32p,
+                                            C.c_uint32, C.c_uint64, C.c_uint64, u8p, u8p]
         L.orc_txlog_validate.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
                                          u64p, u64p, u8p, C.POINTER(C.c_int32)]
         L.orc_sha256_use_shani.argtypes = [C.c_int]
@@ -365,3 +369,34 @@ def txlog_validate(buf, max_entries=1024, max_key_len=1024, max_txs=1 << 40):
                                   sts.ctypes.data_as(C.POINTER(C.c_int32)))
     n = ntx.value
     return st, n, used.value, alh[:n].copy(), sts[:n].copy()
+
+
+def verify_dual_proof(sh, th, md_blob, incl, cons, tbl_alh, last, lin, lap, src, tgt, src_alh,
+                      tgt_alh):
+    """VerifyDualProof (v1).  lin: None or (lin_src, lin_tgt, terms); lap: None or
+    (linear_terms, [inclusion_terms, ...])."""
+    a = np.ascontiguousarray(np.asarray(sh, TX_HEADER).reshape(1))
+    b = np.ascontiguousarray(np.asarray(th, TX_HEADER).reshape(1))
+    mb = _u8(md_blob) if len(md_blob) else np.zeros(1, np.uint8)
+    ip_, ni = _terms(incl)
+    cp_, nc = _terms(cons)
+    lp_, nl = _terms(last)
+    if lin is None:
+        has_lin, ls, lt, lin_p, nlin = 0, 0, 0, None, 0
+    else:
+        has_lin, (ls, lt, lterms) = 1, lin
+        lin_p, nlin = _terms(lterms)
+    if lap is None:
+        has_lap, lap_p, nlap, inc_p, off, ninc = 0, None, 0, None, np.zeros(1, np.uint32), 0
+    else:
+        has_lap = 1
+        lap_p, nlap = _terms(lap[0])
+        off = np.zeros(len(lap[1]) + 1, np.uint32)
+        for k, ip in enumerate(lap[1]):
+            off[k + 1] = off[k] + len(ip)
+        inc_p, _ = _terms([x for ip in lap[1] for x in ip])
+        ninc = len(lap[1])
+    return bool(lib().orc_verify_dual_proof(
+        _p(a.view(np.uint8)), _p(b.view(np.uint8)), _p(mb), ip_, ni, cp_, nc, _p(_u8(tbl_alh)),
+        lp_, nl, has_lin, ls, lt, lin_p, nlin, has_lap, lap_p, nlap, inc_p, _p(off, u32p), ninc,
+        src, tgt, _p(_u8(src_alh)), _p(_u8(tgt_alh))))

@@ -363,9 +363,38 @@ def fixture_store(root):
             assert c.hex() == th["alh"]
             if (t_ - s_) % 7 == 0 or t_ == len(hdrs):
                 linear.append({"src": s_, "tgt": t_, "terms": terms})
+    # DualProof (v1) exactly as ImmuStore.DualProof / LinearAdvanceProof build
+    # them (immustore.go:2392-2463, :2513-2562)
+    dual1 = []
+    for s_ in range(1, len(hdrs) + 1):
+        for t_ in range(s_, len(hdrs) + 1):
+            sh, th = hdrs[s_ - 1], hdrs[t_ - 1]
+            if sh["bltxid"] > th["bltxid"]:
+                continue
+            c = {"src": s_, "tgt": t_, "incl": [], "cons": [], "last": [], "tbl_alh": "00" * 32}
+            if s_ < th["bltxid"]:
+                c["incl"] = [x.hex() for x in aht.inclusion_proof(s_, th["bltxid"])]
+            if sh["bltxid"] > 0:
+                c["cons"] = [x.hex() for x in aht.consistency_proof(sh["bltxid"], th["bltxid"])]
+            if th["bltxid"] > 0:
+                c["tbl_alh"] = hdrs[th["bltxid"] - 1]["alh"]
+                c["last"] = [x.hex() for x in aht.inclusion_proof(th["bltxid"], th["bltxid"])]
+            ls = max(s_, th["bltxid"])
+            c["lin_src"] = ls
+            c["lin"] = [hdrs[ls - 1]["alh"]] + [inner_hash(hdrs[k - 1]).hex()
+                                                 for k in range(ls + 1, t_ + 1)]
+            a0, a1 = sh["bltxid"], min(s_, th["bltxid"])
+            if a1 <= a0 + 1:
+                c["lap"] = None
+            else:
+                lt = [hdrs[a0]["alh"]] + [inner_hash(hdrs[k]).hex() for k in range(a0 + 1, a1)]
+                ips = [[x.hex() for x in aht.inclusion_proof(k, th["bltxid"])]
+                       for k in range(a0 + 1, a1)]
+                c["lap"] = {"terms": lt, "incl": ips}
+            dual1.append(c)
     return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(), "n_values": sum(
         1 for t in txs for e in t["entries"] if "value" in e), "txlog": raw.hex(),
-        "dual_v2": dual, "linear": linear}
+        "dual_v2": dual, "linear": linear, "dual_v1": dual1}
 
 
 # ---------------------------------------------------------------- synthetic

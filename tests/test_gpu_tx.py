@@ -231,3 +231,23 @@ def test_linear_proofs_fixture_and_random(m, ctx, orc, fixtures):
     got = m.verify_linear_proof_batch(items, ctx)
     assert list(got) == exp
     assert any(exp) and not all(exp)
+
+
+def test_dual_proof_v1_fixture_cases(m, ctx, orc, fixtures):
+    from test_tx_oracle import dual_v1_args
+    cols = [[] for _ in range(13)]
+    exp = []
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        assert blob == b""  # all fixture headers carry no tx metadata: one shared blob
+        for c in fx["dual_v1"]:
+            for tamper in (None, "lap", "lin", "last", "tbl"):
+                a = dual_v1_args(c, recs, blob, alhs, tamper)
+                exp.append(orc.verify_dual_proof(*a))
+                for i, v in enumerate(a):
+                    cols[i].append(v)
+    got = m.verify_dual_proof_batch(np.array(cols[0]), np.array(cols[1]), b"", cols[3], cols[4],
+                                    cols[5], cols[6], cols[7], cols[8], cols[9], cols[10],
+                                    cols[11], cols[12], ctx)
+    assert list(got) == exp
+    assert sum(exp) > 400 and not all(exp)

@@ -142,3 +142,43 @@ def test_linear_advance_proof_edges(orc):
     assert orc.verify_linear_advance_proof(None, 5, 6, z, z, 10)
     assert not orc.verify_linear_advance_proof(None, 5, 7, z, z, 10)
     assert not orc.verify_linear_advance_proof(([z, z], []), 5, 7, z, z, 10)
+
+
+def dual_v1_args(c, recs, blob, alhs, tamper=None):
+    """Fixture DualProof (v1) case -> orc.verify_dual_proof arguments."""
+    s, t = c["src"], c["tgt"]
+    dec = lambda xs: [bytes.fromhex(x) for x in xs]  # noqa: E731
+    incl, cons, last = dec(c["incl"]), dec(c["cons"]), dec(c["last"])
+    lin = (c["lin_src"], t, dec(c["lin"]))
+    lap = None if c["lap"] is None else (dec(c["lap"]["terms"]), [dec(x) for x in c["lap"]["incl"]])
+    tbl = bytes.fromhex(c["tbl_alh"])
+    if tamper == "lap" and lap and lap[1] and any(lap[1]):
+        k = next(i for i, x in enumerate(lap[1]) if x)
+        lap[1][k] = [bytes([lap[1][k][0][0] ^ 1]) + lap[1][k][0][1:]] + lap[1][k][1:]
+    if tamper == "lin" and len(lin[2]) > 1:
+        lin = (lin[0], lin[1], lin[2][:-1] + [bytes([lin[2][-1][0] ^ 8]) + lin[2][-1][1:]])
+    if tamper == "last" and last:
+        last = [bytes([last[0][0] ^ 1]) + last[0][1:]] + last[1:]
+    if tamper == "tbl":
+        tbl = bytes(32)
+    return (recs[s - 1], recs[t - 1], blob, incl, cons, tbl, last, lin, lap, s, t, alhs[s - 1],
+            alhs[t - 1])
+
+
+def test_dual_proof_v1_fixture_cases(orc, fixtures):
+    n_lap = 0
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        for c in fx["dual_v1"]:
+            assert orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs)), (name, c["src"],
+                                                                               c["tgt"])
+            if c["lap"] and any(c["lap"]["incl"]):
+                n_lap += 1
+                assert not orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs, "lap"))
+            if len(c["lin"]) > 1:
+                assert not orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs, "lin"))
+            if c["last"]:
+                assert not orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs, "last"))
+            if recs[c["tgt"] - 1]["bl_tx_id"] > 0:
+                assert not orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs, "tbl"))
+    assert n_lap > 10
