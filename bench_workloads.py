@@ -10,6 +10,10 @@
   --workload c2e2e  configs[1] end to end: entries copied host->device from
                     pinned memory, build, levels + root copied back (PCIe
                     inclusive rate, for DESIGN.md; never the headline value).
+  --workload txlog  SURVEY.md 8(a) a14: tx-log read-path validation
+                    (tx.go:388-630) of 2^16 records x 16 entries (16 B keys,
+                    v1, no metadata) through mh_txlog_validate: host parse,
+                    H2D, entry digests + one htree per tx + Alh on the GPU.
 
 Each prints one JSON line.  bench.py stays the driver's headline benchmark.
 """
@@ -36,7 +40,9 @@ def timed(step, steps, warmup, sync):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e"], required=True)
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog"], required=True)
+    p.add_argument("--txs", type=int, default=1 << 16, help="txlog records")
+    p.add_argument("--tx-entries", type=int, default=16, help="txlog entries per record")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--m", type=int, default=10 ** 7, help="c3 appends")
@@ -154,6 +160,57 @@ def main():
                "proof_bytes_GBps": round(P * (D * 32 + 32 + 32 + 24) / (kms * 1e-3) / 1e9, 1),
                "verified": nok, "expected_verified": exp, "bitmap_exact": nok == exp and bool(
                    (ok.cpu().numpy().astype(bool) == ~tamper).all())}
+
+    elif a.workload == "txlog":
+        import struct
+        rng = np.random.default_rng(14)
+        ntx, ne, kl = a.txs, a.tx_entries, 16
+        ent = 2 + 2 + kl + 4 + 8 + 32
+        hdr = 8 + 8 + 8 + 32 + 32 + 2 + 2 + 4
+        rec = hdr + ne * ent + 32
+        buf = np.zeros((ntx, rec), np.uint8)
+        ids = np.arange(1, ntx + 1, dtype=">u8").view(np.uint8).reshape(ntx, 8)
+        buf[:, 0:8] = ids
+        buf[:, 8:16] = np.frombuffer(struct.pack(">Q", 1666885208), np.uint8)
+        buf[:, 24:88] = rng.integers(0, 256, (ntx, 64), dtype=np.uint8)  # blRoot, prevAlh
+        buf[:, 89] = 1  # version 1, mdLen 0
+        buf[:, 92:96] = np.frombuffer(struct.pack(">I", ne), np.uint8)
+        e = buf[:, hdr:hdr + ne * ent].reshape(ntx, ne, ent)
+        e[:, :, 3] = kl
+        e[:, :, 4:4 + kl] = rng.integers(0, 256, (ntx, ne, kl), dtype=np.uint8)
+        e[:, :, 4 + kl + 3] = 100  # vLen
+        e[:, :, 4 + kl + 12:] = rng.integers(0, 256, (ntx, ne, 32), dtype=np.uint8)  # hVal
+        raw = buf.reshape(-1)
+        # seal: the stored Alh of every record is the one the read path recomputes
+        rc, n, used, _, alh, _ = m.txlog_validate(raw, ctx=ctx)
+        assert rc == 0 and n == ntx
+        buf[:, rec - 32:] = alh
+        raw = buf.reshape(-1).copy()
+
+        def step():
+            r = m.txlog_validate(raw, ctx=ctx)
+            assert r[0] == 0 and r[1] == ntx
+
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        t = timed(step, a.steps, a.warmup, sync)
+        ctx.set_timing(False)
+        names = ("txe_assemble", "sha256_csr", "leaf_for", "seg_level", "tx_alh")
+        kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
+        _, _, _, _, _, sts = m.txlog_validate(raw, ctx=ctx)
+        bad = raw.copy()
+        bad[(ntx // 2) * rec + hdr + 4 + kl + 12] ^= 1  # one hVal of the middle record
+        sts_bad = m.txlog_validate(bad, ctx=ctx)[5]
+        comps = ntx * (ne * 2 + 2 * (ne - 1) + 2 + 2)
+        out = {"metric": "tx-log read-path validation (a14), %d records x %d entries" % (ntx, ne),
+               "value": round(ntx / t / 1e6, 3), "unit": "M tx/s",
+               "entries_per_s_M": round(ntx * ne / t / 1e6, 2),
+               "ms_per_step": round(t * 1e3, 3), "log_bytes": int(raw.size),
+               "log_GBps_incl_parse_and_h2d": round(raw.size / t / 1e9, 2),
+               "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
+               "gcomp_per_s_kernels": round(comps / (sum(kt.values()) * 1e-3) / 1e9, 2),
+               "all_valid": bool((sts == 0).all()),
+               "tamper_detected_exactly": bool(list(np.nonzero(sts_bad)[0]) == [ntx // 2])}
 
     else:  # c2e2e
         n, vlen, klen = 1 << 20, 1024, 8

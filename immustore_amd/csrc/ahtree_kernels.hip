@@ -284,17 +284,18 @@ hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64
                                 uint8_t *roots_out, uint32_t *work_ctr) {
     if (!m) return hipSuccess;
     const bool tab = use_node_table();
+    const uint64_t n_end = n0 + m;
     if (tm) tm->begin("aht_leaves", st);
     hipLaunchKernelGGL(k_aht_leaves, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, payloads,
                        m, plen);
     if (tm) tm->end(st);
-    const uint64_t n_end = n0 + m;
     if (tm) tm->begin("aht_perfect", st);
     for (int l = 1; l < 64 && (n_end >> l) != 0; l++) {
         const uint64_t j0 = n0 >> l;             // first j with (j+1)*2^l > n0
         const uint64_t j1 = n_end >> l;          // one past the last j with (j+1)*2^l <= n_end
         if (j1 <= j0) continue;
-        if (tab)
+        // small levels are launch/latency bound: skip the per-workgroup table copy
+        if (tab && j1 - j0 >= (1ull << 18))
             hipLaunchKernelGGL(k_aht_perfect_t,
                                dim3(resident_grid((const void *)k_aht_perfect_t, 512, j1 - j0)),
                                dim3(512), kNodeTabBytes, st, dlog, l, j0, j1 - j0);

@@ -14,9 +14,17 @@ tail -25 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
 cat gpurun_out/bench.json; grep -v amdgpu.ids gpurun_out/bench.err | tail -5
 [ $rc -ne 0 ] && exit $rc
+if [ -n "$WORKLOADS" ]; then
+  for w in $WORKLOADS; do
+    timeout -k 10 300 python bench_workloads.py --workload $w > gpurun_out/w_$w.json 2> gpurun_out/w_$w.err || { grep -v amdgpu.ids gpurun_out/w_$w.err | tail -5; exit 1; }
+    cat gpurun_out/w_$w.json
+  done
+fi
 [ -n "$NO_PROF" ] && exit 0
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?
-tail -3 "$GRAFT_REPO_ROOT/gpurun_out/prof.log"
+# the default bench command (same steps / warmup / builds in flight) under the profiler
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?
+grep '^{"metric"' "$GRAFT_REPO_ROOT/gpurun_out/prof.log" > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json"
+python3 "$GRAFT_REPO_ROOT/tools/prof_summary.py" "$GRAFT_REPO_ROOT/gpurun_out/prof/run_kernel_trace.csv" --steps 20 --warmup 3 | tee "$GRAFT_REPO_ROOT/gpurun_out/prof_summary.json"
 find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*"
 exit $rc
