@@ -16,6 +16,15 @@
                     H2D, entry digests + one htree per tx + Alh on the GPU.
 
 Each prints one JSON line.  bench.py stays the driver's headline benchmark.
+
+Under torch.distributed.run (WORLD_SIZE > 1, one process per GPU) c3 and c5 run
+their SURVEY.md 8(e) multi-GPU forms, weak scaling:
+  c3  every rank appends 2^23 payloads of one global batch (shard = 2^23):
+      local leaves + perfect levels, RCCL all-gather of the 32-byte shard roots,
+      cross-shard nodes, spine (immustore_amd/sharding.py).
+  c5  every rank re-hashes its own 10^6 proofs (split by index, no collective
+      in the timed region).
+MH_DIST_BACKEND=gloo rehearses several ranks on one GPU.
 """
 import argparse
 import json
@@ -38,6 +47,123 @@ def timed(step, steps, warmup, sync):
     return (time.perf_counter() - t0) / steps
 
 
+def distributed_main(a):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import immustore_amd as m
+    from immustore_amd import _native as N
+    from immustore_amd import sharding
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    backend = os.environ.get("MH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if backend == "gloo":
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=dev)
+    stream = torch.cuda.current_stream(dev)
+    ctx = m.Context(dev.index, stream.cuda_stream)
+    L = N.load()
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def timed_max(step):
+        for _ in range(a.warmup):
+            step()
+        sync_all()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        sync_all()
+        t = torch.tensor([(time.perf_counter() - t0) / a.steps], dtype=torch.float64,
+                         device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    if a.workload == "c3":
+        k = 23
+        S = 1 << k
+        m_total = world * S
+        pay = torch.empty(S * 32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 3 + rank))
+        nd = m.nodes_upto(m_total)
+        dlog = torch.empty(nd * 32, dtype=torch.uint8, device=dev)  # globally indexed
+
+        def allgather(ptr):
+            off = ptr - dlog.data_ptr()
+            src = dlog[off:off + 32]
+            if backend == "gloo":
+                out = torch.empty(world * 32, dtype=torch.uint8)
+                dist.all_gather_into_tensor(out, src.cpu())
+                out = out.to(dev)
+            else:
+                out = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+                dist.all_gather_into_tensor(out, src)
+            allgather.keep = out
+            return out.data_ptr()
+
+        def step():
+            sharding.ahtree_sharded_append(ctx, dlog.data_ptr(), pay.data_ptr(), rank, world, k,
+                                           m_total, allgather)
+
+        t = timed_max(step)
+        # the last append's root, on the last rank, vs an independent recurrence
+        # over this rank's own dLog range is checked by tests/test_gpu_sharded.py
+        out = {"metric": "ahtree batch append, sharded, 2^23 payloads per GPU (configs[2] at scale)",
+               "value": round(m_total / t / 1e6, 3), "unit": "M appends/s", "n_gpus": world,
+               "ms_per_step": round(t * 1e3, 3), "scaling": "weak", "appends_total": m_total,
+               "exchange": "all-gather of 32 B per rank (%s)" % backend}
+    elif a.workload == "c5":
+        D = a.depth
+        W = 1 << D
+        P = a.proofs
+        dig = torch.empty(W * 32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_fill_random(ctx.handle, dig.data_ptr(), dig.numel(), 5))
+        levels = torch.empty(m.levels_len(W) * 32, dtype=torch.uint8, device=dev)
+        root = torch.empty(32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_htree_build_digests(ctx.handle, dig.data_ptr(), W, levels.data_ptr(),
+                                             root.data_ptr()))
+        rng = np.random.default_rng(5 + rank)  # this rank's share of the proofs
+        leaf = rng.integers(0, W, P, dtype=np.int64)
+        offs = np.array([m.level_offset(W, lv) for lv in range(D)], np.int64)
+        idx = offs[None, :] + ((leaf[:, None] >> np.arange(D)[None, :]) ^ 1)
+        terms = levels.view(-1, 32)[torch.from_numpy(idx.reshape(-1)).to(dev)].contiguous()
+        digests = dig.view(-1, 32)[torch.from_numpy(leaf).to(dev)].contiguous()
+        roots = root.view(1, 32).expand(P, 32).contiguous()
+        leaf_t = torch.from_numpy(leaf.astype(np.uint64).view(np.int64)).to(dev)
+        width_t = torch.full((P,), W, dtype=torch.int64, device=dev)
+        toff = torch.arange(0, (P + 1) * D, D, dtype=torch.int64, device=dev)
+        ok = torch.zeros(P, dtype=torch.uint8, device=dev)
+
+        def step():
+            N.check(L.mh_dev_htree_verify_inclusion_batch(
+                ctx.handle, P, leaf_t.data_ptr(), width_t.data_ptr(), toff.data_ptr(),
+                terms.data_ptr(), digests.data_ptr(), roots.data_ptr(), ok.data_ptr()))
+
+        t = timed_max(step)
+        nok = torch.tensor([int(ok.sum().item())], dtype=torch.int64,
+                           device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(nok)
+        out = {"metric": "htree inclusion-proof re-hash, 10^6 proofs x depth 24 per GPU",
+               "value": round(world * P / t / 1e6, 3), "unit": "M proofs/s", "n_gpus": world,
+               "ms_per_step": round(t * 1e3, 3), "scaling": "weak",
+               "all_verified": int(nok.item()) == world * P}
+    else:
+        raise SystemExit("multi-GPU mode covers --workload c3 / c5")
+    out["workload"] = a.workload
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    dist.destroy_process_group()
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog"], required=True)
@@ -49,6 +175,8 @@ def main():
     p.add_argument("--proofs", type=int, default=10 ** 6, help="c5 proofs")
     p.add_argument("--depth", type=int, default=24, help="c5 tree depth")
     a = p.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return distributed_main(a)
 
     import numpy as np
     import torch

@@ -154,7 +154,6 @@ struct SpinePairs {
 // the longest wave ~15 % behind the average.  amdgpu_waves_per_eu(6) caps the
 // kernel at 80 VGPRs so three 512-thread workgroups (the LDS limit with the
 // 53 KB table) fit per CU, 6 waves per SIMD.
-template <bool PREFETCH>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k_aht_spine_pairs(uint8_t *__restrict__ dlog,
                                                             uint64_t n0, uint64_t m,
                                                             uint8_t *__restrict__ roots_out,
@@ -199,9 +198,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k
             sk = popsum_below(rest);                                                              \
         }                                                                                         \
         t = t0_;                                                                                  \
-        if (PREFETCH && rest)                                                                     \
-            load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)__builtin_ctzll(rest)) * 32,   \
-                        left);                                                                    \
     } while (0)
         if (!done) MH_SPINE_SETUP();
         for (;;) {
@@ -219,18 +215,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k
             // drop the lowest set bit l of rest (rank popcount(rest) from the
             // top) and prefetch the next step's left node before hashing
             const int l = __builtin_ctzll(rest);
-            if (!PREFETCH) load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)l) * 32, left);
+            load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)l) * 32, left);
             sk -= (l ? ((uint64_t)l << (l - 1)) : 0) +
                   ((uint64_t)(__builtin_popcountll(rest) - 1) << l);
             rest &= rest - 1;
-            uint32_t nxt[8];
-            if (PREFETCH && rest)
-                load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)__builtin_ctzll(rest)) * 32,
-                            nxt);
             node_hash_tab(left, h, h, tab);
             t++;
             store_digest(dlog + (un + (uint64_t)t) * 32, h);
-            if (PREFETCH) copy8(left, nxt);
         }
 #undef MH_SPINE_SETUP
     }
@@ -279,18 +270,22 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }
 
-hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
-                                const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out, uint32_t *work_ctr) {
+// Phase 1: leaves of (n0, n0 + m].
+hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                const uint8_t *payloads, uint64_t m, uint32_t plen) {
     if (!m) return hipSuccess;
-    const bool tab = use_node_table();
-    const uint64_t n_end = n0 + m;
-    if (tm) tm->begin("aht_leaves", st);
+    TimerScope ts(tm, "aht_leaves", st);
     hipLaunchKernelGGL(k_aht_leaves, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, payloads,
                        m, plen);
-    if (tm) tm->end(st);
-    if (tm) tm->begin("aht_perfect", st);
-    for (int l = 1; l < 64 && (n_end >> l) != 0; l++) {
+    return hipGetLastError();
+}
+
+// Phase 2: perfect nodes of levels [lmin, lmax] whose end lies in (n0, n_end].
+hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                 uint64_t n_end, int lmin, int lmax) {
+    const bool tab = use_node_table();
+    TimerScope ts(tm, "aht_perfect", st);
+    for (int l = std::max(lmin, 1); l <= std::min(lmax, 63) && (n_end >> l) != 0; l++) {
         const uint64_t j0 = n0 >> l;             // first j with (j+1)*2^l > n0
         const uint64_t j1 = n_end >> l;          // one past the last j with (j+1)*2^l <= n_end
         if (j1 <= j0) continue;
@@ -303,34 +298,61 @@ hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64
             hipLaunchKernelGGL(k_aht_perfect, dim3(grid_for(j1 - j0, 256)), dim3(256), 0, st, dlog,
                                l, j0, j1 - j0);
     }
-    if (tm) tm->end(st);
-    if (tm) tm->begin("aht_spine", st);
-    if (tab) {
+    return hipGetLastError();
+}
+
+// Phase 3: spine chains of (n0, n0 + m] (every perfect node they read must be
+// in the dLog already).
+hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0, uint64_t m,
+                               uint8_t *roots_out, uint32_t *work_ctr) {
+    if (!m) return hipSuccess;
+    TimerScope ts(tm, "aht_spine", st);
+    const uint64_t n_end = n0 + m;
+    if (use_node_table()) {
         static const SpinePairs pairs = make_spine_pairs();
         if (hipError_t e = hipMemsetAsync(work_ctr, 0, sizeof(uint32_t), st)) return e;
         const uint64_t blk0 = n0 >> 7, nblk = ((n_end - 1) >> 7) - blk0 + 1;
-        static const bool pf = [] {
-            const char *e = getenv("MH_SPINE_PREFETCH");  // A/B knob, default off
-            return e && e[0] == '1';
-        }();
-        if (pf)
-            hipLaunchKernelGGL(
-                k_aht_spine_pairs<true>,
-                dim3(resident_grid((const void *)k_aht_spine_pairs<true>, 512, nblk * 64)),
-                dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
-                work_ctr);
-        else
-            hipLaunchKernelGGL(
-                k_aht_spine_pairs<false>,
-                dim3(resident_grid((const void *)k_aht_spine_pairs<false>, 512, nblk * 64)),
-                dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
-                work_ctr);
+        hipLaunchKernelGGL(k_aht_spine_pairs,
+                           dim3(resident_grid((const void *)k_aht_spine_pairs, 512, nblk * 64)),
+                           dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
+                           work_ctr);
     } else {
         hipLaunchKernelGGL(k_aht_spine, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, m,
                            roots_out);
     }
-    if (tm) tm->end(st);
     return hipGetLastError();
+}
+
+hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                uint8_t *roots_out, uint32_t *work_ctr) {
+    if (!m) return hipSuccess;
+    if (hipError_t e = launch_ahtree_leaves(st, tm, dlog, n0, payloads, m, plen)) return e;
+    if (hipError_t e = launch_ahtree_perfect(st, tm, dlog, n0, n0 + m, 1, 63)) return e;
+    return launch_ahtree_spine(st, tm, dlog, n0, m, roots_out, work_ctr);
+}
+
+// Sharded appends: write the all-gathered shard roots
+// node((r+1) 2^level, level), r < count, into a rank's dLog.
+__global__ void k_aht_put_roots(uint8_t *__restrict__ dlog, int level, uint64_t count,
+                                const uint8_t *__restrict__ roots) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= count) return;
+    const uint64_t e = (r + 1) << level;
+    const uint4 *s = reinterpret_cast<const uint4 *>(roots + r * 32);
+    uint4 *d = reinterpret_cast<uint4 *>(dlog + (dev_nodes_until(e) + (uint64_t)level) * 32);
+    d[0] = s[0];
+    d[1] = s[1];
+}
+
+hipError_t launch_ahtree_put_shard_roots(hipStream_t st, Timer *tm, uint8_t *dlog, int level,
+                                         uint64_t count, const uint8_t *roots) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_aht_put_roots, dim3(grid_for(count, 256)), dim3(256), 0, st, dlog, level,
+                       count, roots);
+    if (hipError_t e = hipGetLastError()) return e;
+    // the cross-shard perfect nodes above them, for every end <= count * 2^level
+    return launch_ahtree_perfect(st, tm, dlog, 0, count << level, level + 1, 63);
 }
 
 }  // namespace mh

@@ -694,6 +694,47 @@ extern "C" int mh_dev_ahtree_append_batch(mh_ctx *c, uint8_t *dlog, uint64_t n0,
     return MH_OK;
 }
 
+extern "C" uint64_t mh_ahtree_node_index(uint64_t n, int level) {
+    return ahtree_nodes_until(n) + (uint64_t)level;
+}
+
+extern "C" int mh_dev_ahtree_append_local(mh_ctx *c, uint8_t *dlog, uint64_t n0,
+                                          const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                          int shard_bits) {
+    if (!c || shard_bits < 0 || shard_bits > 62 || (m && (!dlog || (!payloads && plen))))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n0 & ((1ull << shard_bits) - 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m) return MH_OK;
+    hipSetDevice(c->device);
+    MH_HIP(launch_ahtree_leaves(c->stream, c->tm(), dlog, n0, payloads, m, plen));
+    MH_HIP(launch_ahtree_perfect(c->stream, c->tm(), dlog, n0, n0 + m, 1, shard_bits));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_ahtree_put_shard_roots(mh_ctx *c, uint8_t *dlog, int shard_bits,
+                                             uint64_t count, const uint8_t *roots) {
+    if (!c || shard_bits < 0 || shard_bits > 62 || (count && (!dlog || !roots)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!count) return MH_OK;
+    hipSetDevice(c->device);
+    MH_HIP(launch_ahtree_put_shard_roots(c->stream, c->tm(), dlog, shard_bits, count, roots));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_ahtree_append_spine(mh_ctx *c, uint8_t *dlog, uint64_t n0, uint64_t m,
+                                          uint8_t *roots_out) {
+    if (!c || (m && !dlog)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m) return MH_OK;
+    hipSetDevice(c->device);
+    std::lock_guard<std::mutex> lk(c->mu);
+    MH_HIP(c->s_ctr.ensure(256));
+    MH_HIP(launch_ahtree_spine(c->stream, c->tm(), dlog, n0, m, roots_out,
+                               c->s_ctr.as<uint32_t>()));
+    return MH_OK;
+}
+
 extern "C" int mh_ahtree_new(mh_ctx *c, mh_ahtree **out) {
     if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
     *out = nullptr;

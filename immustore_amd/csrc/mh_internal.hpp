@@ -109,6 +109,15 @@ hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
                                 uint8_t *roots_out, uint32_t *work_ctr);
+// The three phases of launch_ahtree_append, for sharded appends.
+hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                const uint8_t *payloads, uint64_t m, uint32_t plen);
+hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
+                                 uint64_t n_end, int lmin, int lmax);
+hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0, uint64_t m,
+                               uint8_t *roots_out, uint32_t *work_ctr);
+hipError_t launch_ahtree_put_shard_roots(hipStream_t st, Timer *tm, uint8_t *dlog, int level,
+                                         uint64_t count, const uint8_t *roots);
 
 // host-side index math shared with the C API
 uint64_t ahtree_nodes_upto(uint64_t n);

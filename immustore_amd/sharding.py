@@ -1,4 +1,6 @@
-"""Multi-GPU htree build: power-of-two leaf shards + one all-gather of roots.
+"""Multi-GPU builds: power-of-two shards + one all-gather of 32-byte roots.
+
+htree (C2/C4):
 
 SURVEY.md 8(e) / finding 3: if the leaves are cut into contiguous chunks of
 S = 2^k, reducing every chunk with htree's pairing rule and then reducing the
@@ -11,6 +13,16 @@ global levels), the G x 32-byte chunk roots are all-gathered once over RCCL
 
 The payload is 32 B per rank, so the exchange is latency bound (tens of us);
 there is no other data-path collective.
+
+ahtree batch append (C3 at scale): rank r appends
+(r*S, (r+1)*S], S = 2^k.  Its leaves, the perfect nodes of levels <= k and
+every spine node of level < k lie inside its own range; the nodes above level
+k are built from the G shard roots (node((r+1)*S, k)), all-gathered once.
+Each rank keeps a globally indexed dLog and ends with its own range
+byte-identical to a single-device append (ahtree_sharded_append).
+
+Proof verification (C5): proofs are independent -- split by index, no
+collective besides gathering counts / bitmaps.
 """
 from typing import Tuple
 
@@ -48,3 +60,36 @@ def nonempty_roots(gathered, world: int, n: int):
     """Drop the roots of empty shards (ranks past the end of the leaves)."""
     used = sum(1 for r in range(world) if shard_range(r, world, n)[1] > shard_range(r, world, n)[0])
     return gathered[: used * 32]
+
+
+def ahtree_shard_bits(world: int, m: int) -> int:
+    """k such that S = 2^k appends per rank cover m appends (weak scaling passes
+    m = world * S exactly)."""
+    k = 0
+    while (1 << k) * world < m:
+        k += 1
+    return k
+
+
+def ahtree_sharded_append(ctx, dlog_ptr: int, payloads_ptr: int, rank: int, world: int,
+                          shard_bits: int, m_total: int, allgather, plen: int = 32,
+                          roots_out_ptr=None):
+    """This rank's part of appending m_total payloads (global n0 = 0) to an
+    empty tree; payloads_ptr holds only this rank's payloads.  `allgather(ptr)`
+    must all-gather 32 bytes (device pointer) across ranks and return a device
+    pointer to world*32 bytes in rank order.  Returns (n0, m) of this rank."""
+    from . import _native as N
+    L = N.load()
+    S = 1 << shard_bits
+    n0 = min(rank * S, m_total)
+    m = min(S, m_total - n0)
+    N.check(L.mh_dev_ahtree_append_local(ctx.handle, dlog_ptr, n0, payloads_ptr, m, plen,
+                                         shard_bits))
+    # shard root of this rank (any 32 B for a short / empty last shard: unused)
+    idx = L.mh_ahtree_node_index(n0 + S, shard_bits) if m == S else 0
+    gathered = allgather(dlog_ptr + idx * 32)
+    complete = m_total // S
+    N.check(L.mh_dev_ahtree_put_shard_roots(ctx.handle, dlog_ptr, shard_bits,
+                                            min(complete, world), gathered))
+    N.check(L.mh_dev_ahtree_append_spine(ctx.handle, dlog_ptr, n0, m, roots_out_ptr))
+    return n0, m

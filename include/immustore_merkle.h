@@ -213,6 +213,31 @@ int mh_ahtree_dlog_device(mh_ahtree *t, const uint8_t **dptr);
 int mh_dev_ahtree_append_batch(mh_ctx *ctx, uint8_t *dlog, uint64_t n0, const uint8_t *payloads,
                                uint64_t m, uint32_t plen, uint8_t *roots_out);
 uint64_t mh_ahtree_nodes_upto(uint64_t n); /* ahtree.go:492-511 */
+/* dLog index of node(n, level) = nodesUntil(n) + level (ahtree.go:460-462). */
+uint64_t mh_ahtree_node_index(uint64_t n, int level);
+
+/* Sharded batch append.  mh_dev_ahtree_append_batch in three
+ * phases so that G ranks can append one global batch together: rank r owns
+ * appends (n0 + r*S, n0 + (r+1)*S], S = 2^shard_bits, n0 a multiple of S, and
+ * keeps a dLog indexed like the global one (it only fills its own range and
+ * the nodes above shard level).  Every perfect node of level <= shard_bits
+ * and every spine node of a rank lies inside its range except the nodes
+ * above shard level, which are built from the G shard roots.
+ *  1. mh_dev_ahtree_append_local: leaves + perfect nodes of levels
+ *     1..shard_bits ending in (n0, n0 + m];
+ *  2. all-gather the 32-byte shard roots, dLog[mh_ahtree_node_index((r+1)*S
+ *     + n0, shard_bits)] of every complete shard (RCCL, 32 B per rank);
+ *  3. mh_dev_ahtree_put_shard_roots (count = complete shards before the
+ *     global end, roots in shard order, for a batch starting at n0 = 0) writes
+ *     them and the perfect nodes above them; mh_dev_ahtree_append_spine then
+ *     finishes the rank's appends.  The rank's dLog range is byte-identical to
+ *     a single-device append of the whole batch. */
+int mh_dev_ahtree_append_local(mh_ctx *ctx, uint8_t *dlog, uint64_t n0, const uint8_t *payloads,
+                               uint64_t m, uint32_t plen, int shard_bits);
+int mh_dev_ahtree_put_shard_roots(mh_ctx *ctx, uint8_t *dlog, int shard_bits, uint64_t count,
+                                  const uint8_t *roots);
+int mh_dev_ahtree_append_spine(mh_ctx *ctx, uint8_t *dlog, uint64_t n0, uint64_t m,
+                               uint8_t *roots_out);
 
 /* ahtree proof re-hash, batch (verification.go).  kind = MH_AHT_*.
  * INCLUSION:      a = leaf (leafFor(alh)), b = root of j

@@ -82,3 +82,90 @@ def test_shard_ranges_power_of_two():
                 if r < world - 1 and hi < n:
                     assert size and (size & (size - 1)) == 0
             assert covered == n
+
+
+def _aht_model_rank(rank, world, k, pay, orc):
+    """Pure-Python model of immustore_amd.sharding.ahtree_sharded_append's three
+    phases for one rank (ahtree.go:246-322 split by range): returns the rank's
+    dLog entries {index: digest} and its shard root."""
+    import hashlib
+    H = lambda b: hashlib.sha256(b).digest()  # noqa: E731
+    S, m_total = 1 << k, len(pay)
+    n0, m = rank * S, min(S, len(pay) - rank * S)
+    d = {}
+    nu = orc.nodes_until
+    for n in range(n0 + 1, n0 + m + 1):                     # leaves
+        d[nu(n)] = H(b"\x00" + pay[n - 1])
+    for l in range(1, k + 1):                               # perfect, levels <= k
+        for e in range(((n0 >> l) + 1) << l, n0 + m + 1, 1 << l):
+            d[nu(e) + l] = H(b"\x01" + d[nu(e - (1 << (l - 1))) + l - 1] + d[nu(e) + l - 1])
+    root = d[nu(n0 + S) + k] if m == S else b"\0" * 32
+    return d, root, n0, m
+
+
+def _aht_worker(rank, world, port, k, m_total, q):
+    import sys
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root_dir, os.path.join(root_dir, "oracle")]
+    import hashlib
+    import torch.distributed as dist
+    import oracle as orc
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        H = lambda b: hashlib.sha256(b).digest()  # noqa: E731
+        raw = orc.fill_random(32 * m_total, 9)
+        pay = [bytes(raw[32 * i:32 * i + 32]) for i in range(m_total)]
+        d, root, n0, m = _aht_model_rank(rank, world, k, pay, orc)
+        g = torch.empty(world * 32, dtype=torch.uint8)
+        dist.all_gather_into_tensor(g, torch.frombuffer(bytearray(root), dtype=torch.uint8))
+        roots = [bytes(g[32 * r:32 * r + 32].numpy()) for r in range(world)]
+        nu, S = orc.nodes_until, 1 << k
+        complete = min(m_total // S, world)
+        for r in range(complete):                           # put_shard_roots
+            d[nu((r + 1) * S) + k] = roots[r]
+        for l in range(k + 1, 64):
+            if (complete * S) >> l == 0:
+                break
+            for e in range(1 << l, complete * S + 1, 1 << l):
+                d[nu(e) + l] = H(b"\x01" + d[nu(e - (1 << (l - 1))) + l - 1] + d[nu(e) + l - 1])
+        for n in range(n0 + 1, n0 + m + 1):                 # spine (ahtree.go:296-322)
+            h, w, kk, l, c = d[nu(n)], n - 1, n - 1, 0, 1
+            while w > 0:
+                if w & 1:
+                    h = H(b"\x01" + d[nu(kk) + l] + h)
+                    d[nu(n) + c] = h
+                    c += 1
+                kk &= ~(1 << l)
+                w >>= 1
+                l += 1
+        lo, hi = (nu(n0 + 1) if m else 0), (orc.nodes_upto(n0 + m) if m else 0)
+        q.put((rank, lo, b"".join(d[i] for i in range(lo, hi))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,m_total", [(2, 3, 16), (4, 2, 16), (3, 3, 20), (4, 4, 64)])
+def test_sharded_ahtree_append_equals_single_tree(world, k, m_total, orc):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_aht_worker, args=(r, world, port, k, m_total, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (lo, b)) for r, lo, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    t = orc.AHtree()
+    raw = orc.fill_random(32 * m_total, 9).reshape(m_total, 32)
+    t.append_batch(raw)
+    full = t.dlog_bytes()
+    covered = 0
+    for r in range(world):
+        lo, b = res[r]
+        assert full[32 * lo:32 * lo + len(b)] == b, r
+        covered += len(b)
+    assert covered == len(full)
