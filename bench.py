@@ -62,7 +62,7 @@ def parse():
                         "configs[3], 2^23 x 4 KiB per GPU (2^26 entries at 8 GPUs)")
     p.add_argument("--entries", type=int, default=None, help="override entries per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=3,
                    help="independent builds in flight on separate streams (1 = sequential)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU work of the cpu_baseline sample")
@@ -250,7 +250,7 @@ def main():
     lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
     # levels written by one launch of the dominant kernel: the lanes' groups
     # up to level log2(lpl), then each workgroup's subtree 8 levels higher
-    wgl = int(os.environ.get("MH_WG_LEVELS", "8"))
+    wgl = int(os.environ.get("MH_WG_LEVELS", "4"))  # default of launch_entries_fixed
     top = min({1: 0, 2: 1, 4: 2}[lpl] + wgl, max(m.levels_len(n) and (n - 1).bit_length(), 0))
     widths = [-(-n // (1 << l)) for l in range(top + 1)]
     nodes_written = sum(widths)

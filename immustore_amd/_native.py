@@ -206,6 +206,10 @@ SIGNATURES = {
     "mh_ahtree_dlog_device": (i32, [vp, C.POINTER(vp)]),
     "mh_dev_ahtree_append_batch": (i32, [vp, u8p, u64, u8p, u64, u32, u8p]),
     "mh_ahtree_nodes_upto": (u64, [u64]),
+    "mh_htree_inclusion_proof_batch": (i32, [vp, u64, vp, u8p, u32, vp, vp]),
+    "mh_dev_htree_inclusion_proof_batch": (i32, [vp, u8p, u64, u64, vp, u8p, u32, vp, vp]),
+    "mh_ahtree_proof_batch": (i32, [vp, i32, u64, vp, vp, u8p, u32, vp, vp]),
+    "mh_dev_ahtree_proof_batch": (i32, [vp, i32, u8p, u64, u64, vp, vp, u8p, u32, vp, vp]),
     "mh_ahtree_node_index": (u64, [u64, i32]),
     "mh_dev_ahtree_append_local": (i32, [vp, u8p, u64, u8p, u64, u32, i32]),
     "mh_dev_ahtree_put_shard_roots": (i32, [vp, u8p, i32, u64, u8p]),

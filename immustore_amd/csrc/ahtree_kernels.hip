@@ -24,25 +24,6 @@
 
 namespace mh {
 
-// S(x) = sum_{i<x} popcount(i): process the set bits of x from the top; the
-// j-th set bit b (j = 1 for the highest) contributes b*2^(b-1) + (j-1)*2^b.
-__host__ __device__ inline uint64_t popsum_below(uint64_t x) {
-    uint64_t s = 0, j = 0;
-    while (x) {
-        const int b = 63 - __builtin_clzll(x);
-        s += (b ? ((uint64_t)b << (b - 1)) : 0) + (j << b);
-        j++;
-        x &= ~(1ull << b);
-    }
-    return s;
-}
-
-// nodesUpto(n) = n + S(n)           (ahtree.go:492-511)
-// nodesUntil(n) = nodesUpto(n - 1)  (ahtree.go:485-490)
-__host__ __device__ inline uint64_t until_from_s(uint64_t n, uint64_t s_n) {
-    return (n - 1) + s_n - (uint64_t)__builtin_popcountll(n - 1);
-}
-
 uint64_t ahtree_nodes_upto(uint64_t n) { return n + popsum_below(n); }
 uint64_t ahtree_nodes_until(uint64_t n) { return n <= 1 ? 0 : ahtree_nodes_upto(n - 1); }
 

@@ -8,6 +8,7 @@
 // CPU hashing fallback: without a usable device every entry point returns
 // MH_ERR_NO_DEVICE.
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -558,6 +559,61 @@ extern "C" int mh_htree_inclusion_proof(mh_htree *t, uint64_t i, uint8_t *terms,
     return MH_OK;
 }
 
+// Batch proof generation on the device.
+static int proof_batch_host(mh_ctx *c, hipStream_t st, uint64_t n, const uint64_t *a,
+                            const uint64_t *b, uint32_t max_terms, uint8_t *terms,
+                            uint32_t *nterms, int32_t *status,
+                            const std::function<hipError_t(const uint64_t *, const uint64_t *,
+                                                           uint8_t *, uint32_t *, int32_t *)> &run) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipSetDevice(c->device);
+    const uint64_t b_a = 0, b_b = (n * 8 + 255) & ~255ull, b_t = b_b + ((n * 8 + 255) & ~255ull),
+                   b_n = b_t + ((n * max_terms * 32 + 255) & ~255ull),
+                   b_s = b_n + ((n * 4 + 255) & ~255ull), total = b_s + n * 4 + 64;
+    MH_HIP(c->s_msgs.ensure(total));
+    uint8_t *base = c->s_msgs.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base + b_a, a, n * 8, hipMemcpyHostToDevice, st));
+    if (b) MH_HIP(hipMemcpyAsync(base + b_b, b, n * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(run((const uint64_t *)(base + b_a), (const uint64_t *)(base + b_b), base + b_t,
+               (uint32_t *)(base + b_n), (int32_t *)(base + b_s)));
+    MH_HIP(hipMemcpyAsync(terms, base + b_t, n * max_terms * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(nterms, base + b_n, n * 4, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(status, base + b_s, n * 4, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+extern "C" int mh_htree_inclusion_proof_batch(mh_htree *t, uint64_t n, const uint64_t *leaf,
+                                              uint8_t *terms, uint32_t max_terms, uint32_t *nterms,
+                                              int32_t *status) {
+    if (!t || (n && (!leaf || !terms || !nterms || !status || !max_terms)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    const uint8_t *lv = t->levels.as<uint8_t>();
+    const uint64_t w = t->width;
+    hipStream_t st = t->stream;
+    Timer *tm = t->ctx->tm();
+    return proof_batch_host(t->ctx, st, n, leaf, nullptr, max_terms, terms, nterms, status,
+                            [&](const uint64_t *a, const uint64_t *, uint8_t *tt, uint32_t *nt,
+                                int32_t *ss) {
+                                return launch_htree_proof(st, tm, lv, w, n, a, tt, max_terms, nt,
+                                                          ss);
+                            });
+}
+
+extern "C" int mh_dev_htree_inclusion_proof_batch(mh_ctx *c, const uint8_t *levels, uint64_t width,
+                                                  uint64_t n, const uint64_t *leaf, uint8_t *terms,
+                                                  uint32_t max_terms, uint32_t *nterms,
+                                                  int32_t *status) {
+    if (!c || (n && (!levels || !leaf || !terms || !nterms || !status || !max_terms)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    hipSetDevice(c->device);
+    MH_HIP(launch_htree_proof(c->stream, c->tm(), levels, width, n, leaf, terms, max_terms, nterms,
+                              status));
+    return MH_OK;
+}
+
 extern "C" int mh_htree_levels(mh_htree *t, uint8_t *out, uint64_t cap_nodes) {
     if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
     const uint64_t total = mh_htree_levels_len(t->width);
@@ -906,6 +962,7 @@ extern "C" int mh_ahtree_inclusion_proof(mh_ahtree *t, uint64_t i, uint64_t j, u
     *nterms = 0;
     if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;    // ahtree.go:534-536
     if (j > t->size) return MH_ERR_UNEXISTENT_DATA;  // ahtree.go:538-540
+    if (j == 0) return MH_ERR_UNEXISTENT_DATA;       // Go fails reading node(0, .)
     std::vector<uint64_t> s;
     aht_incl(i, j, bits_len64(j - 1), s);
     return aht_emit(t, s, terms, cap, nterms);
@@ -917,9 +974,43 @@ extern "C" int mh_ahtree_consistency_proof(mh_ahtree *t, uint64_t i, uint64_t j,
     *nterms = 0;
     if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;
     if (j > t->size) return MH_ERR_UNEXISTENT_DATA;
+    if (j == 0) return MH_ERR_UNEXISTENT_DATA;
     std::vector<uint64_t> s;
     aht_cons(i, j, bits_len64(j - 1), s);
     return aht_emit(t, s, terms, cap, nterms);
+}
+
+extern "C" int mh_ahtree_proof_batch(mh_ahtree *t, int kind, uint64_t n, const uint64_t *i,
+                                     const uint64_t *j, uint8_t *terms, uint32_t max_terms,
+                                     uint32_t *nterms, int32_t *status) {
+    if (!t || (kind != MH_AHT_INCLUSION && kind != MH_AHT_CONSISTENCY) ||
+        (n && (!i || !j || !terms || !nterms || !status || !max_terms)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    const uint8_t *dl = t->dlog.as<uint8_t>();
+    const uint64_t size = t->size;
+    hipStream_t st = t->stream;
+    Timer *tm = t->ctx->tm();
+    return proof_batch_host(t->ctx, st, n, i, j, max_terms, terms, nterms, status,
+                            [&](const uint64_t *a, const uint64_t *b, uint8_t *tt, uint32_t *nt,
+                                int32_t *ss) {
+                                return launch_ahtree_proof(st, tm, kind, dl, size, n, a, b, tt,
+                                                           max_terms, nt, ss);
+                            });
+}
+
+extern "C" int mh_dev_ahtree_proof_batch(mh_ctx *c, int kind, const uint8_t *dlog, uint64_t size,
+                                         uint64_t n, const uint64_t *i, const uint64_t *j,
+                                         uint8_t *terms, uint32_t max_terms, uint32_t *nterms,
+                                         int32_t *status) {
+    if (!c || (kind != MH_AHT_INCLUSION && kind != MH_AHT_CONSISTENCY) ||
+        (n && (!dlog || !i || !j || !terms || !nterms || !status || !max_terms)))
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!n) return MH_OK;
+    hipSetDevice(c->device);
+    MH_HIP(launch_ahtree_proof(c->stream, c->tm(), kind, dlog, size, n, i, j, terms, max_terms,
+                               nterms, status));
+    return MH_OK;
 }
 
 extern "C" int mh_ahtree_reset_size(mh_ahtree *t, uint64_t new_size) {

@@ -8,6 +8,29 @@
 
 namespace mh {
 
+// S(x) = sum_{i<x} popcount(i): process the set bits of x from the top; the
+// j-th set bit b (j = 1 for the highest) contributes b*2^(b-1) + (j-1)*2^b.
+__host__ __device__ inline uint64_t popsum_below(uint64_t x) {
+    uint64_t s = 0, j = 0;
+    while (x) {
+        const int b = 63 - __builtin_clzll(x);
+        s += (b ? ((uint64_t)b << (b - 1)) : 0) + (j << b);
+        j++;
+        x &= ~(1ull << b);
+    }
+    return s;
+}
+
+// nodesUpto(n) = n + S(n)           (ahtree.go:492-511)
+// nodesUntil(n) = nodesUpto(n - 1)  (ahtree.go:485-490)
+__host__ __device__ inline uint64_t until_from_s(uint64_t n, uint64_t s_n) {
+    return (n - 1) + s_n - (uint64_t)__builtin_popcountll(n - 1);
+}
+
+// nodesUpto(n) for device code (proof_kernels.hip)
+__host__ __device__ inline uint64_t ahtree_nodes_upto_dev(uint64_t n) { return n + popsum_below(n); }
+
+
 constexpr int kMaxLevels = 66;
 
 // Level-major flat layout of an htree of width n (embedded/htree/htree.go:
@@ -152,4 +175,13 @@ hipError_t launch_seg_level(hipStream_t st, Timer *tm, uint64_t nnodes, uint64_t
 // idx[p] == ~0 writes SHA256(nil) (the empty tree's root, htree.go:73-77)
 hipError_t launch_gather32(hipStream_t st, uint64_t n, const uint8_t *src, const uint64_t *idx,
                            uint8_t *out);
+
+// ---------------------------------------------------------------- proofs on the device
+hipError_t launch_htree_proof(hipStream_t st, Timer *tm, const uint8_t *levels, uint64_t w,
+                              uint64_t n, const uint64_t *leaf, uint8_t *terms, uint32_t max_terms,
+                              uint32_t *nterms, int32_t *status);
+hipError_t launch_ahtree_proof(hipStream_t st, Timer *tm, int kind, const uint8_t *dlog,
+                               uint64_t size, uint64_t n, const uint64_t *i, const uint64_t *j,
+                               uint8_t *terms, uint32_t max_terms, uint32_t *nterms,
+                               int32_t *status);
 }  // namespace mh

@@ -14,7 +14,7 @@ Every hash is computed by the HIP kernels of libimmustore_merkle.so.
 """
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -193,6 +193,19 @@ class HTree:
 
     InclusionProof = inclusion_proof
 
+    def inclusion_proof_batch(self, leaves) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Device-generated InclusionProof for many leaves: (terms[n, max, 32],
+        nterms[n], status[n]); terms in Go order."""
+        lv = np.ascontiguousarray(leaves, np.uint64)
+        n = lv.size
+        mt = max(1, (max(self.width, 1) - 1).bit_length())
+        terms = np.zeros((max(n, 1), mt, 32), np.uint8)
+        nt = np.zeros(max(n, 1), np.uint32)
+        st = np.zeros(max(n, 1), np.int32)
+        N.check(self._lib.mh_htree_inclusion_proof_batch(self.handle, n, _addr(lv), _addr(terms),
+                                                         mt, _addr(nt), _addr(st)))
+        return terms[:n], nt[:n], st[:n]
+
     def levels(self) -> np.ndarray:
         tot = levels_len(self.width)
         out = np.zeros((max(tot, 1), 32), np.uint8)
@@ -327,6 +340,19 @@ class AHtree:
         return self._proof(self._lib.mh_ahtree_consistency_proof, i, j)
 
     ConsistencyProof = consistency_proof
+
+    def proof_batch(self, kind: int, i, j, max_terms: int = 128):
+        """Device-generated Inclusion (kind 0) / Consistency (kind 1) proofs for
+        many (i, j): (terms[n, max_terms, 32], nterms[n], status[n])."""
+        a = np.ascontiguousarray(i, np.uint64)
+        b = np.ascontiguousarray(j, np.uint64)
+        n = a.size
+        terms = np.zeros((max(n, 1), max_terms, 32), np.uint8)
+        nt = np.zeros(max(n, 1), np.uint32)
+        st = np.zeros(max(n, 1), np.int32)
+        N.check(self._lib.mh_ahtree_proof_batch(self.handle, kind, n, _addr(a), _addr(b),
+                                                _addr(terms), max_terms, _addr(nt), _addr(st)))
+        return terms[:n], nt[:n], st[:n]
 
     def reset_size(self, new_size: int):
         N.check(self._lib.mh_ahtree_reset_size(self.handle, new_size))

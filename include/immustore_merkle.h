@@ -141,6 +141,13 @@ int mh_htree_inclusion_proof(mh_htree *t, uint64_t i, uint8_t *terms, uint32_t c
                              uint32_t *nterms);
 /* copy of the used levels (mh_htree_levels_len(width) nodes) */
 int mh_htree_levels(mh_htree *t, uint8_t *out, uint64_t cap_nodes);
+/* Many (*HTree).InclusionProof calls at once (htree.go:121-164), generated on
+ * the device from the tree's resident levels: proof p (leaf[p]) gets nterms[p]
+ * terms at terms + p * max_terms * 32, Go order (leaf side first);
+ * status[p] = MH_OK or MH_ERR_ILLEGAL_ARGUMENTS (leaf >= width, or more than
+ * max_terms terms; ceil(log2 width) always suffices). */
+int mh_htree_inclusion_proof_batch(mh_htree *t, uint64_t n, const uint64_t *leaf, uint8_t *terms,
+                                   uint32_t max_terms, uint32_t *nterms, int32_t *status);
 /* device pointer of the handle's level buffer (device-resident consumers) */
 int mh_htree_levels_device(mh_htree *t, const uint8_t **dptr);
 
@@ -176,6 +183,14 @@ int mh_dev_htree_reduce_nodes(mh_ctx *ctx, const uint8_t *nodes, uint64_t w, uin
 /* SHA-256 of n byte ranges buf[off[i], off[i+1]) -> out (n*32). */
 int mh_dev_sha256_batch(mh_ctx *ctx, const uint8_t *buf, const uint64_t *off, uint64_t n,
                         uint8_t *out);
+/* Device variants of the batch proof generators: every pointer is device
+ * memory (levels of a tree of `width` leaves / a dLog of `size` appends). */
+int mh_dev_htree_inclusion_proof_batch(mh_ctx *ctx, const uint8_t *levels, uint64_t width,
+                                       uint64_t n, const uint64_t *leaf, uint8_t *terms,
+                                       uint32_t max_terms, uint32_t *nterms, int32_t *status);
+int mh_dev_ahtree_proof_batch(mh_ctx *ctx, int kind, const uint8_t *dlog, uint64_t size,
+                              uint64_t n, const uint64_t *i, const uint64_t *j, uint8_t *terms,
+                              uint32_t max_terms, uint32_t *nterms, int32_t *status);
 int mh_dev_htree_verify_inclusion_batch(mh_ctx *ctx, uint64_t nproofs, const uint64_t *leaf,
                                         const uint64_t *width, const uint64_t *term_off,
                                         const uint8_t *terms, const uint8_t *digests,
@@ -203,6 +218,14 @@ int mh_ahtree_inclusion_proof(mh_ahtree *t, uint64_t i, uint64_t j, uint8_t *ter
 int mh_ahtree_consistency_proof(mh_ahtree *t, uint64_t i, uint64_t j, uint8_t *terms,
                                 uint32_t cap, uint32_t *nterms);
 /* (*AHtree).ResetSize                                     ahtree.go:375-458 */
+/* Many (*AHtree).InclusionProof (kind MH_AHT_INCLUSION, ahtree.go:525-577) or
+ * ConsistencyProof (MH_AHT_CONSISTENCY, :579-651) calls at once, generated on
+ * the device from the resident dLog; layout as mh_htree_inclusion_proof_batch;
+ * status[p]: MH_OK, MH_ERR_ILLEGAL_ARGUMENTS (i > j, or > max_terms terms),
+ * MH_ERR_UNEXISTENT_DATA (j > size or j == 0).  128 terms always suffice. */
+int mh_ahtree_proof_batch(mh_ahtree *t, int kind, uint64_t n, const uint64_t *i,
+                          const uint64_t *j, uint8_t *terms, uint32_t max_terms, uint32_t *nterms,
+                          int32_t *status);
 int mh_ahtree_reset_size(mh_ahtree *t, uint64_t new_size);
 /* copy dLog digests [first, first+count) (the tree/NNNNNNNN.sha byte stream) */
 int mh_ahtree_dlog(mh_ahtree *t, uint64_t first, uint64_t count, uint8_t *out);

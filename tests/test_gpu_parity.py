@@ -455,3 +455,53 @@ def test_htree_verify_batch_c5_shape(m, ctx, orc):
     got = m.verify_inclusion_batch(proofs, digs, [root] * P, ctx)
     assert list(got) == exp
     assert 0.85 < np.mean(exp) < 0.95
+
+
+# ------------------------------------------------------------------ device proof generation
+def test_htree_inclusion_proof_batch_vs_oracle(m, ctx, orc):
+    """InclusionProof (htree.go:121-164) generated on the
+    device for every leaf of several widths, equal to the oracle's proofs."""
+    rng = np.random.default_rng(12)
+    for w in [1, 2, 3, 5, 8, 17, 100, 1000, 1025, 4096, 5000]:
+        d = rng.integers(0, 256, (w, 32), dtype=np.uint8)
+        t = m.HTree(max(w, 1), ctx)
+        t.build_with(d)
+        lv, _ = orc.htree_build(d)
+        leaves = np.arange(w) if w <= 1025 else rng.integers(0, w, 700)
+        terms, nt, st = t.inclusion_proof_batch(leaves)
+        assert not st.any()
+        for k, i in enumerate(leaves):
+            _, ot = orc.htree_inclusion_proof(lv, w, int(i))
+            assert nt[k] == len(ot) and terms[k, :nt[k]].tobytes() == ot.tobytes(), (w, i)
+        _, _, st = t.inclusion_proof_batch([w])
+        assert st[0] == m._native.MH_ERR_ILLEGAL_ARGUMENTS
+        t.close()
+
+
+def test_ahtree_proof_batch_vs_oracle(m, ctx, orc):
+    """ahtree InclusionProof / ConsistencyProof (ahtree.go:525-651) on the
+    device for all pairs j <= 70 and random pairs up to 10^5."""
+    N_ = 100000
+    pay = orc.fill_random(32 * N_, 21).reshape(N_, 32)
+    t = m.AHtree(ctx)
+    t.append_batch(pay)
+    o = orc.AHtree(N_)
+    o.append_batch(pay)
+    rng = np.random.default_rng(13)
+    pairs = [(i, j) for j in range(1, 71) for i in range(0, j + 1)]
+    jj = rng.integers(1, N_ + 1, 3000)
+    pairs += [(int(rng.integers(1, j + 1)), int(j)) for j in jj] + [(N_, N_), (1, N_)]
+    I = np.array([p[0] for p in pairs], np.uint64)
+    J = np.array([p[1] for p in pairs], np.uint64)
+    for kind, fn in ((0, o.inclusion_proof), (1, o.consistency_proof)):
+        terms, nt, st = t.proof_batch(kind, I, J)
+        assert not st.any()
+        for k, (i, j) in enumerate(pairs):
+            if i == 0:
+                continue  # the oracle's proof walk needs i >= 1
+            _, ot = fn(i, j)
+            assert nt[k] == len(ot) and terms[k, :nt[k]].tobytes() == ot.tobytes(), (kind, i, j)
+    # argument checks (ahtree.go:534-540)
+    _, _, st = t.proof_batch(0, [5, 1, 0], [4, N_ + 1, 0])
+    assert list(st) == [2, 5, 5]
+    t.close()
