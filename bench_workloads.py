@@ -137,7 +137,6 @@ def distributed_main(a):
         terms = levels.view(-1, 32)[torch.from_numpy(idx.reshape(-1)).to(dev)].contiguous()
         digests = dig.view(-1, 32)[torch.from_numpy(leaf).to(dev)].contiguous()
         roots = root.view(1, 32).expand(P, 32).contiguous()
-        leaf_t = torch.from_numpy(leaf.astype(np.uint64).view(np.int64)).to(dev)
         width_t = torch.full((P,), W, dtype=torch.int64, device=dev)
         toff = torch.arange(0, (P + 1) * D, D, dtype=torch.int64, device=dev)
         ok = torch.zeros(P, dtype=torch.uint8, device=dev)
@@ -253,17 +252,29 @@ def main():
         sync()
         rng = np.random.default_rng(5)
         leaf = rng.integers(0, W, P, dtype=np.int64)
-        # width 2^D: the proof of leaf i is its sibling at every level
-        # (htree.go:121-164 on a perfect tree), leaf side first
-        offs = np.array([m.level_offset(W, lv) for lv in range(D)], np.int64)
-        idx = offs[None, :] + ((leaf[:, None] >> np.arange(D)[None, :]) ^ 1)
-        lv = levels.view(-1, 32)
-        terms = lv[torch.from_numpy(idx.reshape(-1)).to(dev)].contiguous()
+        leaf_t = torch.from_numpy(leaf.astype(np.uint64).view(np.int64)).to(dev)
+        # the proofs themselves, generated on the device from the resident
+        # levels (htree.go:121-164 as a gather); width
+        # 2^D: exactly D terms each, so the fixed stride is the CSR layout
+        terms = torch.empty(P * D * 32, dtype=torch.uint8, device=dev)
+        nterms = torch.empty(P, dtype=torch.int32, device=dev)
+        pst = torch.empty(P, dtype=torch.int32, device=dev)
+
+        def gen():
+            N.check(L.mh_dev_htree_inclusion_proof_batch(
+                ctx.handle, levels.data_ptr(), W, P, leaf_t.data_ptr(), terms.data_ptr(), D,
+                nterms.data_ptr(), pst.data_ptr()))
+
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        tgen = timed(gen, a.steps, a.warmup, sync)
+        ctx.set_timing(False)
+        assert int(pst.abs().sum().item()) == 0 and int((nterms != D).sum().item()) == 0
+        gen_ms = ctx.timing("htree_proof")[0] / (a.steps + a.warmup)
         tamper = rng.random(P) < 0.10
         src = np.where(tamper, (leaf + 1) % W, leaf)  # wrong digest for 10 %
         digests = dig.view(-1, 32)[torch.from_numpy(src).to(dev)].contiguous()
         roots = root.view(1, 32).expand(P, 32).contiguous()
-        leaf_t = torch.from_numpy(leaf.astype(np.uint64).view(np.int64)).to(dev)
         width_t = torch.full((P,), W, dtype=torch.int64, device=dev)
         toff = torch.arange(0, (P + 1) * D, D, dtype=torch.int64, device=dev)
         ok = torch.zeros(P, dtype=torch.uint8, device=dev)
@@ -286,6 +297,9 @@ def main():
                "ms_per_step": round(t * 1e3, 3), "kernel_ms": round(kms, 3),
                "gcomp_per_s": round(comps / (kms * 1e-3) / 1e9, 2),
                "proof_bytes_GBps": round(P * (D * 32 + 32 + 32 + 24) / (kms * 1e-3) / 1e9, 1),
+               "proof_generation": {"M_proofs_per_s": round(P / tgen / 1e6, 1),
+                                    "kernel_ms": round(gen_ms, 3),
+                                    "terms_GBps": round(P * D * 32 / (gen_ms * 1e-3) / 1e9, 1)},
                "verified": nok, "expected_verified": exp, "bitmap_exact": nok == exp and bool(
                    (ok.cpu().numpy().astype(bool) == ~tamper).all())}
 
