@@ -163,7 +163,7 @@ def distributed_main(a):
     dist.destroy_process_group()
 
 
-def main():
+def make_parser():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog"], required=True)
     p.add_argument("--txs", type=int, default=1 << 16, help="txlog records")
@@ -173,10 +173,11 @@ def main():
     p.add_argument("--m", type=int, default=10 ** 7, help="c3 appends")
     p.add_argument("--proofs", type=int, default=10 ** 6, help="c5 proofs")
     p.add_argument("--depth", type=int, default=24, help="c5 tree depth")
-    a = p.parse_args()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        return distributed_main(a)
+    return p
 
+
+def run_single(a):
+    """One GPU: run workload a.workload, return its result dict."""
     import numpy as np
     import torch
     import immustore_amd as m
@@ -390,8 +391,15 @@ def main():
                "ms_per_step": round(t * 1e3, 3), "device_resident_ms": round(td * 1e3, 3),
                "h2d_bytes": n * (vlen + klen), "d2h_bytes": nl * 32 + 32}
     out["workload"] = a.workload
-    print(json.dumps(out), flush=True)
     ctx.close()
+    return out
+
+
+def main():
+    a = make_parser().parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return distributed_main(a)
+    print(json.dumps(run_single(a)), flush=True)
 
 
 if __name__ == "__main__":

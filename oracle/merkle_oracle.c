@@ -686,6 +686,21 @@ void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed) {
     }
 }
 
+/* Batch of htree.VerifyInclusion calls (htree.go:166-195), fixed term stride;
+ * the CPU side of BASELINE configs[4].  Returns the number verified. */
+uint64_t orc_htree_verify_batch(uint64_t n, const uint64_t *leaf, uint64_t width,
+                                const uint8_t *terms, uint32_t nterms_each,
+                                const uint8_t *digests, const uint8_t root[32], uint8_t *ok) {
+    uint64_t cnt = 0;
+    for (uint64_t p = 0; p < n; p++) {
+        const int r = orc_htree_verify_inclusion(leaf[p], width, terms + (uint64_t)p * nterms_each * 32,
+                                                 nterms_each, digests + p * 32, root);
+        if (ok) ok[p] = (uint8_t)r;
+        cnt += (uint64_t)r;
+    }
+    return cnt;
+}
+
 /* ------------------------------------------------------------------ tx layer */
 int orc_tx_header_alh(const orc_tx_header *h, const uint8_t *md_blob, uint8_t inner[32],
                       uint8_t alh[32]) {

@@ -49,6 +49,12 @@ int orc_htree_inclusion_proof(const uint8_t *levels, uint64_t width, uint64_t i,
 int orc_htree_verify_inclusion(uint64_t leaf, uint64_t width, const uint8_t *terms,
                                uint32_t nterms, const uint8_t digest[32], const uint8_t root[32]);
 
+/* n VerifyInclusion calls with a fixed term stride (BASELINE configs[4] on
+ * the CPU); returns how many verify, ok[p] (may be NULL) per proof. */
+uint64_t orc_htree_verify_batch(uint64_t n, const uint64_t *leaf, uint64_t width,
+                                const uint8_t *terms, uint32_t nterms_each,
+                                const uint8_t *digests, const uint8_t root[32], uint8_t *ok);
+
 /* Value hash loop (embedded/store/immustore.go:1620-1630) + Tx.BuildHashTree
  * (embedded/store/tx.go:332-355): CSR inputs (offsets have n+1 entries).
  * md / md_off may be NULL (no KV metadata).  hval_override / use_override

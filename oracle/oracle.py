@@ -69,6 +69,9 @@ def lib():
         L.orc_ahtree_verify_last_inclusion.argtypes = [u8p, C.c_uint32, C.c_uint64, u8p, u8p]
         L.orc_fill_random.argtypes = [u8p, C.c_uint64, C.c_uint64]
         L.orc_tx_header_alh.argtypes = [u8p, u8p, u8p, u8p]
+        L.orc_htree_verify_batch.restype = C.c_uint64
+        L.orc_htree_verify_batch.argtypes = [C.c_uint64, u64p, C.c_uint64, u8p, C.c_uint32, u8p,
+                                             u8p, u8p]
         L.orc_verify_linear_proof.argtypes = [C.c_uint64, C.c_uint64, u8p, C.c_uint32, C.c_uint64,
                                               C.c_uint64, u8p, u8p]
         L.orc_verify_linear_advance_proof.argtypes = [C.c_int, u8p, C.c_uint32, u8p, u32p,
@@ -400,3 +403,15 @@ def verify_dual_proof(sh, th, md_blob, incl, cons, tbl_alh, last, lin, lap, src,
         _p(a.view(np.uint8)), _p(b.view(np.uint8)), _p(mb), ip_, ni, cp_, nc, _p(_u8(tbl_alh)),
         lp_, nl, has_lin, ls, lt, lin_p, nlin, has_lap, lap_p, nlap, inc_p, _p(off, u32p), ninc,
         src, tgt, _p(_u8(src_alh)), _p(_u8(tgt_alh))))
+
+
+def htree_verify_batch(leaf, width, terms, digests, root):
+    """terms: (n, D, 32) uint8; returns (count verified, ok[n])."""
+    lf = np.ascontiguousarray(leaf, np.uint64)
+    t = np.ascontiguousarray(terms, np.uint8)
+    d = np.ascontiguousarray(digests, np.uint8)
+    n, D = t.shape[0], t.shape[1]
+    ok = np.zeros(max(n, 1), np.uint8)
+    c = lib().orc_htree_verify_batch(n, _p(lf, u64p), width, _p(t), D, _p(d), _p(_u8(root)),
+                                     _p(ok))
+    return c, ok[:n]
