@@ -14,6 +14,13 @@
                     (tx.go:388-630) of 2^16 records x 16 entries (16 B keys,
                     v1, no metadata) through mh_txlog_validate: host parse,
                     H2D, entry digests + one htree per tx + Alh on the GPU.
+  --workload commit SURVEY.md 8(f) row 1: ImmuStore.precommit hashing over a
+                    batch of 2^16 txs x 16 entries x 1 KiB values (8 B keys,
+                    v1) in pinned host memory through mh_precommit_batch: value
+                    hashes, entry digests, one htree per tx, hVals + Eh copied
+                    back; chunked two-stream pipeline vs one chunk, next to the
+                    plain pinned H2D rate of the same bytes (the PCIe bound) and
+                    the oracle on 16 host threads.
 
 Each prints one JSON line.  bench.py stays the driver's headline benchmark.
 
@@ -165,9 +172,11 @@ def distributed_main(a):
 
 def make_parser():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog"], required=True)
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit"], required=True)
     p.add_argument("--txs", type=int, default=1 << 16, help="txlog records")
     p.add_argument("--tx-entries", type=int, default=16, help="txlog entries per record")
+    p.add_argument("--vlen", type=int, default=1024, help="commit value bytes")
+    p.add_argument("--chunk-mib", type=int, default=64, help="commit pipeline chunk")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--m", type=int, default=10 ** 7, help="c3 appends")
@@ -354,6 +363,77 @@ def run_single(a):
                "gcomp_per_s_kernels": round(comps / (sum(kt.values()) * 1e-3) / 1e9, 2),
                "all_valid": bool((sts == 0).all()),
                "tamper_detected_exactly": bool(list(np.nonzero(sts_bad)[0]) == [ntx // 2])}
+
+    elif a.workload == "commit":
+        ntx, per, vlen = a.txs, a.tx_entries, a.vlen
+        n = ntx * per
+        vals = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()
+        g = torch.Generator().manual_seed(2)
+        for k in range(0, n * vlen, 1 << 28):  # chunked: bounded host temporaries
+            e = min(n * vlen, k + (1 << 28))
+            vals[k:e].copy_(torch.randint(0, 256, (e - k,), dtype=torch.uint8, generator=g))
+        keys = torch.from_numpy(np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8)
+                                .copy()).pin_memory()
+        pin_u64 = lambda x: torch.from_numpy(x.view(np.int64)).pin_memory().numpy().view(np.uint64)  # noqa: E731
+        b = dict(tx_off=pin_u64(np.arange(0, n + 1, per, dtype=np.uint64)), keys=keys.numpy(),
+                 key_off=pin_u64(np.arange(0, 8 * n + 1, 8, dtype=np.uint64)), vals=vals.numpy(),
+                 val_off=pin_u64(np.arange(0, vlen * n + 1, vlen, dtype=np.uint64)))
+        hv = torch.empty(n * 32, dtype=torch.uint8).pin_memory().numpy().reshape(n, 32)
+        eh = torch.empty(ntx * 32, dtype=torch.uint8).pin_memory().numpy().reshape(ntx, 32)
+        res = {}
+        for name, chunk in (("pipelined", a.chunk_mib << 20), ("one_chunk", n * (vlen + 8) + 1)):
+            p = m.CommitPipe(ctx, chunk_bytes=chunk)
+
+            def step():
+                _, _, st = p.precommit_csr(1, hvals_out=hv, eh_out=eh, **b)
+                assert (st == 0).all()
+
+            res[name] = timed(step, a.steps, a.warmup, sync)
+            p.close()
+        # the PCIe bound: plain pinned H2D of the same value + key bytes
+        dv = torch.empty(n * vlen, dtype=torch.uint8, device=dev)
+        dk = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+
+        def h2d():
+            dv.copy_(vals, non_blocking=True)
+            dk.copy_(keys, non_blocking=True)
+
+        t_h2d = timed(h2d, a.steps, a.warmup, sync)
+        # parity spot check: the oracle on the first 512 txs
+        sys.path.insert(0, os.path.join(HERE, "oracle"))
+        import oracle as orc
+        orc.use_shani(True)
+        k = 512
+        sub = dict(tx_off=b["tx_off"][:k + 1].copy(), keys=b["keys"], key_off=b["key_off"],
+                   vals=b["vals"], val_off=b["val_off"])
+        _, eh_o, _ = orc.precommit_batch(1, nthreads=16, **sub)
+        parity = bool(np.array_equal(eh_o, eh[:k]))
+        # CPU baseline: the oracle over all txs on 16 host threads (1 warm-up, median of 3)
+        cpu = []
+        for r in range(4):
+            t0 = time.perf_counter()
+            orc.precommit_batch(1, nthreads=16, **b)
+            if r:
+                cpu.append(time.perf_counter() - t0)
+        t_cpu = float(np.median(cpu))
+        gib = n * vlen / 2 ** 30
+        t = res["pipelined"]
+        out = {"metric": "precommit hashing of a tx batch incl. pinned H2D and D2H of hVals + Eh",
+               "value": round(gib / t, 3), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 3),
+               "txs_per_s": round(ntx / t), "entries_per_s": round(n / t),
+               "one_chunk_ms": round(res["one_chunk"] * 1e3, 3),
+               "one_chunk_gibs": round(gib / res["one_chunk"], 3),
+               "h2d_only_ms": round(t_h2d * 1e3, 3),
+               "h2d_only_gbs": round(n * (vlen + 8) / t_h2d / 1e9, 2),
+               "frac_of_h2d_bound": round(t_h2d / t, 4),
+               "config": {"txs": ntx, "entries_per_tx": per, "value_len": vlen, "key_len": 8,
+                          "chunk_mib": a.chunk_mib},
+               "parity_first_512_txs": parity,
+               "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 16,
+                                "kind": "port",
+                                "sample": "oracle orc_precommit_batch over the same batch, 16 "
+                                          "threads, SHA-NI=%s, median of 3 = %.3f s"
+                                          % (orc.has_shani(), t_cpu)}}
 
     else:  # c2e2e
         n, vlen, klen = 1 << 20, 1024, 8

@@ -19,5 +19,7 @@ from . import txlayer
 from .txlayer import (TX_HEADER, tx_alh_batch, htree_build_many, verify_linear_proof_batch,
                       verify_dual_proof_v2_batch, VerifyDualProofV2, verify_dual_proof_batch,
                       txlog_validate)
+from . import commit
+from .commit import CommitPipe, EntrySpec
 
 __all__ = [n for n in dir() if not n.startswith("_")]

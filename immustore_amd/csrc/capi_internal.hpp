@@ -144,3 +144,72 @@ struct mh_ahtree {
     DevBuf dlog, in, roots, idx, out, ctr;
 };
 
+// ---------------------------------------------------------------- tx layer helpers
+// Sub-allocations of one device scratch buffer (256-byte aligned).
+struct Layout {
+    uint64_t total = 0;
+    uint64_t add(uint64_t bytes) {
+        const uint64_t o = total;
+        total = (total + bytes + 255) & ~255ull;
+        return o;
+    }
+};
+
+// ---------------------------------------------------------------- many trees
+// Level plan of a batch of htrees (htree.go:85-110 per tree): level 0 are the
+// leaves of all trees back to back, every further level appends the nodes of
+// the trees that still have more than one node.
+struct TreePlan {
+    std::vector<uint64_t> cur, prev, prevw;  // items, grouped by level
+    struct Level {
+        uint64_t base, nodes, item0, nitems;
+    };
+    std::vector<Level> levels;
+    std::vector<uint64_t> root_idx;  // per tree: node index of the root, ~0 = empty tree
+    uint64_t total_nodes = 0;
+
+    void build(uint64_t ntrees, const uint64_t *leaf_off) {
+        const uint64_t o0 = leaf_off[0];
+        root_idx.assign(ntrees, ~0ull);
+        struct Act {
+            uint64_t t, base, w;
+        };
+        std::vector<Act> act, nxt;
+        for (uint64_t t = 0; t < ntrees; t++) {
+            const uint64_t w = leaf_off[t + 1] - leaf_off[t];
+            if (w == 1) root_idx[t] = leaf_off[t] - o0;
+            if (w > 1) act.push_back({t, leaf_off[t] - o0, w});
+        }
+        uint64_t next = leaf_off[ntrees] - o0;
+        while (!act.empty()) {
+            Level L{next, 0, cur.size(), act.size()};
+            nxt.clear();
+            for (const Act &a : act) {
+                const uint64_t cw = (a.w + 1) / 2;
+                cur.push_back(next);
+                prev.push_back(a.base);
+                prevw.push_back(a.w);
+                if (cw == 1)
+                    root_idx[a.t] = next;
+                else
+                    nxt.push_back({a.t, next, cw});
+                next += cw;
+                L.nodes += cw;
+            }
+            levels.push_back(L);
+            act.swap(nxt);
+        }
+        total_nodes = next;
+    }
+};
+
+// bytes of pinned staging run_tree_plan_on needs for plan P over ntrees trees
+inline uint64_t plan_index_bytes(const TreePlan &P, uint64_t ntrees) {
+    return (3 * P.cur.size() + ntrees) * 8;
+}
+
+// Leaves + levels + roots of a planned batch (capi_tx.hip).
+int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,
+                  const uint8_t *d_digests, uint8_t *d_roots);
+int run_tree_plan_on(DevBuf &scratch, hipStream_t st, Timer *tm, const TreePlan &P, uint64_t ntrees,
+                     uint64_t nleaves, const uint8_t *d_digests, uint8_t *d_roots, uint8_t *pinned);

@@ -12,16 +12,6 @@
 
 namespace {
 
-// Sub-allocations of one device scratch buffer (256-byte aligned).
-struct Layout {
-    uint64_t total = 0;
-    uint64_t add(uint64_t bytes) {
-        const uint64_t o = total;
-        total = (total + bytes + 255) & ~255ull;
-        return o;
-    }
-};
-
 // Header preconditions shared by every entry point that hashes headers.
 int check_header(const mh_tx_header &h, uint64_t md_blob_len, bool have_blob) {
     if (h.version > 1) return MH_ERR_ILLEGAL_ARGUMENTS;
@@ -33,83 +23,6 @@ int check_header(const mh_tx_header &h, uint64_t md_blob_len, bool have_blob) {
     return MH_OK;
 }
 
-// ---------------------------------------------------------------- many trees
-// Level plan of a batch of htrees (htree.go:85-110 per tree): level 0 are the
-// leaves of all trees back to back, every further level appends the nodes of
-// the trees that still have more than one node.
-struct TreePlan {
-    std::vector<uint64_t> cur, prev, prevw;  // items, grouped by level
-    struct Level {
-        uint64_t base, nodes, item0, nitems;
-    };
-    std::vector<Level> levels;
-    std::vector<uint64_t> root_idx;  // per tree: node index of the root, ~0 = empty tree
-    uint64_t total_nodes = 0;
-
-    void build(uint64_t ntrees, const uint64_t *leaf_off) {
-        const uint64_t o0 = leaf_off[0];
-        root_idx.assign(ntrees, ~0ull);
-        struct Act {
-            uint64_t t, base, w;
-        };
-        std::vector<Act> act, nxt;
-        for (uint64_t t = 0; t < ntrees; t++) {
-            const uint64_t w = leaf_off[t + 1] - leaf_off[t];
-            if (w == 1) root_idx[t] = leaf_off[t] - o0;
-            if (w > 1) act.push_back({t, leaf_off[t] - o0, w});
-        }
-        uint64_t next = leaf_off[ntrees] - o0;
-        while (!act.empty()) {
-            Level L{next, 0, cur.size(), act.size()};
-            nxt.clear();
-            for (const Act &a : act) {
-                const uint64_t cw = (a.w + 1) / 2;
-                cur.push_back(next);
-                prev.push_back(a.base);
-                prevw.push_back(a.w);
-                if (cw == 1)
-                    root_idx[a.t] = next;
-                else
-                    nxt.push_back({a.t, next, cw});
-                next += cw;
-                L.nodes += cw;
-            }
-            levels.push_back(L);
-            act.swap(nxt);
-        }
-        total_nodes = next;
-    }
-};
-
-// Leaves + levels + roots of a planned batch on `st`.  d_digests: E x 32 on
-// the device; d_roots: ntrees x 32.  Uses the ctx's s_tree scratch.
-int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,
-                  const uint8_t *d_digests, uint8_t *d_roots) {
-    Layout L;
-    const uint64_t nitems = P.cur.size();
-    const uint64_t b_nodes = L.add(std::max<uint64_t>(P.total_nodes, 1) * 32);
-    const uint64_t b_cur = L.add(nitems * 8), b_prev = L.add(nitems * 8),
-                   b_prevw = L.add(nitems * 8), b_root = L.add(ntrees * 8);
-    MH_HIP(c->s_tree.ensure(L.total));
-    uint8_t *base = c->s_tree.as<uint8_t>();
-    uint8_t *nodes = base + b_nodes;
-    if (nitems) {
-        MH_HIP(hipMemcpyAsync(base + b_cur, P.cur.data(), nitems * 8, hipMemcpyHostToDevice, st));
-        MH_HIP(hipMemcpyAsync(base + b_prev, P.prev.data(), nitems * 8, hipMemcpyHostToDevice, st));
-        MH_HIP(hipMemcpyAsync(base + b_prevw, P.prevw.data(), nitems * 8, hipMemcpyHostToDevice,
-                              st));
-    }
-    MH_HIP(hipMemcpyAsync(base + b_root, P.root_idx.data(), ntrees * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(launch_leaf_for(st, c->tm(), nleaves, d_digests, nodes));  // htree.go:79-83
-    for (const auto &lv : P.levels)
-        MH_HIP(launch_seg_level(st, c->tm(), lv.nodes, lv.base, (uint32_t)lv.nitems,
-                                (const uint64_t *)(base + b_cur) + lv.item0,
-                                (const uint64_t *)(base + b_prev) + lv.item0,
-                                (const uint64_t *)(base + b_prevw) + lv.item0, nodes));
-    MH_HIP(launch_gather32(st, ntrees, nodes, (const uint64_t *)(base + b_root), d_roots));
-    return MH_OK;
-}
-
 uint64_t be_at(const uint8_t *p, int n) {
     uint64_t v = 0;
     for (int i = 0; i < n; i++) v = (v << 8) | p[i];
@@ -117,6 +30,57 @@ uint64_t be_at(const uint8_t *p, int n) {
 }
 
 }  // namespace
+
+// Leaves + levels + roots of a planned batch on `st`.  d_digests: E x 32 on
+// the device; d_roots: ntrees x 32.  run_tree_plan uses the ctx's s_tree
+// scratch, run_tree_plan_on the caller's.
+int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,
+                  const uint8_t *d_digests, uint8_t *d_roots) {
+    return run_tree_plan_on(c->s_tree, st, c->tm(), P, ntrees, nleaves, d_digests, d_roots, nullptr);
+}
+
+int run_tree_plan_on(DevBuf &scratch, hipStream_t st, Timer *tm, const TreePlan &P, uint64_t ntrees,
+                     uint64_t nleaves, const uint8_t *d_digests, uint8_t *d_roots, uint8_t *pinned) {
+    Layout L;
+    const uint64_t nitems = P.cur.size();
+    const uint64_t b_nodes = L.add(std::max<uint64_t>(P.total_nodes, 1) * 32);
+    const uint64_t b_cur = L.add(nitems * 8), b_prev = L.add(nitems * 8),
+                   b_prevw = L.add(nitems * 8), b_root = L.add(ntrees * 8);
+    MH_HIP(scratch.ensure(L.total));
+    uint8_t *base = scratch.as<uint8_t>();
+    uint8_t *nodes = base + b_nodes;
+    // index arrays: straight from the plan's vectors, or through `pinned`
+    // (plan_index_bytes(P, ntrees) bytes the caller keeps alive until `st`
+    // has passed this point) so the copies stay asynchronous
+    const uint64_t *src_cur = P.cur.data(), *src_prev = P.prev.data(),
+                   *src_prevw = P.prevw.data(), *src_root = P.root_idx.data();
+    if (pinned) {
+        uint64_t *q = reinterpret_cast<uint64_t *>(pinned);
+        memcpy(q, src_cur, nitems * 8);
+        memcpy(q + nitems, src_prev, nitems * 8);
+        memcpy(q + 2 * nitems, src_prevw, nitems * 8);
+        memcpy(q + 3 * nitems, src_root, ntrees * 8);
+        src_cur = q;
+        src_prev = q + nitems;
+        src_prevw = q + 2 * nitems;
+        src_root = q + 3 * nitems;
+    }
+    if (nitems) {
+        MH_HIP(hipMemcpyAsync(base + b_cur, src_cur, nitems * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_prev, src_prev, nitems * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_prevw, src_prevw, nitems * 8, hipMemcpyHostToDevice, st));
+    }
+    MH_HIP(hipMemcpyAsync(base + b_root, src_root, ntrees * 8, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_leaf_for(st, tm, nleaves, d_digests, nodes));  // htree.go:79-83
+    for (const auto &lv : P.levels)
+        MH_HIP(launch_seg_level(st, tm, lv.nodes, lv.base, (uint32_t)lv.nitems,
+                                (const uint64_t *)(base + b_cur) + lv.item0,
+                                (const uint64_t *)(base + b_prev) + lv.item0,
+                                (const uint64_t *)(base + b_prevw) + lv.item0, nodes));
+    MH_HIP(launch_gather32(st, ntrees, nodes, (const uint64_t *)(base + b_root), d_roots));
+    return MH_OK;
+}
+
 
 // ------------------------------------------------------------------ a7
 extern "C" int mh_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,

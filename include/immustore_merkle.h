@@ -380,6 +380,42 @@ int mh_txlog_validate(mh_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t ma
                       uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx, uint64_t *consumed,
                       mh_tx_header *hdrs, uint8_t *alh, int32_t *status);
 
+/* ------------------------------------------------------------ commit path */
+/* the hashing of ImmuStore.precommit / preCommitWith
+ * (immustore.go:1620-1632 and 2301-2313: hVal = SHA256(value), or
+ * EntrySpec.HashValue when IsValueTruncated, then Tx.BuildHashTree
+ * tx.go:332-355 -> header Eh) for a batch of transactions, plus the
+ * replicated-tx check `tx.header.Eh != hdr.Eh` (immustore.go:1649-1654).
+ * A pipe owns a copy stream, a compute stream and three slots of device /
+ * pinned buffers; a batch is cut into chunks of whole transactions
+ * (~chunk_bytes of keys + values each, 0 = 64 MiB) whose host->device copies
+ * run back to back under the hashing of the previous chunks.  Outputs in
+ * pinned memory receive the device->host copies directly.  Not synchronised:
+ * one pipe per goroutine. */
+typedef struct mh_commit_pipe mh_commit_pipe;
+int mh_commit_pipe_new(mh_ctx *ctx, uint64_t chunk_bytes, mh_commit_pipe **out);
+int mh_commit_pipe_free(mh_commit_pipe *p);
+/* Transaction t owns entries [tx_off[t], tx_off[t+1]) (tx_off: ntx + 1
+ * entries, ascending); entry e has key keys[key_off[e] .. key_off[e+1]), KV
+ * metadata (KVMetadata.Bytes(), kv_metadata.go:207-219) md[md_off[e] ..
+ * md_off[e+1]) and value vals[val_off[e] .. val_off[e+1]) -- offsets index
+ * the host arrays directly; md / md_off may both be NULL (no metadata).
+ * hval_override + use_override (both or neither) model IsValueTruncated.
+ * Outputs, host memory: hvals_out[e - tx_off[0]] (may be NULL), eh_out[t]
+ * (may be NULL) and status[t]: MH_OK; MH_ERR_MAX_WIDTH_EXCEEDED if the tx has
+ * more than max_width entries (htree.go:69-71; 0 = no limit);
+ * MH_ERR_METADATA_UNSUPPORTED for KV metadata under version 0 (tx.go:691-693);
+ * MH_ERR_ILLEGAL_ARGUMENTS if expect_eh (ntx x 32, may be NULL) differs from
+ * the built Eh ("entries hash (Eh) differs", immustore.go:1651).  eh_out is
+ * zeroed for the first two.  Pinned inputs (mh_host_alloc_pinned) make the
+ * copies asynchronous DMA; pageable inputs work at the runtime's staged rate. */
+int mh_precommit_batch(mh_commit_pipe *p, int version, uint64_t max_width, uint64_t ntx,
+                       const uint64_t *tx_off, const uint8_t *keys, const uint64_t *key_off,
+                       const uint8_t *md, const uint64_t *md_off, const uint8_t *vals,
+                       const uint64_t *val_off, const uint8_t *hval_override,
+                       const uint8_t *use_override, const uint8_t *expect_eh, uint8_t *hvals_out,
+                       uint8_t *eh_out, int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -398,6 +398,86 @@ int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32
     return OK;
 }
 
+/* ------------------------------------------------------- precommit batch */
+/* ImmuStore.precommit over many transactions (immustore.go:1620-1632, the
+ * Eh check of :1649-1654): orc_build_entries per tx, txs spread over
+ * nthreads threads (contiguous tx ranges). */
+typedef struct {
+    int version;
+    uint64_t max_width, t0, t1;
+    const uint64_t *tx_off;
+    const uint8_t *keys, *md, *vals, *ov, *use, *expect;
+    const uint64_t *key_off, *md_off, *val_off;
+    uint8_t *hvals, *eh;
+    int32_t *status;
+} pc_job;
+
+static void *pc_worker(void *arg) {
+    pc_job *j = (pc_job *)arg;
+    const uint64_t E0 = j->tx_off[0];
+    for (uint64_t t = j->t0; t < j->t1; t++) {
+        const uint64_t e0 = j->tx_off[t], n = j->tx_off[t + 1] - e0;
+        int st = OK;
+        uint8_t root[32];
+        if (j->max_width && n > j->max_width) {
+            st = ERR_MAX_WIDTH; /* htree.go:69-71 */
+        } else {
+            st = orc_build_entries(j->version, n, j->keys, j->key_off + e0, j->md,
+                                   j->md_off ? j->md_off + e0 : NULL, j->vals, j->val_off + e0,
+                                   j->ov ? j->ov + e0 * 32 : NULL, j->use ? j->use + e0 : NULL,
+                                   j->hvals ? j->hvals + (e0 - E0) * 32 : NULL, NULL, root);
+        }
+        if (st == OK && j->expect && memcmp(j->expect + t * 32, root, 32) != 0)
+            st = ERR_ILLEGAL_ARGS; /* "entries hash (Eh) differs" immustore.go:1651 */
+        if (j->eh) {
+            if (st == OK || st == ERR_ILLEGAL_ARGS)
+                memcpy(j->eh + t * 32, root, 32);
+            else
+                memset(j->eh + t * 32, 0, 32);
+        }
+        j->status[t] = st;
+    }
+    return NULL;
+}
+
+int orc_precommit_batch(int version, uint64_t max_width, uint64_t ntx, const uint64_t *tx_off,
+                        const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
+                        const uint64_t *md_off, const uint8_t *vals, const uint64_t *val_off,
+                        const uint8_t *hval_override, const uint8_t *use_override,
+                        const uint8_t *expect_eh, uint8_t *hvals_out, uint8_t *eh_out,
+                        int32_t *status, int nthreads) {
+    if (ntx == 0) return OK;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    if ((uint64_t)nthreads > ntx) nthreads = (int)ntx;
+    pc_job jobs[64];
+    pthread_t th[64];
+    /* split by entry count so threads get similar work */
+    const uint64_t E = tx_off[ntx] - tx_off[0];
+    uint64_t t = 0;
+    for (int k = 0; k < nthreads; k++) {
+        pc_job *j = &jobs[k];
+        j->version = version;
+        j->max_width = max_width;
+        j->tx_off = tx_off;
+        j->keys = keys; j->md = md; j->vals = vals;
+        j->ov = hval_override; j->use = use_override; j->expect = expect_eh;
+        j->key_off = key_off; j->md_off = md_off; j->val_off = val_off;
+        j->hvals = hvals_out; j->eh = eh_out; j->status = status;
+        j->t0 = t;
+        const uint64_t target = tx_off[0] + E * (uint64_t)(k + 1) / (uint64_t)nthreads;
+        while (t < ntx && (k == nthreads - 1 || tx_off[t + 1] <= target)) t++;
+        j->t1 = t;
+    }
+    if (nthreads == 1) {
+        pc_worker(&jobs[0]);
+    } else {
+        for (int k = 0; k < nthreads; k++) pthread_create(&th[k], NULL, pc_worker, &jobs[k]);
+        for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+    }
+    return OK;
+}
+
 /* ------------------------------------------------------------- tx header */
 int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmdlen,
                       uint32_t nentries, const uint8_t eh[32], uint64_t bltxid,

@@ -71,6 +71,16 @@ int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32
                             const uint8_t *vals, uint32_t val_len, uint8_t *hvals_out,
                             uint8_t *levels, uint8_t root[32], int nthreads);
 
+/* ImmuStore.precommit over ntx transactions (immustore.go:1620-1632, 2301-2313;
+ * Eh check :1649-1654): same contract as mh_precommit_batch
+ * (include/immustore_merkle.h); nthreads splits the txs. */
+int orc_precommit_batch(int version, uint64_t max_width, uint64_t ntx, const uint64_t *tx_off,
+                        const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
+                        const uint64_t *md_off, const uint8_t *vals, const uint64_t *val_off,
+                        const uint8_t *hval_override, const uint8_t *use_override,
+                        const uint8_t *expect_eh, uint8_t *hvals_out, uint8_t *eh_out,
+                        int32_t *status, int nthreads);
+
 /* TxHeader.innerHash / Alh: embedded/store/tx.go:249-319. */
 int orc_tx_inner_hash(uint64_t ts, int version, const uint8_t *txmd, size_t txmdlen,
                       uint32_t nentries, const uint8_t eh[32], uint64_t bltxid,

@@ -86,6 +86,9 @@ def lib():
         L.orc_txlog_validate.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
                                          u64p, u64p, u8p, C.POINTER(C.c_int32)]
         L.orc_sha256_use_shani.argtypes = [C.c_int]
+        L.orc_precommit_batch.argtypes = [C.c_int, C.c_uint64, C.c_uint64, u64p, u8p, u64p, u8p,
+                                          u64p, u8p, u64p, u8p, u8p, u8p, u8p, u8p,
+                                          C.POINTER(C.c_int32), C.c_int]
         _LIB = L
     return _LIB
 
@@ -180,6 +183,25 @@ def build_entries(version, keys, mds, vals, overrides=None):
     st = lib().orc_build_entries(version, n, _p(kb), _p(ko, u64p), _p(mb), _p(mo, u64p), _p(vb),
                                  _p(vo, u64p), _p(ov), _p(use), _p(hv), _p(lv), _p(root))
     return st, hv[:n], lv[:levels_len(n)], root.tobytes()
+
+
+def precommit_batch(version, tx_off, keys, key_off, vals, val_off, md=None, md_off=None,
+                    hval_override=None, use_override=None, expect_eh=None, max_width=0,
+                    nthreads=1):
+    """ImmuStore.precommit over many txs (immustore.go:1620-1632, :1649-1654), CSR
+    numpy inputs as for mh_precommit_batch -> (hvals [E,32], eh [ntx,32], status)."""
+    ntx = len(tx_off) - 1
+    ne = int(tx_off[-1] - tx_off[0]) if ntx > 0 else 0
+    hv = np.zeros((max(ne, 1), 32), np.uint8)
+    eh = np.zeros((max(ntx, 1), 32), np.uint8)
+    st = np.zeros(max(ntx, 1), np.int32)
+    tx_off = np.ascontiguousarray(tx_off, np.uint64)
+    lib().orc_precommit_batch(version, max_width, ntx, _p(tx_off, u64p), _p(keys),
+                              _p(key_off, u64p), _p(md), _p(md_off, u64p), _p(vals),
+                              _p(val_off, u64p), _p(hval_override), _p(use_override),
+                              _p(expect_eh), _p(hv), _p(eh),
+                              st.ctypes.data_as(C.POINTER(C.c_int32)), nthreads)
+    return hv[:ne], eh[:ntx], st[:ntx]
 
 
 def tx_inner_hash(ts, version, txmd, nentries, eh, bltxid, blroot):

@@ -1,0 +1,126 @@
+"""GPU parity of the commit path over many transactions (SURVEY.md 8(f) row 1,
+mh_precommit_batch): the Go stores' own Eh (tests/golden) and the oracle's
+orc_precommit_batch on seeded ragged batches, bit-exact hVals / Eh and the
+same per-tx statuses, through the two-stream chunked pipeline (small chunk
+sizes force many chunks through both slots)."""
+import numpy as np
+import pytest
+
+from commit_util import fixture_batch, random_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def m():
+    import torch  # noqa: F401
+    import immustore_amd as m
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return m
+
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("store", ["long_linear_proof", "v110_defaultdb", "v110_systemdb"])
+@pytest.mark.parametrize("trunc", [0, 3])
+@pytest.mark.parametrize("chunk", [0, 1])
+def test_precommit_fixture_stores(m, ctx, fixtures, store, trunc, chunk):
+    version, b, eh_ref = fixture_batch(fixtures[store], trunc)
+    p = m.CommitPipe(ctx, chunk_bytes=chunk)
+    try:
+        hv, eh, st = p.precommit_csr(version, **b)
+        assert (st == 0).all()
+        assert np.array_equal(eh, eh_ref)
+        _, _, st2 = p.precommit_csr(version, expect_eh=eh_ref, **b)
+        assert (st2 == 0).all()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("version", [0, 1])
+@pytest.mark.parametrize("chunk", [1 << 10, 1 << 16, 0])
+def test_precommit_random_vs_oracle(m, ctx, orc, version, chunk):
+    rng = np.random.default_rng(100 + version * 7 + chunk % 97)
+    b = random_batch(rng, 300, version=version, md_prob=0.2 if version else 0.0)
+    hv_o, eh_o, st_o = orc.precommit_batch(version, **b)
+    p = m.CommitPipe(ctx, chunk_bytes=chunk)
+    try:
+        hv, eh, st = p.precommit_csr(version, **b)
+        assert np.array_equal(st, st_o)
+        assert np.array_equal(eh, eh_o)
+        assert np.array_equal(hv, hv_o)
+        # the same pipe again (buffers reused), with an expected-Eh mismatch
+        bad = eh_o.copy()
+        bad[[3, 150], 0] ^= 0x80
+        _, eh2, st2 = p.precommit_csr(version, expect_eh=bad, **b)
+        assert sorted(np.nonzero(st2)[0].tolist()) == [3, 150] and (st2[[3, 150]] == 2).all()
+        assert np.array_equal(eh2, eh_o)
+    finally:
+        p.close()
+
+
+def test_precommit_statuses_vs_oracle(m, ctx, orc):
+    rng = np.random.default_rng(5)
+    b = random_batch(rng, 120, version=1, md_prob=0.3)
+    p = m.CommitPipe(ctx, chunk_bytes=1 << 12)
+    try:
+        for version, mw in ((1, 16), (0, 0), (0, 25)):
+            hv_o, eh_o, st_o = orc.precommit_batch(version, max_width=mw, **b)
+            hv, eh, st = p.precommit_csr(version, max_width=mw, **b)
+            assert np.array_equal(st, st_o), (version, mw)
+            assert np.array_equal(eh, eh_o), (version, mw)
+            ok = np.repeat(st_o == 0, np.diff(b["tx_off"].astype(np.int64)))
+            assert np.array_equal(hv[ok], hv_o[ok])
+    finally:
+        p.close()
+
+
+def test_precommit_entryspec_api(m, ctx, orc):
+    """The EntrySpec-list mirror; empty txs give SHA256(nil) (htree.go:73-77)."""
+    E = m.EntrySpec
+    txs = [[E(b"k1", b"v1"), E(b"k2", b"", md=b"\x00\x01"), E(b"k3", hash_value=b"\x11" * 32)],
+           [],
+           [E(b"key", b"x" * 5000)]]
+    p = m.CommitPipe(ctx)
+    try:
+        hvs, eh, st = p.precommit(1, txs)
+    finally:
+        p.close()
+    assert (st == 0).all()
+    import hashlib
+    assert eh[1].tobytes() == hashlib.sha256(b"").digest()
+    for t, es in enumerate(txs):
+        s, hv, _, root = orc.build_entries(1, [e.key for e in es], [e.md for e in es],
+                                           [e.value for e in es],
+                                           [e.hash_value for e in es])
+        assert s == 0 and root == eh[t].tobytes()
+        assert np.array_equal(hv, hvs[t])
+
+
+def test_precommit_large_batch_pinned(m, ctx, orc):
+    """~96 MiB of values in pinned host memory through 64 MiB chunks: both
+    slots busy, results identical to the oracle (4 host threads)."""
+    import torch
+    ntx, per, vlen = 3072, 32, 1024
+    n = ntx * per
+    vals = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()
+    vals.copy_(torch.randint(0, 256, (n * vlen,), dtype=torch.uint8,
+                             generator=torch.Generator().manual_seed(9)))
+    keys = np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8).copy()
+    b = dict(tx_off=np.arange(0, n + 1, per, dtype=np.uint64), keys=keys,
+             key_off=np.arange(0, 8 * n + 1, 8, dtype=np.uint64), vals=vals.numpy(),
+             val_off=np.arange(0, vlen * n + 1, vlen, dtype=np.uint64))
+    hv_o, eh_o, st_o = orc.precommit_batch(1, nthreads=4, **b)
+    p = m.CommitPipe(ctx)
+    try:
+        hv, eh, st = p.precommit_csr(1, **b)
+    finally:
+        p.close()
+    assert (st == 0).all() and (st_o == 0).all()
+    assert np.array_equal(eh, eh_o) and np.array_equal(hv, hv_o)

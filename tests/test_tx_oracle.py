@@ -182,3 +182,55 @@ def test_dual_proof_v1_fixture_cases(orc, fixtures):
             if recs[c["tgt"] - 1]["bl_tx_id"] > 0:
                 assert not orc.verify_dual_proof(*dual_v1_args(c, recs, blob, alhs, "tbl"))
     assert n_lap > 10
+
+
+# ---------------------------------------------------------- precommit (8(f) row 1)
+@pytest.mark.parametrize("store", ["long_linear_proof", "v110_defaultdb", "v110_systemdb"])
+@pytest.mark.parametrize("trunc", [0, 3])
+def test_precommit_batch_fixture_stores(orc, fixtures, store, trunc):
+    """Every stored Eh from the Go stores' own entries (values or, for every
+    third entry, the stored hVal as a truncated value), 1 and 4 threads."""
+    from commit_util import fixture_batch
+    version, b, eh_ref = fixture_batch(fixtures[store], trunc)
+    for th in (1, 4):
+        hv, eh, st = orc.precommit_batch(version, nthreads=th, **b)
+        assert (st == 0).all()
+        assert np.array_equal(eh, eh_ref)
+        _, eh2, st2 = orc.precommit_batch(version, expect_eh=eh_ref, **b)
+        assert (st2 == 0).all()
+
+
+def test_precommit_batch_statuses(orc):
+    from commit_util import random_batch
+    rng = np.random.default_rng(11)
+    b = random_batch(rng, 50, version=1)
+    hv, eh, st = orc.precommit_batch(1, **b)
+    assert (st == 0).all()
+    # per-tx restatement: orc.build_entries over each tx's entries
+    to = b["tx_off"]
+    for t in range(50):
+        e0, e1 = int(to[t]), int(to[t + 1])
+        ks = [b["keys"][int(b["key_off"][e]):int(b["key_off"][e + 1])].tobytes() for e in range(e0, e1)]
+        vs = [b["vals"][int(b["val_off"][e]):int(b["val_off"][e + 1])].tobytes() for e in range(e0, e1)]
+        mds = [b["md"][int(b["md_off"][e]):int(b["md_off"][e + 1])].tobytes() if "md" in b else b""
+               for e in range(e0, e1)]
+        ovs = None
+        if "use_override" in b:
+            ovs = [b["hval_override"][e].tobytes() if b["use_override"][e] else None
+                   for e in range(e0, e1)]
+        s1, hv1, _, root = orc.build_entries(1, ks, mds, vs, ovs)
+        assert s1 == 0 and root == eh[t].tobytes()
+        assert np.array_equal(hv1, hv[e0:e1])
+    # expected-Eh mismatch -> ErrIllegalArguments, max width, v0 + metadata
+    bad = eh.copy()
+    bad[7, 3] ^= 1
+    _, eh2, st2 = orc.precommit_batch(1, expect_eh=bad, **b)
+    assert list(np.nonzero(st2)[0]) == [7] and st2[7] == 2 and np.array_equal(eh2, eh)
+    widths = np.diff(to.astype(np.int64))
+    _, eh3, st3 = orc.precommit_batch(1, max_width=20, **b)
+    assert ((st3 == 1) == (widths > 20)).all()
+    assert not eh3[widths > 20].any()
+    _, eh4, st4 = orc.precommit_batch(0, **b)
+    has_md = np.array([int(b["md_off"][int(to[t + 1])] - b["md_off"][int(to[t])]) > 0
+                       for t in range(50)])
+    assert ((st4 == 6) == has_md).all()
