@@ -205,6 +205,9 @@ SIGNATURES = {
     "mh_ahtree_dlog": (i32, [vp, u64, u64, u8p]),
     "mh_ahtree_dlog_device": (i32, [vp, C.POINTER(vp)]),
     "mh_dev_ahtree_append_batch": (i32, [vp, u8p, u64, u8p, u64, u32, u8p]),
+    "mh_ahtree_append_batch_logs": (i32, [vp, u8p, u64, u32, u64, u8p, u8p, u8p]),
+    "mh_dev_ahtree_append_batch_logs": (i32, [vp, u8p, u64, u8p, u64, u32, u64, u8p, u8p, u8p]),
+    "mh_dev_ahtree_log_records": (i32, [vp, u8p, u64, u32, u64, u8p, u8p]),
     "mh_ahtree_nodes_upto": (u64, [u64]),
     "mh_htree_inclusion_proof_batch": (i32, [vp, u64, vp, u8p, u32, vp, vp]),
     "mh_dev_htree_inclusion_proof_batch": (i32, [vp, u8p, u64, u64, vp, u8p, u32, vp, vp]),

@@ -31,22 +31,77 @@ __device__ __forceinline__ uint64_t dev_nodes_until(uint64_t n) {
     return until_from_s(n, popsum_below(n));
 }
 
-// phase 1: d_0 = leaf of payload (plen == 32: one block, the store's Alh)
+// phase 1: d_0 = leaf of payload (plen == 32: one block, the store's Alh),
+// plus, when asked, the appendable records of the same appends (SURVEY.md
+// 8(f) row 4): pLog BE32 len || payload (ahtree.go:266-282) and cLog
+// BE64 poff || BE32 len (ahtree.go:341-351), written while the payload is in
+// registers.  dlog == nullptr writes only the records.  For 32-byte payloads
+// the workgroup stages its 256 records in LDS and stores them as contiguous
+// dwords (36-byte / 12-byte records would otherwise be strided per lane).
 __global__ __launch_bounds__(256) void k_aht_leaves(uint8_t *__restrict__ dlog, uint64_t n0,
                                                     const uint8_t *__restrict__ payloads,
-                                                    uint64_t m, uint32_t plen) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
+                                                    uint64_t m, uint32_t plen, AhtLogs lg) {
+    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t i = base + threadIdx.x;
+    const bool live = i < m;
+    const bool logs = lg.plog || lg.clog;
+    const bool staged = logs && plen == 32 && !((uintptr_t)lg.plog & 3) && !((uintptr_t)lg.clog & 3);
+    if (!live && !staged) return;
     const uint64_t n = n0 + 1 + i;
-    uint32_t h[8];
-    if (plen == 32) {
-        uint32_t d[8];
-        load_digest(payloads + i * 32, d);
-        leaf_hash(d, h);
-    } else {
+    uint32_t raw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (live && plen == 32) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(payloads + i * 32);
+        const uint4 b = *reinterpret_cast<const uint4 *>(payloads + i * 32 + 16);
+        raw[0] = a.x; raw[1] = a.y; raw[2] = a.z; raw[3] = a.w;
+        raw[4] = b.x; raw[5] = b.y; raw[6] = b.z; raw[7] = b.w;
+        if (dlog) {
+            uint32_t d[8], h[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) d[j] = bswap(raw[j]);
+            leaf_hash(d, h);
+            store_digest(dlog + dev_nodes_until(n) * 32, h);
+        }
+    } else if (live && dlog) {
+        uint32_t h[8];
         sha256_bytes(payloads + i * (uint64_t)plen, plen, 0x00, h);
+        store_digest(dlog + dev_nodes_until(n) * 32, h);
     }
-    store_digest(dlog + dev_nodes_until(n) * 32, h);
+    if (!logs) return;
+    const uint64_t rec = 4 + (uint64_t)plen;
+    const uint64_t poff = lg.p_off0 + i * rec;
+    if (staged) {
+        __shared__ uint32_t sp[256 * 9];
+        __shared__ uint32_t sc[256 * 3];
+        const int t = threadIdx.x;
+        sp[t * 9] = bswap(32u);
+#pragma unroll
+        for (int j = 0; j < 8; j++) sp[t * 9 + 1 + j] = raw[j];
+        sc[t * 3 + 0] = bswap((uint32_t)(poff >> 32));
+        sc[t * 3 + 1] = bswap((uint32_t)poff);
+        sc[t * 3 + 2] = bswap(32u);
+        __syncthreads();
+        const uint64_t cnt = m - base < 256 ? m - base : 256;
+        if (lg.plog) {
+            uint32_t *dp = reinterpret_cast<uint32_t *>(lg.plog) + base * 9;
+            for (uint32_t k = t; k < cnt * 9; k += 256) dp[k] = sp[k];
+        }
+        if (lg.clog) {
+            uint32_t *dc = reinterpret_cast<uint32_t *>(lg.clog) + base * 3;
+            for (uint32_t k = t; k < cnt * 3; k += 256) dc[k] = sc[k];
+        }
+        return;
+    }
+    if (lg.plog) {
+        uint8_t *r = lg.plog + i * rec;
+        for (int k = 0; k < 4; k++) r[k] = (uint8_t)(plen >> (24 - 8 * k));
+        const uint8_t *src = payloads + i * (uint64_t)plen;
+        for (uint32_t k = 0; k < plen; k++) r[4 + k] = src[k];
+    }
+    if (lg.clog) {
+        uint8_t *c = lg.clog + i * 12;
+        for (int k = 0; k < 8; k++) c[k] = (uint8_t)(poff >> (56 - 8 * k));
+        for (int k = 0; k < 4; k++) c[8 + k] = (uint8_t)(plen >> (24 - 8 * k));
+    }
 }
 
 // phase 2: perfect nodes of level l ending at e = (j+1)*2^l, j in [j0, j0+cnt)
@@ -253,11 +308,12 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) {
 
 // Phase 1: leaves of (n0, n0 + m].
 hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
-                                const uint8_t *payloads, uint64_t m, uint32_t plen) {
+                                const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                const AhtLogs &lg) {
     if (!m) return hipSuccess;
-    TimerScope ts(tm, "aht_leaves", st);
+    TimerScope ts(tm, dlog ? "aht_leaves" : "aht_records", st);
     hipLaunchKernelGGL(k_aht_leaves, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, payloads,
-                       m, plen);
+                       m, plen, lg);
     return hipGetLastError();
 }
 
@@ -306,9 +362,9 @@ hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_
 
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out, uint32_t *work_ctr) {
+                                uint8_t *roots_out, uint32_t *work_ctr, const AhtLogs &lg) {
     if (!m) return hipSuccess;
-    if (hipError_t e = launch_ahtree_leaves(st, tm, dlog, n0, payloads, m, plen)) return e;
+    if (hipError_t e = launch_ahtree_leaves(st, tm, dlog, n0, payloads, m, plen, lg)) return e;
     if (hipError_t e = launch_ahtree_perfect(st, tm, dlog, n0, n0 + m, 1, 63)) return e;
     return launch_ahtree_spine(st, tm, dlog, n0, m, roots_out, work_ctr);
 }

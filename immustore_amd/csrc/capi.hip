@@ -750,6 +750,47 @@ extern "C" int mh_dev_ahtree_append_batch(mh_ctx *c, uint8_t *dlog, uint64_t n0,
     return MH_OK;
 }
 
+// the pLog / cLog records of a batch (ahtree.go:266-282,
+// 341-351), alone or fused into the append's leaf phase.
+static bool logs_ok(const uint8_t *payloads, uint64_t m, uint32_t plen, uint64_t p_off0) {
+    if (m && !payloads && plen) return false;
+    const uint64_t rec = 4 + (uint64_t)plen;
+    return !m || (m <= (~0ull - p_off0) / rec);  // offsets stay in uint64
+}
+
+extern "C" int mh_dev_ahtree_log_records(mh_ctx *c, const uint8_t *payloads, uint64_t m,
+                                         uint32_t plen, uint64_t p_off0, uint8_t *plog,
+                                         uint8_t *clog) {
+    if (!c || !logs_ok(payloads, m, plen, p_off0)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m || (!plog && !clog)) return MH_OK;
+    hipSetDevice(c->device);
+    AhtLogs lg;
+    lg.plog = plog;
+    lg.clog = clog;
+    lg.p_off0 = p_off0;
+    MH_HIP(launch_ahtree_leaves(c->stream, c->tm(), nullptr, 0, payloads, m, plen, lg));
+    return MH_OK;
+}
+
+extern "C" int mh_dev_ahtree_append_batch_logs(mh_ctx *c, uint8_t *dlog, uint64_t n0,
+                                               const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                               uint64_t p_off0, uint8_t *plog, uint8_t *clog,
+                                               uint8_t *roots_out) {
+    if (!c || (m && !dlog) || !logs_ok(payloads, m, plen, p_off0)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (!m) return MH_OK;
+    hipSetDevice(c->device);
+    AhtLogs lg;
+    lg.plog = plog;
+    lg.clog = clog;
+    lg.p_off0 = p_off0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    MH_HIP(c->s_ctr.ensure(256));
+    MH_HIP(launch_ahtree_append(c->stream, c->tm(), dlog, n0, payloads, m, plen, roots_out,
+                                c->s_ctr.as<uint32_t>(), lg));
+    return MH_OK;
+}
+
 extern "C" uint64_t mh_ahtree_node_index(uint64_t n, int level) {
     return ahtree_nodes_until(n) + (uint64_t)level;
 }
@@ -835,27 +876,54 @@ static int aht_reserve(mh_ahtree *t, uint64_t new_size) {
     return MH_OK;
 }
 
-extern "C" int mh_ahtree_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m,
-                                      uint32_t plen, uint8_t *roots_out) {
-    if (!t || (m && !payloads && plen)) return MH_ERR_ILLEGAL_ARGUMENTS;
+static int aht_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m, uint32_t plen,
+                            uint64_t p_off0, uint8_t *plog_out, uint8_t *clog_out,
+                            uint8_t *roots_out) {
+    if (!t || !logs_ok(payloads, m, plen, p_off0)) return MH_ERR_ILLEGAL_ARGUMENTS;
     if (!m) return MH_OK;
     hipSetDevice(t->ctx->device);
     int st = aht_reserve(t, t->size + m);
     if (st) return st;
-    MH_HIP(t->in.ensure((uint64_t)m * plen));
-    if (plen) MH_HIP(hipMemcpyAsync(t->in.p, payloads, (uint64_t)m * plen, hipMemcpyHostToDevice, t->stream));
+    const uint64_t rec = 4 + (uint64_t)plen;
+    // one device buffer: payloads | pLog records | cLog entries | roots
+    const uint64_t b_pay = 0, b_plog = (m * plen + 15) & ~15ull;
+    const uint64_t b_clog = b_plog + (plog_out ? (m * rec + 15) & ~15ull : 0);
+    const uint64_t b_end = b_clog + (clog_out ? (m * 12 + 15) & ~15ull : 0);
+    MH_HIP(t->in.ensure(b_end ? b_end : 16));
+    uint8_t *base = t->in.as<uint8_t>();
+    if (plen)
+        MH_HIP(hipMemcpyAsync(base + b_pay, payloads, m * plen, hipMemcpyHostToDevice, t->stream));
     uint8_t *rd = nullptr;
     if (roots_out) {
         MH_HIP(t->roots.ensure(m * 32));
         rd = t->roots.as<uint8_t>();
     }
+    AhtLogs lg;
+    lg.plog = plog_out ? base + b_plog : nullptr;
+    lg.clog = clog_out ? base + b_clog : nullptr;
+    lg.p_off0 = p_off0;
     MH_HIP(t->ctr.ensure(256));
     MH_HIP(launch_ahtree_append(t->stream, t->ctx->tm(), t->dlog.as<uint8_t>(), t->size,
-                                t->in.as<uint8_t>(), m, plen, rd, t->ctr.as<uint32_t>()));
+                                base + b_pay, m, plen, rd, t->ctr.as<uint32_t>(), lg));
     if (roots_out) MH_HIP(hipMemcpyAsync(roots_out, rd, m * 32, hipMemcpyDeviceToHost, t->stream));
+    if (plog_out)
+        MH_HIP(hipMemcpyAsync(plog_out, lg.plog, m * rec, hipMemcpyDeviceToHost, t->stream));
+    if (clog_out)
+        MH_HIP(hipMemcpyAsync(clog_out, lg.clog, m * 12, hipMemcpyDeviceToHost, t->stream));
     MH_HIP(hipStreamSynchronize(t->stream));
     t->size += m;
     return MH_OK;
+}
+
+extern "C" int mh_ahtree_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m,
+                                      uint32_t plen, uint8_t *roots_out) {
+    return aht_append_batch(t, payloads, m, plen, 0, nullptr, nullptr, roots_out);
+}
+
+extern "C" int mh_ahtree_append_batch_logs(mh_ahtree *t, const uint8_t *payloads, uint64_t m,
+                                           uint32_t plen, uint64_t p_off0, uint8_t *plog_out,
+                                           uint8_t *clog_out, uint8_t *roots_out) {
+    return aht_append_batch(t, payloads, m, plen, p_off0, plog_out, clog_out, roots_out);
 }
 
 extern "C" int mh_ahtree_append(mh_ahtree *t, const uint8_t *payload, uint64_t plen, uint64_t *n,

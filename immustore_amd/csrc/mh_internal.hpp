@@ -129,12 +129,23 @@ hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np
 // ---- ahtree batch append (embedded/ahtree/ahtree.go:246-373)
 // work_ctr: 4 bytes of device memory private to this launch's stream order
 // (the spine kernel's work queue; reset on `st` before the launch).
+// Optional appendable record streams of the appended payloads (SURVEY.md
+// 8(f) row 4): pLog records BE32 len || payload at plog + i*(4+plen), cLog
+// entries BE64 (p_off0 + i*(4+plen)) || BE32 len at clog + i*12.
+struct AhtLogs {
+    uint8_t *plog = nullptr;
+    uint8_t *clog = nullptr;
+    uint64_t p_off0 = 0;
+};
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out, uint32_t *work_ctr);
+                                uint8_t *roots_out, uint32_t *work_ctr,
+                                const AhtLogs &lg = AhtLogs());
 // The three phases of launch_ahtree_append, for sharded appends.
+// dlog == nullptr: records only.
 hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
-                                const uint8_t *payloads, uint64_t m, uint32_t plen);
+                                const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                const AhtLogs &lg = AhtLogs());
 hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                  uint64_t n_end, int lmin, int lmax);
 hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0, uint64_t m,

@@ -303,6 +303,20 @@ class AHtree:
         N.check(self._lib.mh_ahtree_append_batch(self.handle, _addr(p), m, plen, _addr(roots)))
         return roots[:m] if with_roots else None
 
+    def append_batch_logs(self, payloads, p_off0: int = 0):
+        """append_batch + the batch's pLog / cLog record streams (what
+        (*AHtree).Append hands to t.pLog.Append / the cLog buffer,
+        ahtree.go:266-282, 341-351) -> (plog bytes, clog bytes)."""
+        p = np.ascontiguousarray(payloads, np.uint8)
+        if p.ndim == 1:
+            p = p.reshape(1, -1)
+        m, plen = p.shape
+        plog = np.zeros(max(1, m * (4 + plen)), np.uint8)
+        clog = np.zeros(max(1, m * 12), np.uint8)
+        N.check(self._lib.mh_ahtree_append_batch_logs(self.handle, _addr(p), m, plen, p_off0,
+                                                      _addr(plog), _addr(clog), None))
+        return plog[:m * (4 + plen)].tobytes(), clog[:m * 12].tobytes()
+
     def size(self) -> int:
         s = C.c_uint64(0)
         N.check(self._lib.mh_ahtree_size(self.handle, C.byref(s)))

@@ -198,7 +198,8 @@ int mh_dev_htree_verify_inclusion_batch(mh_ctx *ctx, uint64_t nproofs, const uin
 
 /* ----------------------------------------------------------------- ahtree */
 /* In-memory append-only tree whose dLog (ahtree.go:60-84, tree/NNNNNNNN.sha) lives
- * in HBM.  No pLog/cLog files: persistence stays with the Go appendables. */
+ * in HBM.  No pLog/cLog files: persistence stays with the Go appendables, which
+ * mh_ahtree_append_batch_logs feeds with ready-made record streams. */
 int mh_ahtree_new(mh_ctx *ctx, mh_ahtree **out);
 int mh_ahtree_free(mh_ahtree *t);
 /* (*AHtree).Append(d)                                   ahtree.go:246-373 */
@@ -208,6 +209,17 @@ int mh_ahtree_append(mh_ahtree *t, const uint8_t *payload, uint64_t plen, uint64
  * immustore.go:1198-1232). roots_out (m*32, RootAt(n0+1..n0+m)) may be NULL. */
 int mh_ahtree_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m, uint32_t plen,
                            uint8_t *roots_out);
+/* mh_ahtree_append_batch that also returns the batch's appendable records
+ * (SURVEY.md 8(f) row 4), ready for the Go appendables' Append calls of
+ * (*AHtree).Append: plog_out (m*(4+plen) bytes, the data/NNNNNNNN.dat
+ * stream: BE32 plen || payload per append, ahtree.go:266-282) and clog_out
+ * (m*12 bytes, the commit/NNNNNNNN.di stream: BE64 pLog offset || BE32 plen,
+ * ahtree.go:341-351); p_off0 = the pLog size before the batch (t.pLogSize).
+ * The dLog bytes of the batch are mh_ahtree_dlog(nodes_upto(n0),
+ * nodes_upto(n0+m) - nodes_upto(n0)).  Either output may be NULL. */
+int mh_ahtree_append_batch_logs(mh_ahtree *t, const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                uint64_t p_off0, uint8_t *plog_out, uint8_t *clog_out,
+                                uint8_t *roots_out);
 int mh_ahtree_size(mh_ahtree *t, uint64_t *size);
 /* (*AHtree).Root / RootAt                                ahtree.go:727-771 */
 int mh_ahtree_root(mh_ahtree *t, uint64_t *n, uint8_t root[32]);
@@ -235,6 +247,16 @@ int mh_ahtree_dlog_device(mh_ahtree *t, const uint8_t **dptr);
  * room for nodesUpto(n0+m); payloads m*plen bytes. */
 int mh_dev_ahtree_append_batch(mh_ctx *ctx, uint8_t *dlog, uint64_t n0, const uint8_t *payloads,
                                uint64_t m, uint32_t plen, uint8_t *roots_out);
+/* Device variants of the appendable records: fused into the append's leaf
+ * phase (the payload is read once), or alone (e.g. per rank of a sharded
+ * append: rank r passes p_off0 + r*S*(4+plen)).  plog / clog: device memory
+ * of m*(4+plen) / m*12 bytes, either may be NULL. */
+int mh_dev_ahtree_append_batch_logs(mh_ctx *ctx, uint8_t *dlog, uint64_t n0,
+                                    const uint8_t *payloads, uint64_t m, uint32_t plen,
+                                    uint64_t p_off0, uint8_t *plog, uint8_t *clog,
+                                    uint8_t *roots_out);
+int mh_dev_ahtree_log_records(mh_ctx *ctx, const uint8_t *payloads, uint64_t m, uint32_t plen,
+                              uint64_t p_off0, uint8_t *plog, uint8_t *clog);
 uint64_t mh_ahtree_nodes_upto(uint64_t n); /* ahtree.go:492-511 */
 /* dLog index of node(n, level) = nodesUntil(n) + level (ahtree.go:460-462). */
 uint64_t mh_ahtree_node_index(uint64_t n, int level);

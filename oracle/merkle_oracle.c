@@ -534,6 +534,13 @@ uint64_t orc_ahtree_nodes_upto(uint64_t n) {
 
 uint64_t orc_ahtree_nodes_until(uint64_t n) { return n == 1 ? 0 : orc_ahtree_nodes_upto(n - 1); }
 
+static void put_be32(uint8_t *b, uint32_t v) {
+    for (int k = 0; k < 4; k++) b[k] = (uint8_t)(v >> (24 - 8 * k));
+}
+static void put_be64(uint8_t *b, uint64_t v) {
+    for (int k = 0; k < 8; k++) b[k] = (uint8_t)(v >> (56 - 8 * k));
+}
+
 static const uint8_t *aht_node(const uint8_t *dlog, uint64_t k, int l) {
     /* ahtree.go:460-462 node(n,l) = dLog[nodesUntil(n)+l] */
     return dlog + (orc_ahtree_nodes_until(k) + (uint64_t)l) * 32;
@@ -569,6 +576,27 @@ int orc_ahtree_append_batch(uint8_t *dlog, uint64_t n_before, const uint8_t *pay
                             uint64_t m, size_t plen) {
     for (uint64_t i = 0; i < m; i++) orc_ahtree_append(dlog, n_before + i, payloads + i * plen, plen, NULL);
     return OK;
+}
+
+/* The appendable record streams of m appends of plen-byte payloads
+ * (ahtree.go:266-282: pLog gets BE32 len(d) then d; :341-351: cLog gets
+ * BE64 poff || BE32 len(d), poff = pLog offset of the length prefix).
+ * p_off0 = pLog size before the batch (t.pLogSize).  plog / clog may be NULL. */
+void orc_ahtree_log_records(const uint8_t *payloads, uint64_t m, size_t plen, uint64_t p_off0,
+                            uint8_t *plog, uint8_t *clog) {
+    for (uint64_t i = 0; i < m; i++) {
+        const uint64_t poff = p_off0 + i * (4 + (uint64_t)plen);
+        if (plog) {
+            uint8_t *r = plog + i * (4 + (uint64_t)plen);
+            put_be32(r, (uint32_t)plen);
+            if (plen) memcpy(r + 4, payloads + i * plen, plen);
+        }
+        if (clog) {
+            uint8_t *c = clog + i * 12;
+            put_be64(c, poff);
+            put_be32(c + 8, (uint32_t)plen);
+        }
+    }
 }
 
 int orc_ahtree_root_at(const uint8_t *dlog, uint64_t size, uint64_t n, uint8_t out[32]) {

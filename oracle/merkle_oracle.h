@@ -153,6 +153,11 @@ int orc_ahtree_append(uint8_t *dlog, uint64_t n_before, const uint8_t *payload, 
 /* Fixed-size payload batch (syncBinaryLinking analog, immustore.go:1198-1232). */
 int orc_ahtree_append_batch(uint8_t *dlog, uint64_t n_before, const uint8_t *payloads,
                             uint64_t m, size_t plen);
+/* pLog records (BE32 len || payload, ahtree.go:266-282) and cLog entries
+ * (BE64 poff || BE32 len, ahtree.go:341-351) of m appends; p_off0 = pLog size
+ * before the batch.  plog / clog may be NULL. */
+void orc_ahtree_log_records(const uint8_t *payloads, uint64_t m, size_t plen, uint64_t p_off0,
+                            uint8_t *plog, uint8_t *clog);
 int orc_ahtree_root_at(const uint8_t *dlog, uint64_t size, uint64_t n, uint8_t out[32]);
 int orc_ahtree_inclusion_proof(const uint8_t *dlog, uint64_t size, uint64_t i, uint64_t j,
                                uint8_t *terms, uint32_t *nterms);

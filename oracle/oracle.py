@@ -58,6 +58,8 @@ def lib():
         L.orc_ahtree_nodes_until.argtypes = [C.c_uint64]
         L.orc_ahtree_append.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t, u8p]
         L.orc_ahtree_append_batch.argtypes = [u8p, C.c_uint64, u8p, C.c_uint64, C.c_size_t]
+        L.orc_ahtree_log_records.argtypes = [u8p, C.c_uint64, C.c_size_t, C.c_uint64, u8p, u8p]
+        L.orc_ahtree_log_records.restype = None
         L.orc_ahtree_root_at.argtypes = [u8p, C.c_uint64, C.c_uint64, u8p]
         L.orc_ahtree_inclusion_proof.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]
         L.orc_ahtree_consistency_proof.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, u8p, u32p]
@@ -254,6 +256,17 @@ class AHtree:
         self._grow(self.size + m)
         lib().orc_ahtree_append_batch(_p(self.dlog), self.size, _p(p), m, plen)
         self.size += m
+
+    def append_batch_logs(self, payloads, p_off0):
+        """append_batch plus the pLog / cLog record streams of the batch
+        (ahtree.go:266-282, 341-351) -> (plog bytes, clog bytes)."""
+        p = np.ascontiguousarray(payloads, np.uint8)
+        m, plen = p.shape
+        plog = np.zeros(max(1, m * (4 + plen)), np.uint8)
+        clog = np.zeros(max(1, m * 12), np.uint8)
+        lib().orc_ahtree_log_records(_p(p), m, plen, p_off0, _p(plog), _p(clog))
+        self.append_batch(p)
+        return plog[:m * (4 + plen)].tobytes(), clog[:m * 12].tobytes()
 
     def dlog_bytes(self):
         return self.dlog[:nodes_upto(self.size)].tobytes()

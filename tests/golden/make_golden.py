@@ -26,6 +26,7 @@ File formats followed (reference, read as text):
 - tx record: embedded/store/immustore.go:1812-1924 and tx.go:437-603
 - ahtree pLog record: BE32 len + payload (embedded/ahtree/ahtree.go:266-279)
 - ahtree dLog: 32-byte digests (ahtree.go:324-333)
+- ahtree cLog entry: BE64 pLog offset + BE32 payload len (ahtree.go:341-345)
 """
 import hashlib
 import json
@@ -338,6 +339,14 @@ def fixture_store(root):
     ours = b"".join(aht.dlog)
     assert ours[:len(dlog)] == dlog, "dLog mismatch"
     assert n_aht == nodes_upto(len(payloads))
+    # the cLog: one 12-byte entry per append pointing at its pLog record
+    clog = read_appendable(os.path.join(root, "aht/commit/00000000.di"))
+    assert len(clog) == 12 * len(payloads), "cLog size"
+    q = 0
+    for k, pay in enumerate(payloads):
+        poff, ln = struct.unpack(">QI", clog[12 * k:12 * k + 12])
+        assert poff == q and ln == len(pay) // 2, "cLog entry %d" % k
+        q += 4 + ln
     # raw tx-log records (data file of the reference's test store) for the
     # read-path validation tests, and dual / linear proofs built the way
     # ImmuStore.DualProofV2 / LinearProof build them (immustore.go:2356-2387,
@@ -392,7 +401,8 @@ def fixture_store(root):
                        for k in range(a0 + 1, a1)]
                 c["lap"] = {"terms": lt, "incl": ips}
             dual1.append(c)
-    return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(), "n_values": sum(
+    return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(),
+        "aht_plog": pl.hex(), "aht_clog": clog.hex(), "n_values": sum(
         1 for t in txs for e in t["entries"] if "value" in e), "txlog": raw.hex(),
         "dual_v2": dual, "linear": linear, "dual_v1": dual1}
 

@@ -7,6 +7,8 @@ tests/golden/make_golden.py from /root/reference/test/...):
   stored after each tx (a2-a4, a7; tx.go:249-355, htree.go:68-113)
 - appending the stored Alh stream to an ahtree reproduces Go's dLog byte for
   byte (a8-a9, ahtree.go:246-373) and BlRoot (ahtree.go:749-771)
+- the pLog / cLog record streams of those appends equal Go's aht/data and
+  aht/commit files (8(f) row 4, ahtree.go:266-282, 341-351)
 Reference known-answer tables: nodesUpto(1..16) (ahtree_test.go:36-64), empty
 root SHA256(nil) (htree_test.go:36-38).
 """
@@ -72,6 +74,22 @@ def test_fixture_alh_chain(orc, fixtures, store):
     b = orc.AHtree()
     b.append_batch(np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]]))
     assert b.dlog_bytes() == dlog
+
+
+@pytest.mark.parametrize("store", ["long_linear_proof", "v110_defaultdb", "v110_systemdb"])
+@pytest.mark.parametrize("split", [0, 1, 7])
+def test_fixture_appendable_streams(orc, fixtures, store, split):
+    """pLog / cLog / dLog byte streams of the Go-written aht/{data,commit,tree}
+    files, rebuilt by appending the stored payloads in two batches."""
+    fx = fixtures[store]
+    pays = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
+    split = min(split, len(pays))
+    t = orc.AHtree()
+    p1, c1 = t.append_batch_logs(pays[:split], 0)
+    p2, c2 = t.append_batch_logs(pays[split:], len(p1))
+    assert p1 + p2 == bytes.fromhex(fx["aht_plog"])
+    assert c1 + c2 == bytes.fromhex(fx["aht_clog"])
+    assert t.dlog_bytes() == bytes.fromhex(fx["aht_dlog"])
 
 
 def test_nodes_upto_table(orc, synthetic):
