@@ -30,6 +30,7 @@ MH_ERR_CORRUPTED_MAX_ENTRIES = 15
 MH_ERR_CORRUPTED_MAX_KEYLEN = 16
 MH_ERR_CORRUPTED_UNKNOWN_VERSION = 17
 MH_ERR_TRUNCATED = 18
+MH_ERR_BUFFER_TOO_SMALL = 19
 
 MH_AHT_INCLUSION = 0
 MH_AHT_CONSISTENCY = 1
@@ -122,6 +123,10 @@ class ErrUnexpectedEOF(MerkleError):
     pass
 
 
+class ErrBufferTooSmall(MerkleError):
+    pass
+
+
 class HipError(MerkleError):
     pass
 
@@ -145,6 +150,7 @@ _ERRORS = {
     MH_ERR_CORRUPTED_MAX_KEYLEN: ErrCorruptedTxDataMaxKeyLenExceeded,
     MH_ERR_CORRUPTED_UNKNOWN_VERSION: ErrCorruptedTxDataUnknownHeaderVersion,
     MH_ERR_TRUNCATED: ErrUnexpectedEOF,
+    MH_ERR_BUFFER_TOO_SMALL: ErrBufferTooSmall,
 }
 
 vp = C.c_void_p
@@ -205,6 +211,11 @@ SIGNATURES = {
     "mh_ahtree_dlog": (i32, [vp, u64, u64, u8p]),
     "mh_ahtree_dlog_device": (i32, [vp, C.POINTER(vp)]),
     "mh_dev_ahtree_append_batch": (i32, [vp, u8p, u64, u8p, u64, u32, u8p]),
+    "mh_pb_scratch_size": (u64, [u64]),
+    "mh_htree_inclusion_proof_pb_batch": (i32, [vp, u64, vp, u8p, u64, vp, vp]),
+    "mh_ahtree_dual_proof_v2_pb_batch": (i32, [vp, u64, vp, vp, u8p, u64, u8p, u64, vp, vp]),
+    "mh_dev_htree_inclusion_proof_pb_batch": (i32, [vp, i32, u8p, u64, u64, vp, u8p, u64, vp, vp, vp]),
+    "mh_dev_dual_proof_v2_pb_batch": (i32, [vp, i32, u8p, u64, u64, vp, vp, u8p, u8p, u64, vp, vp, vp]),
     "mh_ahtree_append_batch_logs": (i32, [vp, u8p, u64, u32, u64, u8p, u8p, u8p]),
     "mh_dev_ahtree_append_batch_logs": (i32, [vp, u8p, u64, u8p, u64, u32, u64, u8p, u8p, u8p]),
     "mh_dev_ahtree_log_records": (i32, [vp, u8p, u64, u32, u64, u8p, u8p]),

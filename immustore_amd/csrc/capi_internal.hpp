@@ -132,6 +132,7 @@ struct mh_htree {
     uint64_t width = 0;
     uint8_t root[32];
     DevBuf levels, in_a, in_b, in_c, off_a, off_b, off_c, ov, use, hv, msgoff, msgs, digests;
+    DevBuf w_in, w_out;  // wire formats (capi_wire.hip)
     void *pinned = nullptr;
     uint64_t pinned_cap = 0;
     LevelGeom geom;
@@ -142,7 +143,19 @@ struct mh_ahtree {
     hipStream_t stream = nullptr;
     uint64_t size = 0;
     DevBuf dlog, in, roots, idx, out, ctr;
+    DevBuf w_in, w_out;  // wire formats (capi_wire.hip)
 };
+
+// Header preconditions shared by every entry point that reads headers.
+inline int check_header(const mh_tx_header &h, uint64_t md_blob_len, bool have_blob) {
+    if (h.version > 1) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (h.md_len) {
+        if (h.version == 0) return MH_ERR_METADATA_UNSUPPORTED;
+        if (h.md_len > MH_MAX_TX_METADATA_LEN || !have_blob) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((uint64_t)h.md_off + h.md_len > md_blob_len) return MH_ERR_ILLEGAL_ARGUMENTS;
+    }
+    return MH_OK;
+}
 
 // ---------------------------------------------------------------- tx layer helpers
 // Sub-allocations of one device scratch buffer (256-byte aligned).

@@ -12,17 +12,6 @@
 
 namespace {
 
-// Header preconditions shared by every entry point that hashes headers.
-int check_header(const mh_tx_header &h, uint64_t md_blob_len, bool have_blob) {
-    if (h.version > 1) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (h.md_len) {
-        if (h.version == 0) return MH_ERR_METADATA_UNSUPPORTED;
-        if (h.md_len > MH_MAX_TX_METADATA_LEN || !have_blob) return MH_ERR_ILLEGAL_ARGUMENTS;
-        if ((uint64_t)h.md_off + h.md_len > md_blob_len) return MH_ERR_ILLEGAL_ARGUMENTS;
-    }
-    return MH_OK;
-}
-
 uint64_t be_at(const uint8_t *p, int n) {
     uint64_t v = 0;
     for (int i = 0; i < n; i++) v = (v << 8) | p[i];

@@ -195,4 +195,15 @@ hipError_t launch_ahtree_proof(hipStream_t st, Timer *tm, int kind, const uint8_
                                uint64_t size, uint64_t n, const uint64_t *i, const uint64_t *j,
                                uint8_t *terms, uint32_t max_terms, uint32_t *nterms,
                                int32_t *status);
+
+// ---------------------------------------------------------------- wire formats (wire_kernels.hip)
+// phase bit 1: sizes + status + off[0..n]; bit 2: write messages
+uint64_t pb_scratch_bytes(uint64_t n);
+hipError_t launch_pb_dual_v2(hipStream_t st, Timer *tm, int phase, const uint8_t *dlog,
+                             uint64_t size, uint64_t n, const MhTxHeader *src,
+                             const MhTxHeader *tgt, const uint8_t *md_blob, uint8_t *out,
+                             uint64_t out_cap, uint64_t *off, int32_t *status, uint8_t *scratch);
+hipError_t launch_pb_inclusion(hipStream_t st, Timer *tm, int phase, const uint8_t *levels,
+                               uint64_t w, uint64_t n, const uint64_t *leaf, uint8_t *out,
+                               uint64_t out_cap, uint64_t *off, int32_t *status, uint8_t *scratch);
 }  // namespace mh

@@ -206,6 +206,14 @@ class HTree:
                                                          mt, _addr(nt), _addr(st)))
         return terms[:n], nt[:n], st[:n]
 
+    def inclusion_proof_pb_batch(self, leaves) -> Tuple[List[bytes], np.ndarray]:
+        """InclusionProof protobuf messages (schema.proto:534, InclusionProofToProto
+        database_protoconv.go:115-121) of many leaves, generated and encoded on
+        the device -> (messages, status[n])."""
+        lv = np.ascontiguousarray(leaves, np.uint64)
+        return _pb_call(lambda out, cap, off, st: self._lib.mh_htree_inclusion_proof_pb_batch(
+            self.handle, lv.size, _addr(lv), _addr(out), cap, _addr(off), _addr(st)), lv.size)
+
     def levels(self) -> np.ndarray:
         tot = levels_len(self.width)
         out = np.zeros((max(tot, 1), 32), np.uint8)
@@ -216,6 +224,23 @@ class HTree:
         p = C.c_void_p()
         N.check(self._lib.mh_htree_levels_device(self.handle, C.byref(p)))
         return p.value
+
+
+def _pb_call(call, n, guess: int = 0):
+    """Run a packed-protobuf batch call, growing the output once on
+    MH_ERR_BUFFER_TOO_SMALL -> (list of message bytes, status[n])."""
+    off = np.zeros(n + 1, np.uint64)
+    st = np.zeros(max(n, 1), np.int32)
+    cap = guess or 2048 * max(n, 1)
+    for _ in range(2):
+        out = np.zeros(max(cap, 1), np.uint8)
+        r = call(out, cap, off, st)
+        if r == N.MH_ERR_BUFFER_TOO_SMALL:
+            cap = int(off[n])
+            continue
+        N.check(r)
+        return [out[off[k]:off[k + 1]].tobytes() for k in range(n)], st[:n]
+    raise N.ErrBufferTooSmall(N.MH_ERR_BUFFER_TOO_SMALL)
 
 
 def _csr(items):
@@ -367,6 +392,17 @@ class AHtree:
         N.check(self._lib.mh_ahtree_proof_batch(self.handle, kind, n, _addr(a), _addr(b),
                                                 _addr(terms), max_terms, _addr(nt), _addr(st)))
         return terms[:n], nt[:n], st[:n]
+
+    def dual_proof_v2_pb_batch(self, src_hdrs, tgt_hdrs, md_blob=b""):
+        """ImmuStore.DualProofV2 (immustore.go:2356-2387) for many header pairs
+        (TX_HEADER records, txlayer.py), each encoded on the device as the
+        DualProofV2 protobuf message (schema.proto:437) -> (messages, status[n])."""
+        from .txlayer import _blob, _hdrs
+        s, t = _hdrs(src_hdrs), _hdrs(tgt_hdrs)
+        bp, bl = _blob(md_blob)
+        return _pb_call(lambda out, cap, off, st: self._lib.mh_ahtree_dual_proof_v2_pb_batch(
+            self.handle, s.size, _addr(s), _addr(t), _addr(bp), bl, _addr(out), cap, _addr(off),
+            _addr(st)), s.size)
 
     def reset_size(self, new_size: int):
         N.check(self._lib.mh_ahtree_reset_size(self.handle, new_size))

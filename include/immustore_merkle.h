@@ -54,6 +54,7 @@ extern "C" {
 #define MH_ERR_CORRUPTED_MAX_KEYLEN 16  /* ErrCorruptedTxDataMaxKeyLenExceeded immustore.go:75 */
 #define MH_ERR_CORRUPTED_UNKNOWN_VERSION 17 /* ErrCorruptedTxDataUnknownHeaderVersion immustore.go:74 */
 #define MH_ERR_TRUNCATED 18             /* record cut short (io.ErrUnexpectedEOF from the reader) */
+#define MH_ERR_BUFFER_TOO_SMALL 19      /* output capacity below the encoded size (wire formats) */
 
 #define MH_MAX_TX_METADATA_LEN 268 /* maxTxMetadataLen tx_metadata.go:36-39 */
 #define MH_MAX_KV_METADATA_LEN 11  /* maxKVMetadataLen kv_metadata.go:41-43 */
@@ -437,6 +438,52 @@ int mh_precommit_batch(mh_commit_pipe *p, int version, uint64_t max_width, uint6
                        const uint64_t *val_off, const uint8_t *hval_override,
                        const uint8_t *use_override, const uint8_t *expect_eh, uint8_t *hvals_out,
                        uint8_t *eh_out, int32_t *status);
+
+/* ------------------------------------------------------------ wire formats
+ * proofs as the protobuf messages the gRPC server sends
+ * (pkg/api/schema/schema.proto, Go conversion pkg/api/schema/database_protoconv.go,
+ * marshalled as protobuf-go does: field-number order, proto3 zero values
+ * omitted), generated AND encoded on the device from the resident tree, so a
+ * batch of VerifiableGet / VerifiableTxByIdV2 answers is one device->host
+ * copy of ready-to-send bytes.  Message p is out[off[p] .. off[p+1]) (off has
+ * n + 1 entries, off[0] = 0); a message that fails is empty and status[p]
+ * holds the Go error.  If out_cap < off[n] nothing is written to out, off and
+ * status are filled and MH_ERR_BUFFER_TOO_SMALL is returned (call again with
+ * a buffer of off[n] bytes). */
+
+/* InclusionProof messages (schema.proto:534-540, InclusionProofToProto
+ * database_protoconv.go:115-121) of (*HTree).InclusionProof(leaf[p])
+ * (htree.go:121-164) over the tree's last build; status[p] MH_OK or
+ * MH_ERR_ILLEGAL_ARGUMENTS (leaf >= width). */
+int mh_htree_inclusion_proof_pb_batch(mh_htree *t, uint64_t n, const uint64_t *leaf, uint8_t *out,
+                                      uint64_t out_cap, uint64_t *off, int32_t *status);
+/* DualProofV2 messages (schema.proto:437-445; DualProofV2ToProto /
+ * TxHeaderToProto / TxMetadataToProto database_protoconv.go:152-193) of
+ * ImmuStore.DualProofV2(src[p], tgt[p]) (immustore.go:2356-2387: the ahtree
+ * InclusionProof(src.ID, tgt.BlTxID) and ConsistencyProof(max(1,
+ * src.BlTxID), tgt.BlTxID)) over t's dLog.  Header metadata (md_len bytes of
+ * TxMetadata.Bytes() at md_blob + md_off) is re-encoded as the TxMetadata
+ * message; md_len == 0 is Go's nil Metadata (a header read from the tx log,
+ * tx.go:483-501).  status[p]: MH_OK, MH_ERR_ILLEGAL_ARGUMENTS (src.ID == 0),
+ * MH_ERR_SOURCE_TX_NEWER, MH_ERR_UNEXPECTED_LINKING, MH_ERR_UNEXISTENT_DATA
+ * (tgt.BlTxID beyond the tree), MH_ERR_CORRUPTED_DATA (metadata bytes). */
+int mh_ahtree_dual_proof_v2_pb_batch(mh_ahtree *t, uint64_t n, const mh_tx_header *src,
+                                     const mh_tx_header *tgt, const uint8_t *md_blob,
+                                     uint64_t md_blob_len, uint8_t *out, uint64_t out_cap,
+                                     uint64_t *off, int32_t *status);
+/* Device variants (all pointers device memory, asynchronous, no allocation):
+ * scratch = mh_pb_scratch_size(n) bytes; messages beyond out_cap get status
+ * MH_ERR_BUFFER_TOO_SMALL.  phase: 1 = sizes + offsets only, 2 = write only
+ * (after a phase-1 call with the same inputs), 3 = both. */
+uint64_t mh_pb_scratch_size(uint64_t n);
+int mh_dev_htree_inclusion_proof_pb_batch(mh_ctx *ctx, int phase, const uint8_t *levels,
+                                          uint64_t width, uint64_t n, const uint64_t *leaf,
+                                          uint8_t *out, uint64_t out_cap, uint64_t *off,
+                                          int32_t *status, void *scratch);
+int mh_dev_dual_proof_v2_pb_batch(mh_ctx *ctx, int phase, const uint8_t *dlog, uint64_t size,
+                                  uint64_t n, const mh_tx_header *src, const mh_tx_header *tgt,
+                                  const uint8_t *md_blob, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *off, int32_t *status, void *scratch);
 
 #ifdef __cplusplus
 }
