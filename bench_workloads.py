@@ -14,6 +14,11 @@
                     (tx.go:388-630) of 2^16 records x 16 entries (16 B keys,
                     v1, no metadata) through mh_txlog_validate: host parse,
                     H2D, entry digests + one htree per tx + Alh on the GPU.
+  --workload wire   SURVEY.md 8(f) row 4: proofs as protobuf messages built on
+                    the device -- 10^6 DualProofV2 (ImmuStore.DualProofV2 over
+                    a 2^24-append ahtree + TxHeader encoding) and 10^6 htree
+                    InclusionProof messages over a 2^24-leaf tree; sizes pass,
+                    scan, write pass; a sample checked against oracle/wire.py.
   --workload commit SURVEY.md 8(f) row 1: ImmuStore.precommit hashing over a
                     batch of 2^16 txs x 16 entries x 1 KiB values (8 B keys,
                     v1) in pinned host memory through mh_precommit_batch: value
@@ -172,7 +177,10 @@ def distributed_main(a):
 
 def make_parser():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit"], required=True)
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire"],
+                   required=True)
+    p.add_argument("--logs", action="store_true",
+                   help="c3: also write the pLog / cLog appendable records (8(f) row 4)")
     p.add_argument("--txs", type=int, default=1 << 16, help="txlog records")
     p.add_argument("--tx-entries", type=int, default=16, help="txlog entries per record")
     p.add_argument("--vlen", type=int, default=1024, help="commit value bytes")
@@ -206,10 +214,18 @@ def run_single(a):
         N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 3))
         nd = m.nodes_upto(M)
         dlog = torch.empty(nd * 32, dtype=torch.uint8, device=dev)
+        if a.logs:
+            plog = torch.empty(M * 36, dtype=torch.uint8, device=dev)
+            clog = torch.empty(M * 12, dtype=torch.uint8, device=dev)
 
         def step():
-            N.check(L.mh_dev_ahtree_append_batch(ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(), M,
-                                                 32, None))
+            if a.logs:
+                N.check(L.mh_dev_ahtree_append_batch_logs(
+                    ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(), M, 32, 0, plog.data_ptr(),
+                    clog.data_ptr(), None))
+            else:
+                N.check(L.mh_dev_ahtree_append_batch(ctx.handle, dlog.data_ptr(), 0,
+                                                     pay.data_ptr(), M, 32, None))
 
         ctx.timing_reset()
         ctx.set_timing(True)
@@ -247,6 +263,18 @@ def run_single(a):
                "gcomp_per_s": round(comps / t / 1e9, 2),
                "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
                "spot_check_vs_reference_recurrence": bool(ok)}
+        if a.logs:
+            # records of the first / last appends vs the format (ahtree.go:266-282, 341-351)
+            import struct
+            pl = plog.view(-1, 36)
+            cl = clog.view(-1, 12)
+            for n in (0, 1, M - 1):
+                ok &= bytes(pl[n].cpu().numpy()) == struct.pack(">I", 32) + bytes(
+                    pay_h[n].cpu().numpy())
+                ok &= bytes(cl[n].cpu().numpy()) == struct.pack(">QI", 36 * n, 32)
+            out["metric"] += " + pLog/cLog appendable records"
+            out["records_bytes"] = M * 48
+            out["spot_check_vs_reference_recurrence"] = bool(ok)
 
     elif a.workload == "c5":
         D = a.depth
@@ -435,7 +463,7 @@ def run_single(a):
                                           "threads, SHA-NI=%s, median of 3 = %.3f s"
                                           % (orc.has_shani(), t_cpu)}}
 
-    else:  # c2e2e
+    elif a.workload == "c2e2e":
         n, vlen, klen = 1 << 20, 1024, 8
         hv = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()
         hk = torch.empty(n * klen, dtype=torch.uint8).pin_memory()
@@ -470,6 +498,126 @@ def run_single(a):
                "value": round(n * vlen / t / 2 ** 30, 3), "unit": "GiB/s",
                "ms_per_step": round(t * 1e3, 3), "device_resident_ms": round(td * 1e3, 3),
                "h2d_bytes": n * (vlen + klen), "d2h_bytes": nl * 32 + 32}
+    elif a.workload == "wire":
+        from immustore_amd.txlayer import TX_HEADER
+        P = a.proofs
+        D = a.depth
+        W = 1 << D
+        rng = np.random.default_rng(12)
+        # ahtree of W appends and a W-leaf htree, both resident
+        pay = torch.empty(W * 32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 12))
+        dlog = torch.empty(m.nodes_upto(W) * 32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_ahtree_append_batch(ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(), W, 32,
+                                             None))
+        levels = torch.empty(m.levels_len(W) * 32, dtype=torch.uint8, device=dev)
+        root = torch.empty(32, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_htree_build_digests(ctx.handle, pay.data_ptr(), W, levels.data_ptr(),
+                                             root.data_ptr()))
+        # header pairs: tgt.ID in [2, W+1] (BlTxID = ID-1 <= W), src.ID in [1, tgt.ID)
+        tid = rng.integers(2, W + 2, P).astype(np.uint64)
+        sid = (rng.random(P) * (tid - 1)).astype(np.uint64) + 1
+
+        def hdrs(ids):
+            h = np.zeros(P, TX_HEADER)
+            h["id"] = ids
+            h["bl_tx_id"] = ids - 1
+            h["ts"] = 1666885208 + ids.astype(np.int64)
+            h["version"] = 1
+            h["nentries"] = 16
+            for f in ("bl_root", "prev_alh", "eh"):
+                h[f] = rng.integers(0, 256, (P, 32), dtype=np.uint8)
+            return torch.from_numpy(h.view(np.uint8).reshape(-1)).to(dev)
+
+        hs, ht = hdrs(sid), hdrs(tid)
+        off = torch.empty(P + 1, dtype=torch.int64, device=dev)
+        st = torch.empty(P, dtype=torch.int32, device=dev)
+        scratch = torch.empty(L.mh_pb_scratch_size(P), dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_dual_proof_v2_pb_batch(ctx.handle, 1, dlog.data_ptr(), W, P,
+                                                hs.data_ptr(), ht.data_ptr(), None, None, 0,
+                                                off.data_ptr(), st.data_ptr(),
+                                                scratch.data_ptr()))
+        sync()
+        total = int(off[P].item())
+        outb = torch.empty(total, dtype=torch.uint8, device=dev)
+
+        def step_dual():
+            N.check(L.mh_dev_dual_proof_v2_pb_batch(ctx.handle, 3, dlog.data_ptr(), W, P,
+                                                    hs.data_ptr(), ht.data_ptr(), None,
+                                                    outb.data_ptr(), total, off.data_ptr(),
+                                                    st.data_ptr(), scratch.data_ptr()))
+
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        td = timed(step_dual, a.steps, a.warmup, sync)
+        ctx.set_timing(False)
+        kd = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("pb_dual_size",
+                                                                   "pb_dual_write")}
+        assert int(st.abs().sum().item()) == 0
+        # sample check against the oracle (C-oracle proofs + protobuf runtime)
+        sys.path.insert(0, os.path.join(HERE, "oracle"))
+        import oracle as O
+        import wire as WR
+        # the oracle walks the device dLog (its values are pinned by the parity
+        # tests; this checks the proof assembly and the encoding)
+        o = O.AHtree(1)
+        o.dlog = dlog.view(-1, 32).cpu().numpy()
+        o.size = W
+        hs_h = hs.cpu().numpy().view(TX_HEADER)
+        ht_h = ht.cpu().numpy().view(TX_HEADER)
+        offs = off.cpu().numpy()
+        ob = outb.cpu().numpy()
+
+        def rec(r):
+            return {"id": int(r["id"]), "ts": int(r["ts"]), "bltxid": int(r["bl_tx_id"]),
+                    "blroot": r["bl_root"].tobytes(), "prevalh": r["prev_alh"].tobytes(),
+                    "eh": r["eh"].tobytes(), "version": int(r["version"]),
+                    "nentries": int(r["nentries"]), "md": b""}
+
+        ok = True
+        for k in [int(x) for x in rng.integers(0, P, 300)]:
+            ok &= WR.dual_proof_v2_pb(rec(hs_h[k]), rec(ht_h[k]), o) == (
+                0, ob[offs[k]:offs[k + 1]].tobytes())
+        # htree InclusionProof messages over the W-leaf tree
+        leaf = torch.from_numpy(rng.integers(0, W, P).astype(np.int64)).to(dev)
+        off2 = torch.empty(P + 1, dtype=torch.int64, device=dev)
+        N.check(L.mh_dev_htree_inclusion_proof_pb_batch(ctx.handle, 1, levels.data_ptr(), W, P,
+                                                        leaf.data_ptr(), None, 0, off2.data_ptr(),
+                                                        st.data_ptr(), scratch.data_ptr()))
+        sync()
+        total2 = int(off2[P].item())
+        outi = torch.empty(total2, dtype=torch.uint8, device=dev)
+
+        def step_incl():
+            N.check(L.mh_dev_htree_inclusion_proof_pb_batch(
+                ctx.handle, 3, levels.data_ptr(), W, P, leaf.data_ptr(), outi.data_ptr(), total2,
+                off2.data_ptr(), st.data_ptr(), scratch.data_ptr()))
+
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        ti = timed(step_incl, a.steps, a.warmup, sync)
+        ctx.set_timing(False)
+        ki = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("pb_incl_size",
+                                                                   "pb_incl_write")}
+        assert int(st.abs().sum().item()) == 0
+        lv_h = levels.view(-1, 32).cpu().numpy()
+        leaf_h = leaf.cpu().numpy()
+        offs2 = off2.cpu().numpy()
+        oi = outi.cpu().numpy()
+        for k in [int(x) for x in rng.integers(0, P, 300)]:
+            ok &= WR.htree_inclusion_proof_pb(lv_h, W, int(leaf_h[k])) == (
+                0, oi[offs2[k]:offs2[k + 1]].tobytes())
+        out = {"metric": "DualProofV2 protobuf messages built on the device, 10^6 x (2^24 tree)",
+               "value": round(P / td / 1e6, 3), "unit": "M messages/s",
+               "ms_per_step": round(td * 1e3, 3), "bytes_out": total,
+               "out_GBps": round(total / td / 1e9, 1),
+               "kernel_ms": {k: round(v, 3) for k, v in kd.items()},
+               "inclusion_proof_pb": {"M_messages_per_s": round(P / ti / 1e6, 3),
+                                      "ms_per_step": round(ti * 1e3, 3), "bytes_out": total2,
+                                      "out_GBps": round(total2 / ti / 1e9, 1),
+                                      "kernel_ms": {k: round(v, 3) for k, v in ki.items()}},
+               "sample_vs_oracle": bool(ok)}
+
     out["workload"] = a.workload
     ctx.close()
     return out
