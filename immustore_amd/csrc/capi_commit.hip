@@ -31,24 +31,6 @@ __global__ void k_rebase3(uint64_t n, uint64_t *__restrict__ a, uint64_t *__rest
     c[i] -= c0;
 }
 
-struct PinBuf {
-    void *p = nullptr;
-    uint64_t cap = 0;
-    hipError_t ensure(uint64_t bytes) {
-        if (bytes <= cap && p) return hipSuccess;
-        if (p) hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        const uint64_t c = std::max<uint64_t>(bytes + 64, 4096);
-        hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
-        if (e == hipSuccess) cap = c;
-        return e;
-    }
-    ~PinBuf() {
-        if (p) hipHostFree(p);
-    }
-};
-
 }  // namespace
 
 // Three slots of device / pinned buffers; one copy stream carries every

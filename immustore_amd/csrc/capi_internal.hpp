@@ -114,6 +114,29 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging (hipHostMalloc), grown on demand.
+struct PinBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const uint64_t c = std::max<uint64_t>(bytes + 64, 4096);
+        hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    template <class T>
+    T *as() const {
+        return reinterpret_cast<T *>(p);
+    }
+    ~PinBuf() {
+        if (p) hipHostFree(p);
+    }
+};
+
 struct mh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -122,6 +145,8 @@ struct mh_ctx {
     std::mutex mu;  // guards scratch for mh_dev_* calls
     DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs, s_ctr;
     DevBuf s_tx, s_tree;  // tx layer (capi_tx.hip)
+    DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
+    PinBuf p_tx;          // its pinned staging of the parsed index arrays
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
 };
 

@@ -6,6 +6,7 @@
 // per-proof verdicts; every SHA-256 runs in tx_kernels.hip / verify_kernels.hip
 // / htree_kernels.hip.
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "capi_internal.hpp"
@@ -517,125 +518,276 @@ extern "C" int mh_verify_dual_proof_batch(mh_ctx *c, const mh_dual_proof_batch *
 }
 
 // ------------------------------------------------------------------ a14
+namespace {
+
+// Records of one stretch of a tx log (the structure readHeader / readEntry
+// read, tx.go:419-603; no hashing).
+struct HopOut {
+    std::vector<mh_tx_header> H;
+    std::vector<uint64_t> alh_pos, ent_start, msg;  // per record
+    uint64_t start = 0, end = 0;  // first record parsed / where parsing stopped
+    int rc = MH_OK;
+    bool stopped = false;  // EOF (id 0 / end of buffer) or a structural error
+};
+
+struct HopLimits {
+    uint32_t max_entries, max_key_len;
+};
+
+inline uint64_t be16p(const uint8_t *q) { return (uint64_t)((uint32_t)q[0] << 8 | q[1]); }
+
+// Parse the record at p.  Returns MH_OK and fills h / first / alh / msg, or
+// the structural error; *eof for an id-0 tail or a buffer too short for an id.
+int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &lim,
+               mh_tx_header &h, uint64_t &first, uint64_t &alh, uint64_t &msg, bool &eof) {
+    eof = false;
+    if (p + 8 > len) { eof = true; return MH_OK; }
+    memset(&h, 0, sizeof h);
+    h.id = be_at(buf + p, 8);
+    if (h.id == 0) { eof = true; return MH_OK; }  // preallocated tail, read as EOF (tx.go:427-430)
+    if (p + 90 > len) return MH_ERR_TRUNCATED;
+    h.ts = (int64_t)be_at(buf + p + 8, 8);
+    h.bl_tx_id = be_at(buf + p + 16, 8);
+    memcpy(h.bl_root, buf + p + 24, 32);
+    memcpy(h.prev_alh, buf + p + 56, 32);
+    h.version = (uint32_t)be16p(buf + p + 88);
+    uint64_t q = p + 90;
+    if (h.version == 0) {
+        if (q + 2 > len) return MH_ERR_TRUNCATED;
+        h.nentries = (uint32_t)be16p(buf + q);
+        q += 2;
+    } else if (h.version == 1) {
+        if (q + 2 > len) return MH_ERR_TRUNCATED;
+        h.md_len = (uint32_t)be16p(buf + q);
+        q += 2;
+        if (h.md_len > MH_MAX_TX_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+        if (q + h.md_len + 4 > len) return MH_ERR_TRUNCATED;
+        if (q > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
+        h.md_off = (uint32_t)q;
+        q += h.md_len;
+        h.nentries = (uint32_t)be_at(buf + q, 4);
+        q += 4;
+    } else {
+        return MH_ERR_CORRUPTED_UNKNOWN_VERSION;
+    }
+    if (h.nentries > lim.max_entries) return MH_ERR_CORRUPTED_MAX_ENTRIES;
+    first = q;
+    const uint64_t v1 = h.version == 1;
+    msg = 0;
+    for (uint32_t e = 0; e < h.nentries; e++) {
+        if (q + 2 > len) return MH_ERR_TRUNCATED;
+        const uint64_t ml = be16p(buf + q);
+        if (ml > MH_MAX_KV_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+        if (q + 2 + ml + 2 > len) return MH_ERR_TRUNCATED;
+        const uint64_t kl = be16p(buf + q + 2 + ml);
+        if (kl > lim.max_key_len) return MH_ERR_CORRUPTED_MAX_KEYLEN;
+        if (q + 4 + ml + kl + 12 + 32 > len) return MH_ERR_TRUNCATED;
+        q += 4 + ml + kl + 12 + 32;
+        msg += (v1 ? 4 + ml + kl : kl) + 32;
+    }
+    if (q + 32 > len) return MH_ERR_TRUNCATED;
+    alh = q;
+    return MH_OK;
+}
+
+// Records starting in [p, stop), at most max_recs of them.
+void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint64_t max_recs,
+               const HopLimits &lim, HopOut &o) {
+    o.start = p;
+    while (p < stop && o.H.size() < max_recs) {
+        mh_tx_header h;
+        uint64_t first = 0, alh = 0, msg = 0;
+        bool eof = false;
+        const int rc = hop_record(buf, len, p, lim, h, first, alh, msg, eof);
+        if (rc != MH_OK || eof) {
+            o.rc = rc;
+            o.stopped = true;
+            break;
+        }
+        o.H.push_back(h);
+        o.alh_pos.push_back(alh);
+        o.ent_start.push_back(first);
+        o.msg.push_back(msg);
+        p = alh + 32;
+    }
+    o.end = p;
+}
+
+// A position that parses as 3 consecutive records with consecutive ids (or
+// as records up to the end of the log): where a chunk's speculative parse
+// starts.  Only a guess -- the merge accepts a chunk only if the previous
+// chunk's parse ended exactly there.
+uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint64_t to,
+                           const HopLimits &lim) {
+    for (uint64_t q = from; q < to; q++) {
+        uint64_t p = q, prev_id = 0;
+        int ok = 0;
+        for (; ok < 3; ok++) {
+            mh_tx_header h;
+            uint64_t first, alh, msg;
+            bool eof;
+            if (hop_record(buf, len, p, lim, h, first, alh, msg, eof) != MH_OK) break;
+            if (eof) { ok = 3; break; }
+            if (ok && h.id != prev_id + 1) break;
+            prev_id = h.id;
+            p = alh + 32;
+        }
+        if (ok >= 3) return q;
+    }
+    return ~0ull;
+}
+
+// The whole hop: one thread below 8 MiB, else up to 8 threads parse chunks
+// from speculated record starts; chunks whose start does not match the
+// previous chunk's end are re-parsed sequentially, so the result is always
+// the sequential parse's.
+void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits &lim,
+             HopOut &out) {
+    unsigned T = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (len < (8ull << 20)) T = 1;
+    if (T == 1) {
+        hop_range(buf, len, 0, ~0ull, max_txs, lim, out);
+        return;
+    }
+    std::vector<uint64_t> cut(T + 1);
+    for (unsigned k = 0; k <= T; k++) cut[k] = len / T * k;
+    cut[T] = ~0ull;
+    std::vector<HopOut> part(T);
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < T; k++)
+        th.emplace_back([&, k] {
+            const uint64_t s = k ? find_record_start(buf, len, cut[k], std::min(cut[k + 1], len), lim) : 0;
+            if (s == ~0ull) {
+                part[k].start = ~0ull;
+                return;
+            }
+            hop_range(buf, len, s, cut[k + 1], max_txs, lim, part[k]);
+        });
+    for (auto &t : th) t.join();
+    uint64_t pos = 0;
+    out.start = 0;
+    for (unsigned k = 0; k < T; k++) {
+        if (pos >= cut[k + 1]) continue;  // a record spanning this whole chunk
+        HopOut redo, *o = &part[k];
+        if (o->start != pos) {            // speculation missed: parse this chunk for real
+            hop_range(buf, len, pos, cut[k + 1], max_txs, lim, redo);
+            o = &redo;
+        }
+        const uint64_t room = max_txs - out.H.size();
+        const uint64_t take = std::min<uint64_t>(room, o->H.size());
+        out.H.insert(out.H.end(), o->H.begin(), o->H.begin() + take);
+        out.alh_pos.insert(out.alh_pos.end(), o->alh_pos.begin(), o->alh_pos.begin() + take);
+        out.ent_start.insert(out.ent_start.end(), o->ent_start.begin(), o->ent_start.begin() + take);
+        out.msg.insert(out.msg.end(), o->msg.begin(), o->msg.begin() + take);
+        if (take < o->H.size()) {         // max_txs reached inside this chunk
+            pos = out.alh_pos.back() + 32;
+            break;
+        }
+        pos = o->end;
+        if (o->stopped) {
+            out.rc = o->rc;
+            out.stopped = true;
+            break;
+        }
+        if (out.H.size() == max_txs) break;
+    }
+    out.end = pos;
+}
+
+}  // namespace
+
 extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                                  uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                                  uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
                                  int32_t *status_out) {
     if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    // ---- host parse (tx.go:419-603): structure only, no hashing
-    std::vector<mh_tx_header> H;
-    std::vector<uint64_t> alh_pos, leaf_off{0}, rec_off, msg_off{0};
-    std::vector<uint8_t> ver;
-    uint64_t p = 0;
-    int rc = MH_OK;
-    while (H.size() < max_txs) {
-        const uint64_t p0 = p;
-        if (p + 8 > len) break;
-        mh_tx_header h;
-        memset(&h, 0, sizeof h);
-        h.id = be_at(buf + p, 8);
-        if (h.id == 0) break;  // preallocated tail, read as EOF (tx.go:427-430)
-        if (p + 90 > len) { rc = MH_ERR_TRUNCATED; break; }
-        h.ts = (int64_t)be_at(buf + p + 8, 8);
-        h.bl_tx_id = be_at(buf + p + 16, 8);
-        memcpy(h.bl_root, buf + p + 24, 32);
-        memcpy(h.prev_alh, buf + p + 56, 32);
-        h.version = (uint32_t)be_at(buf + p + 88, 2);
-        p += 90;
-        if (h.version == 0) {
-            if (p + 2 > len) { rc = MH_ERR_TRUNCATED; break; }
-            h.nentries = (uint32_t)be_at(buf + p, 2);
-            p += 2;
-        } else if (h.version == 1) {
-            if (p + 2 > len) { rc = MH_ERR_TRUNCATED; break; }
-            h.md_len = (uint32_t)be_at(buf + p, 2);
-            p += 2;
-            if (h.md_len > MH_MAX_TX_METADATA_LEN) { rc = MH_ERR_CORRUPTED_DATA; break; }
-            if (p + h.md_len + 4 > len) { rc = MH_ERR_TRUNCATED; break; }
-            h.md_off = (uint32_t)p;
-            if (p > 0xffffffffull) { rc = MH_ERR_ILLEGAL_ARGUMENTS; break; }
-            p += h.md_len;
-            h.nentries = (uint32_t)be_at(buf + p, 4);
-            p += 4;
-        } else {
-            rc = MH_ERR_CORRUPTED_UNKNOWN_VERSION;
-            break;
-        }
-        if (h.nentries > max_entries) { rc = MH_ERR_CORRUPTED_MAX_ENTRIES; break; }
-        const size_t e0 = rec_off.size();
-        int bad = MH_OK;
-        for (uint32_t e = 0; e < h.nentries; e++) {
-            const uint64_t q = p;
-            if (p + 2 > len) { bad = MH_ERR_TRUNCATED; break; }
-            const uint64_t ml = be_at(buf + p, 2);
-            if (ml > MH_MAX_KV_METADATA_LEN) { bad = MH_ERR_CORRUPTED_DATA; break; }
-            if (p + 2 + ml + 2 > len) { bad = MH_ERR_TRUNCATED; break; }
-            const uint64_t kl = be_at(buf + p + 2 + ml, 2);
-            if (kl > max_key_len) { bad = MH_ERR_CORRUPTED_MAX_KEYLEN; break; }
-            if (p + 4 + ml + kl + 12 + 32 > len) { bad = MH_ERR_TRUNCATED; break; }
-            p += 4 + ml + kl + 12 + 32;
-            rec_off.push_back(q);
-            ver.push_back((uint8_t)h.version);
-            msg_off.push_back(msg_off.back() + (h.version == 1 ? 4 + ml + kl : kl) + 32);
-        }
-        if (bad == MH_OK && p + 32 > len) bad = MH_ERR_TRUNCATED;
-        if (bad != MH_OK) {
-            rc = bad;
-            rec_off.resize(e0);
-            ver.resize(e0);
-            msg_off.resize(e0 + 1);
-            p = p0;
-            break;
-        }
-        alh_pos.push_back(p);
-        p += 32;
-        leaf_off.push_back(rec_off.size());
-        H.push_back(h);
-        (void)p0;
-    }
-    if (rc != MH_OK) {
-        // p was left inside the failing record by the header-level breaks
-        uint64_t last_end = alh_pos.empty() ? 0 : alh_pos.back() + 32;
-        p = last_end;
-    }
-    const uint64_t ntx = H.size(), E = rec_off.size();
-    if (ntx_out) *ntx_out = ntx;
-    if (consumed_out) *consumed_out = p;
-    if (!ntx) return rc;
-    // ---- device: digests, trees, Alh
+    // The raw records go to the device first: the copy (DMA when buf is
+    // pinned) runs under the host hop below.
     std::lock_guard<std::mutex> lk(c->mu);
     hipSetDevice(c->device);
     hipStream_t st = c->stream;
+    if (len) {
+        MH_HIP(c->s_txlog.ensure(len));
+        MH_HIP(hipMemcpyAsync(c->s_txlog.p, buf, len, hipMemcpyHostToDevice, st));
+    }
+    uint8_t *dbuf = c->s_txlog.as<uint8_t>();
+    // ---- host hop (tx.go:419-603): record structure and limits only.  Per
+    // entry the host reads the two lengths it needs to find the next entry
+    // (several threads over a long log, hop_all); the per-entry index (record
+    // offsets, versions, message lengths) is rebuilt on the device from each
+    // tx's first entry (k_txe_index).
+    HopOut hop;
+    hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
+    const std::vector<mh_tx_header> &H = hop.H;
+    const std::vector<uint64_t> &alh_pos = hop.alh_pos, &ent_start = hop.ent_start;
+    std::vector<uint64_t> leaf_off(H.size() + 1);
+    uint64_t E = 0, msg_total = 0, wmax = 0;
+    leaf_off[0] = 0;
+    for (size_t k = 0; k < H.size(); k++) {
+        E += H[k].nentries;
+        leaf_off[k + 1] = E;
+        wmax = std::max<uint64_t>(wmax, H[k].nentries);
+        msg_total += hop.msg[k];
+    }
+    const int rc = hop.rc;
+    const uint64_t p = hop.end;
+    // on an error p is the failing record's offset = the end of the last good one
+    const uint64_t ntx = H.size();
+    if (ntx_out) *ntx_out = ntx;
+    if (consumed_out) *consumed_out = p;
+    if (!ntx) {
+        MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
+        return rc;
+    }
+    // ---- device: entry index, digests, trees, Alh
+    // small trees (every tx here: a handful of entries) get their roots one
+    // lane per tree; a batch with a wide tx goes through the host tree plan
+    const bool small = wmax <= kSmallTreeMax;
     TreePlan P;
-    P.build(ntx, leaf_off.data());
-    const uint64_t used = p;  // bytes of buf covered by the parsed records
+    if (!small) P.build(ntx, leaf_off.data());
     Layout L;
-    const uint64_t b_buf = L.add(used), b_rec = L.add(E * 8), b_ver = L.add(E),
-                   b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_off.back()),
-                   b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_h = L.add(ntx * sizeof(mh_tx_header)),
-                   b_ap = L.add(ntx * 8), b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride),
-                   b_a = L.add(ntx * 32), b_st = L.add(ntx * 4);
+    const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
+                   b_ml = L.add(E * 8), b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_total),
+                   b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
+                   b_h = L.add(ntx * sizeof(mh_tx_header)), b_ap = L.add(ntx * 8),
+                   b_es = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
+                   b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
+                   b_st = L.add(ntx * 4), b_tmp = L.add(pb_scan_temp_bytes(E));
     MH_HIP(c->s_tx.ensure(L.total));
     uint8_t *base = c->s_tx.as<uint8_t>();
-    MH_HIP(hipMemcpyAsync(base + b_buf, buf, used, hipMemcpyHostToDevice, st));
-    if (E) {
-        MH_HIP(hipMemcpyAsync(base + b_rec, rec_off.data(), E * 8, hipMemcpyHostToDevice, st));
-        MH_HIP(hipMemcpyAsync(base + b_ver, ver.data(), E, hipMemcpyHostToDevice, st));
-    }
-    MH_HIP(hipMemcpyAsync(base + b_mo, msg_off.data(), (E + 1) * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_h, H.data(), ntx * sizeof(mh_tx_header), hipMemcpyHostToDevice,
-                          st));
-    MH_HIP(hipMemcpyAsync(base + b_ap, alh_pos.data(), ntx * 8, hipMemcpyHostToDevice, st));
-    // entry digests (tx.go:578-585 -> 690-731)
-    MH_HIP(launch_txe_assemble(st, c->tm(), E, base + b_buf, (const uint64_t *)(base + b_rec),
+    // the parsed arrays (headers, Alh positions, first entries, leaf offsets)
+    // are contiguous in the device layout: one pinned staging copy, one DMA
+    const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_h;
+    const uint64_t pin_bytes = idx_bytes + (small ? 0 : plan_index_bytes(P, ntx));
+    MH_HIP(c->p_tx.ensure(pin_bytes));
+    uint8_t *pin = c->p_tx.as<uint8_t>();
+    memcpy(pin, H.data(), ntx * sizeof(mh_tx_header));
+    memcpy(pin + (b_ap - b_h), alh_pos.data(), ntx * 8);
+    memcpy(pin + (b_es - b_h), ent_start.data(), ntx * 8);
+    memcpy(pin + (b_lo - b_h), leaf_off.data(), (ntx + 1) * 8);
+    MH_HIP(hipMemcpyAsync(base + b_h, pin, idx_bytes, hipMemcpyHostToDevice, st));
+    // per-entry index, then entry digests (tx.go:578-585 -> 690-731)
+    MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
+                            (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
+                            (uint64_t *)(base + b_rec), base + b_ver, (uint64_t *)(base + b_ml)));
+    MH_HIP(scan_offsets_u64(st, E, (const uint64_t *)(base + b_ml), (uint64_t *)(base + b_mo),
+                            base + b_tmp));
+    MH_HIP(launch_txe_assemble(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec),
                                base + b_ver, (const uint64_t *)(base + b_mo), base + b_msg));
     MH_HIP(launch_sha256_csr(st, c->tm(), base + b_msg, (const uint64_t *)(base + b_mo), E,
                              nullptr, nullptr, base + b_dig));
     // one htree per tx (tx.go:617-621)
-    if (int e = run_tree_plan(c, st, P, ntx, E, base + b_dig, base + b_eh)) return e;
+    if (small) {
+        MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_dig, base + b_lv));  // htree.go:79-83
+        MH_HIP(launch_small_roots(st, c->tm(), ntx, (const uint64_t *)(base + b_lo), base + b_lv,
+                                  base + b_eh));
+    } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_dig,
+                                        base + b_eh, pin + idx_bytes)) {
+        return e;
+    }
     // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
-    MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), base + b_buf,
-                         base + b_eh, base + b_s, base + b_buf, (const uint64_t *)(base + b_ap),
+    MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), dbuf,
+                         base + b_eh, base + b_s, dbuf, (const uint64_t *)(base + b_ap),
                          nullptr, base + b_a, (int32_t *)(base + b_st)));
     std::vector<uint8_t> eh(hdrs_out ? ntx * 32 : 0);
     if (status_out)

@@ -177,6 +177,15 @@ hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uin
                                 const uint64_t *cnt, const uint64_t *term_off,
                                 const uint8_t *terms, const uint64_t *first,
                                 const uint8_t *end_alh, uint8_t *leaves_src, uint8_t *ok);
+// roots of many htrees (widths leaf_off[t+1]-leaf_off[t], small), one lane
+// each, in place over nodes = their leaf hashes back to back
+constexpr uint64_t kSmallTreeMax = 64;
+hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
+                              uint8_t *nodes, uint8_t *roots);
+hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                            const MhTxHeader *hdrs, const uint64_t *ent_start,
+                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver,
+                            uint64_t *msg_len);
 hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
                                const uint64_t *rec_off, const uint8_t *ver,
                                const uint64_t *msg_off, uint8_t *msgs);
@@ -199,6 +208,10 @@ hipError_t launch_ahtree_proof(hipStream_t st, Timer *tm, int kind, const uint8_
 // ---------------------------------------------------------------- wire formats (wire_kernels.hip)
 // phase bit 1: sizes + status + off[0..n]; bit 2: write messages
 uint64_t pb_scratch_bytes(uint64_t n);
+// exclusive-offset scan: out[0] = 0, out[k+1] = sum in[0..k]; temp: pb_scan_temp_bytes(n)
+size_t pb_scan_temp_bytes(uint64_t n);
+hipError_t scan_offsets_u64(hipStream_t st, uint64_t n, const uint64_t *in, uint64_t *out,
+                            uint8_t *temp);
 hipError_t launch_pb_dual_v2(hipStream_t st, Timer *tm, int phase, const uint8_t *dlog,
                              uint64_t size, uint64_t n, const MhTxHeader *src,
                              const MhTxHeader *tgt, const uint8_t *md_blob, uint8_t *out,

@@ -217,6 +217,103 @@ __global__ __launch_bounds__(256) void k_txe_assemble(uint64_t n, const uint8_t 
     for (int k = 0; k < 32; k++) *o++ = hv[k];
 }
 
+// Entry index of a run of tx records (tx.go:520-588 readEntry, structure
+// only), one lane per tx: the host hop already validated every length, so
+// the lane walks its entries from ent_start[t] and records each entry's
+// record offset, header version and entry-digest message length
+// (TxEntryDigest_v1_2: BE16 mdLen + md + BE16 kLen + key + hVal; v1_1:
+// key + hVal, tx.go:690-731) for the inclusive scan into msg_off.
+__global__ __launch_bounds__(256) void k_txe_index(uint64_t ntx, const uint8_t *__restrict__ buf,
+                                                   const MhTxHeader *__restrict__ hdrs,
+                                                   const uint64_t *__restrict__ ent_start,
+                                                   const uint64_t *__restrict__ leaf_off,
+                                                   uint64_t *__restrict__ rec_off,
+                                                   uint8_t *__restrict__ ver,
+                                                   uint64_t *__restrict__ msg_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx) return;
+    const uint8_t v = (uint8_t)hdrs[t].version;
+    uint64_t q = ent_start[t];
+    for (uint64_t e = leaf_off[t]; e < leaf_off[t + 1]; e++) {
+        const uint32_t ml = ((uint32_t)buf[q] << 8) | buf[q + 1];
+        const uint32_t kl = ((uint32_t)buf[q + 2 + ml] << 8) | buf[q + 3 + ml];
+        rec_off[e] = q;
+        ver[e] = v;
+        msg_len[e] = (v == 1 ? 4 + ml + kl : kl) + 32;
+        q += 4 + ml + kl + 12 + 32;
+    }
+}
+
+hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                            const MhTxHeader *hdrs, const uint64_t *ent_start,
+                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver,
+                            uint64_t *msg_len) {
+    if (!ntx) return hipSuccess;
+    TimerScope ts(tm, "txe_index", st);
+    hipLaunchKernelGGL(k_txe_index, dim3(grid_for(ntx, 256)), dim3(256), 0, st, ntx, buf, hdrs,
+                       ent_start, leaf_off, rec_off, ver, msg_len);
+    return hipGetLastError();
+}
+
+__device__ __constant__ static const uint8_t kEmptyRootDev[32] = {
+    0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
+    0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+
+// Roots of many small htrees, one lane per tree, level by level in place
+// over the tree's own leaf range (exactly htree.go:85-110: node k of the next
+// level = H(node 2k, node 2k+1) written to slot k -- slots 2k, 2k+1 >= k are
+// read first -- and an odd last node promoted to slot (w-1)/2).  nodes holds
+// the leaf hashes of all trees back to back and is consumed.  Width 0 gives
+// SHA256(nil) (htree.go:73-77).  For batches whose widest tree is small
+// (immudb txs: a handful of entries) this replaces the host tree plan.
+__global__ __launch_bounds__(256) void k_small_roots(uint64_t ntrees,
+                                                     const uint64_t *__restrict__ leaf_off,
+                                                     uint8_t *__restrict__ nodes,
+                                                     uint8_t *__restrict__ roots) {
+    extern __shared__ uint32_t tab[];
+    node_tab_init(tab);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntrees) return;
+    uint8_t *lv = nodes + (leaf_off[t] - leaf_off[0]) * 32;
+    uint64_t w = leaf_off[t + 1] - leaf_off[t];
+    const uint4 *src;
+    if (w == 0) {
+        src = reinterpret_cast<const uint4 *>(kEmptyRootDev);
+    } else {
+        while (w > 1) {
+            const uint64_t half = w / 2;
+            for (uint64_t k = 0; k < half; k++) {
+                uint32_t a[8], b[8], h[8];
+                load_digest(lv + 64 * k, a);
+                load_digest(lv + 64 * k + 32, b);
+                node_hash_tab(a, b, h, tab);
+                store_digest(lv + 32 * k, h);
+            }
+            if (w & 1) {  // promote the odd last node
+                const uint4 *q = reinterpret_cast<const uint4 *>(lv + 32 * (w - 1));
+                uint4 *d = reinterpret_cast<uint4 *>(lv + 32 * half);
+                const uint4 x = q[0], y = q[1];
+                d[0] = x;
+                d[1] = y;
+            }
+            w = (w + 1) / 2;
+        }
+        src = reinterpret_cast<const uint4 *>(lv);
+    }
+    uint4 *d = reinterpret_cast<uint4 *>(roots + t * 32);
+    d[0] = src[0];
+    d[1] = src[1];
+}
+
+hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
+                              uint8_t *nodes, uint8_t *roots) {
+    if (!ntrees) return hipSuccess;
+    TimerScope ts(tm, "small_roots", st);
+    hipLaunchKernelGGL(k_small_roots, dim3(grid_for(ntrees, 256)), dim3(256), kNodeTabBytes, st,
+                       ntrees, leaf_off, nodes, roots);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- many trees
 // Level l of a batch of independent htrees.  Item k describes one tree that
 // still has > 1 node at level l-1: its nodes at level l are written at
@@ -256,10 +353,6 @@ __global__ __launch_bounds__(256) void k_seg_level(uint64_t nnodes, uint64_t lev
         store_digest(nodes + g * 32, o);
     }
 }
-
-__device__ __constant__ static const uint8_t kEmptyRootDev[32] = {
-    0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
-    0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
 
 __global__ __launch_bounds__(256) void k_gather32(uint64_t n, const uint8_t *__restrict__ src,
                                                   const uint64_t *__restrict__ idx,

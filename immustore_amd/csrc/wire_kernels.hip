@@ -409,6 +409,15 @@ uint64_t pb_scratch_bytes(uint64_t n) {
     return 2 * ((n * 8 + 255) & ~255ull) + ((pb_scan_temp_bytes(n) + 255) & ~255ull) + 256;
 }
 
+// in[0..n) -> out[0..n] with out[0] = 0, out[k+1] = in[0] + ... + in[k]
+hipError_t scan_offsets_u64(hipStream_t st, uint64_t n, const uint64_t *in, uint64_t *out,
+                            uint8_t *temp) {
+    if (hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st)) return e;
+    if (!n) return hipSuccess;
+    size_t bytes = pb_scan_temp_bytes(n);
+    return hipcub::DeviceScan::InclusiveSum(temp, bytes, in, out + 1, (int)n, st);
+}
+
 // sizes -> off[0..n] (off[0] = 0)
 static hipError_t pb_offsets(hipStream_t st, uint64_t n, const uint64_t *sizes, uint64_t *off,
                              uint8_t *temp) {

@@ -205,12 +205,14 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
     status is the structural error that stopped parsing (0 at a clean end);
     per_tx[k] is 0 or MH_ERR_CORRUPTED_DATA (ALH mismatch)."""
     b = _u8(buf)
-    cap = max(1, len(b) // 90 + 1)
+    cap = max(1, len(b) // 122 + 1)  # a record is >= 122 bytes (90 + 32)
     if max_txs is not None:
         cap = max(1, min(cap, max_txs))
-    hd = np.zeros(cap, TX_HEADER)
-    alh = np.zeros((cap, 32), np.uint8)
-    sts = np.zeros(cap, np.int32)
+    # outputs are written for the parsed records only: no zero fill, and the
+    # results are returned as views (no copies of the unused capacity)
+    hd = np.empty(cap, TX_HEADER)
+    alh = np.empty((cap, 32), np.uint8)
+    sts = np.empty(cap, np.int32)
     ntx, used = C.c_uint64(0), C.c_uint64(0)
     rc = N.load().mh_txlog_validate(_ctx(ctx).handle, _addr(b) if b.size else None, b.size,
                                     max_entries, max_key_len,
@@ -219,4 +221,4 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
     if rc < 0:
         N.check(rc)
     k = ntx.value
-    return rc, k, used.value, hd[:k].copy(), alh[:k].copy(), sts[:k].copy()
+    return rc, k, used.value, hd[:k], alh[:k], sts[:k]

@@ -154,6 +154,68 @@ def test_txlog_validate_synthetic_vs_oracle(m, ctx, orc):
         assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), cut
 
 
+@pytest.mark.parametrize("max_entries", [64, 65, 300])
+def test_txlog_validate_tree_paths(m, ctx, orc, max_entries):
+    """Batches whose widest tx has <= 64 entries take the one-lane-per-tree
+    root kernel, wider ones the host tree plan: both agree with the oracle."""
+    rng = np.random.default_rng(max_entries)
+    raw = _synthetic_txlog(rng, 60, orc, max_entries=max_entries)
+    rc, n, used, hdrs, alh, sts = m.txlog_validate(raw, ctx=ctx)
+    o = orc.txlog_validate(raw)
+    assert (rc, n, used) == (o[0], o[1], o[2]) == (0, 60, len(raw))
+    assert np.array_equal(alh, o[3]) and list(sts) == [0] * 60
+
+
+def _bulk_txlog(rng, ntx):
+    """A long run of structurally valid records (ragged entry counts, key and
+    metadata sizes, v0/v1) with unsealed Alh values: > 8 MiB, so the host
+    parse runs on several threads from speculated record starts."""
+    out = bytearray()
+    starts = []
+    for k in range(ntx):
+        starts.append(len(out))
+        ver = 1 if k % 3 else 0
+        ne = int(rng.integers(0, 24))
+        txmd = b"" if ver == 0 else bytes([1, 0, k % 7]) + bytes(k % 7)
+        hdr = struct.pack(">QQQ", k + 1, 1000 + k, k) + bytes(64) + struct.pack(">H", ver)
+        hdr += struct.pack(">H", ne) if ver == 0 else struct.pack(">H", len(txmd)) + txmd + \
+            struct.pack(">I", ne)
+        ents = bytearray()
+        for e in range(ne):
+            md = b"" if ver == 0 else bytes([0]) * ((k + e) % 2)
+            key = bytes([e % 251]) * int(rng.integers(1, 400))
+            ents += struct.pack(">H", len(md)) + md + struct.pack(">H", len(key)) + key
+            ents += struct.pack(">IQ", 10, e) + bytes([k % 256]) * 32
+        out += hdr + ents + bytes([7]) * 32
+    return bytes(out), starts
+
+
+def test_txlog_validate_parallel_hop(m, ctx, orc):
+    """The multi-threaded record hop equals the sequential parse (the oracle)
+    on a ~20 MB log: clean, with a structural error deep inside, cut short,
+    with a zeroed (preallocated) tail and with max_txs inside a chunk."""
+    rng = np.random.default_rng(77)
+    raw, starts = _bulk_txlog(rng, 9000)
+    assert len(raw) > (8 << 20)
+
+    def same(buf, **kw):
+        a = m.txlog_validate(buf, ctx=ctx, **kw)
+        b = orc.txlog_validate(buf, **kw)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), kw
+        assert list(a[5]) == list(b[4]) and np.array_equal(a[4], b[3])
+        return a
+
+    a = same(raw)
+    assert (a[0], a[1], a[2]) == (0, 9000, len(raw))
+    bad = bytearray(raw)
+    bad[starts[6543] + 89] = 7  # unknown header version
+    a = same(bytes(bad))
+    assert (a[0], a[1], a[2]) == (17, 6543, starts[6543])
+    same(raw[:len(raw) - 100])
+    same(raw[:starts[5000]] + bytes(3 << 20))
+    same(raw, max_txs=4321)
+
+
 def test_dual_proof_v2_fixture_cases(m, ctx, orc, fixtures):
     seen = set()
     for name, fx in fixtures.items():
