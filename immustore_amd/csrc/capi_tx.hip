@@ -119,19 +119,29 @@ extern "C" int mh_htree_build_many(mh_ctx *c, uint64_t ntrees, const uint64_t *l
         if (leaf_off[t + 1] < leaf_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
     const uint64_t E = leaf_off[ntrees] - leaf_off[0];
     if (E && !digests) return MH_ERR_ILLEGAL_ARGUMENTS;
+    uint64_t wmax = 0;
+    for (uint64_t t = 0; t < ntrees; t++) wmax = std::max(wmax, leaf_off[t + 1] - leaf_off[t]);
     std::lock_guard<std::mutex> lk(c->mu);
     hipSetDevice(c->device);
     hipStream_t st = c->stream;
-    TreePlan P;
-    P.build(ntrees, leaf_off);
     Layout L;
-    const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_r = L.add(ntrees * 32);
+    const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
+                   b_lo = L.add((ntrees + 1) * 8), b_r = L.add(ntrees * 32);
     MH_HIP(c->s_tx.ensure(L.total));
     uint8_t *base = c->s_tx.as<uint8_t>();
     if (E)
         MH_HIP(hipMemcpyAsync(base + b_d, digests + leaf_off[0] * 32, E * 32,
                               hipMemcpyHostToDevice, st));
-    if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
+    if (wmax <= kSmallTreeMax) {  // one lane per tree, no host plan
+        MH_HIP(hipMemcpyAsync(base + b_lo, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_d, base + b_lv));  // htree.go:79-83
+        MH_HIP(launch_small_roots(st, c->tm(), ntrees, (const uint64_t *)(base + b_lo),
+                                  base + b_lv, base + b_r));
+    } else {
+        TreePlan P;
+        P.build(ntrees, leaf_off);
+        if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
+    }
     MH_HIP(hipMemcpyAsync(roots, base + b_r, ntrees * 32, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
     return MH_OK;
@@ -618,7 +628,11 @@ void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint
 // starts.  Only a guess -- the merge accepts a chunk only if the previous
 // chunk's parse ended exactly there.
 uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint64_t to,
-                           const HopLimits &lim) {
+                           const HopLimits &lim0) {
+    // bounded speculation: a 256 KiB window and candidate records of at most
+    // 4096 entries (a miss only costs a sequential re-parse of the chunk)
+    const HopLimits lim{std::min<uint32_t>(lim0.max_entries, 4096), lim0.max_key_len};
+    to = std::min<uint64_t>(to, from + (256u << 10));
     for (uint64_t q = from; q < to; q++) {
         uint64_t p = q, prev_id = 0;
         int ok = 0;

@@ -79,6 +79,11 @@ def test_htree_build_many_vs_oracle(m, ctx, orc):
     roots = m.htree_build_many(trees, ctx)
     for t, r in zip(trees, roots):
         assert r.tobytes() == orc.htree_build(t)[1]
+    # every width <= 64: the one-lane-per-tree kernel instead of the host plan
+    small = [t for t in trees if len(t) <= 64] + [rng.integers(0, 256, (64, 32), dtype=np.uint8)]
+    roots = m.htree_build_many(small, ctx)
+    for t, r in zip(small, roots):
+        assert r.tobytes() == orc.htree_build(t)[1]
 
 
 def test_txlog_validate_fixture_stores(m, ctx, fixtures):
