@@ -212,6 +212,7 @@ SIGNATURES = {
     "mh_ahtree_dlog_device": (i32, [vp, C.POINTER(vp)]),
     "mh_dev_ahtree_append_batch": (i32, [vp, u8p, u64, u8p, u64, u32, u8p]),
     "mh_pb_scratch_size": (u64, [u64]),
+    "mh_txlog_scan": (i32, [u8p, u64, u32, u32, u64, vp, vp, vp, vp]),
     "mh_htree_inclusion_proof_pb_batch": (i32, [vp, u64, vp, u8p, u64, vp, vp]),
     "mh_ahtree_dual_proof_v2_pb_batch": (i32, [vp, u64, vp, vp, u8p, u64, u8p, u64, vp, vp]),
     "mh_dev_htree_inclusion_proof_pb_batch": (i32, [vp, i32, u8p, u64, u64, vp, u8p, u64, vp, vp, vp]),

@@ -710,6 +710,23 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
 
 }  // namespace
 
+// Structure-only read of a run of tx records (host, no device): the record
+// hop of mh_txlog_validate on its own.
+extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                             uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
+                             uint64_t *consumed_out, mh_tx_header *hdrs_out,
+                             uint64_t *alh_off_out) {
+    if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
+    HopOut hop;
+    hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
+    const uint64_t ntx = hop.H.size();
+    if (ntx_out) *ntx_out = ntx;
+    if (consumed_out) *consumed_out = hop.end;
+    if (hdrs_out && ntx) memcpy(hdrs_out, hop.H.data(), ntx * sizeof(mh_tx_header));
+    if (alh_off_out && ntx) memcpy(alh_off_out, hop.alh_pos.data(), ntx * 8);
+    return hop.rc;
+}
+
 extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                                  uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                                  uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,

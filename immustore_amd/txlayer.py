@@ -222,3 +222,23 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
         N.check(rc)
     k = ntx.value
     return rc, k, used.value, hd[:k], alh[:k], sts[:k]
+
+
+def txlog_scan(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
+               max_key_len: int = DEFAULT_MAX_KEY_LEN, max_txs: Optional[int] = None):
+    """Record structure only (host, no device) -> (status, ntx, consumed,
+    hdrs[ntx] TX_HEADER with eh zero, alh_off[ntx])."""
+    b = _u8(buf)
+    cap = max(1, len(b) // 122 + 1)
+    if max_txs is not None:
+        cap = max(1, min(cap, max_txs))
+    hd = np.zeros(cap, TX_HEADER)
+    ao = np.zeros(cap, np.uint64)
+    ntx, used = C.c_uint64(0), C.c_uint64(0)
+    rc = N.load().mh_txlog_scan(_addr(b) if b.size else None, b.size, max_entries, max_key_len,
+                                cap if max_txs is None else min(cap, max_txs), C.byref(ntx),
+                                C.byref(used), _addr(hd), _addr(ao))
+    if rc < 0:
+        N.check(rc)
+    k = ntx.value
+    return rc, k, used.value, hd[:k], ao[:k]

@@ -399,6 +399,14 @@ int mh_verify_dual_proof_batch(mh_ctx *ctx, const mh_dual_proof_batch *b, uint8_
  * alh (recomputed).  KV / tx metadata are hashed as stored; the reference
  * re-serializes its parsed attributes, which gives the same bytes for every
  * record it writes. */
+/* The record structure alone (host only, no hashing, no device): the same
+ * parse as mh_txlog_validate (readHeader / readEntry limits and errors,
+ * tx.go:419-603) returning the headers (eh zero) and the offset of each
+ * record's stored Alh.  Long runs are parsed by several threads from
+ * speculated record starts; the result is always the sequential parse's. */
+int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entries, uint32_t max_key_len,
+                  uint64_t max_txs, uint64_t *ntx, uint64_t *consumed, mh_tx_header *hdrs,
+                  uint64_t *alh_off);
 int mh_txlog_validate(mh_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                       uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx, uint64_t *consumed,
                       mh_tx_header *hdrs, uint8_t *alh, int32_t *status);

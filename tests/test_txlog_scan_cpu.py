@@ -1,0 +1,83 @@
+"""The tx-log record hop (mh_txlog_scan: the structure-only part of
+mh_txlog_validate, host code, no device) against the oracle's sequential parse
+(orc_txlog_validate, tx.go:419-603): the reference's Go-written tx logs,
+synthetic records with every structural error, and > 8 MiB logs that take the
+multi-threaded hop from speculated record starts."""
+import numpy as np
+import pytest
+
+from tx_util import _bulk_txlog, _synthetic_txlog
+
+
+@pytest.fixture(scope="module")
+def txl():
+    from immustore_amd import txlayer
+    return txlayer
+
+
+def same(txl, orc, buf, **kw):
+    a = txl.txlog_scan(buf, **kw)
+    b = orc.txlog_validate(buf, **kw)
+    assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), kw
+    ao = a[4]
+    if a[1]:
+        # every record ends with its stored Alh: the parse stops right after the last one
+        assert int(ao[-1]) + 32 == a[2]
+        assert np.all(np.diff(ao.astype(np.int64)) > 0)
+    return a
+
+
+def test_scan_fixture_logs(txl, orc, fixtures):
+    for name, fx in fixtures.items():
+        raw = bytes.fromhex(fx["txlog"])
+        a = same(txl, orc, raw)
+        assert a[0] == 0 and a[1] == len(fx["txs"])
+        assert [int(v) for v in a[3]["version"]] == [t["header"]["version"] for t in fx["txs"]]
+
+
+def test_scan_synthetic_errors(txl, orc):
+    rng = np.random.default_rng(5)
+    raw = _synthetic_txlog(rng, 120, orc)
+    same(txl, orc, raw)
+    for kw in ({"max_entries": 5}, {"max_key_len": 10}, {"max_txs": 17}, {"max_txs": 0}):
+        same(txl, orc, raw, **kw)
+    for cut in (0, 1, 7, 8, 50, 89, 90, 91, len(raw) // 3, len(raw) - 33, len(raw) - 1):
+        same(txl, orc, raw[:cut])
+    bad = bytearray(raw)
+    for pos in np.random.default_rng(9).integers(0, len(raw), 60):
+        bad[int(pos)] ^= 0x40
+        same(txl, orc, bytes(bad))
+
+
+def test_scan_parallel_hop_matches_sequential(txl, orc):
+    rng = np.random.default_rng(78)
+    raw, starts = _bulk_txlog(rng, 9000)
+    assert len(raw) > (8 << 20)
+    a = same(txl, orc, raw)
+    assert (a[0], a[1], a[2]) == (0, 9000, len(raw))
+    for k, code in ((1, 17), (4444, 17), (8999, 17)):  # unknown version in chunk 0 / middle / last
+        bad = bytearray(raw)
+        bad[starts[k] + 89] = 9
+        a = same(txl, orc, bytes(bad))
+        assert (a[0], a[1], a[2]) == (code, k, starts[k])
+    bad = bytearray(raw)
+    bad[starts[6000] + 95] = 0xFF  # nentries of a v1 record beyond max_entries (or truncation)
+    same(txl, orc, bytes(bad))
+    same(txl, orc, raw[:len(raw) - 100])
+    same(txl, orc, raw[:starts[5000]] + bytes(3 << 20))
+    for mt in (1, 4321, 8999, 9000, 10 ** 6):
+        same(txl, orc, raw, max_txs=mt)
+    # records that span whole hop chunks: 3 txs of 90 000 entries (~4.6 MB each)
+    import struct
+    recs = bytearray()
+    for k in range(3):
+        ne = 90000
+        recs += struct.pack(">QQQ", k + 1, 5, k) + bytes(64) + struct.pack(">HHI", 1, 0, ne)
+        ent = struct.pack(">HH", 0, 8) + b"k" * 8 + struct.pack(">IQ", 1, 2) + bytes(32)
+        recs += ent * ne + bytes(32)
+    recs = bytes(recs)
+    assert len(recs) > (8 << 20)
+    a = same(txl, orc, recs, max_entries=1 << 20)
+    assert (a[0], a[1]) == (0, 3)
+    same(txl, orc, recs, max_entries=1000)  # MaxTxEntries exceeded in the first record
+    same(txl, orc, recs[:len(recs) // 2], max_entries=1 << 20)

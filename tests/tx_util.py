@@ -1,4 +1,6 @@
 """Helpers shared by the tx-layer tests: fixture headers -> TX_HEADER records."""
+import struct
+
 import numpy as np
 
 TX_HEADER = np.dtype([("id", "<u8"), ("ts", "<i8"), ("bl_tx_id", "<u8"), ("bl_root", "u1", 32),
@@ -28,3 +30,61 @@ def headers_from_fixture(txs):
 
 def inner_hashes(orc, recs, blob):
     return [orc.tx_header_alh(recs[k], blob)[1] for k in range(len(recs))]
+
+
+def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True):
+    """Tx records in the immustore.go:1812-1924 layout with a valid Alh chain
+    (the stored alh of each record is the oracle's Alh over its own fields)."""
+    out = bytearray()
+    prev = orc.sha256(b"")
+    for k in range(ntx):
+        ver = int(rng.integers(0, 2)) if version_mix else 1
+        ne = int(rng.integers(0, max_entries + 1)) if k % 5 else int(rng.integers(1, 3))
+        txmd = b"" if ver == 0 else bytes(rng.integers(0, 256, [0, 0, 3, 268][k % 4], dtype=np.uint8))
+        ents, digs = bytearray(), []
+        for e in range(ne):
+            md = b"" if ver == 0 else [b"", b"\x00", b"\x01" + struct.pack(">Q", e), b"\x02",
+                                       b"\x00\x01" + struct.pack(">Q", k) + b"\x02"][(k + e) % 5]
+            key = bytes(rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8))
+            hv = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+            ents += struct.pack(">H", len(md)) + md + struct.pack(">H", len(key)) + key
+            ents += struct.pack(">IQ", int(rng.integers(0, 1 << 20)), int(rng.integers(0, 1 << 40)))
+            ents += hv
+            digs.append(orc.entry_digest(ver, key, md, hv)[1])
+        eh = orc.htree_build(np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))[1] if ne \
+            else orc.sha256(b"")
+        ts, bl = int(rng.integers(0, 1 << 40)), int(rng.integers(0, k + 1))
+        blroot = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        st, inner = orc.tx_inner_hash(ts, ver, txmd, ne, eh, bl, blroot)
+        assert st == 0
+        alh = orc.tx_alh(k + 1, prev, inner)
+        hdr = struct.pack(">QQQ", k + 1, ts, bl) + blroot + prev + struct.pack(">H", ver)
+        hdr += struct.pack(">H", ne) if ver == 0 else struct.pack(">H", len(txmd)) + txmd + \
+            struct.pack(">I", ne)
+        out += hdr + ents + alh
+        prev = alh
+    return bytes(out)
+
+
+def _bulk_txlog(rng, ntx):
+    """A long run of structurally valid records (ragged entry counts, key and
+    metadata sizes, v0/v1) with unsealed Alh values: > 8 MiB, so the host
+    parse runs on several threads from speculated record starts."""
+    out = bytearray()
+    starts = []
+    for k in range(ntx):
+        starts.append(len(out))
+        ver = 1 if k % 3 else 0
+        ne = int(rng.integers(0, 24))
+        txmd = b"" if ver == 0 else bytes([1, 0, k % 7]) + bytes(k % 7)
+        hdr = struct.pack(">QQQ", k + 1, 1000 + k, k) + bytes(64) + struct.pack(">H", ver)
+        hdr += struct.pack(">H", ne) if ver == 0 else struct.pack(">H", len(txmd)) + txmd + \
+            struct.pack(">I", ne)
+        ents = bytearray()
+        for e in range(ne):
+            md = b"" if ver == 0 else bytes([0]) * ((k + e) % 2)
+            key = bytes([e % 251]) * int(rng.integers(1, 400))
+            ents += struct.pack(">H", len(md)) + md + struct.pack(">H", len(key)) + key
+            ents += struct.pack(">IQ", 10, e) + bytes([k % 256]) * 32
+        out += hdr + ents + bytes([7]) * 32
+    return bytes(out), starts
