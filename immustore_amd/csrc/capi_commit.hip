@@ -121,9 +121,14 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
     const uint64_t m0 = R.md_off ? R.md_off[e0] : 0, mb = R.md_off ? R.md_off[e1] - m0 : 0;
     // trees of this chunk (leaf offsets relative to the chunk)
     std::vector<uint64_t> loff(nt + 1);
+    uint64_t wmax = 0;
     for (uint64_t k = 0; k <= nt; k++) loff[k] = R.tx_off[t0 + k] - e0;
+    for (uint64_t k = 0; k < nt; k++) wmax = std::max(wmax, loff[k + 1] - loff[k]);
+    // small trees (every tx of the chunk <= kSmallTreeMax entries): one lane
+    // per tree on the device, no host tree plan
+    const bool small = wmax <= kSmallTreeMax;
     TreePlan P;
-    P.build(nt, loff.data());
+    if (!small) P.build(nt, loff.data());
     Layout L;
     const uint64_t b_k = L.add(kb), b_m = L.add(mb), b_v = L.add(vb);
     const uint64_t b_ko = L.add((n + 1) * 8), b_mo = L.add(R.md_off ? (n + 1) * 8 : 0),
@@ -132,9 +137,11 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
     const uint64_t b_hv = L.add(n * 32), b_go = L.add((n + 1) * 8),
                    b_msg = L.add(n * (R.version == 1 ? 36 : 32) + kb + (R.version == 1 ? mb : 0) +
                                  64),
-                   b_dig = L.add(std::max<uint64_t>(n, 1) * 32), b_eh = L.add(nt * 32);
+                   b_dig = L.add(std::max<uint64_t>(n, 1) * 32), b_eh = L.add(nt * 32),
+                   b_lv = L.add(small ? std::max<uint64_t>(n, 1) * 32 : 0),
+                   b_lo = L.add(small ? (nt + 1) * 8 : 0);
     MH_HIP(s.arena.ensure(L.total));
-    const uint64_t idx_bytes = (plan_index_bytes(P, nt) + 255) & ~255ull;
+    const uint64_t idx_bytes = ((small ? (nt + 1) * 8 : plan_index_bytes(P, nt)) + 255) & ~255ull;
     MH_HIP(s.pin.ensure(idx_bytes + n * 32 + nt * 32));
     s.res_off = idx_bytes;
     uint8_t *base = s.arena.as<uint8_t>();
@@ -174,9 +181,16 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
         MH_HIP(launch_sha256_csr(st, tm, base + b_msg, go, n, nullptr, nullptr, base + b_dig));
     }
     // ---- one htree per tx (tx.go:347 -> htree.go:68-113), Eh = root
-    if (int e = run_tree_plan_on(s.tree, st, tm, P, nt, n, base + b_dig, base + b_eh,
-                                 reinterpret_cast<uint8_t *>(s.pin.p)))
+    if (small) {
+        memcpy(s.pin.p, loff.data(), (nt + 1) * 8);
+        MH_HIP(hipMemcpyAsync(base + b_lo, s.pin.p, (nt + 1) * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_leaf_for(st, tm, n, base + b_dig, base + b_lv));  // htree.go:79-83
+        MH_HIP(launch_small_roots(st, tm, nt, (const uint64_t *)(base + b_lo), base + b_lv,
+                                  base + b_eh));
+    } else if (int e = run_tree_plan_on(s.tree, st, tm, P, nt, n, base + b_dig, base + b_eh,
+                                        reinterpret_cast<uint8_t *>(s.pin.p))) {
         return e;
+    }
     // ---- device -> the caller's pinned outputs, or pinned staging
     uint8_t *res = reinterpret_cast<uint8_t *>(s.pin.p) + s.res_off;
     uint8_t *hv_dst = R.hv_pinned ? R.hvals_out + (e0 - R.tx_off[0]) * 32 : res;

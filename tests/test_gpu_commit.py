@@ -65,6 +65,23 @@ def test_precommit_random_vs_oracle(m, ctx, orc, version, chunk):
         p.close()
 
 
+@pytest.mark.parametrize("max_entries", [64, 65, 300])
+def test_precommit_tree_paths_vs_oracle(m, ctx, orc, max_entries):
+    """Chunks whose widest tx has <= 64 entries get one-lane-per-tree roots,
+    wider ones the host tree plan (both within one batch when chunks differ)."""
+    rng = np.random.default_rng(max_entries)
+    b = random_batch(rng, 60, version=1, max_entries=max_entries, vlens=(0, 33, 100))
+    hv_o, eh_o, st_o = orc.precommit_batch(1, **b)
+    for chunk in (1 << 12, 0):
+        p = m.CommitPipe(ctx, chunk_bytes=chunk)
+        try:
+            hv, eh, st = p.precommit_csr(1, **b)
+        finally:
+            p.close()
+        assert np.array_equal(st, st_o) and np.array_equal(eh, eh_o)
+        assert np.array_equal(hv, hv_o)
+
+
 def test_precommit_statuses_vs_oracle(m, ctx, orc):
     rng = np.random.default_rng(5)
     b = random_batch(rng, 120, version=1, md_prob=0.3)
