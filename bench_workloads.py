@@ -6,7 +6,9 @@
                     (leaves + perfect nodes + spine chains = the full dLog).
   --workload c5     configs[4]: htree.VerifyInclusion re-hash of 10^6 proofs of
                     depth 24 over a 2^24-leaf tree, 10 % tampered, bit-exact
-                    result bitmap checked against the expected count.
+                    result bitmap checked against the expected count; plus the
+                    ahtree set: 10^6 inclusion + 10^6 consistency proofs over a
+                    2^24-append tree (j = 2^24, random i), 10 % tampered.
   --workload c2e2e  configs[1] end to end: entries copied host->device from
                     pinned memory, build, levels + root copied back (PCIe
                     inclusive rate, for DESIGN.md; never the headline value).
@@ -190,7 +192,88 @@ def make_parser():
     p.add_argument("--m", type=int, default=10 ** 7, help="c3 appends")
     p.add_argument("--proofs", type=int, default=10 ** 6, help="c5 proofs")
     p.add_argument("--depth", type=int, default=24, help="c5 tree depth")
+    p.add_argument("--no-ahtree", action="store_true", help="c5: htree proofs only")
     return p
+
+
+def np_nodes_until(n):
+    """nodesUntil(n) = nodesUpto(n-1) (ahtree.go:485-511) for a uint64 array:
+    n - 1 + sum_{x < n-1} popcount(x), summed bit by bit."""
+    import numpy as np
+    x = np.asarray(n, np.uint64) - np.uint64(1)
+    s = x.copy()
+    for k in range(63):
+        hi = (x >> np.uint64(k + 1)) << np.uint64(k)
+        lo = x & np.uint64((1 << (k + 1)) - 1)
+        s += hi + np.where(lo > np.uint64(1 << k), lo - np.uint64(1 << k), np.uint64(0))
+    return s
+
+
+def c5_ahtree(a, m, N, L, ctx, dev, sync):
+    """configs[4]'s ahtree half: 10^6 inclusion and 10^6 consistency proofs
+    against a 2^24-append tree (j = 2^24, random i), generated on the device
+    from the resident dLog, 10 % tampered (one bit of the first term), then
+    re-hashed by ahtree.VerifyInclusion / VerifyConsistency
+    (ahtree/verification.go:21-109); the bitmaps must be exact."""
+    import numpy as np
+    import torch
+    P, W = a.proofs, 1 << a.depth
+    rng = np.random.default_rng(55)
+    pay = torch.empty(W * 32, dtype=torch.uint8, device=dev)
+    N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 55))
+    dlog = torch.empty(m.nodes_upto(W) * 32, dtype=torch.uint8, device=dev)
+    N.check(L.mh_dev_ahtree_append_batch(ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(), W, 32,
+                                         None))
+    dl = dlog.view(-1, 32)
+    res = {}
+    for kind, name, S in ((0, "inclusion", 64), (1, "consistency", 128)):
+        iv = rng.integers(1, W + 1, P).astype(np.uint64)
+        jv = np.full(P, W, np.uint64)
+        it = torch.from_numpy(iv.view(np.int64)).to(dev)
+        jt = torch.from_numpy(jv.view(np.int64)).to(dev)
+        terms = torch.empty(P * S * 32, dtype=torch.uint8, device=dev)
+        nt = torch.empty(P, dtype=torch.int32, device=dev)
+        st = torch.empty(P, dtype=torch.int32, device=dev)
+        N.check(L.mh_dev_ahtree_proof_batch(ctx.handle, kind, dlog.data_ptr(), W, P, it.data_ptr(),
+                                            jt.data_ptr(), terms.data_ptr(), S, nt.data_ptr(),
+                                            st.data_ptr()))
+        sync()
+        assert int(st.abs().sum().item()) == 0
+        # compact the fixed-stride proofs into the CSR layout of the verifier
+        cnt = nt.to(torch.int64)
+        off = torch.zeros(P + 1, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(cnt, 0)
+        rows = torch.repeat_interleave(torch.arange(P, device=dev), cnt)
+        pos = torch.arange(int(off[P].item()), device=dev) - off[:-1][rows]
+        flat = terms.view(P, S, 32)[rows, pos].contiguous()
+        tamper = (rng.random(P) < 0.10) & (cnt.cpu().numpy() > 0)
+        tp = torch.from_numpy(np.nonzero(tamper)[0]).to(dev)
+        flat[off[:-1][tp], 0] ^= 1
+        # a / b: VerifyInclusion(leaf(i), root(j)), VerifyConsistency(root(i), root(j))
+        pc = lambda v: np.array([bin(int(x - 1)).count("1") for x in v], np.uint64)  # noqa: E731
+        root_idx = lambda v: np.asarray(np_nodes_until(v)) + pc(v)  # noqa: E731
+        ai = np_nodes_until(iv) if kind == 0 else root_idx(iv)
+        bi = root_idx(jv[:1]).repeat(P)
+        av = dl[torch.from_numpy(ai.view(np.int64)).to(dev)].contiguous()
+        bv = dl[torch.from_numpy(bi.view(np.int64)).to(dev)].contiguous()
+        ok = torch.zeros(P, dtype=torch.uint8, device=dev)
+
+        def step():
+            N.check(L.mh_dev_ahtree_verify_batch(ctx.handle, kind, P, it.data_ptr(), jt.data_ptr(),
+                                                 off.data_ptr(), flat.data_ptr(), av.data_ptr(),
+                                                 bv.data_ptr(), ok.data_ptr(), None))
+
+        ctx.timing_reset()
+        ctx.set_timing(True)
+        t = timed(step, a.steps, a.warmup, sync)
+        ctx.set_timing(False)
+        kms = ctx.timing("ahtree_verify")[0] / (a.steps + a.warmup)
+        okh = ok.cpu().numpy().astype(bool)
+        res[name] = {"M_proofs_per_s": round(P / t / 1e6, 1), "ms_per_step": round(t * 1e3, 3),
+                     "kernel_ms": round(kms, 3), "mean_terms": round(float(cnt.float().mean()), 2),
+                     "bitmap_exact": bool((okh == ~tamper).all()),
+                     "tampered": int(tamper.sum())}
+    return res
 
 
 def run_single(a):
@@ -340,6 +423,8 @@ def run_single(a):
                                     "terms_GBps": round(P * D * 32 / (gen_ms * 1e-3) / 1e9, 1)},
                "verified": nok, "expected_verified": exp, "bitmap_exact": nok == exp and bool(
                    (ok.cpu().numpy().astype(bool) == ~tamper).all())}
+        if not a.no_ahtree:
+            out["ahtree"] = c5_ahtree(a, m, N, L, ctx, dev, sync)
 
     elif a.workload == "txlog":
         import struct
