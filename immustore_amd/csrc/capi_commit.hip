@@ -210,39 +210,43 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
 }  // namespace
 
 extern "C" int mh_commit_pipe_new(mh_ctx *c, uint64_t chunk_bytes, mh_commit_pipe **out) {
-    if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
-    *out = nullptr;
-    MH_HIP(hipSetDevice(c->device));
-    mh_commit_pipe *p = new mh_commit_pipe();
-    p->ctx = c;
-    p->chunk_bytes = chunk_bytes ? chunk_bytes : (64ull << 20);
-    hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->comp, hipStreamNonBlocking);
-    for (auto &s : p->slot) {
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.in, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-    }
-    if (e != hipSuccess) {
-        mh_commit_pipe_free(p);
-        return -(int)e;
-    }
-    *out = p;
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
+        *out = nullptr;
+        MH_HIP(hipSetDevice(c->device));
+        mh_commit_pipe *p = new mh_commit_pipe();
+        p->ctx = c;
+        p->chunk_bytes = chunk_bytes ? chunk_bytes : (64ull << 20);
+        hipError_t e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->comp, hipStreamNonBlocking);
+        for (auto &s : p->slot) {
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.in, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        }
+        if (e != hipSuccess) {
+            mh_commit_pipe_free(p);
+            return -(int)e;
+        }
+        *out = p;
+        return MH_OK;
+    });
 }
 
 extern "C" int mh_commit_pipe_free(mh_commit_pipe *p) {
-    if (!p) return MH_OK;
-    hipSetDevice(p->ctx->device);
-    if (p->copy) hipStreamSynchronize(p->copy);
-    if (p->comp) hipStreamSynchronize(p->comp);
-    for (auto &s : p->slot) {
-        if (s.in) hipEventDestroy(s.in);
-        if (s.done) hipEventDestroy(s.done);
-    }
-    if (p->copy) hipStreamDestroy(p->copy);
-    if (p->comp) hipStreamDestroy(p->comp);
-    delete p;
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!p) return MH_OK;
+        hipSetDevice(p->ctx->device);
+        if (p->copy) hipStreamSynchronize(p->copy);
+        if (p->comp) hipStreamSynchronize(p->comp);
+        for (auto &s : p->slot) {
+            if (s.in) hipEventDestroy(s.in);
+            if (s.done) hipEventDestroy(s.done);
+        }
+        if (p->copy) hipStreamDestroy(p->copy);
+        if (p->comp) hipStreamDestroy(p->comp);
+        delete p;
+        return MH_OK;
+    });
 }
 
 extern "C" int mh_precommit_batch(mh_commit_pipe *p, int version, uint64_t max_width,
@@ -252,67 +256,69 @@ extern "C" int mh_precommit_batch(mh_commit_pipe *p, int version, uint64_t max_w
                                   const uint64_t *val_off, const uint8_t *hval_override,
                                   const uint8_t *use_override, const uint8_t *expect_eh,
                                   uint8_t *hvals_out, uint8_t *eh_out, int32_t *status) {
-    if (!p || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (ntx == 0) return MH_OK;
-    if (!tx_off || !key_off || !val_off || !status) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if ((md == nullptr) != (md_off == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    for (uint64_t t = 0; t < ntx; t++)
-        if (tx_off[t + 1] < tx_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
-    // per-tx errors decided on the host (the Go call would return them):
-    // htree.ErrMaxWidthExceeded (htree.go:69-71), ErrMetadataUnsupported for
-    // KV metadata under a v0 header (tx.go:691-693)
-    for (uint64_t t = 0; t < ntx; t++) {
-        int32_t st = MH_OK;
-        if (max_width && tx_off[t + 1] - tx_off[t] > max_width) st = MH_ERR_MAX_WIDTH_EXCEEDED;
-        if (st == MH_OK && version == 0 && md_off && md_off[tx_off[t + 1]] > md_off[tx_off[t]])
-            st = MH_ERR_METADATA_UNSUPPORTED;
-        status[t] = st;
-    }
-    MH_HIP(hipSetDevice(p->ctx->device));
-    Req R{version, max_width, tx_off, keys, key_off, md, md_off, vals, val_off, hval_override,
-          use_override, expect_eh, hvals_out, eh_out, status, is_pinned(hvals_out),
-          is_pinned(eh_out)};
-    // chunks of whole transactions, ~chunk_bytes of keys + values (and at
-    // most 2^22 entries) each, round robin over the slots; each chunk's
-    // offsets are checked just before it is enqueued, under the GPU work of
-    // the chunks before it
-    constexpr uint64_t kMaxChunkEntries = 1ull << 22;
-    uint64_t t = 0;
-    int k = 0, rc = MH_OK;
-    while (t < ntx) {
-        uint64_t t1 = t + 1;
-        while (t1 < ntx) {
-            const uint64_t e0 = tx_off[t], e1 = tx_off[t1 + 1];
-            if (val_off[e1] - val_off[e0] + (key_off[e1] - key_off[e0]) > p->chunk_bytes) break;
-            if (e1 - e0 > kMaxChunkEntries) break;
-            t1++;
+    return mh_guard([&]() -> int {
+        if (!p || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (ntx == 0) return MH_OK;
+        if (!tx_off || !key_off || !val_off || !status) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((md == nullptr) != (md_off == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        for (uint64_t t = 0; t < ntx; t++)
+            if (tx_off[t + 1] < tx_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // per-tx errors decided on the host (the Go call would return them):
+        // htree.ErrMaxWidthExceeded (htree.go:69-71), ErrMetadataUnsupported for
+        // KV metadata under a v0 header (tx.go:691-693)
+        for (uint64_t t = 0; t < ntx; t++) {
+            int32_t st = MH_OK;
+            if (max_width && tx_off[t + 1] - tx_off[t] > max_width) st = MH_ERR_MAX_WIDTH_EXCEEDED;
+            if (st == MH_OK && version == 0 && md_off && md_off[tx_off[t + 1]] > md_off[tx_off[t]])
+                st = MH_ERR_METADATA_UNSUPPORTED;
+            status[t] = st;
         }
-        bool ok = true;
-        for (uint64_t e = tx_off[t]; e < tx_off[t1] && ok; e++) {
-            ok = key_off[e + 1] >= key_off[e] && val_off[e + 1] >= val_off[e] &&
-                 (!md_off || md_off[e + 1] >= md_off[e]);
+        MH_HIP(hipSetDevice(p->ctx->device));
+        Req R{version, max_width, tx_off, keys, key_off, md, md_off, vals, val_off, hval_override,
+              use_override, expect_eh, hvals_out, eh_out, status, is_pinned(hvals_out),
+              is_pinned(eh_out)};
+        // chunks of whole transactions, ~chunk_bytes of keys + values (and at
+        // most 2^22 entries) each, round robin over the slots; each chunk's
+        // offsets are checked just before it is enqueued, under the GPU work of
+        // the chunks before it
+        constexpr uint64_t kMaxChunkEntries = 1ull << 22;
+        uint64_t t = 0;
+        int k = 0, rc = MH_OK;
+        while (t < ntx) {
+            uint64_t t1 = t + 1;
+            while (t1 < ntx) {
+                const uint64_t e0 = tx_off[t], e1 = tx_off[t1 + 1];
+                if (val_off[e1] - val_off[e0] + (key_off[e1] - key_off[e0]) > p->chunk_bytes) break;
+                if (e1 - e0 > kMaxChunkEntries) break;
+                t1++;
+            }
+            bool ok = true;
+            for (uint64_t e = tx_off[t]; e < tx_off[t1] && ok; e++) {
+                ok = key_off[e + 1] >= key_off[e] && val_off[e + 1] >= val_off[e] &&
+                     (!md_off || md_off[e + 1] >= md_off[e]);
+            }
+            if (ok && tx_off[t1] > tx_off[t]) {
+                const uint64_t e0 = tx_off[t], e1 = tx_off[t1];
+                ok = !((key_off[e1] > key_off[e0] && !keys) || (val_off[e1] > val_off[e0] && !vals) ||
+                       (md_off && md_off[e1] > md_off[e0] && !md));
+            }
+            if (!ok) {
+                rc = MH_ERR_ILLEGAL_ARGUMENTS;
+                break;
+            }
+            mh_commit_pipe::Slot &s = p->slot[k % kSlots];
+            if ((rc = drain(s, R))) break;
+            if ((rc = enqueue(p, s, R, t, t1))) break;
+            t = t1;
+            k++;
         }
-        if (ok && tx_off[t1] > tx_off[t]) {
-            const uint64_t e0 = tx_off[t], e1 = tx_off[t1];
-            ok = !((key_off[e1] > key_off[e0] && !keys) || (val_off[e1] > val_off[e0] && !vals) ||
-                   (md_off && md_off[e1] > md_off[e0] && !md));
+        // drain every slot in chunk order (also after an error: nothing is left
+        // in flight)
+        for (int j = 0; j < kSlots; j++) {
+            int e = drain(p->slot[(k + j) % kSlots], R);
+            if (!rc) rc = e;
         }
-        if (!ok) {
-            rc = MH_ERR_ILLEGAL_ARGUMENTS;
-            break;
-        }
-        mh_commit_pipe::Slot &s = p->slot[k % kSlots];
-        if ((rc = drain(s, R))) break;
-        if ((rc = enqueue(p, s, R, t, t1))) break;
-        t = t1;
-        k++;
-    }
-    // drain every slot in chunk order (also after an error: nothing is left
-    // in flight)
-    for (int j = 0; j < kSlots; j++) {
-        int e = drain(p->slot[(k + j) % kSlots], R);
-        if (!rc) rc = e;
-    }
-    return rc;
+        return rc;
+    });
 }

@@ -4,12 +4,27 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
 #include "mh_internal.hpp"
 
 using namespace mh;
+
+// Every extern "C" int entry point runs its body through mh_guard: a C++
+// exception (std::bad_alloc from a host vector, std::system_error from a
+// thread) becomes a status instead of crossing the C ABI.
+template <class F>
+inline int mh_guard(F &&f) noexcept {
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return MH_ERR_OUT_OF_MEMORY;
+    } catch (...) {
+        return MH_ERR_ILLEGAL_STATE;
+    }
+}
 
 #define MH_HIP(expr)                                        \
     do {                                                    \

@@ -76,75 +76,81 @@ int run_tree_plan_on(DevBuf &scratch, hipStream_t st, Timer *tm, const TreePlan 
 extern "C" int mh_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
                                const uint8_t *md_blob, uint64_t md_blob_len, uint8_t *inner_out,
                                uint8_t *alh_out) {
-    if (!c || (n && (!hdrs || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (!n) return MH_OK;
-    for (uint64_t k = 0; k < n; k++)
-        if (int e = check_header(hdrs[k], md_blob_len, md_blob != nullptr)) return e;
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    Layout L;
-    const uint64_t b_h = L.add(n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
-                   b_s = L.add(n * kTxInnerStride), b_in = L.add(n * 32), b_a = L.add(n * 32);
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    MH_HIP(hipMemcpyAsync(base + b_h, hdrs, n * sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
-    if (md_blob && md_blob_len)
-        MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
-    MH_HIP(launch_tx_alh(st, c->tm(), n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
-                         base + b_s, nullptr, nullptr, base + b_in, base + b_a, nullptr));
-    if (inner_out) MH_HIP(hipMemcpyAsync(inner_out, base + b_in, n * 32, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipMemcpyAsync(alh_out, base + b_a, n * 32, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!hdrs || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!n) return MH_OK;
+        for (uint64_t k = 0; k < n; k++)
+            if (int e = check_header(hdrs[k], md_blob_len, md_blob != nullptr)) return e;
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        Layout L;
+        const uint64_t b_h = L.add(n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
+                       b_s = L.add(n * kTxInnerStride), b_in = L.add(n * 32), b_a = L.add(n * 32);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        MH_HIP(hipMemcpyAsync(base + b_h, hdrs, n * sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
+        if (md_blob && md_blob_len)
+            MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_tx_alh(st, c->tm(), n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
+                             base + b_s, nullptr, nullptr, base + b_in, base + b_a, nullptr));
+        if (inner_out) MH_HIP(hipMemcpyAsync(inner_out, base + b_in, n * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(alh_out, base + b_a, n * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
 }
 
 extern "C" int mh_dev_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
                                    const uint8_t *md_blob, const uint8_t *eh, uint8_t *scratch,
                                    uint8_t *inner_out, uint8_t *alh_out) {
-    if (!c || (n && (!hdrs || !scratch || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (!n) return MH_OK;
-    hipSetDevice(c->device);
-    MH_HIP(launch_tx_alh(c->stream, c->tm(), n, hdrs, md_blob, eh, scratch, nullptr, nullptr,
-                         inner_out, alh_out, nullptr));
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!hdrs || !scratch || !alh_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!n) return MH_OK;
+        hipSetDevice(c->device);
+        MH_HIP(launch_tx_alh(c->stream, c->tm(), n, hdrs, md_blob, eh, scratch, nullptr, nullptr,
+                             inner_out, alh_out, nullptr));
+        return MH_OK;
+    });
 }
 
 // ------------------------------------------------------------------ a3 x many
 extern "C" int mh_htree_build_many(mh_ctx *c, uint64_t ntrees, const uint64_t *leaf_off,
                                    const uint8_t *digests, uint8_t *roots) {
-    if (!c || (ntrees && (!leaf_off || !roots))) return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (!ntrees) return MH_OK;
-    for (uint64_t t = 0; t < ntrees; t++)
-        if (leaf_off[t + 1] < leaf_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
-    const uint64_t E = leaf_off[ntrees] - leaf_off[0];
-    if (E && !digests) return MH_ERR_ILLEGAL_ARGUMENTS;
-    uint64_t wmax = 0;
-    for (uint64_t t = 0; t < ntrees; t++) wmax = std::max(wmax, leaf_off[t + 1] - leaf_off[t]);
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    Layout L;
-    const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
-                   b_lo = L.add((ntrees + 1) * 8), b_r = L.add(ntrees * 32);
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    if (E)
-        MH_HIP(hipMemcpyAsync(base + b_d, digests + leaf_off[0] * 32, E * 32,
-                              hipMemcpyHostToDevice, st));
-    if (wmax <= kSmallTreeMax) {  // one lane per tree, no host plan
-        MH_HIP(hipMemcpyAsync(base + b_lo, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
-        MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_d, base + b_lv));  // htree.go:79-83
-        MH_HIP(launch_small_roots(st, c->tm(), ntrees, (const uint64_t *)(base + b_lo),
-                                  base + b_lv, base + b_r));
-    } else {
-        TreePlan P;
-        P.build(ntrees, leaf_off);
-        if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
-    }
-    MH_HIP(hipMemcpyAsync(roots, base + b_r, ntrees * 32, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!c || (ntrees && (!leaf_off || !roots))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!ntrees) return MH_OK;
+        for (uint64_t t = 0; t < ntrees; t++)
+            if (leaf_off[t + 1] < leaf_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t E = leaf_off[ntrees] - leaf_off[0];
+        if (E && !digests) return MH_ERR_ILLEGAL_ARGUMENTS;
+        uint64_t wmax = 0;
+        for (uint64_t t = 0; t < ntrees; t++) wmax = std::max(wmax, leaf_off[t + 1] - leaf_off[t]);
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        Layout L;
+        const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
+                       b_lo = L.add((ntrees + 1) * 8), b_r = L.add(ntrees * 32);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        if (E)
+            MH_HIP(hipMemcpyAsync(base + b_d, digests + leaf_off[0] * 32, E * 32,
+                                  hipMemcpyHostToDevice, st));
+        if (wmax <= kSmallTreeMax) {  // one lane per tree, no host plan
+            MH_HIP(hipMemcpyAsync(base + b_lo, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
+            MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_d, base + b_lv));  // htree.go:79-83
+            MH_HIP(launch_small_roots(st, c->tm(), ntrees, (const uint64_t *)(base + b_lo),
+                                      base + b_lv, base + b_r));
+        } else {
+            TreePlan P;
+            P.build(ntrees, leaf_off);
+            if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
+        }
+        MH_HIP(hipMemcpyAsync(roots, base + b_r, ntrees * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
 }
 
 // ------------------------------------------------------------------ a13
@@ -153,40 +159,42 @@ extern "C" int mh_verify_linear_proof_batch(mh_ctx *c, uint64_t n, const uint64_
                                             const uint8_t *terms, const uint64_t *src,
                                             const uint64_t *tgt, const uint8_t *src_alh,
                                             const uint8_t *tgt_alh, uint8_t *ok) {
-    if (!c || (n && (!proof_src || !proof_tgt || !term_off || !src || !tgt || !src_alh ||
-                     !tgt_alh || !ok)))
-        return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (!n) return MH_OK;
-    const uint64_t nterms = term_off[n] - term_off[0];
-    if (nterms && !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    std::vector<uint64_t> to(n + 1);
-    for (uint64_t p = 0; p <= n; p++) to[p] = term_off[p] - term_off[0];
-    Layout L;
-    const uint64_t b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_s = L.add(n * 8),
-                   b_t = L.add(n * 8), b_off = L.add((n + 1) * 8), b_terms = L.add(nterms * 32),
-                   b_sa = L.add(n * 32), b_ta = L.add(n * 32), b_ok = L.add(n);
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    MH_HIP(hipMemcpyAsync(base + b_ps, proof_src, n * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_pt, proof_tgt, n * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_s, src, n * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_t, tgt, n * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_off, to.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    if (nterms)
-        MH_HIP(hipMemcpyAsync(base + b_terms, terms + term_off[0] * 32, nterms * 32,
-                              hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_sa, src_alh, n * 32, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_ta, tgt_alh, n * 32, hipMemcpyHostToDevice, st));
-    MH_HIP(launch_linear_verify(st, c->tm(), n, (const uint64_t *)(base + b_ps),
-                                (const uint64_t *)(base + b_pt), (const uint64_t *)(base + b_s),
-                                (const uint64_t *)(base + b_t), (const uint64_t *)(base + b_off),
-                                base + b_terms, base + b_sa, base + b_ta, base + b_ok));
-    MH_HIP(hipMemcpyAsync(ok, base + b_ok, n, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    return MH_OK;
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!proof_src || !proof_tgt || !term_off || !src || !tgt || !src_alh ||
+                         !tgt_alh || !ok)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!n) return MH_OK;
+        const uint64_t nterms = term_off[n] - term_off[0];
+        if (nterms && !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        std::vector<uint64_t> to(n + 1);
+        for (uint64_t p = 0; p <= n; p++) to[p] = term_off[p] - term_off[0];
+        Layout L;
+        const uint64_t b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_s = L.add(n * 8),
+                       b_t = L.add(n * 8), b_off = L.add((n + 1) * 8), b_terms = L.add(nterms * 32),
+                       b_sa = L.add(n * 32), b_ta = L.add(n * 32), b_ok = L.add(n);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        MH_HIP(hipMemcpyAsync(base + b_ps, proof_src, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_pt, proof_tgt, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_s, src, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_t, tgt, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_off, to.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+        if (nterms)
+            MH_HIP(hipMemcpyAsync(base + b_terms, terms + term_off[0] * 32, nterms * 32,
+                                  hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_sa, src_alh, n * 32, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_ta, tgt_alh, n * 32, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_linear_verify(st, c->tm(), n, (const uint64_t *)(base + b_ps),
+                                    (const uint64_t *)(base + b_pt), (const uint64_t *)(base + b_s),
+                                    (const uint64_t *)(base + b_t), (const uint64_t *)(base + b_off),
+                                    base + b_terms, base + b_sa, base + b_ta, base + b_ok));
+        MH_HIP(hipMemcpyAsync(ok, base + b_ok, n, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
 }
 
 extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_header *sh,
@@ -196,335 +204,339 @@ extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_
                                              const uint8_t *cons_terms, const uint64_t *src,
                                              const uint64_t *tgt, const uint8_t *src_alh,
                                              const uint8_t *tgt_alh, int32_t *status) {
-    if (!c || (n && (!sh || !th || !incl_off || !cons_off || !src || !tgt || !src_alh ||
-                     !tgt_alh || !status)))
-        return MH_ERR_ILLEGAL_ARGUMENTS;
-    if (!n) return MH_OK;
-    const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
-    if ((ni && !incl_terms) || (nc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    // verification.go:305-316: argument checks on the host, headers that
-    // cannot be hashed (unknown version, bad md) fail as ErrIllegalArguments
-    std::vector<mh_tx_header> hh(2 * n);
-    std::vector<uint8_t> expect(2 * n * 32);
-    for (uint64_t p = 0; p < n; p++) {
-        int32_t s = MH_OK;
-        if (sh[p].id == 0 || sh[p].id != src[p] || th[p].id != tgt[p])
-            s = MH_ERR_ILLEGAL_ARGUMENTS;
-        else if (src[p] > tgt[p])
-            s = MH_ERR_SOURCE_TX_NEWER;
-        else if (check_header(sh[p], md_blob_len, md_blob != nullptr) ||
-                 check_header(th[p], md_blob_len, md_blob != nullptr))
-            s = MH_ERR_ILLEGAL_ARGUMENTS;
-        status[p] = s;
-        hh[p] = sh[p];
-        hh[n + p] = th[p];
-        if (s != MH_OK) {  // keep the kernel's reads inside md_blob; result unused
-            hh[p].version = hh[n + p].version = 1;
-            hh[p].md_len = hh[n + p].md_len = 0;
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!sh || !th || !incl_off || !cons_off || !src || !tgt || !src_alh ||
+                         !tgt_alh || !status)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!n) return MH_OK;
+        const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
+        if ((ni && !incl_terms) || (nc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // verification.go:305-316: argument checks on the host, headers that
+        // cannot be hashed (unknown version, bad md) fail as ErrIllegalArguments
+        std::vector<mh_tx_header> hh(2 * n);
+        std::vector<uint8_t> expect(2 * n * 32);
+        for (uint64_t p = 0; p < n; p++) {
+            int32_t s = MH_OK;
+            if (sh[p].id == 0 || sh[p].id != src[p] || th[p].id != tgt[p])
+                s = MH_ERR_ILLEGAL_ARGUMENTS;
+            else if (src[p] > tgt[p])
+                s = MH_ERR_SOURCE_TX_NEWER;
+            else if (check_header(sh[p], md_blob_len, md_blob != nullptr) ||
+                     check_header(th[p], md_blob_len, md_blob != nullptr))
+                s = MH_ERR_ILLEGAL_ARGUMENTS;
+            status[p] = s;
+            hh[p] = sh[p];
+            hh[n + p] = th[p];
+            if (s != MH_OK) {  // keep the kernel's reads inside md_blob; result unused
+                hh[p].version = hh[n + p].version = 1;
+                hh[p].md_len = hh[n + p].md_len = 0;
+            }
+            memcpy(&expect[p * 32], src_alh + p * 32, 32);
+            memcpy(&expect[(n + p) * 32], tgt_alh + p * 32, 32);
         }
-        memcpy(&expect[p * 32], src_alh + p * 32, 32);
-        memcpy(&expect[(n + p) * 32], tgt_alh + p * 32, 32);
-    }
-    std::vector<uint64_t> io(n + 1), co(n + 1), ii(n), ij(n), ci(n);
-    std::vector<uint8_t> sel(n), sbl(n * 32), tbl(n * 32);
-    for (uint64_t p = 0; p <= n; p++) {
-        io[p] = incl_off[p] - incl_off[0];
-        co[p] = cons_off[p] - cons_off[0];
-    }
-    for (uint64_t p = 0; p < n; p++) {
-        ii[p] = src[p];                                    // verification.go:342-348
-        ij[p] = th[p].bl_tx_id;
-        sel[p] = src[p] == 1;                              // :354-370
-        ci[p] = src[p] == 1 ? src[p] : sh[p].bl_tx_id;
-        memcpy(&sbl[p * 32], sh[p].bl_root, 32);
-        memcpy(&tbl[p * 32], th[p].bl_root, 32);
-    }
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    Layout L;
-    const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
-                   b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
-                   b_st = L.add(2 * n * 4), b_leaf = L.add(n * 32), b_sbl = L.add(n * 32),
-                   b_tbl = L.add(n * 32), b_ca = L.add(n * 32), b_sel = L.add(n),
-                   b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
-                   b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8), b_it = L.add(ni * 32),
-                   b_ct = L.add(nc * 32), b_oki = L.add(n), b_okc = L.add(n);
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
-                     : hipSuccess;
-    };
-    MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
-    if (md_blob) MH_HIP(h2d(b_md, md_blob, md_blob_len));
-    MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
-    MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
-    MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
-    MH_HIP(h2d(b_sel, sel.data(), n));
-    MH_HIP(h2d(b_ii, ii.data(), n * 8));
-    MH_HIP(h2d(b_ij, ij.data(), n * 8));
-    MH_HIP(h2d(b_ci, ci.data(), n * 8));
-    MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
-    MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
-    if (ni) MH_HIP(h2d(b_it, incl_terms + incl_off[0] * 32, ni * 32));
-    if (nc) MH_HIP(h2d(b_ct, cons_terms + cons_off[0] * 32, nc * 32));
-    // Alh of both headers vs the given ones (verification.go:318-326)
-    MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, (const MhTxHeader *)(base + b_h), base + b_md,
-                         nullptr, base + b_s, base + b_x, nullptr, nullptr, nullptr,
-                         (int32_t *)(base + b_st)));
-    // leafFor(sourceAlh) (verification.go:346), then the two ahtree proofs
-    MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
-    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
-                                (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
-                                base + b_it, base + b_leaf, base + b_tbl, base + b_oki, nullptr));
-    MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
-    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
-                                (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
-                                (const uint64_t *)(base + b_co), base + b_ct, base + b_ca,
-                                base + b_tbl, base + b_okc, nullptr));
-    std::vector<int32_t> ast(2 * n);
-    std::vector<uint8_t> oki(n), okc(n);
-    MH_HIP(hipMemcpyAsync(ast.data(), base + b_st, 2 * n * 4, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipMemcpyAsync(oki.data(), base + b_oki, n, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipMemcpyAsync(okc.data(), base + b_okc, n, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    for (uint64_t p = 0; p < n; p++) {
-        if (status[p] != MH_OK) continue;
-        if (ast[p] != MH_OK || ast[n + p] != MH_OK) {
-            status[p] = MH_ERR_ILLEGAL_ARGUMENTS;
-        } else if (sh[p].id - 1 != sh[p].bl_tx_id || th[p].id - 1 != th[p].bl_tx_id) {
-            status[p] = MH_ERR_UNEXPECTED_LINKING;  // :328-330
-        } else if (src[p] == tgt[p]) {
-            status[p] = MH_OK;  // :332-334
-        } else if (!oki[p]) {
-            status[p] = MH_ERR_INCLUSION_NOT_VALID;
-        } else if (!okc[p]) {
-            status[p] = MH_ERR_CONSISTENCY_NOT_VALID;
+        std::vector<uint64_t> io(n + 1), co(n + 1), ii(n), ij(n), ci(n);
+        std::vector<uint8_t> sel(n), sbl(n * 32), tbl(n * 32);
+        for (uint64_t p = 0; p <= n; p++) {
+            io[p] = incl_off[p] - incl_off[0];
+            co[p] = cons_off[p] - cons_off[0];
         }
-    }
-    return MH_OK;
+        for (uint64_t p = 0; p < n; p++) {
+            ii[p] = src[p];                                    // verification.go:342-348
+            ij[p] = th[p].bl_tx_id;
+            sel[p] = src[p] == 1;                              // :354-370
+            ci[p] = src[p] == 1 ? src[p] : sh[p].bl_tx_id;
+            memcpy(&sbl[p * 32], sh[p].bl_root, 32);
+            memcpy(&tbl[p * 32], th[p].bl_root, 32);
+        }
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        Layout L;
+        const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
+                       b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
+                       b_st = L.add(2 * n * 4), b_leaf = L.add(n * 32), b_sbl = L.add(n * 32),
+                       b_tbl = L.add(n * 32), b_ca = L.add(n * 32), b_sel = L.add(n),
+                       b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
+                       b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8), b_it = L.add(ni * 32),
+                       b_ct = L.add(nc * 32), b_oki = L.add(n), b_okc = L.add(n);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
+            return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
+                         : hipSuccess;
+        };
+        MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
+        if (md_blob) MH_HIP(h2d(b_md, md_blob, md_blob_len));
+        MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
+        MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
+        MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
+        MH_HIP(h2d(b_sel, sel.data(), n));
+        MH_HIP(h2d(b_ii, ii.data(), n * 8));
+        MH_HIP(h2d(b_ij, ij.data(), n * 8));
+        MH_HIP(h2d(b_ci, ci.data(), n * 8));
+        MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
+        MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
+        if (ni) MH_HIP(h2d(b_it, incl_terms + incl_off[0] * 32, ni * 32));
+        if (nc) MH_HIP(h2d(b_ct, cons_terms + cons_off[0] * 32, nc * 32));
+        // Alh of both headers vs the given ones (verification.go:318-326)
+        MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, (const MhTxHeader *)(base + b_h), base + b_md,
+                             nullptr, base + b_s, base + b_x, nullptr, nullptr, nullptr,
+                             (int32_t *)(base + b_st)));
+        // leafFor(sourceAlh) (verification.go:346), then the two ahtree proofs
+        MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
+        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
+                                    (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
+                                    base + b_it, base + b_leaf, base + b_tbl, base + b_oki, nullptr));
+        MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
+        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
+                                    (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
+                                    (const uint64_t *)(base + b_co), base + b_ct, base + b_ca,
+                                    base + b_tbl, base + b_okc, nullptr));
+        std::vector<int32_t> ast(2 * n);
+        std::vector<uint8_t> oki(n), okc(n);
+        MH_HIP(hipMemcpyAsync(ast.data(), base + b_st, 2 * n * 4, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(oki.data(), base + b_oki, n, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(okc.data(), base + b_okc, n, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        for (uint64_t p = 0; p < n; p++) {
+            if (status[p] != MH_OK) continue;
+            if (ast[p] != MH_OK || ast[n + p] != MH_OK) {
+                status[p] = MH_ERR_ILLEGAL_ARGUMENTS;
+            } else if (sh[p].id - 1 != sh[p].bl_tx_id || th[p].id - 1 != th[p].bl_tx_id) {
+                status[p] = MH_ERR_UNEXPECTED_LINKING;  // :328-330
+            } else if (src[p] == tgt[p]) {
+                status[p] = MH_OK;  // :332-334
+            } else if (!oki[p]) {
+                status[p] = MH_ERR_INCLUSION_NOT_VALID;
+            } else if (!okc[p]) {
+                status[p] = MH_ERR_CONSISTENCY_NOT_VALID;
+            }
+        }
+        return MH_OK;
+    });
 }
 
 extern "C" int mh_verify_dual_proof_batch(mh_ctx *c, const mh_dual_proof_batch *B, uint8_t *ok) {
-    if (!c || !B || (B->n && !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    const uint64_t n = B->n;
-    if (!n) return MH_OK;
-    if (!B->src_hdr || !B->tgt_hdr || !B->incl_off || !B->cons_off || !B->target_bl_tx_alh ||
-        !B->last_off || !B->has_linear || !B->linear_src || !B->linear_tgt || !B->linear_off ||
-        !B->has_advance || !B->advance_off || !B->advance_incl_first || !B->advance_incl_off ||
-        !B->src || !B->tgt || !B->src_alh || !B->tgt_alh)
-        return MH_ERR_ILLEGAL_ARGUMENTS;
-    const mh_tx_header *sh = B->src_hdr, *th = B->tgt_hdr;
-    const uint64_t ni = B->incl_off[n] - B->incl_off[0], nc = B->cons_off[n] - B->cons_off[0],
-                   nl = B->last_off[n] - B->last_off[0], nlin = B->linear_off[n] - B->linear_off[0],
-                   nadv = B->advance_off[n] - B->advance_off[0],
-                   Q = B->advance_incl_first[n] - B->advance_incl_first[0],
-                   nq = Q ? B->advance_incl_off[B->advance_incl_first[n]] -
-                                B->advance_incl_off[B->advance_incl_first[0]]
-                          : 0;
-    if ((ni && !B->incl_terms) || (nc && !B->cons_terms) || (nl && !B->last_terms) ||
-        (nlin && !B->linear_terms) || (nadv && !B->advance_terms) ||
-        (nq && !B->advance_incl_terms))
-        return MH_ERR_ILLEGAL_ARGUMENTS;
-    const uint64_t q0 = B->advance_incl_first[0], qt0 = Q ? B->advance_incl_off[q0] : 0;
+    return mh_guard([&]() -> int {
+        if (!c || !B || (B->n && !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t n = B->n;
+        if (!n) return MH_OK;
+        if (!B->src_hdr || !B->tgt_hdr || !B->incl_off || !B->cons_off || !B->target_bl_tx_alh ||
+            !B->last_off || !B->has_linear || !B->linear_src || !B->linear_tgt || !B->linear_off ||
+            !B->has_advance || !B->advance_off || !B->advance_incl_first || !B->advance_incl_off ||
+            !B->src || !B->tgt || !B->src_alh || !B->tgt_alh)
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        const mh_tx_header *sh = B->src_hdr, *th = B->tgt_hdr;
+        const uint64_t ni = B->incl_off[n] - B->incl_off[0], nc = B->cons_off[n] - B->cons_off[0],
+                       nl = B->last_off[n] - B->last_off[0], nlin = B->linear_off[n] - B->linear_off[0],
+                       nadv = B->advance_off[n] - B->advance_off[0],
+                       Q = B->advance_incl_first[n] - B->advance_incl_first[0],
+                       nq = Q ? B->advance_incl_off[B->advance_incl_first[n]] -
+                                    B->advance_incl_off[B->advance_incl_first[0]]
+                              : 0;
+        if ((ni && !B->incl_terms) || (nc && !B->cons_terms) || (nl && !B->last_terms) ||
+            (nlin && !B->linear_terms) || (nadv && !B->advance_terms) ||
+            (nq && !B->advance_incl_terms))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t q0 = B->advance_incl_first[0], qt0 = Q ? B->advance_incl_off[q0] : 0;
 
-    // ---- host side: argument checks and per-check operands (verification.go:128-235)
-    std::vector<uint8_t> alive(n, 1), adv_state(n, 0);  // 0 run chain, 1 true, 2 false
-    std::vector<mh_tx_header> hh(2 * n);
-    std::vector<uint8_t> expect(2 * n * 32), lin_sa(n * 32), end_alh(n * 32), sbl(n * 32),
-        tbl(n * 32);
-    std::vector<uint64_t> ii(n), ij(n), ci(n), li(n), ls(n), lt(n), lo(n + 1), io(n + 1),
-        co(n + 1), lso(n + 1);
-    std::vector<uint64_t> a_start, a_cnt, a_t0, a_first, a_idx;
-    std::vector<uint8_t> a_end;
-    for (uint64_t p = 0; p <= n; p++) {
-        io[p] = B->incl_off[p] - B->incl_off[0];
-        co[p] = B->cons_off[p] - B->cons_off[0];
-        lso[p] = B->last_off[p] - B->last_off[0];
-        lo[p] = B->linear_off[p] - B->linear_off[0];
-    }
-    for (uint64_t p = 0; p < n; p++) {
-        const uint64_t src = B->src[p], tgt = B->tgt[p];
-        if (sh[p].id != src || th[p].id != tgt || sh[p].id == 0 || sh[p].id > th[p].id ||
-            check_header(sh[p], B->md_blob_len, B->md_blob != nullptr) ||
-            check_header(th[p], B->md_blob_len, B->md_blob != nullptr))
-            alive[p] = 0;
-        hh[p] = sh[p];
-        hh[n + p] = th[p];
-        if (!alive[p]) {
-            hh[p].version = hh[n + p].version = 1;
-            hh[p].md_len = hh[n + p].md_len = 0;
+        // ---- host side: argument checks and per-check operands (verification.go:128-235)
+        std::vector<uint8_t> alive(n, 1), adv_state(n, 0);  // 0 run chain, 1 true, 2 false
+        std::vector<mh_tx_header> hh(2 * n);
+        std::vector<uint8_t> expect(2 * n * 32), lin_sa(n * 32), end_alh(n * 32), sbl(n * 32),
+            tbl(n * 32);
+        std::vector<uint64_t> ii(n), ij(n), ci(n), li(n), ls(n), lt(n), lo(n + 1), io(n + 1),
+            co(n + 1), lso(n + 1);
+        std::vector<uint64_t> a_start, a_cnt, a_t0, a_first, a_idx;
+        std::vector<uint8_t> a_end;
+        for (uint64_t p = 0; p <= n; p++) {
+            io[p] = B->incl_off[p] - B->incl_off[0];
+            co[p] = B->cons_off[p] - B->cons_off[0];
+            lso[p] = B->last_off[p] - B->last_off[0];
+            lo[p] = B->linear_off[p] - B->linear_off[0];
         }
-        memcpy(&expect[p * 32], B->src_alh + p * 32, 32);
-        memcpy(&expect[(n + p) * 32], B->tgt_alh + p * 32, 32);
-        memcpy(&sbl[p * 32], sh[p].bl_root, 32);
-        memcpy(&tbl[p * 32], th[p].bl_root, 32);
-        const uint64_t tbl_id = th[p].bl_tx_id;
-        ii[p] = src;
-        ij[p] = tbl_id;
-        ci[p] = sh[p].bl_tx_id;
-        li[p] = tbl_id;
-        const bool a_branch = src < tbl_id;  // verification.go:195 vs :214
-        ls[p] = a_branch ? tbl_id : src;
-        lt[p] = tgt;
-        memcpy(&lin_sa[p * 32], a_branch ? B->target_bl_tx_alh + p * 32 : B->src_alh + p * 32, 32);
-        const uint64_t start = sh[p].bl_tx_id, end = a_branch ? src : tbl_id;
-        memcpy(&end_alh[p * 32], a_branch ? B->src_alh + p * 32 : B->target_bl_tx_alh + p * 32, 32);
-        // VerifyLinearAdvanceProof preconditions (verification.go:90-104)
-        const uint64_t f0 = B->advance_incl_first[p], f1 = B->advance_incl_first[p + 1];
-        if (end < start) {
-            adv_state[p] = 2;
-        } else if (end <= start + 1) {
-            adv_state[p] = 1;
-        } else if (!B->has_advance[p] ||
-                   B->advance_off[p + 1] - B->advance_off[p] != end - start ||
-                   f1 - f0 != end - start - 1) {
-            adv_state[p] = 2;
-        } else {
-            adv_state[p] = 0;
-            a_idx.push_back(p);
-            a_start.push_back(start);
-            a_cnt.push_back(end - start - 1);
-            a_t0.push_back(B->advance_off[p] - B->advance_off[0]);
-            a_first.push_back(f0 - q0);
-            a_end.insert(a_end.end(), &end_alh[p * 32], &end_alh[p * 32] + 32);
+        for (uint64_t p = 0; p < n; p++) {
+            const uint64_t src = B->src[p], tgt = B->tgt[p];
+            if (sh[p].id != src || th[p].id != tgt || sh[p].id == 0 || sh[p].id > th[p].id ||
+                check_header(sh[p], B->md_blob_len, B->md_blob != nullptr) ||
+                check_header(th[p], B->md_blob_len, B->md_blob != nullptr))
+                alive[p] = 0;
+            hh[p] = sh[p];
+            hh[n + p] = th[p];
+            if (!alive[p]) {
+                hh[p].version = hh[n + p].version = 1;
+                hh[p].md_len = hh[n + p].md_len = 0;
+            }
+            memcpy(&expect[p * 32], B->src_alh + p * 32, 32);
+            memcpy(&expect[(n + p) * 32], B->tgt_alh + p * 32, 32);
+            memcpy(&sbl[p * 32], sh[p].bl_root, 32);
+            memcpy(&tbl[p * 32], th[p].bl_root, 32);
+            const uint64_t tbl_id = th[p].bl_tx_id;
+            ii[p] = src;
+            ij[p] = tbl_id;
+            ci[p] = sh[p].bl_tx_id;
+            li[p] = tbl_id;
+            const bool a_branch = src < tbl_id;  // verification.go:195 vs :214
+            ls[p] = a_branch ? tbl_id : src;
+            lt[p] = tgt;
+            memcpy(&lin_sa[p * 32], a_branch ? B->target_bl_tx_alh + p * 32 : B->src_alh + p * 32, 32);
+            const uint64_t start = sh[p].bl_tx_id, end = a_branch ? src : tbl_id;
+            memcpy(&end_alh[p * 32], a_branch ? B->src_alh + p * 32 : B->target_bl_tx_alh + p * 32, 32);
+            // VerifyLinearAdvanceProof preconditions (verification.go:90-104)
+            const uint64_t f0 = B->advance_incl_first[p], f1 = B->advance_incl_first[p + 1];
+            if (end < start) {
+                adv_state[p] = 2;
+            } else if (end <= start + 1) {
+                adv_state[p] = 1;
+            } else if (!B->has_advance[p] ||
+                       B->advance_off[p + 1] - B->advance_off[p] != end - start ||
+                       f1 - f0 != end - start - 1) {
+                adv_state[p] = 2;
+            } else {
+                adv_state[p] = 0;
+                a_idx.push_back(p);
+                a_start.push_back(start);
+                a_cnt.push_back(end - start - 1);
+                a_t0.push_back(B->advance_off[p] - B->advance_off[0]);
+                a_first.push_back(f0 - q0);
+                a_end.insert(a_end.end(), &end_alh[p * 32], &end_alh[p * 32] + 32);
+            }
         }
-    }
-    // nested inclusion proofs (every q; those of proofs not run are ignored)
-    std::vector<uint64_t> qi(std::max<uint64_t>(Q, 1)), qj(std::max<uint64_t>(Q, 1)),
-        qo(Q + 1);
-    std::vector<uint8_t> qroot(std::max<uint64_t>(Q, 1) * 32);
-    for (uint64_t q = 0; q <= Q; q++) qo[q] = B->advance_incl_off[q0 + q] - qt0;
-    for (uint64_t k = 0; k < a_idx.size(); k++) {
-        const uint64_t p = a_idx[k];
-        for (uint64_t x = 0; x < a_cnt[k]; x++) {
-            const uint64_t q = a_first[k] + x;
-            qi[q] = a_start[k] + 1 + x;  // txID, verification.go:108-114
-            qj[q] = th[p].bl_tx_id;
-            memcpy(&qroot[q * 32], th[p].bl_root, 32);
+        // nested inclusion proofs (every q; those of proofs not run are ignored)
+        std::vector<uint64_t> qi(std::max<uint64_t>(Q, 1)), qj(std::max<uint64_t>(Q, 1)),
+            qo(Q + 1);
+        std::vector<uint8_t> qroot(std::max<uint64_t>(Q, 1) * 32);
+        for (uint64_t q = 0; q <= Q; q++) qo[q] = B->advance_incl_off[q0 + q] - qt0;
+        for (uint64_t k = 0; k < a_idx.size(); k++) {
+            const uint64_t p = a_idx[k];
+            for (uint64_t x = 0; x < a_cnt[k]; x++) {
+                const uint64_t q = a_first[k] + x;
+                qi[q] = a_start[k] + 1 + x;  // txID, verification.go:108-114
+                qj[q] = th[p].bl_tx_id;
+                memcpy(&qroot[q * 32], th[p].bl_root, 32);
+            }
         }
-    }
-    const uint64_t na = a_idx.size();
+        const uint64_t na = a_idx.size();
 
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    Layout L;
-    const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(B->md_blob_len),
-                   b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
-                   b_ast = L.add(2 * n * 4), b_tba = L.add(n * 32), b_lfa = L.add(n * 32),
-                   b_lft = L.add(n * 32), b_sbl = L.add(n * 32), b_tbl = L.add(n * 32),
-                   b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
-                   b_li = L.add(n * 8), b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8),
-                   b_lso = L.add((n + 1) * 8), b_it = L.add(ni * 32), b_ct = L.add(nc * 32),
-                   b_lt = L.add(nl * 32), b_oki = L.add(n), b_okc = L.add(n), b_okl = L.add(n),
-                   b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_ls = L.add(n * 8),
-                   b_ltg = L.add(n * 8), b_lo = L.add((n + 1) * 8), b_lterm = L.add(nlin * 32),
-                   b_lsa = L.add(n * 32), b_ta = L.add(n * 32), b_oklin = L.add(n),
-                   b_ast0 = L.add(na * 8), b_acnt = L.add(na * 8), b_at0 = L.add(na * 8),
-                   b_afirst = L.add(na * 8), b_aend = L.add(na * 32), b_aterm = L.add(nadv * 32),
-                   b_aok = L.add(na), b_qsrc = L.add(Q * 32), b_qleaf = L.add(Q * 32),
-                   b_qi = L.add(Q * 8), b_qj = L.add(Q * 8), b_qo = L.add((Q + 1) * 8),
-                   b_qroot = L.add(Q * 32), b_qterm = L.add(nq * 32), b_qok = L.add(Q);
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
-                     : hipSuccess;
-    };
-    auto U = [&](uint64_t off) { return (const uint64_t *)(base + off); };
-    MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
-    if (B->md_blob) MH_HIP(h2d(b_md, B->md_blob, B->md_blob_len));
-    MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
-    MH_HIP(h2d(b_tba, B->target_bl_tx_alh, n * 32));
-    MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
-    MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
-    MH_HIP(h2d(b_ii, ii.data(), n * 8));
-    MH_HIP(h2d(b_ij, ij.data(), n * 8));
-    MH_HIP(h2d(b_ci, ci.data(), n * 8));
-    MH_HIP(h2d(b_li, li.data(), n * 8));
-    MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
-    MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
-    MH_HIP(h2d(b_lso, lso.data(), (n + 1) * 8));
-    MH_HIP(h2d(b_it, ni ? B->incl_terms + B->incl_off[0] * 32 : nullptr, ni * 32));
-    MH_HIP(h2d(b_ct, nc ? B->cons_terms + B->cons_off[0] * 32 : nullptr, nc * 32));
-    MH_HIP(h2d(b_lt, nl ? B->last_terms + B->last_off[0] * 32 : nullptr, nl * 32));
-    MH_HIP(h2d(b_ps, B->linear_src, n * 8));
-    MH_HIP(h2d(b_pt, B->linear_tgt, n * 8));
-    MH_HIP(h2d(b_ls, ls.data(), n * 8));
-    MH_HIP(h2d(b_ltg, lt.data(), n * 8));
-    MH_HIP(h2d(b_lo, lo.data(), (n + 1) * 8));
-    MH_HIP(h2d(b_lterm, nlin ? B->linear_terms + B->linear_off[0] * 32 : nullptr, nlin * 32));
-    MH_HIP(h2d(b_lsa, lin_sa.data(), n * 32));
-    MH_HIP(h2d(b_ta, B->tgt_alh, n * 32));
-    MH_HIP(h2d(b_ast0, a_start.data(), na * 8));
-    MH_HIP(h2d(b_acnt, a_cnt.data(), na * 8));
-    MH_HIP(h2d(b_at0, a_t0.data(), na * 8));
-    MH_HIP(h2d(b_afirst, a_first.data(), na * 8));
-    MH_HIP(h2d(b_aend, a_end.data(), na * 32));
-    MH_HIP(h2d(b_aterm, nadv ? B->advance_terms + B->advance_off[0] * 32 : nullptr, nadv * 32));
-    MH_HIP(h2d(b_qi, qi.data(), Q * 8));
-    MH_HIP(h2d(b_qj, qj.data(), Q * 8));
-    MH_HIP(h2d(b_qo, qo.data(), (Q + 1) * 8));
-    MH_HIP(h2d(b_qroot, qroot.data(), Q * 32));
-    MH_HIP(h2d(b_qterm, nq ? B->advance_incl_terms + qt0 * 32 : nullptr, nq * 32));
-    Timer *tm = c->tm();
-    // header Alh (verification.go:141-150)
-    MH_HIP(launch_tx_alh(st, tm, 2 * n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
-                         base + b_s, base + b_x, nullptr, nullptr, nullptr,
-                         (int32_t *)(base + b_ast)));
-    // inclusion / consistency / last inclusion (verification.go:152-190)
-    MH_HIP(launch_leaf_for(st, tm, n, base + b_x, base + b_lfa));
-    MH_HIP(launch_leaf_for(st, tm, n, base + b_tba, base + b_lft));
-    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, n, U(b_ii), U(b_ij), U(b_io),
-                                base + b_it, base + b_lfa, base + b_tbl, base + b_oki, nullptr));
-    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_CONSISTENCY, n, U(b_ci), U(b_ij), U(b_co),
-                                base + b_ct, base + b_sbl, base + b_tbl, base + b_okc, nullptr));
-    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_LAST_INCLUSION, n, U(b_li), U(b_li), U(b_lso),
-                                base + b_lt, base + b_lft, base + b_tbl, base + b_okl, nullptr));
-    // linear proof (verification.go:195-197 / :214-216)
-    MH_HIP(launch_linear_verify(st, tm, n, U(b_ps), U(b_pt), U(b_ls), U(b_ltg), U(b_lo),
-                                base + b_lterm, base + b_lsa, base + b_ta, base + b_oklin));
-    // linear advance proofs: chain, then the nested inclusion proofs
-    MH_HIP(launch_advance_chain(st, tm, na, U(b_ast0), U(b_acnt), U(b_at0), base + b_aterm,
-                                U(b_afirst), base + b_aend, base + b_qsrc, base + b_aok));
-    MH_HIP(launch_leaf_for(st, tm, Q, base + b_qsrc, base + b_qleaf));
-    MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, Q, U(b_qi), U(b_qj), U(b_qo),
-                                base + b_qterm, base + b_qleaf, base + b_qroot, base + b_qok,
-                                nullptr));
-    std::vector<int32_t> ast(2 * n);
-    std::vector<uint8_t> oki(n), okc(n), okl(n), oklin(n), aok(std::max<uint64_t>(na, 1)),
-        qok(std::max<uint64_t>(Q, 1));
-    auto d2h = [&](void *dst, uint64_t off, uint64_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(dst, base + off, bytes, hipMemcpyDeviceToHost, st)
-                     : hipSuccess;
-    };
-    MH_HIP(d2h(ast.data(), b_ast, 2 * n * 4));
-    MH_HIP(d2h(oki.data(), b_oki, n));
-    MH_HIP(d2h(okc.data(), b_okc, n));
-    MH_HIP(d2h(okl.data(), b_okl, n));
-    MH_HIP(d2h(oklin.data(), b_oklin, n));
-    MH_HIP(d2h(aok.data(), b_aok, na));
-    MH_HIP(d2h(qok.data(), b_qok, Q));
-    MH_HIP(hipStreamSynchronize(st));
-    std::vector<uint8_t> adv_ok(n, 0);
-    for (uint64_t k = 0; k < na; k++) {
-        bool all = aok[k] != 0;
-        for (uint64_t x = 0; x < a_cnt[k] && all; x++) all = qok[a_first[k] + x] != 0;
-        adv_ok[a_idx[k]] = all;
-    }
-    for (uint64_t p = 0; p < n; p++) {
-        const uint64_t src = B->src[p], tbl_id = th[p].bl_tx_id;
-        bool r = alive[p] && ast[p] == MH_OK && ast[n + p] == MH_OK;
-        if (r && src < tbl_id) r = oki[p];
-        if (r && sh[p].bl_tx_id > 0) r = okc[p];
-        if (r && tbl_id > 0) r = okl[p];
-        if (r) r = B->has_linear[p] && oklin[p];
-        if (r) r = adv_state[p] == 1 || (adv_state[p] == 0 && adv_ok[p]);
-        ok[p] = r ? 1 : 0;
-    }
-    return MH_OK;
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        Layout L;
+        const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(B->md_blob_len),
+                       b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
+                       b_ast = L.add(2 * n * 4), b_tba = L.add(n * 32), b_lfa = L.add(n * 32),
+                       b_lft = L.add(n * 32), b_sbl = L.add(n * 32), b_tbl = L.add(n * 32),
+                       b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
+                       b_li = L.add(n * 8), b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8),
+                       b_lso = L.add((n + 1) * 8), b_it = L.add(ni * 32), b_ct = L.add(nc * 32),
+                       b_lt = L.add(nl * 32), b_oki = L.add(n), b_okc = L.add(n), b_okl = L.add(n),
+                       b_ps = L.add(n * 8), b_pt = L.add(n * 8), b_ls = L.add(n * 8),
+                       b_ltg = L.add(n * 8), b_lo = L.add((n + 1) * 8), b_lterm = L.add(nlin * 32),
+                       b_lsa = L.add(n * 32), b_ta = L.add(n * 32), b_oklin = L.add(n),
+                       b_ast0 = L.add(na * 8), b_acnt = L.add(na * 8), b_at0 = L.add(na * 8),
+                       b_afirst = L.add(na * 8), b_aend = L.add(na * 32), b_aterm = L.add(nadv * 32),
+                       b_aok = L.add(na), b_qsrc = L.add(Q * 32), b_qleaf = L.add(Q * 32),
+                       b_qi = L.add(Q * 8), b_qj = L.add(Q * 8), b_qo = L.add((Q + 1) * 8),
+                       b_qroot = L.add(Q * 32), b_qterm = L.add(nq * 32), b_qok = L.add(Q);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
+            return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
+                         : hipSuccess;
+        };
+        auto U = [&](uint64_t off) { return (const uint64_t *)(base + off); };
+        MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
+        if (B->md_blob) MH_HIP(h2d(b_md, B->md_blob, B->md_blob_len));
+        MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
+        MH_HIP(h2d(b_tba, B->target_bl_tx_alh, n * 32));
+        MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
+        MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
+        MH_HIP(h2d(b_ii, ii.data(), n * 8));
+        MH_HIP(h2d(b_ij, ij.data(), n * 8));
+        MH_HIP(h2d(b_ci, ci.data(), n * 8));
+        MH_HIP(h2d(b_li, li.data(), n * 8));
+        MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
+        MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
+        MH_HIP(h2d(b_lso, lso.data(), (n + 1) * 8));
+        MH_HIP(h2d(b_it, ni ? B->incl_terms + B->incl_off[0] * 32 : nullptr, ni * 32));
+        MH_HIP(h2d(b_ct, nc ? B->cons_terms + B->cons_off[0] * 32 : nullptr, nc * 32));
+        MH_HIP(h2d(b_lt, nl ? B->last_terms + B->last_off[0] * 32 : nullptr, nl * 32));
+        MH_HIP(h2d(b_ps, B->linear_src, n * 8));
+        MH_HIP(h2d(b_pt, B->linear_tgt, n * 8));
+        MH_HIP(h2d(b_ls, ls.data(), n * 8));
+        MH_HIP(h2d(b_ltg, lt.data(), n * 8));
+        MH_HIP(h2d(b_lo, lo.data(), (n + 1) * 8));
+        MH_HIP(h2d(b_lterm, nlin ? B->linear_terms + B->linear_off[0] * 32 : nullptr, nlin * 32));
+        MH_HIP(h2d(b_lsa, lin_sa.data(), n * 32));
+        MH_HIP(h2d(b_ta, B->tgt_alh, n * 32));
+        MH_HIP(h2d(b_ast0, a_start.data(), na * 8));
+        MH_HIP(h2d(b_acnt, a_cnt.data(), na * 8));
+        MH_HIP(h2d(b_at0, a_t0.data(), na * 8));
+        MH_HIP(h2d(b_afirst, a_first.data(), na * 8));
+        MH_HIP(h2d(b_aend, a_end.data(), na * 32));
+        MH_HIP(h2d(b_aterm, nadv ? B->advance_terms + B->advance_off[0] * 32 : nullptr, nadv * 32));
+        MH_HIP(h2d(b_qi, qi.data(), Q * 8));
+        MH_HIP(h2d(b_qj, qj.data(), Q * 8));
+        MH_HIP(h2d(b_qo, qo.data(), (Q + 1) * 8));
+        MH_HIP(h2d(b_qroot, qroot.data(), Q * 32));
+        MH_HIP(h2d(b_qterm, nq ? B->advance_incl_terms + qt0 * 32 : nullptr, nq * 32));
+        Timer *tm = c->tm();
+        // header Alh (verification.go:141-150)
+        MH_HIP(launch_tx_alh(st, tm, 2 * n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
+                             base + b_s, base + b_x, nullptr, nullptr, nullptr,
+                             (int32_t *)(base + b_ast)));
+        // inclusion / consistency / last inclusion (verification.go:152-190)
+        MH_HIP(launch_leaf_for(st, tm, n, base + b_x, base + b_lfa));
+        MH_HIP(launch_leaf_for(st, tm, n, base + b_tba, base + b_lft));
+        MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, n, U(b_ii), U(b_ij), U(b_io),
+                                    base + b_it, base + b_lfa, base + b_tbl, base + b_oki, nullptr));
+        MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_CONSISTENCY, n, U(b_ci), U(b_ij), U(b_co),
+                                    base + b_ct, base + b_sbl, base + b_tbl, base + b_okc, nullptr));
+        MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_LAST_INCLUSION, n, U(b_li), U(b_li), U(b_lso),
+                                    base + b_lt, base + b_lft, base + b_tbl, base + b_okl, nullptr));
+        // linear proof (verification.go:195-197 / :214-216)
+        MH_HIP(launch_linear_verify(st, tm, n, U(b_ps), U(b_pt), U(b_ls), U(b_ltg), U(b_lo),
+                                    base + b_lterm, base + b_lsa, base + b_ta, base + b_oklin));
+        // linear advance proofs: chain, then the nested inclusion proofs
+        MH_HIP(launch_advance_chain(st, tm, na, U(b_ast0), U(b_acnt), U(b_at0), base + b_aterm,
+                                    U(b_afirst), base + b_aend, base + b_qsrc, base + b_aok));
+        MH_HIP(launch_leaf_for(st, tm, Q, base + b_qsrc, base + b_qleaf));
+        MH_HIP(launch_ahtree_verify(st, tm, MH_AHT_INCLUSION, Q, U(b_qi), U(b_qj), U(b_qo),
+                                    base + b_qterm, base + b_qleaf, base + b_qroot, base + b_qok,
+                                    nullptr));
+        std::vector<int32_t> ast(2 * n);
+        std::vector<uint8_t> oki(n), okc(n), okl(n), oklin(n), aok(std::max<uint64_t>(na, 1)),
+            qok(std::max<uint64_t>(Q, 1));
+        auto d2h = [&](void *dst, uint64_t off, uint64_t bytes) -> hipError_t {
+            return bytes ? hipMemcpyAsync(dst, base + off, bytes, hipMemcpyDeviceToHost, st)
+                         : hipSuccess;
+        };
+        MH_HIP(d2h(ast.data(), b_ast, 2 * n * 4));
+        MH_HIP(d2h(oki.data(), b_oki, n));
+        MH_HIP(d2h(okc.data(), b_okc, n));
+        MH_HIP(d2h(okl.data(), b_okl, n));
+        MH_HIP(d2h(oklin.data(), b_oklin, n));
+        MH_HIP(d2h(aok.data(), b_aok, na));
+        MH_HIP(d2h(qok.data(), b_qok, Q));
+        MH_HIP(hipStreamSynchronize(st));
+        std::vector<uint8_t> adv_ok(n, 0);
+        for (uint64_t k = 0; k < na; k++) {
+            bool all = aok[k] != 0;
+            for (uint64_t x = 0; x < a_cnt[k] && all; x++) all = qok[a_first[k] + x] != 0;
+            adv_ok[a_idx[k]] = all;
+        }
+        for (uint64_t p = 0; p < n; p++) {
+            const uint64_t src = B->src[p], tbl_id = th[p].bl_tx_id;
+            bool r = alive[p] && ast[p] == MH_OK && ast[n + p] == MH_OK;
+            if (r && src < tbl_id) r = oki[p];
+            if (r && sh[p].bl_tx_id > 0) r = okc[p];
+            if (r && tbl_id > 0) r = okl[p];
+            if (r) r = B->has_linear[p] && oklin[p];
+            if (r) r = adv_state[p] == 1 || (adv_state[p] == 0 && adv_ok[p]);
+            ok[p] = r ? 1 : 0;
+        }
+        return MH_OK;
+    });
 }
 
 // ------------------------------------------------------------------ a14
@@ -667,16 +679,22 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
     for (unsigned k = 0; k <= T; k++) cut[k] = len / T * k;
     cut[T] = ~0ull;
     std::vector<HopOut> part(T);
+    auto work = [&](unsigned k) {
+        const uint64_t s = k ? find_record_start(buf, len, cut[k], std::min(cut[k + 1], len), lim) : 0;
+        if (s == ~0ull) {
+            part[k].start = ~0ull;
+            return;
+        }
+        hop_range(buf, len, s, cut[k + 1], max_txs, lim, part[k]);
+    };
     std::vector<std::thread> th;
-    for (unsigned k = 0; k < T; k++)
-        th.emplace_back([&, k] {
-            const uint64_t s = k ? find_record_start(buf, len, cut[k], std::min(cut[k + 1], len), lim) : 0;
-            if (s == ~0ull) {
-                part[k].start = ~0ull;
-                return;
-            }
-            hop_range(buf, len, s, cut[k + 1], max_txs, lim, part[k]);
-        });
+    unsigned started = 0;
+    try {  // no thread (resource limits): the remaining chunks run on this one
+        for (; started + 1 < T; started++) th.emplace_back(work, started + 1);
+    } catch (...) {
+    }
+    work(0);
+    for (unsigned k = started + 1; k < T; k++) work(k);
     for (auto &t : th) t.join();
     uint64_t pos = 0;
     out.start = 0;
@@ -716,120 +734,124 @@ extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entr
                              uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                              uint64_t *consumed_out, mh_tx_header *hdrs_out,
                              uint64_t *alh_off_out) {
-    if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
-    HopOut hop;
-    hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
-    const uint64_t ntx = hop.H.size();
-    if (ntx_out) *ntx_out = ntx;
-    if (consumed_out) *consumed_out = hop.end;
-    if (hdrs_out && ntx) memcpy(hdrs_out, hop.H.data(), ntx * sizeof(mh_tx_header));
-    if (alh_off_out && ntx) memcpy(alh_off_out, hop.alh_pos.data(), ntx * 8);
-    return hop.rc;
+    return mh_guard([&]() -> int {
+        if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
+        HopOut hop;
+        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
+        const uint64_t ntx = hop.H.size();
+        if (ntx_out) *ntx_out = ntx;
+        if (consumed_out) *consumed_out = hop.end;
+        if (hdrs_out && ntx) memcpy(hdrs_out, hop.H.data(), ntx * sizeof(mh_tx_header));
+        if (alh_off_out && ntx) memcpy(alh_off_out, hop.alh_pos.data(), ntx * 8);
+        return hop.rc;
+    });
 }
 
 extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                                  uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                                  uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
                                  int32_t *status_out) {
-    if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
-    // The raw records go to the device first: the copy (DMA when buf is
-    // pinned) runs under the host hop below.
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = c->stream;
-    if (len) {
-        MH_HIP(c->s_txlog.ensure(len));
-        MH_HIP(hipMemcpyAsync(c->s_txlog.p, buf, len, hipMemcpyHostToDevice, st));
-    }
-    uint8_t *dbuf = c->s_txlog.as<uint8_t>();
-    // ---- host hop (tx.go:419-603): record structure and limits only.  Per
-    // entry the host reads the two lengths it needs to find the next entry
-    // (several threads over a long log, hop_all); the per-entry index (record
-    // offsets, versions, message lengths) is rebuilt on the device from each
-    // tx's first entry (k_txe_index).
-    HopOut hop;
-    hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
-    const std::vector<mh_tx_header> &H = hop.H;
-    const std::vector<uint64_t> &alh_pos = hop.alh_pos, &ent_start = hop.ent_start;
-    std::vector<uint64_t> leaf_off(H.size() + 1);
-    uint64_t E = 0, msg_total = 0, wmax = 0;
-    leaf_off[0] = 0;
-    for (size_t k = 0; k < H.size(); k++) {
-        E += H[k].nentries;
-        leaf_off[k + 1] = E;
-        wmax = std::max<uint64_t>(wmax, H[k].nentries);
-        msg_total += hop.msg[k];
-    }
-    const int rc = hop.rc;
-    const uint64_t p = hop.end;
-    // on an error p is the failing record's offset = the end of the last good one
-    const uint64_t ntx = H.size();
-    if (ntx_out) *ntx_out = ntx;
-    if (consumed_out) *consumed_out = p;
-    if (!ntx) {
-        MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
-        return rc;
-    }
-    // ---- device: entry index, digests, trees, Alh
-    // small trees (every tx here: a handful of entries) get their roots one
-    // lane per tree; a batch with a wide tx goes through the host tree plan
-    const bool small = wmax <= kSmallTreeMax;
-    TreePlan P;
-    if (!small) P.build(ntx, leaf_off.data());
-    Layout L;
-    const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
-                   b_ml = L.add(E * 8), b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_total),
-                   b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
-                   b_h = L.add(ntx * sizeof(mh_tx_header)), b_ap = L.add(ntx * 8),
-                   b_es = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
-                   b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
-                   b_st = L.add(ntx * 4), b_tmp = L.add(pb_scan_temp_bytes(E));
-    MH_HIP(c->s_tx.ensure(L.total));
-    uint8_t *base = c->s_tx.as<uint8_t>();
-    // the parsed arrays (headers, Alh positions, first entries, leaf offsets)
-    // are contiguous in the device layout: one pinned staging copy, one DMA
-    const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_h;
-    const uint64_t pin_bytes = idx_bytes + (small ? 0 : plan_index_bytes(P, ntx));
-    MH_HIP(c->p_tx.ensure(pin_bytes));
-    uint8_t *pin = c->p_tx.as<uint8_t>();
-    memcpy(pin, H.data(), ntx * sizeof(mh_tx_header));
-    memcpy(pin + (b_ap - b_h), alh_pos.data(), ntx * 8);
-    memcpy(pin + (b_es - b_h), ent_start.data(), ntx * 8);
-    memcpy(pin + (b_lo - b_h), leaf_off.data(), (ntx + 1) * 8);
-    MH_HIP(hipMemcpyAsync(base + b_h, pin, idx_bytes, hipMemcpyHostToDevice, st));
-    // per-entry index, then entry digests (tx.go:578-585 -> 690-731)
-    MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
-                            (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
-                            (uint64_t *)(base + b_rec), base + b_ver, (uint64_t *)(base + b_ml)));
-    MH_HIP(scan_offsets_u64(st, E, (const uint64_t *)(base + b_ml), (uint64_t *)(base + b_mo),
-                            base + b_tmp));
-    MH_HIP(launch_txe_assemble(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec),
-                               base + b_ver, (const uint64_t *)(base + b_mo), base + b_msg));
-    MH_HIP(launch_sha256_csr(st, c->tm(), base + b_msg, (const uint64_t *)(base + b_mo), E,
-                             nullptr, nullptr, base + b_dig));
-    // one htree per tx (tx.go:617-621)
-    if (small) {
-        MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_dig, base + b_lv));  // htree.go:79-83
-        MH_HIP(launch_small_roots(st, c->tm(), ntx, (const uint64_t *)(base + b_lo), base + b_lv,
-                                  base + b_eh));
-    } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_dig,
-                                        base + b_eh, pin + idx_bytes)) {
-        return e;
-    }
-    // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
-    MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), dbuf,
-                         base + b_eh, base + b_s, dbuf, (const uint64_t *)(base + b_ap),
-                         nullptr, base + b_a, (int32_t *)(base + b_st)));
-    std::vector<uint8_t> eh(hdrs_out ? ntx * 32 : 0);
-    if (status_out)
-        MH_HIP(hipMemcpyAsync(status_out, base + b_st, ntx * 4, hipMemcpyDeviceToHost, st));
-    if (alh_out) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
-    if (hdrs_out) MH_HIP(hipMemcpyAsync(eh.data(), base + b_eh, ntx * 32, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    if (hdrs_out)
-        for (uint64_t k = 0; k < ntx; k++) {
-            hdrs_out[k] = H[k];
-            memcpy(hdrs_out[k].eh, &eh[k * 32], 32);
+    return mh_guard([&]() -> int {
+        if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // The raw records go to the device first: the copy (DMA when buf is
+        // pinned) runs under the host hop below.
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        if (len) {
+            MH_HIP(c->s_txlog.ensure(len));
+            MH_HIP(hipMemcpyAsync(c->s_txlog.p, buf, len, hipMemcpyHostToDevice, st));
         }
-    return rc;
+        uint8_t *dbuf = c->s_txlog.as<uint8_t>();
+        // ---- host hop (tx.go:419-603): record structure and limits only.  Per
+        // entry the host reads the two lengths it needs to find the next entry
+        // (several threads over a long log, hop_all); the per-entry index (record
+        // offsets, versions, message lengths) is rebuilt on the device from each
+        // tx's first entry (k_txe_index).
+        HopOut hop;
+        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
+        const std::vector<mh_tx_header> &H = hop.H;
+        const std::vector<uint64_t> &alh_pos = hop.alh_pos, &ent_start = hop.ent_start;
+        std::vector<uint64_t> leaf_off(H.size() + 1);
+        uint64_t E = 0, msg_total = 0, wmax = 0;
+        leaf_off[0] = 0;
+        for (size_t k = 0; k < H.size(); k++) {
+            E += H[k].nentries;
+            leaf_off[k + 1] = E;
+            wmax = std::max<uint64_t>(wmax, H[k].nentries);
+            msg_total += hop.msg[k];
+        }
+        const int rc = hop.rc;
+        const uint64_t p = hop.end;
+        // on an error p is the failing record's offset = the end of the last good one
+        const uint64_t ntx = H.size();
+        if (ntx_out) *ntx_out = ntx;
+        if (consumed_out) *consumed_out = p;
+        if (!ntx) {
+            MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
+            return rc;
+        }
+        // ---- device: entry index, digests, trees, Alh
+        // small trees (every tx here: a handful of entries) get their roots one
+        // lane per tree; a batch with a wide tx goes through the host tree plan
+        const bool small = wmax <= kSmallTreeMax;
+        TreePlan P;
+        if (!small) P.build(ntx, leaf_off.data());
+        Layout L;
+        const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
+                       b_ml = L.add(E * 8), b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_total),
+                       b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
+                       b_h = L.add(ntx * sizeof(mh_tx_header)), b_ap = L.add(ntx * 8),
+                       b_es = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
+                       b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
+                       b_st = L.add(ntx * 4), b_tmp = L.add(pb_scan_temp_bytes(E));
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        // the parsed arrays (headers, Alh positions, first entries, leaf offsets)
+        // are contiguous in the device layout: one pinned staging copy, one DMA
+        const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_h;
+        const uint64_t pin_bytes = idx_bytes + (small ? 0 : plan_index_bytes(P, ntx));
+        MH_HIP(c->p_tx.ensure(pin_bytes));
+        uint8_t *pin = c->p_tx.as<uint8_t>();
+        memcpy(pin, H.data(), ntx * sizeof(mh_tx_header));
+        memcpy(pin + (b_ap - b_h), alh_pos.data(), ntx * 8);
+        memcpy(pin + (b_es - b_h), ent_start.data(), ntx * 8);
+        memcpy(pin + (b_lo - b_h), leaf_off.data(), (ntx + 1) * 8);
+        MH_HIP(hipMemcpyAsync(base + b_h, pin, idx_bytes, hipMemcpyHostToDevice, st));
+        // per-entry index, then entry digests (tx.go:578-585 -> 690-731)
+        MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
+                                (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
+                                (uint64_t *)(base + b_rec), base + b_ver, (uint64_t *)(base + b_ml)));
+        MH_HIP(scan_offsets_u64(st, E, (const uint64_t *)(base + b_ml), (uint64_t *)(base + b_mo),
+                                base + b_tmp));
+        MH_HIP(launch_txe_assemble(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec),
+                                   base + b_ver, (const uint64_t *)(base + b_mo), base + b_msg));
+        MH_HIP(launch_sha256_csr(st, c->tm(), base + b_msg, (const uint64_t *)(base + b_mo), E,
+                                 nullptr, nullptr, base + b_dig));
+        // one htree per tx (tx.go:617-621)
+        if (small) {
+            MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_dig, base + b_lv));  // htree.go:79-83
+            MH_HIP(launch_small_roots(st, c->tm(), ntx, (const uint64_t *)(base + b_lo), base + b_lv,
+                                      base + b_eh));
+        } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_dig,
+                                            base + b_eh, pin + idx_bytes)) {
+            return e;
+        }
+        // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
+        MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), dbuf,
+                             base + b_eh, base + b_s, dbuf, (const uint64_t *)(base + b_ap),
+                             nullptr, base + b_a, (int32_t *)(base + b_st)));
+        std::vector<uint8_t> eh(hdrs_out ? ntx * 32 : 0);
+        if (status_out)
+            MH_HIP(hipMemcpyAsync(status_out, base + b_st, ntx * 4, hipMemcpyDeviceToHost, st));
+        if (alh_out) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
+        if (hdrs_out) MH_HIP(hipMemcpyAsync(eh.data(), base + b_eh, ntx * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        if (hdrs_out)
+            for (uint64_t k = 0; k < ntx; k++) {
+                hdrs_out[k] = H[k];
+                memcpy(hdrs_out[k].eh, &eh[k * 32], 32);
+            }
+        return rc;
+    });
 }
