@@ -544,9 +544,19 @@ namespace {
 
 // Records of one stretch of a tx log (the structure readHeader / readEntry
 // read, tx.go:419-603; no hashing).
+// Per record: where it starts, where its stored Alh is, its entry count and
+// the bytes of its entry-digest messages.  The headers themselves are only
+// kept when asked (mh_txlog_scan); the validation path rebuilds them on the
+// device from the raw record bytes (k_tx_hdr_from_raw).
+struct HopRec {
+    uint64_t rec, alh, msg;
+    uint32_t nent, pad;
+};
+
 struct HopOut {
-    std::vector<mh_tx_header> H;
-    std::vector<uint64_t> alh_pos, ent_start, msg;  // per record
+    std::vector<HopRec> R;
+    std::vector<mh_tx_header> H;  // want_headers only
+    bool want_headers = false;
     uint64_t start = 0, end = 0;  // first record parsed / where parsing stopped
     int rc = MH_OK;
     bool stopped = false;  // EOF (id 0 / end of buffer) or a structural error
@@ -616,7 +626,7 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
 void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint64_t max_recs,
                const HopLimits &lim, HopOut &o) {
     o.start = p;
-    while (p < stop && o.H.size() < max_recs) {
+    while (p < stop && o.R.size() < max_recs) {
         mh_tx_header h;
         uint64_t first = 0, alh = 0, msg = 0;
         bool eof = false;
@@ -626,10 +636,8 @@ void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint
             o.stopped = true;
             break;
         }
-        o.H.push_back(h);
-        o.alh_pos.push_back(alh);
-        o.ent_start.push_back(first);
-        o.msg.push_back(msg);
+        o.R.push_back(HopRec{p, alh, msg, h.nentries, 0});
+        if (o.want_headers) o.H.push_back(h);
         p = alh + 32;
     }
     o.end = p;
@@ -668,7 +676,8 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
 // previous chunk's end are re-parsed sequentially, so the result is always
 // the sequential parse's.
 void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits &lim,
-             HopOut &out) {
+             HopOut &out, bool want_headers) {
+    out.want_headers = want_headers;
     unsigned T = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
     if (len < (8ull << 20)) T = 1;
     if (T == 1) {
@@ -679,6 +688,7 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
     for (unsigned k = 0; k <= T; k++) cut[k] = len / T * k;
     cut[T] = ~0ull;
     std::vector<HopOut> part(T);
+    for (auto &pt : part) pt.want_headers = want_headers;
     auto work = [&](unsigned k) {
         const uint64_t s = k ? find_record_start(buf, len, cut[k], std::min(cut[k + 1], len), lim) : 0;
         if (s == ~0ull) {
@@ -701,18 +711,17 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
     for (unsigned k = 0; k < T; k++) {
         if (pos >= cut[k + 1]) continue;  // a record spanning this whole chunk
         HopOut redo, *o = &part[k];
+        redo.want_headers = want_headers;
         if (o->start != pos) {            // speculation missed: parse this chunk for real
             hop_range(buf, len, pos, cut[k + 1], max_txs, lim, redo);
             o = &redo;
         }
-        const uint64_t room = max_txs - out.H.size();
-        const uint64_t take = std::min<uint64_t>(room, o->H.size());
-        out.H.insert(out.H.end(), o->H.begin(), o->H.begin() + take);
-        out.alh_pos.insert(out.alh_pos.end(), o->alh_pos.begin(), o->alh_pos.begin() + take);
-        out.ent_start.insert(out.ent_start.end(), o->ent_start.begin(), o->ent_start.begin() + take);
-        out.msg.insert(out.msg.end(), o->msg.begin(), o->msg.begin() + take);
-        if (take < o->H.size()) {         // max_txs reached inside this chunk
-            pos = out.alh_pos.back() + 32;
+        const uint64_t room = max_txs - out.R.size();
+        const uint64_t take = std::min<uint64_t>(room, o->R.size());
+        out.R.insert(out.R.end(), o->R.begin(), o->R.begin() + take);
+        if (want_headers) out.H.insert(out.H.end(), o->H.begin(), o->H.begin() + take);
+        if (take < o->R.size()) {         // max_txs reached inside this chunk
+            pos = out.R.back().alh + 32;
             break;
         }
         pos = o->end;
@@ -721,7 +730,7 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
             out.stopped = true;
             break;
         }
-        if (out.H.size() == max_txs) break;
+        if (out.R.size() == max_txs) break;
     }
     out.end = pos;
 }
@@ -737,12 +746,13 @@ extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entr
     return mh_guard([&]() -> int {
         if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
         HopOut hop;
-        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
-        const uint64_t ntx = hop.H.size();
+        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, hdrs_out != nullptr);
+        const uint64_t ntx = hop.R.size();
         if (ntx_out) *ntx_out = ntx;
         if (consumed_out) *consumed_out = hop.end;
         if (hdrs_out && ntx) memcpy(hdrs_out, hop.H.data(), ntx * sizeof(mh_tx_header));
-        if (alh_off_out && ntx) memcpy(alh_off_out, hop.alh_pos.data(), ntx * 8);
+        if (alh_off_out)
+            for (uint64_t k = 0; k < ntx; k++) alh_off_out[k] = hop.R[k].alh;
         return hop.rc;
     });
 }
@@ -769,55 +779,66 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // offsets, versions, message lengths) is rebuilt on the device from each
         // tx's first entry (k_txe_index).
         HopOut hop;
-        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop);
-        const std::vector<mh_tx_header> &H = hop.H;
-        const std::vector<uint64_t> &alh_pos = hop.alh_pos, &ent_start = hop.ent_start;
-        std::vector<uint64_t> leaf_off(H.size() + 1);
-        uint64_t E = 0, msg_total = 0, wmax = 0;
-        leaf_off[0] = 0;
-        for (size_t k = 0; k < H.size(); k++) {
-            E += H[k].nentries;
-            leaf_off[k + 1] = E;
-            wmax = std::max<uint64_t>(wmax, H[k].nentries);
-            msg_total += hop.msg[k];
-        }
+        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
+        const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
-        const uint64_t p = hop.end;
-        // on an error p is the failing record's offset = the end of the last good one
-        const uint64_t ntx = H.size();
+        // on an error hop.end is the failing record's offset = the end of the last good one
         if (ntx_out) *ntx_out = ntx;
-        if (consumed_out) *consumed_out = p;
+        if (consumed_out) *consumed_out = hop.end;
         if (!ntx) {
             MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
             return rc;
         }
-        // ---- device: entry index, digests, trees, Alh
+        uint64_t E = 0, msg_total = 0, wmax = 0;
+        for (const HopRec &r : hop.R) {
+            E += r.nent;
+            wmax = std::max<uint64_t>(wmax, r.nent);
+            msg_total += r.msg;
+        }
+        // ---- device: headers, entry index, digests, trees, Alh
         // small trees (every tx here: a handful of entries) get their roots one
         // lane per tree; a batch with a wide tx goes through the host tree plan
         const bool small = wmax <= kSmallTreeMax;
-        TreePlan P;
-        if (!small) P.build(ntx, leaf_off.data());
         Layout L;
         const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
                        b_ml = L.add(E * 8), b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_total),
                        b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
-                       b_h = L.add(ntx * sizeof(mh_tx_header)), b_ap = L.add(ntx * 8),
-                       b_es = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
+                       b_h = L.add(ntx * sizeof(mh_tx_header)), b_es = L.add(ntx * 8),
+                       b_ro = L.add(ntx * 8), b_ap = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
                        b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
                        b_st = L.add(ntx * 4), b_tmp = L.add(pb_scan_temp_bytes(E));
         MH_HIP(c->s_tx.ensure(L.total));
         uint8_t *base = c->s_tx.as<uint8_t>();
-        // the parsed arrays (headers, Alh positions, first entries, leaf offsets)
-        // are contiguous in the device layout: one pinned staging copy, one DMA
-        const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_h;
+        // record offsets, Alh positions and leaf offsets are contiguous in the
+        // device layout: written once into pinned staging, one DMA
+        const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_ro;
+        std::vector<uint64_t> leaf_off;
+        TreePlan P;
+        if (!small) {
+            leaf_off.resize(ntx + 1);
+            leaf_off[0] = 0;
+            for (uint64_t k = 0; k < ntx; k++) leaf_off[k + 1] = leaf_off[k] + hop.R[k].nent;
+            P.build(ntx, leaf_off.data());
+        }
         const uint64_t pin_bytes = idx_bytes + (small ? 0 : plan_index_bytes(P, ntx));
         MH_HIP(c->p_tx.ensure(pin_bytes));
         uint8_t *pin = c->p_tx.as<uint8_t>();
-        memcpy(pin, H.data(), ntx * sizeof(mh_tx_header));
-        memcpy(pin + (b_ap - b_h), alh_pos.data(), ntx * 8);
-        memcpy(pin + (b_es - b_h), ent_start.data(), ntx * 8);
-        memcpy(pin + (b_lo - b_h), leaf_off.data(), (ntx + 1) * 8);
-        MH_HIP(hipMemcpyAsync(base + b_h, pin, idx_bytes, hipMemcpyHostToDevice, st));
+        {
+            uint64_t *ro = reinterpret_cast<uint64_t *>(pin);
+            uint64_t *ap = reinterpret_cast<uint64_t *>(pin + (b_ap - b_ro));
+            uint64_t *lo = reinterpret_cast<uint64_t *>(pin + (b_lo - b_ro));
+            uint64_t acc = 0;
+            for (uint64_t k = 0; k < ntx; k++) {
+                ro[k] = hop.R[k].rec;
+                ap[k] = hop.R[k].alh;
+                lo[k] = acc;
+                acc += hop.R[k].nent;
+            }
+            lo[ntx] = acc;
+        }
+        MH_HIP(hipMemcpyAsync(base + b_ro, pin, idx_bytes, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), ntx, dbuf, (const uint64_t *)(base + b_ro),
+                                      (MhTxHeader *)(base + b_h), (uint64_t *)(base + b_es)));
         // per-entry index, then entry digests (tx.go:578-585 -> 690-731)
         MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
                                 (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
@@ -841,17 +862,15 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), dbuf,
                              base + b_eh, base + b_s, dbuf, (const uint64_t *)(base + b_ap),
                              nullptr, base + b_a, (int32_t *)(base + b_st)));
-        std::vector<uint8_t> eh(hdrs_out ? ntx * 32 : 0);
         if (status_out)
             MH_HIP(hipMemcpyAsync(status_out, base + b_st, ntx * 4, hipMemcpyDeviceToHost, st));
         if (alh_out) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
-        if (hdrs_out) MH_HIP(hipMemcpyAsync(eh.data(), base + b_eh, ntx * 32, hipMemcpyDeviceToHost, st));
+        if (hdrs_out) {  // the device headers with the rebuilt Eh
+            MH_HIP(launch_put_eh(st, ntx, base + b_eh, (MhTxHeader *)(base + b_h)));
+            MH_HIP(hipMemcpyAsync(hdrs_out, base + b_h, ntx * sizeof(mh_tx_header),
+                                  hipMemcpyDeviceToHost, st));
+        }
         MH_HIP(hipStreamSynchronize(st));
-        if (hdrs_out)
-            for (uint64_t k = 0; k < ntx; k++) {
-                hdrs_out[k] = H[k];
-                memcpy(hdrs_out[k].eh, &eh[k * 32], 32);
-            }
         return rc;
     });
 }

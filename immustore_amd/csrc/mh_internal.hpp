@@ -182,6 +182,10 @@ hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uin
 constexpr uint64_t kSmallTreeMax = 64;
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
                               uint8_t *nodes, uint8_t *roots);
+// headers + first-entry offsets of tx records from the raw log (md_off relative to buf)
+hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                                  const uint64_t *rec_off, MhTxHeader *hdrs, uint64_t *ent_start);
+hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
 hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                             const MhTxHeader *hdrs, const uint64_t *ent_start,
                             const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver,

@@ -217,6 +217,70 @@ __global__ __launch_bounds__(256) void k_txe_assemble(uint64_t n, const uint8_t 
     for (int k = 0; k < 32; k++) *o++ = hv[k];
 }
 
+// TxHeader of each record from the raw tx-log bytes (the fields readHeader
+// reads, tx.go:419-518; the host hop already validated the structure), plus
+// the offset of its first entry.  md_off is relative to the log buffer.
+__global__ __launch_bounds__(256) void k_tx_hdr_from_raw(uint64_t ntx, const uint8_t *__restrict__ buf,
+                                                         const uint64_t *__restrict__ rec_off,
+                                                         MhTxHeader *__restrict__ hdrs,
+                                                         uint64_t *__restrict__ ent_start) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx) return;
+    const uint64_t p = rec_off[t];
+    const uint8_t *r = buf + p;
+    auto be = [&](int o, int n) {
+        uint64_t v = 0;
+        for (int k = 0; k < n; k++) v = v << 8 | r[o + k];
+        return v;
+    };
+    MhTxHeader h;
+    h.id = be(0, 8);
+    h.ts = (int64_t)be(8, 8);
+    h.bl_tx_id = be(16, 8);
+    for (int k = 0; k < 32; k++) {
+        h.bl_root[k] = r[24 + k];
+        h.prev_alh[k] = r[56 + k];
+        h.eh[k] = 0;
+    }
+    h.version = (uint32_t)be(88, 2);
+    uint64_t q = 90;
+    if (h.version == 0) {
+        h.nentries = (uint32_t)be(90, 2);
+        h.md_len = 0;
+        h.md_off = 0;
+        q = 92;
+    } else {
+        h.md_len = (uint32_t)be(90, 2);
+        h.md_off = (uint32_t)(p + 92);
+        h.nentries = (uint32_t)be(92 + h.md_len, 4);
+        q = 96 + h.md_len;
+    }
+    hdrs[t] = h;
+    ent_start[t] = p + q;
+}
+
+__global__ __launch_bounds__(256) void k_put_eh(uint64_t n, const uint8_t *__restrict__ eh,
+                                                MhTxHeader *__restrict__ hdrs) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    for (int k = 0; k < 32; k++) hdrs[t].eh[k] = eh[t * 32 + k];
+}
+
+hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                                  const uint64_t *rec_off, MhTxHeader *hdrs, uint64_t *ent_start) {
+    if (!ntx) return hipSuccess;
+    TimerScope ts(tm, "tx_hdr_from_raw", st);
+    hipLaunchKernelGGL(k_tx_hdr_from_raw, dim3(grid_for(ntx, 256)), dim3(256), 0, st, ntx, buf,
+                       rec_off, hdrs, ent_start);
+    return hipGetLastError();
+}
+
+hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_put_eh, dim3(grid_for(n, 256)), dim3(256), 0, st, n, eh, hdrs);
+    return hipGetLastError();
+}
+
 // Entry index of a run of tx records (tx.go:520-588 readEntry, structure
 // only), one lane per tx: the host hop already validated every length, so
 // the lane walks its entries from ent_start[t] and records each entry's
