@@ -20,14 +20,15 @@
 // Two passes, one lane per message: k_pb_*_size (status, byte size and term
 // counts; no memory reads beyond the headers), an inclusive scan of the sizes
 // (hipcub) into off[1..n], then k_pb_*_write (headers streamed through a
-// register-staged ByteWriter as dword stores, each 34-byte term record
-// written at its final place as the walk meets it).  Measured alternatives
-// (10^6 DualProofV2 over a 2^24-append tree, MI355X): one wave per message
-// doing the walks and header encoding itself: 25 ms (64x the serial index
-// math of one lane); walks stored as index lists in the size pass + one wave
-// per message materialising coalesced dwords: 8.1 ms (scattered index-list
-// stores, latency-bound waves); this form: 4.7 ms (5.4 ms before the
-// branch-free 34-byte field writer).
+// register-staged ByteWriter as dword stores; the 34-byte term records built
+// per round in LDS and written by the whole wave, staged_records).  Measured
+// on MI355X, 10^6 DualProofV2 over a 2^24-append tree: one wave per message
+// doing the walks and header encoding itself, 25 ms (64x the serial index
+// math); index lists stored by the size pass + one wave per message
+// materialising dwords, 8.1 ms; one lane per message storing its own records,
+// 4.5 ms (64 scattered lines per store); records staged per wave, 4 per lane
+// per round, 3.0 ms (8 per round: 3.7 ms, LDS occupancy; 2: 4.0 ms, flush
+// overhead).
 #include <algorithm>
 
 #include <hipcub/hipcub.hpp>
@@ -301,16 +302,83 @@ __device__ inline void put_header(ByteWriter &bw, uint32_t tag, const MhTxHeader
     }
 }
 
-// One 34-byte repeated-bytes record (tag, 32, node) at p; node 16-byte aligned
-__device__ __forceinline__ void put_record(uint8_t *p, uint32_t tag, const uint8_t *node) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(node);
+// ------------------------------------------------------------ staged term records
+// Each lane owns one message, but its term records leave through LDS: per
+// round a lane builds up to kRpr records of its walk in its LDS slot -- in
+// message order, at the byte alignment of their global destination -- and
+// then the wave writes every lane's span (up to 272 contiguous bytes) with
+// all 64 lanes storing consecutive dwords.  One message per lane keeps the
+// serial index walks parallel; the staging turns 64 scattered lines per
+// store instruction into 2-3 contiguous ones.
+#ifndef MH_PB_RPR
+#define MH_PB_RPR 4  // A/B (tools/pb_ab.sh): 4 beats 8 (LDS occupancy) and 2 (flush overhead)
+#endif
+constexpr uint32_t kRpr = MH_PB_RPR;  // records per lane per round
+constexpr uint32_t kSlotBytes = (3 + kRpr * 34 + 15) / 16 * 16;  // + alignment bytes, 16-byte rows
+
+__device__ __forceinline__ void load_node(const uint8_t *node, uint32_t x[8]) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(node);  // 32-byte nodes, 16-byte aligned
     const uint4 a = q[0], b = q[1];
-    const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    put_rec34(p, tag, x);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
 }
 
-// One lane per message: headers streamed, then each term record written at
-// its place (the walks meet terms in reverse proof order, proof_walk.hpp).
+// Records q = 0 .. cnt-1 of the walk `gen` (walk order) go to
+// rec_base + 34 * (cnt - 1 - q) (proof order, proof_walk.hpp).  Wave-uniform
+// control flow: every lane of the wave calls this (inactive lanes with cnt 0).
+template <class Gen>
+__device__ __forceinline__ void staged_records(uint8_t *rec_base, uint32_t cnt, uint32_t tag,
+                                               Gen &gen, const uint8_t *__restrict__ nodes,
+                                               uint8_t *wave_lds, int lane) {
+    uint8_t *slot = wave_lds + lane * kSlotBytes;
+    uint32_t done = 0;
+    while (__any(done < cnt)) {
+        const uint32_t cr = done < cnt ? min(kRpr, cnt - done) : 0;
+        uint8_t *g = rec_base + 34ull * (cnt - done - cr);  // span start (message order)
+        const uint32_t a = (uint32_t)((uintptr_t)g & 3);
+        // gather in pairs (two node loads in flight), build in LDS
+        for (uint32_t k = 0; k < cr; k += 2) {
+            uint32_t x[8], y[8];
+            const uint64_t n0 = gen.next();
+            const uint64_t n1 = k + 1 < cr ? gen.next() : n0;
+            load_node(nodes + n0 * 32, x);
+            load_node(nodes + n1 * 32, y);
+            put_rec34(slot + a + 34 * (cr - 1 - k), tag, x);
+            if (k + 1 < cr) put_rec34(slot + a + 34 * (cr - 2 - k), tag, y);
+        }
+        done += cr;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t ga = (uint64_t)(uintptr_t)g;
+        const uint32_t len = 34 * cr;
+        for (int sl = 0; sl < 64; sl++) {  // span of lane sl, read with v_readlane (scalar)
+            const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)len, sl);
+            if (!ls) continue;
+            const uint64_t gs =
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ga >> 32), sl) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ga, sl);
+            const uint32_t as = (uint32_t)(gs & 3);
+            const uint32_t nd = (as + ls + 3) / 4;
+            uint32_t *gw = reinterpret_cast<uint32_t *>(gs - as);
+            const uint32_t *lw = reinterpret_cast<const uint32_t *>(wave_lds + sl * kSlotBytes);
+            for (uint32_t d = lane; d < nd; d += 64) {
+                const uint32_t lo = d == 0 ? as : 0;
+                const uint32_t hi = min(4u, as + ls - 4 * d);
+                const uint32_t v = lw[d];
+                if (lo == 0 && hi == 4) {
+                    gw[d] = v;
+                } else {
+                    uint8_t *gb = reinterpret_cast<uint8_t *>(gw + d);
+                    for (uint32_t e = lo; e < hi; e++) gb[e] = (uint8_t)(v >> (8 * e));
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // every span is out before the slots are rebuilt
+    }
+}
+
+// One lane per message: header fields streamed from registers, term records
+// staged per wave (staged_records).
 __global__ __launch_bounds__(256) void k_pb_dual_write(const uint8_t *__restrict__ dlog, uint64_t size,
                                                        uint64_t n, const MhTxHeader *__restrict__ src,
                                                        const MhTxHeader *__restrict__ tgt,
@@ -319,29 +387,40 @@ __global__ __launch_bounds__(256) void k_pb_dual_write(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ cnt,
                                                        uint8_t *__restrict__ out, uint64_t out_cap,
                                                        int32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[256 * kSlotBytes];
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n || status[p] != MH_OK) return;
-    if (off[p + 1] > out_cap) {
+    const int lane = threadIdx.x & 63;
+    uint8_t *wave_lds = lds + (threadIdx.x & ~63) * kSlotBytes;
+    bool active = p < n && status[p] == MH_OK;
+    if (active && off[p + 1] > out_cap) {
         status[p] = MH_ERR_BUFFER_TOO_SMALL;
-        return;
+        active = false;
     }
-    const MhTxHeader &S = src[p], &T = tgt[p];
-    const PbDual d = pb_dual(S, T, md_blob, size);
-    uint8_t *o = out + off[p];
-    ByteWriter bw(o);
-    put_header(bw, 0x0a, S, d.s, md_blob);
-    put_header(bw, 0x12, T, d.t, md_blob);
-    bw.finish();
-    if (!d.proofs) return;
-    uint8_t *rec = o + framed(d.s.body) + framed(d.t.body);
-    const uint32_t ni = cnt[2 * p], nc = cnt[2 * p + 1];
-    ahtree_walk(false, d.ii, d.ij, [&](uint32_t q, uint64_t x) {
-        put_record(rec + 34ull * (ni - 1 - q), 0x1a, dlog + x * 32);
-    });
-    rec += 34ull * ni;
-    ahtree_walk(true, d.ci, d.ij, [&](uint32_t q, uint64_t x) {
-        put_record(rec + 34ull * (nc - 1 - q), 0x22, dlog + x * 32);
-    });
+    uint8_t *rec = out;
+    uint32_t ni = 0, nc = 0;
+    uint64_t ii = 1, ij = 1, ci = 1;
+    if (active) {
+        const MhTxHeader &S = src[p], &T = tgt[p];
+        const PbDual d = pb_dual(S, T, md_blob, size);
+        uint8_t *o = out + off[p];
+        ByteWriter bw(o);
+        put_header(bw, 0x0a, S, d.s, md_blob);
+        put_header(bw, 0x12, T, d.t, md_blob);
+        bw.finish();
+        rec = o + framed(d.s.body) + framed(d.t.body);
+        if (d.proofs) {
+            ni = cnt[2 * p];
+            nc = cnt[2 * p + 1];
+            ii = d.ii;
+            ij = d.ij;
+            ci = d.ci;
+        }
+    }
+    if (!__any(ni + nc > 0)) return;  // wave-uniform from here on
+    AhtreeWalk gi(false, ii, ij);
+    staged_records(rec, ni, 0x1a, gi, dlog, wave_lds, lane);
+    AhtreeWalk gc(true, ci, ij);
+    staged_records(rec + 34ull * ni, nc, 0x22, gc, dlog, wave_lds, lane);
 }
 
 // ------------------------------------------------------------ InclusionProof (htree)
@@ -377,23 +456,31 @@ __global__ __launch_bounds__(256) void k_pb_incl_write(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ cnt,
                                                        uint8_t *__restrict__ out, uint64_t out_cap,
                                                        int32_t *__restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[256 * kSlotBytes];
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n || status[p] != MH_OK) return;
-    if (off[p + 1] > out_cap) {
+    const int lane = threadIdx.x & 63;
+    uint8_t *wave_lds = lds + (threadIdx.x & ~63) * kSlotBytes;
+    bool active = p < n && status[p] == MH_OK;
+    if (active && off[p + 1] > out_cap) {
         status[p] = MH_ERR_BUFFER_TOO_SMALL;
-        return;
+        active = false;
     }
-    const uint64_t i = leaf[p];
-    uint8_t *o = out + off[p];
-    ByteWriter bw(o);
-    if ((uint32_t)i) { bw.put8(0x08); bw.varint(i32v((uint32_t)i)); }
-    if ((uint32_t)w) { bw.put8(0x10); bw.varint(i32v((uint32_t)w)); }
-    bw.finish();
-    uint8_t *rec = o + pb_incl_prefix(i, w);
-    const uint32_t c = cnt[2 * p];
-    htree_walk(i, w, [&](uint32_t q, uint64_t x) {
-        put_record(rec + 34ull * (c - 1 - q), 0x1a, levels + x * 32);
-    });
+    uint8_t *rec = out;
+    uint32_t c = 0;
+    uint64_t i = 0;
+    if (active) {
+        i = leaf[p];
+        uint8_t *o = out + off[p];
+        ByteWriter bw(o);
+        if ((uint32_t)i) { bw.put8(0x08); bw.varint(i32v((uint32_t)i)); }
+        if ((uint32_t)w) { bw.put8(0x10); bw.varint(i32v((uint32_t)w)); }
+        bw.finish();
+        rec = o + pb_incl_prefix(i, w);
+        c = cnt[2 * p];
+    }
+    if (!__any(c > 0)) return;
+    HtreeWalk g(i, active ? w : 0);
+    staged_records(rec, c, 0x1a, g, levels, wave_lds, lane);
 }
 
 // ------------------------------------------------------------ launchers
