@@ -678,7 +678,10 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
 void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits &lim,
              HopOut &out, bool want_headers) {
     out.want_headers = want_headers;
-    unsigned T = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+#ifndef MH_HOP_THREADS
+#define MH_HOP_THREADS 8
+#endif
+    unsigned T = std::min((unsigned)MH_HOP_THREADS, std::max(1u, std::thread::hardware_concurrency()));
     if (len < (8ull << 20)) T = 1;
     if (T == 1) {
         hop_range(buf, len, 0, ~0ull, max_txs, lim, out);
