@@ -326,10 +326,13 @@ __device__ __forceinline__ void load_node(const uint8_t *node, uint32_t x[8]) {
 // Records q = 0 .. cnt-1 of the walk `gen` (walk order) go to
 // rec_base + 34 * (cnt - 1 - q) (proof order, proof_walk.hpp).  Wave-uniform
 // control flow: every lane of the wave calls this (inactive lanes with cnt 0).
+// A walk that ends before `cnt` terms (the size pass and the writer would
+// disagree -- never seen, the two forms are tested against each other) reads
+// node 0 instead of faulting and sets *bad.
 template <class Gen>
 __device__ __forceinline__ void staged_records(uint8_t *rec_base, uint32_t cnt, uint32_t tag,
                                                Gen &gen, const uint8_t *__restrict__ nodes,
-                                               uint8_t *wave_lds, int lane) {
+                                               uint8_t *wave_lds, int lane, bool *bad) {
     uint8_t *slot = wave_lds + lane * kSlotBytes;
     uint32_t done = 0;
     while (__any(done < cnt)) {
@@ -339,8 +342,12 @@ __device__ __forceinline__ void staged_records(uint8_t *rec_base, uint32_t cnt, 
         // gather in pairs (two node loads in flight), build in LDS
         for (uint32_t k = 0; k < cr; k += 2) {
             uint32_t x[8], y[8];
-            const uint64_t n0 = gen.next();
-            const uint64_t n1 = k + 1 < cr ? gen.next() : n0;
+            uint64_t n0 = gen.next();
+            uint64_t n1 = k + 1 < cr ? gen.next() : n0;
+            if (n0 == ~0ull || n1 == ~0ull) {
+                *bad = true;
+                n0 = n1 = 0;
+            }
             load_node(nodes + n0 * 32, x);
             load_node(nodes + n1 * 32, y);
             put_rec34(slot + a + 34 * (cr - 1 - k), tag, x);
@@ -417,10 +424,12 @@ __global__ __launch_bounds__(256) void k_pb_dual_write(const uint8_t *__restrict
         }
     }
     if (!__any(ni + nc > 0)) return;  // wave-uniform from here on
+    bool bad = false;
     AhtreeWalk gi(false, ii, ij);
-    staged_records(rec, ni, 0x1a, gi, dlog, wave_lds, lane);
+    staged_records(rec, ni, 0x1a, gi, dlog, wave_lds, lane, &bad);
     AhtreeWalk gc(true, ci, ij);
-    staged_records(rec + 34ull * ni, nc, 0x22, gc, dlog, wave_lds, lane);
+    staged_records(rec + 34ull * ni, nc, 0x22, gc, dlog, wave_lds, lane, &bad);
+    if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
 }
 
 // ------------------------------------------------------------ InclusionProof (htree)
@@ -479,8 +488,10 @@ __global__ __launch_bounds__(256) void k_pb_incl_write(const uint8_t *__restrict
         c = cnt[2 * p];
     }
     if (!__any(c > 0)) return;
+    bool bad = false;
     HtreeWalk g(i, active ? w : 0);
-    staged_records(rec, c, 0x1a, g, levels, wave_lds, lane);
+    staged_records(rec, c, 0x1a, g, levels, wave_lds, lane, &bad);
+    if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
 }
 
 // ------------------------------------------------------------ launchers
