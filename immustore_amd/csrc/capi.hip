@@ -56,6 +56,7 @@ extern "C" const char *mh_status_string(int st) {
 
 extern "C" int mh_device_count(int *count) {
     return mh_guard([&]() -> int {
+        if (!count) return MH_ERR_ILLEGAL_ARGUMENTS;
         int n = 0;
         hipError_t e = hipGetDeviceCount(&n);
         if (e != hipSuccess) {
