@@ -77,3 +77,51 @@ def test_null_pointers_with_live_context():
         assert checked >= 30
     finally:
         ctx.close()
+
+
+def _first_param_functions(kind):
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "immustore_merkle.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\bint\s+(mh_[a-z0-9_]+)\s*\(\s*" + kind + r"\s*\*", src))
+
+
+@pytest.mark.gpu
+def test_null_pointers_with_live_handles():
+    """Entry points taking an mh_htree / mh_ahtree / mh_commit_pipe handle:
+    live (empty) handles, NULL pointers, sizes 3 -> a Go sentinel status."""
+    import torch  # noqa: F401
+    import immustore_amd as m
+    from immustore_amd import _native as N
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    L = N.load()
+    ctx = m.Context(0)
+    handles = {}
+    try:
+        for kind, mk in (("mh_htree", lambda h: L.mh_htree_new(ctx.handle, 1024, C.byref(h))),
+                         ("mh_ahtree", lambda h: L.mh_ahtree_new(ctx.handle, C.byref(h))),
+                         ("mh_commit_pipe",
+                          lambda h: L.mh_commit_pipe_new(ctx.handle, 0, C.byref(h)))):
+            h = C.c_void_p()
+            N.check(mk(h))
+            handles[kind] = h
+        allowed = {0, 2, 3, 4, 5, 7, 19}
+        checked = 0
+        for kind, h in handles.items():
+            for name in sorted(_first_param_functions(kind)):
+                if name.endswith("_free"):
+                    continue
+                res, argtypes = N.SIGNATURES[name]
+                rc = getattr(L, name)(*_zero_args(argtypes, fill_int=3, ctx=h))
+                assert rc in allowed, (name, rc)
+                checked += 1
+        assert checked >= 20
+        ctx.synchronize()
+    finally:
+        L.mh_htree_free(handles.get("mh_htree"))
+        L.mh_ahtree_free(handles.get("mh_ahtree"))
+        L.mh_commit_pipe_free(handles.get("mh_commit_pipe"))
+        ctx.close()
