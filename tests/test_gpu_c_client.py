@@ -1,0 +1,71 @@
+"""The C ABI driven from plain C (tests/c_client/mh_client.c, built by
+__graft_entry__.build()): what a cgo shim does, with no Python or torch in the
+process.  Its printed roots and proofs must equal the oracle's
+(htree.go:64-164, ahtree.go:149-651) on the same deterministic inputs."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CLIENT = os.path.join(HERE, "c_client", "mh_client")
+
+
+def _inputs(w, m):
+    d = ((np.arange(w * 32, dtype=np.uint64) * 131 + 7) & 0xFF).astype(np.uint8).reshape(w, 32)
+    p = ((np.arange(m * 32, dtype=np.uint64) * 29 + 3) & 0xFF).astype(np.uint8).reshape(m, 32)
+    return d, p
+
+
+def _run(w, m):
+    if not os.path.exists(CLIENT):
+        pytest.fail("tests/c_client/mh_client not built (run __graft_entry__.build())")
+    r = subprocess.run([CLIENT, str(w), str(m)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    out = {}
+    for line in r.stdout.splitlines():
+        k, _, v = line.partition(" ")
+        out[k] = v
+    assert "done" in out
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,m", [(1000, 777), (1, 3), (2, 4), (4096, 1 << 12), (65537, 100003)])
+def test_c_client_matches_oracle(w, m):
+    out = _run(w, m)
+    d, p = _inputs(w, m)
+    lv, root = O.htree_build(d)
+    assert out["htree_root"] == root.hex()
+    assert out["max_width_exceeded"] == "1"
+    st, terms = O.htree_inclusion_proof(lv, w, w // 3)
+    assert st == 0
+    assert out["htree_proof"] == terms.tobytes().hex()
+    assert out["htree_verify"] == "1"
+    assert out["htree_verify_tampered"] == ("0" if len(terms) else "1")
+
+    t = O.AHtree(cap=m)
+    t.append_batch(p)
+    assert out["ahtree_size"] == str(m)
+    assert out["ahtree_root"] == t.root_at(m)[1].hex()
+    assert out["ahtree_root_half"] == t.root_at(m // 2)[1].hex()
+    st, inc = t.inclusion_proof(m // 3, m)
+    assert st == 0 and out["ahtree_incl"] == inc.tobytes().hex()
+    st, cons = t.consistency_proof(m // 2, m)
+    assert st == 0 and out["ahtree_cons"] == cons.tobytes().hex()
+    assert out["empty_root_at"] == "1"
+
+
+def test_c_client_links_and_reports_no_device():
+    """CPU: the C client resolves every ABI symbol it uses from the shared
+    library and, without a device, fails through the ABI's status path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible: covered by the gpu test")
+    subprocess.run(["make", "-s", "-C", os.path.dirname(CLIENT)], check=True)
+    r = subprocess.run([CLIENT, "8", "8"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "abi 1" in r.stdout, (r.stdout, r.stderr)
+    assert "mh_ctx_create" in r.stderr
