@@ -647,7 +647,10 @@ extern "C" int mh_htree_inclusion_proof_batch(mh_htree *t, uint64_t n, const uin
         if (!n) return MH_OK;
         const uint8_t *lv = t->levels.as<uint8_t>();
         const uint64_t w = t->width;
-        hipStream_t st = t->stream;
+        // the context's scratch is used, so run on the context's stream (after
+        // any mh_dev_* work queued there); the handle's own stream is idle
+        // between host calls (each one synchronises it before returning)
+        hipStream_t st = t->ctx->stream;
         Timer *tm = t->ctx->tm();
         return proof_batch_host(t->ctx, st, n, leaf, nullptr, max_terms, terms, nterms, status,
                                 [&](const uint64_t *a, const uint64_t *, uint8_t *tt, uint32_t *nt,
@@ -1161,7 +1164,7 @@ extern "C" int mh_ahtree_proof_batch(mh_ahtree *t, int kind, uint64_t n, const u
         if (!n) return MH_OK;
         const uint8_t *dl = t->dlog.as<uint8_t>();
         const uint64_t size = t->size;
-        hipStream_t st = t->stream;
+        hipStream_t st = t->ctx->stream;  // ctx scratch: see mh_htree_inclusion_proof_batch
         Timer *tm = t->ctx->tm();
         return proof_batch_host(t->ctx, st, n, i, j, max_terms, terms, nterms, status,
                                 [&](const uint64_t *a, const uint64_t *b, uint8_t *tt, uint32_t *nt,

@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <unordered_map>
 #include <new>
 #include <string>
 #include <vector>
@@ -57,6 +59,9 @@ struct EventTimer : Timer {
         }
         return e;
     }
+    // launches from several threads may interleave: end() closes the record
+    // its own thread opened last (a stack per thread, so scopes may nest)
+    std::unordered_map<std::thread::id, std::vector<size_t>> open;
     void begin(const char *name, hipStream_t st) override {
         std::lock_guard<std::mutex> g(mu);
         Rec r;
@@ -64,11 +69,15 @@ struct EventTimer : Timer {
         r.a = take();
         r.b = take();
         hipEventRecord(r.a, st);
+        open[std::this_thread::get_id()].push_back(recs.size());
         recs.push_back(r);
     }
     void end(hipStream_t st) override {
         std::lock_guard<std::mutex> g(mu);
-        hipEventRecord(recs.back().b, st);
+        auto it = open.find(std::this_thread::get_id());
+        if (it == open.end() || it->second.empty()) return;
+        hipEventRecord(recs[it->second.back()].b, st);
+        it->second.pop_back();
     }
     int sum(const char *prefix, double *ms, uint64_t *cnt) {
         std::lock_guard<std::mutex> g(mu);
@@ -96,6 +105,7 @@ struct EventTimer : Timer {
             pool.push_back(r.b);
         }
         recs.clear();
+        open.clear();
     }
     ~EventTimer() {
         for (auto &r : recs) {

@@ -16,7 +16,10 @@
  *    level-major copy of Go's HTree.levels: level l holds ceil(n/2^l) nodes
  *    (including the promoted odd node) starting at node mh_htree_level_offset.
  *  - mh_htree / mh_ahtree handles are not synchronised (like Go's HTree); use
- *    one handle per goroutine.  An mh_ctx may be shared by many handles.
+ *    one handle per goroutine.  An mh_ctx may be shared by many handles, and
+ *    calls on different handles of one context may run concurrently from
+ *    different threads (the context's scratch is locked and used on its own
+ *    stream only).
  *  - mh_dev_* functions take DEVICE pointers, are asynchronous on the
  *    context's stream and never allocate; all other functions take HOST
  *    pointers and return after the result is in host memory.
