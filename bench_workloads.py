@@ -461,8 +461,16 @@ def run_single(a):
             r = m.txlog_validate(raw_pageable, ctx=ctx)
             assert r[0] == 0 and r[1] == ntx
 
+        # outputs kept across calls in pinned memory, as the cgo shim keeps
+        # its arena (fresh pageable outputs cost page faults on every call)
+        from immustore_amd.txlayer import TX_HEADER
+        outs = (torch.empty(ntx * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy()
+                .view(TX_HEADER),
+                torch.empty(ntx * 32, dtype=torch.uint8).pin_memory().numpy().reshape(ntx, 32),
+                torch.empty(ntx, dtype=torch.int32).pin_memory().numpy())
+
         def step():
-            r = m.txlog_validate(raw, ctx=ctx)
+            r = m.txlog_validate(raw, ctx=ctx, out=outs)
             assert r[0] == 0 and r[1] == ntx
 
         t_pageable = timed(step_pageable, a.steps, a.warmup, sync)
@@ -472,6 +480,26 @@ def run_single(a):
         ctx.set_timing(False)
         names = ("txe_index", "txe_assemble", "sha256_csr", "leaf_for", "seg_level", "tx_alh")
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
+        # breakdown: the host hop alone (mh_txlog_scan, no headers out) and a
+        # plain pinned H2D of the log
+        import ctypes
+        from immustore_amd import _native as Nn
+        lib = Nn.load()
+        cnt, used = ctypes.c_uint64(0), ctypes.c_uint64(0)
+
+        def hop_only():
+            rc = lib.mh_txlog_scan(ctypes.c_void_p(raw.ctypes.data), raw.size, 1024, 1024, ntx,
+                                   ctypes.byref(cnt), ctypes.byref(used), None, None)
+            assert rc == 0 and cnt.value == ntx
+
+        t_hop = timed(hop_only, a.steps, a.warmup, lambda: None)
+        dlog = torch.empty(raw.size, dtype=torch.uint8, device=dev)
+
+        def h2d():
+            dlog.copy_(pin, non_blocking=True)
+
+        t_h2d = timed(h2d, a.steps, a.warmup, sync)
+        del dlog
         _, _, _, _, _, sts = m.txlog_validate(raw, ctx=ctx)
         bad = raw_pageable.copy()
         bad[(ntx // 2) * rec + hdr + 4 + kl + 12] ^= 1  # one hVal of the middle record
@@ -485,6 +513,7 @@ def run_single(a):
                "pageable_input": {"ms_per_step": round(t_pageable * 1e3, 3),
                                   "M_tx_per_s": round(ntx / t_pageable / 1e6, 3)},
                "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
+               "host_hop_only_ms": round(t_hop * 1e3, 3), "h2d_only_ms": round(t_h2d * 1e3, 3),
                "gcomp_per_s_kernels": round(comps / (sum(kt.values()) * 1e-3) / 1e9, 2),
                "all_valid": bool((sts == 0).all()),
                "tamper_detected_exactly": bool(list(np.nonzero(sts_bad)[0]) == [ntx // 2])}

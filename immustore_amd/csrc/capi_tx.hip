@@ -6,6 +6,7 @@
 // per-proof verdicts; every SHA-256 runs in tx_kernels.hip / verify_kernels.hip
 // / htree_kernels.hip.
 #include <cstring>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -644,9 +645,16 @@ void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint
 }
 
 // A position that parses as 3 consecutive records with consecutive ids (or
-// as records up to the end of the log): where a chunk's speculative parse
+// as records up to the end of the log or a zero tail): where a chunk's speculative parse
 // starts.  Only a guess -- the merge accepts a chunk only if the previous
 // chunk's parse ended exactly there.
+bool zero_run(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t n) {
+    const uint64_t e = std::min(len, p + n);
+    for (uint64_t k = p; k < e; k++)
+        if (buf[k]) return false;
+    return true;
+}
+
 uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint64_t to,
                            const HopLimits &lim0) {
     // bounded speculation: a 256 KiB window and candidate records of at most
@@ -661,7 +669,14 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
             uint64_t first, alh, msg;
             bool eof;
             if (hop_record(buf, len, p, lim, h, first, alh, msg, eof) != MH_OK) break;
-            if (eof) { ok = 3; break; }
+            if (eof) {
+                // the end of the log, or a zero-filled preallocated tail after at
+                // least one record -- not 8 zero bytes inside a record (a zero
+                // vOff field read as an id-0 "tail")
+                if (p + 8 <= len && (ok == 0 || !zero_run(buf, len, p, 256))) break;
+                ok = 3;
+                break;
+            }
             if (ok && h.id != prev_id + 1) break;
             prev_id = h.id;
             p = alh + 32;
@@ -678,10 +693,14 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
 void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits &lim,
              HopOut &out, bool want_headers) {
     out.want_headers = want_headers;
-#ifndef MH_HOP_THREADS
-#define MH_HOP_THREADS 8
-#endif
-    unsigned T = std::min((unsigned)MH_HOP_THREADS, std::max(1u, std::thread::hardware_concurrency()));
+    // threads: MH_HOP_THREADS from the environment (read once), default 16,
+    // never more than the machine has
+    static const unsigned kHopThreads = [] {
+        const char *e = getenv("MH_HOP_THREADS");
+        const long v = e ? strtol(e, nullptr, 10) : 16;
+        return (unsigned)std::min(64l, std::max(1l, v));
+    }();
+    unsigned T = std::min(kHopThreads, std::max(1u, std::thread::hardware_concurrency()));
     if (len < (8ull << 20)) T = 1;
     if (T == 1) {
         hop_range(buf, len, 0, ~0ull, max_txs, lim, out);
@@ -771,18 +790,43 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         hipStream_t st = c->stream;
-        if (len) {
-            MH_HIP(c->s_txlog.ensure(len));
-            MH_HIP(hipMemcpyAsync(c->s_txlog.p, buf, len, hipMemcpyHostToDevice, st));
-        }
+        if (len) MH_HIP(c->s_txlog.ensure(len));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
+        // The copy call itself can hold its caller for the whole transfer
+        // (measured: a 75 MB pinned H2D kept the host busy ~1.3 ms), so it is
+        // issued from a helper thread while this one hops; joined before
+        // anything else goes on the stream.
+        hipError_t cp_err = hipSuccess;
+        std::thread cp;
+        if (len) {
+            auto issue = [&]() {
+                hipSetDevice(c->device);
+                cp_err = hipMemcpyAsync(dbuf, buf, len, hipMemcpyHostToDevice, st);
+            };
+            if (len >= (8ull << 20)) {
+                try {
+                    cp = std::thread(issue);
+                } catch (...) {  // no thread: issue it here
+                    issue();
+                }
+            } else {
+                issue();
+            }
+        }
         // ---- host hop (tx.go:419-603): record structure and limits only.  Per
         // entry the host reads the two lengths it needs to find the next entry
         // (several threads over a long log, hop_all); the per-entry index (record
         // offsets, versions, message lengths) is rebuilt on the device from each
         // tx's first entry (k_txe_index).
         HopOut hop;
-        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
+        try {
+            hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
+        } catch (...) {
+            if (cp.joinable()) cp.join();
+            throw;
+        }
+        if (cp.joinable()) cp.join();
+        MH_HIP(cp_err);
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
         // on an error hop.end is the failing record's offset = the end of the last good one

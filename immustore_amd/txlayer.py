@@ -199,29 +199,41 @@ def verify_dual_proof_batch(src_hdrs, tgt_hdrs, md_blob, incl, cons, target_bl_t
 
 def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
                    max_key_len: int = DEFAULT_MAX_KEY_LEN, max_txs: Optional[int] = None,
-                   ctx: Optional[Context] = None):
+                   ctx: Optional[Context] = None, out=None):
     """-> (status, ntx, consumed, hdrs[ntx] TX_HEADER (Eh rebuilt), alh[ntx,32], per_tx[ntx])
 
     status is the structural error that stopped parsing (0 at a clean end);
-    per_tx[k] is 0 or MH_ERR_CORRUPTED_DATA (ALH mismatch)."""
+    per_tx[k] is 0 or MH_ERR_CORRUPTED_DATA (ALH mismatch).
+
+    out: optional (hdrs, alh, per_tx) arrays kept by the caller across calls
+    (e.g. in pinned memory, as a cgo shim keeps its arena); hdrs may be None
+    when the headers are not wanted.  Their length caps the records read."""
     b = _u8(buf)
     cap = max(1, len(b) // 122 + 1)  # a record is >= 122 bytes (90 + 32)
     if max_txs is not None:
         cap = max(1, min(cap, max_txs))
-    # outputs are written for the parsed records only: no zero fill, and the
-    # results are returned as views (no copies of the unused capacity)
-    hd = np.empty(cap, TX_HEADER)
-    alh = np.empty((cap, 32), np.uint8)
-    sts = np.empty(cap, np.int32)
+    if out is not None:
+        hd, alh, sts = out
+        cap = max(1, min(cap, len(alh), len(sts), len(hd) if hd is not None else cap))
+        assert alh.dtype == np.uint8 and alh.shape[1:] == (32,) and sts.dtype == np.int32
+        assert hd is None or hd.dtype == TX_HEADER
+        assert all(a is None or a.flags.c_contiguous for a in out)
+    else:
+        # outputs are written for the parsed records only: no zero fill, and
+        # the results are returned as views (no copies of the unused capacity)
+        hd = np.empty(cap, TX_HEADER)
+        alh = np.empty((cap, 32), np.uint8)
+        sts = np.empty(cap, np.int32)
     ntx, used = C.c_uint64(0), C.c_uint64(0)
     rc = N.load().mh_txlog_validate(_ctx(ctx).handle, _addr(b) if b.size else None, b.size,
                                     max_entries, max_key_len,
                                     cap if max_txs is None else min(cap, max_txs), C.byref(ntx),
-                                    C.byref(used), _addr(hd), _addr(alh), _addr(sts))
+                                    C.byref(used), _addr(hd) if hd is not None else None,
+                                    _addr(alh), _addr(sts))
     if rc < 0:
         N.check(rc)
     k = ntx.value
-    return rc, k, used.value, hd[:k], alh[:k], sts[:k]
+    return rc, k, used.value, (hd[:k] if hd is not None else None), alh[:k], sts[:k]
 
 
 def txlog_scan(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,

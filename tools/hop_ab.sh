@@ -1,5 +1,7 @@
-cd "$GRAFT_REPO_ROOT"
-for r in 1 2; do for lib in "" build/lib_t16.so build/lib_t4.so; do
-  MH_LIB_PATH=$lib timeout -k 10 120 python -u bench_workloads.py --workload txlog > gpurun_out/hop_ab.json 2>/dev/null || exit 1
-  python3 -c "import json;d=json.load(open('gpurun_out/hop_ab.json'));print('${lib:-t8}', d['ms_per_step'], d['pageable_input']['ms_per_step'])"
-done; done
+# tx-log validation A/B by host hop thread count (MH_HOP_THREADS, read at run time)
+# usage on the box: bash tools/hop_ab.sh  -> gpurun_out/hopab.log
+set -e
+for t in 8 16 12 16 8; do
+  echo "threads=$t" >> gpurun_out/hopab.log
+  MH_HOP_THREADS=$t timeout -k 10 120 python bench_workloads.py --workload txlog --steps 30 --warmup 3 >> gpurun_out/hopab.log 2>&1
+done
