@@ -12,7 +12,8 @@ cd ../../build/obj_asan
      -fno-gpu-sanitize -o ../lib_asan.so *.o
 cd ../..
 ASAN=$(find /opt/rocm/lib/llvm -name "libclang_rt.asan-x86_64.so" | head -1)
-export LD_PRELOAD=$ASAN ASAN_OPTIONS=detect_leaks=0 MH_LIB_PATH=build/lib_asan.so
+# the sanitizer runtime goes first; anything already preloaded stays in the list
+export LD_PRELOAD="$ASAN${LD_PRELOAD:+:$LD_PRELOAD}" ASAN_OPTIONS=detect_leaks=0 MH_LIB_PATH=build/lib_asan.so
 python -m pytest tests/test_txlog_scan_cpu.py tests/test_abi.py -q -p no:cacheprovider
 python - <<'PY'
 import sys; sys.path.insert(0, '.')
