@@ -478,7 +478,7 @@ def run_single(a):
         ctx.set_timing(True)
         t = timed(step, a.steps, a.warmup, sync)
         ctx.set_timing(False)
-        names = ("txe_index", "txe_assemble", "sha256_csr", "leaf_for", "seg_level", "tx_alh")
+        names = ("tx_hdr_from_raw", "txe_index", "txe_leaf", "small_roots", "seg_level", "tx_alh")
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
         # breakdown: the host hop alone (mh_txlog_scan, no headers out) and a
         # plain pinned H2D of the log

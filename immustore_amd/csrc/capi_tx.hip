@@ -836,11 +836,10 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
             return rc;
         }
-        uint64_t E = 0, msg_total = 0, wmax = 0;
+        uint64_t E = 0, wmax = 0;
         for (const HopRec &r : hop.R) {
             E += r.nent;
             wmax = std::max<uint64_t>(wmax, r.nent);
-            msg_total += r.msg;
         }
         // ---- device: headers, entry index, digests, trees, Alh
         // small trees (every tx here: a handful of entries) get their roots one
@@ -848,12 +847,11 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         const bool small = wmax <= kSmallTreeMax;
         Layout L;
         const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
-                       b_ml = L.add(E * 8), b_mo = L.add((E + 1) * 8), b_msg = L.add(msg_total),
-                       b_dig = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
+                       b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
                        b_h = L.add(ntx * sizeof(mh_tx_header)), b_es = L.add(ntx * 8),
                        b_ro = L.add(ntx * 8), b_ap = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
                        b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
-                       b_st = L.add(ntx * 4), b_tmp = L.add(pb_scan_temp_bytes(E));
+                       b_st = L.add(ntx * 4);
         MH_HIP(c->s_tx.ensure(L.total));
         uint8_t *base = c->s_tx.as<uint8_t>();
         // record offsets, Alh positions and leaf offsets are contiguous in the
@@ -886,22 +884,19 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         MH_HIP(hipMemcpyAsync(base + b_ro, pin, idx_bytes, hipMemcpyHostToDevice, st));
         MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), ntx, dbuf, (const uint64_t *)(base + b_ro),
                                       (MhTxHeader *)(base + b_h), (uint64_t *)(base + b_es)));
-        // per-entry index, then entry digests (tx.go:578-585 -> 690-731)
+        // per-entry index, then entry digests hashed in place from the raw
+        // entry records (tx.go:578-585 -> 690-731); small trees take the
+        // leaves straight away (htree.go:79-83)
         MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
                                 (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
-                                (uint64_t *)(base + b_rec), base + b_ver, (uint64_t *)(base + b_ml)));
-        MH_HIP(scan_offsets_u64(st, E, (const uint64_t *)(base + b_ml), (uint64_t *)(base + b_mo),
-                                base + b_tmp));
-        MH_HIP(launch_txe_assemble(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec),
-                                   base + b_ver, (const uint64_t *)(base + b_mo), base + b_msg));
-        MH_HIP(launch_sha256_csr(st, c->tm(), base + b_msg, (const uint64_t *)(base + b_mo), E,
-                                 nullptr, nullptr, base + b_dig));
+                                (uint64_t *)(base + b_rec), base + b_ver));
+        MH_HIP(launch_txe_leaf(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec), base + b_ver,
+                               small, base + b_lv));
         // one htree per tx (tx.go:617-621)
         if (small) {
-            MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_dig, base + b_lv));  // htree.go:79-83
             MH_HIP(launch_small_roots(st, c->tm(), ntx, (const uint64_t *)(base + b_lo), base + b_lv,
                                       base + b_eh));
-        } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_dig,
+        } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_lv,
                                             base + b_eh, pin + idx_bytes)) {
             return e;
         }

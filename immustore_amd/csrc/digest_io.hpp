@@ -96,4 +96,69 @@ __device__ inline void sha256_bytes(const uint8_t *p, uint64_t len, int pre, uin
     for (int j = 0; j < 8; j++) out[j] = s.h[j];
 }
 
+// ============================================================================
+// SHA-256 of p[0:la] || p[la+12 : la+44]: an entry-digest message read in
+// place from a raw tx-log entry record (BE16 mdLen | md | BE16 kLen | key |
+// BE32 vLen | BE64 vOff | hVal, tx.go:520-588), skipping the 12 bytes of
+// vLen / vOff between the head and hVal.  Both views of the record have the
+// same alignment (12 = 3 dwords), so every message word is a byte-select of
+// two alignbyte words.  Full blocks may read up to 36 bytes past hVal, still
+// inside the record (its 32-byte Alh follows the last entry); the last block's
+// loads are guarded to [p, p + la + 44).
+// ============================================================================
+__device__ inline void sha256_skip12(const uint8_t *p, uint32_t la, uint32_t out[8]) {
+    State s;
+    s.init();
+    const uint32_t L = la + 32;
+    const uint32_t al = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - al);
+    const uint8_t *end = p + la + 44;
+    const uint32_t nfull = L >> 6;
+    auto word = [&](const uint32_t d[20], int j, uint32_t x0) {
+        const uint32_t w1 = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        const uint32_t w2 = bswap(__builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], al));
+        const int v = (int)la - (int)(x0 + 4 * j);  // head bytes in this word
+        const uint32_t m = v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu << (32 - 8 * v)));
+        return (w1 & m) | (w2 & ~m);
+    };
+    for (uint32_t b = 0; b < nfull; b++) {
+        const uint32_t *qq = base + b * 16;
+        uint32_t d[20], w[16];
+#pragma unroll
+        for (int j = 0; j < 20; j++) d[j] = qq[j];
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = word(d, j, b * 64);
+        compress(s, w);
+    }
+    const uint32_t rem = L - nfull * 64;
+    const uint32_t *qq = base + nfull * 16;
+    uint32_t d[20], w[32];
+#pragma unroll
+    for (int j = 0; j < 20; j++) d[j] = ld_guard(qq + j, p, end);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t x = word(d, j, nfull * 64);
+        const int v = (int)rem - 4 * j;  // valid bytes in this word
+        const uint32_t m = v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu << (32 - 8 * v)));
+        x &= m;
+        if (v >= 0 && v < 4) x |= 0x80u << (24 - 8 * v);
+        w[j] = x;
+    }
+#pragma unroll
+    for (int j = 16; j < 32; j++) w[j] = 0;
+    const uint64_t bits = (uint64_t)L * 8;
+    if (rem < 56) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(s, w);
+    } else {
+        w[30] = (uint32_t)(bits >> 32);
+        w[31] = (uint32_t)bits;
+        compress(s, w);
+        compress(s, w + 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[j] = s.h[j];
+}
+
 }  // namespace mh

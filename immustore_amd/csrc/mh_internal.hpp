@@ -188,11 +188,11 @@ hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
 hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                             const MhTxHeader *hdrs, const uint64_t *ent_start,
-                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver,
-                            uint64_t *msg_len);
-hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
-                               const uint64_t *rec_off, const uint8_t *ver,
-                               const uint64_t *msg_off, uint8_t *msgs);
+                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver);
+// entry digests (leaf = false) or their htree leaves, hashed in place from
+// the raw tx-log entry records (k_txe_leaf)
+hipError_t launch_txe_leaf(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
+                           const uint64_t *rec_off, const uint8_t *ver, bool leaf, uint8_t *out);
 hipError_t launch_seg_level(hipStream_t st, Timer *tm, uint64_t nnodes, uint64_t level_base,
                             uint32_t nitems, const uint64_t *cur_base, const uint64_t *prev_base,
                             const uint64_t *prev_w, uint8_t *nodes);

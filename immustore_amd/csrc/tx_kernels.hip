@@ -195,26 +195,30 @@ __global__ __launch_bounds__(256) void k_advance_chain(
     ok[p] = d == 0;
 }
 
-// Entry-digest messages straight from raw tx-log entry records
-// (tx.go:520-588): a record at rec is  BE16 mdLen | md | BE16 kLen | key |
-// BE32 vLen | BE64 vOff | hVal.  v1 message = record[0 : 4+md+key] || hVal,
-// v0 message = key || hVal (tx.go:690-731).
-__global__ __launch_bounds__(256) void k_txe_assemble(uint64_t n, const uint8_t *__restrict__ buf,
-                                                      const uint64_t *__restrict__ rec_off,
-                                                      const uint8_t *__restrict__ ver,
-                                                      const uint64_t *__restrict__ msg_off,
-                                                      uint8_t *__restrict__ msgs) {
+// Entry digest (tx.go:690-731) -- and, with leaf != 0, its htree leaf
+// SHA256(0x00 || digest) (htree.go:79-83) -- hashed in place from the raw
+// tx-log entry record (sha256_skip12): no message buffer, no offsets scan.
+__global__ __launch_bounds__(256) void k_txe_leaf(uint64_t n, const uint8_t *__restrict__ buf,
+                                                  const uint64_t *__restrict__ rec_off,
+                                                  const uint8_t *__restrict__ ver, int leaf,
+                                                  uint8_t *__restrict__ out) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     const uint8_t *r = buf + rec_off[e];
     const uint32_t ml = ((uint32_t)r[0] << 8) | r[1];
     const uint32_t kl = ((uint32_t)r[2 + ml] << 8) | r[3 + ml];
-    uint8_t *o = msgs + msg_off[e];
-    const uint8_t *src = ver[e] == 1 ? r : r + 4 + ml;
-    const uint32_t head = ver[e] == 1 ? 4 + ml + kl : kl;
-    for (uint32_t k = 0; k < head; k++) *o++ = src[k];
-    const uint8_t *hv = r + 4 + ml + kl + 12;
-    for (int k = 0; k < 32; k++) *o++ = hv[k];
+    uint32_t d[8];
+    if (ver[e] == 1)
+        sha256_skip12(r, 4 + ml + kl, d);
+    else
+        sha256_skip12(r + 4 + ml, kl, d);
+    if (leaf) {
+        uint32_t h[8];
+        leaf_hash(d, h);
+        store_digest(out + e * 32, h);
+    } else {
+        store_digest(out + e * 32, d);
+    }
 }
 
 // TxHeader of each record from the raw tx-log bytes (the fields readHeader
@@ -284,16 +288,13 @@ hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHead
 // Entry index of a run of tx records (tx.go:520-588 readEntry, structure
 // only), one lane per tx: the host hop already validated every length, so
 // the lane walks its entries from ent_start[t] and records each entry's
-// record offset, header version and entry-digest message length
-// (TxEntryDigest_v1_2: BE16 mdLen + md + BE16 kLen + key + hVal; v1_1:
-// key + hVal, tx.go:690-731) for the inclusive scan into msg_off.
+// record offset and header version for k_txe_leaf.
 __global__ __launch_bounds__(256) void k_txe_index(uint64_t ntx, const uint8_t *__restrict__ buf,
                                                    const MhTxHeader *__restrict__ hdrs,
                                                    const uint64_t *__restrict__ ent_start,
                                                    const uint64_t *__restrict__ leaf_off,
                                                    uint64_t *__restrict__ rec_off,
-                                                   uint8_t *__restrict__ ver,
-                                                   uint64_t *__restrict__ msg_len) {
+                                                   uint8_t *__restrict__ ver) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
     const uint8_t v = (uint8_t)hdrs[t].version;
@@ -303,19 +304,17 @@ __global__ __launch_bounds__(256) void k_txe_index(uint64_t ntx, const uint8_t *
         const uint32_t kl = ((uint32_t)buf[q + 2 + ml] << 8) | buf[q + 3 + ml];
         rec_off[e] = q;
         ver[e] = v;
-        msg_len[e] = (v == 1 ? 4 + ml + kl : kl) + 32;
         q += 4 + ml + kl + 12 + 32;
     }
 }
 
 hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                             const MhTxHeader *hdrs, const uint64_t *ent_start,
-                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver,
-                            uint64_t *msg_len) {
+                            const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver) {
     if (!ntx) return hipSuccess;
     TimerScope ts(tm, "txe_index", st);
     hipLaunchKernelGGL(k_txe_index, dim3(grid_for(ntx, 256)), dim3(256), 0, st, ntx, buf, hdrs,
-                       ent_start, leaf_off, rec_off, ver, msg_len);
+                       ent_start, leaf_off, rec_off, ver);
     return hipGetLastError();
 }
 
@@ -478,13 +477,12 @@ hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uin
     return hipGetLastError();
 }
 
-hipError_t launch_txe_assemble(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
-                               const uint64_t *rec_off, const uint8_t *ver,
-                               const uint64_t *msg_off, uint8_t *msgs) {
+hipError_t launch_txe_leaf(hipStream_t st, Timer *tm, uint64_t n, const uint8_t *buf,
+                           const uint64_t *rec_off, const uint8_t *ver, bool leaf, uint8_t *out) {
     if (!n) return hipSuccess;
-    TimerScope ts(tm, "txe_assemble", st);
-    hipLaunchKernelGGL(k_txe_assemble, dim3(grid_for(n, 256)), dim3(256), 0, st, n, buf, rec_off,
-                       ver, msg_off, msgs);
+    TimerScope ts(tm, "txe_leaf", st);
+    hipLaunchKernelGGL(k_txe_leaf, dim3(grid_for(n, 256)), dim3(256), 0, st, n, buf, rec_off, ver,
+                       leaf ? 1 : 0, out);
     return hipGetLastError();
 }
 

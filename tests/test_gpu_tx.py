@@ -125,6 +125,21 @@ def test_txlog_validate_synthetic_vs_oracle(m, ctx, orc):
         assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), cut
 
 
+def test_txlog_validate_message_lengths(m, ctx, orc):
+    """Entry-digest messages hashed in place from the raw records
+    (k_txe_leaf): every key length 0..140 (all padding remainders, one-, two-
+    and three-block messages, each byte alignment) and keys up to the 1024-byte
+    limit, v0 and v1 with every KV-metadata shape."""
+    rng = np.random.default_rng(77)
+    lens = list(range(141)) + [255, 256, 511, 1000, 1019, 1020, 1021, 1022, 1023, 1024]
+    raw = _synthetic_txlog(rng, 200, orc, max_entries=12,
+                           key_len=lambda k, e: lens[(k * 12 + e) % len(lens)])
+    rc, n, used, hdrs, alh, sts = m.txlog_validate(raw, ctx=ctx)
+    o = orc.txlog_validate(raw)
+    assert (rc, n, used) == (o[0], o[1], o[2]) == (0, 200, len(raw))
+    assert np.array_equal(alh, o[3]) and list(sts) == [0] * 200
+
+
 @pytest.mark.parametrize("max_entries", [64, 65, 300])
 def test_txlog_validate_tree_paths(m, ctx, orc, max_entries):
     """Batches whose widest tx has <= 64 entries take the one-lane-per-tree

@@ -32,7 +32,7 @@ def inner_hashes(orc, recs, blob):
     return [orc.tx_header_alh(recs[k], blob)[1] for k in range(len(recs))]
 
 
-def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True):
+def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True, key_len=None):
     """Tx records in the immustore.go:1812-1924 layout with a valid Alh chain
     (the stored alh of each record is the oracle's Alh over its own fields)."""
     out = bytearray()
@@ -45,7 +45,8 @@ def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True):
         for e in range(ne):
             md = b"" if ver == 0 else [b"", b"\x00", b"\x01" + struct.pack(">Q", e), b"\x02",
                                        b"\x00\x01" + struct.pack(">Q", k) + b"\x02"][(k + e) % 5]
-            key = bytes(rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8))
+            kl = key_len(k, e) if key_len else int(rng.integers(0, 70))
+            key = bytes(rng.integers(0, 256, kl, dtype=np.uint8))
             hv = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
             ents += struct.pack(">H", len(md)) + md + struct.pack(">H", len(key)) + key
             ents += struct.pack(">IQ", int(rng.integers(0, 1 << 20)), int(rng.integers(0, 1 << 40)))
