@@ -550,7 +550,7 @@ namespace {
 // kept when asked (mh_txlog_scan); the validation path rebuilds them on the
 // device from the raw record bytes (k_tx_hdr_from_raw).
 struct HopRec {
-    uint64_t rec, alh, msg;
+    uint64_t rec, alh;
     uint32_t nent, pad;
 };
 
@@ -569,10 +569,10 @@ struct HopLimits {
 
 inline uint64_t be16p(const uint8_t *q) { return (uint64_t)((uint32_t)q[0] << 8 | q[1]); }
 
-// Parse the record at p.  Returns MH_OK and fills h / first / alh / msg, or
+// Parse the record at p.  Returns MH_OK and fills h / first / alh, or
 // the structural error; *eof for an id-0 tail or a buffer too short for an id.
 int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &lim,
-               mh_tx_header &h, uint64_t &first, uint64_t &alh, uint64_t &msg, bool &eof) {
+               mh_tx_header &h, uint64_t &first, uint64_t &alh, bool &eof) {
     eof = false;
     if (p + 8 > len) { eof = true; return MH_OK; }
     memset(&h, 0, sizeof h);
@@ -605,8 +605,6 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
     }
     if (h.nentries > lim.max_entries) return MH_ERR_CORRUPTED_MAX_ENTRIES;
     first = q;
-    const uint64_t v1 = h.version == 1;
-    msg = 0;
     for (uint32_t e = 0; e < h.nentries; e++) {
         if (q + 2 > len) return MH_ERR_TRUNCATED;
         const uint64_t ml = be16p(buf + q);
@@ -616,7 +614,6 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
         if (kl > lim.max_key_len) return MH_ERR_CORRUPTED_MAX_KEYLEN;
         if (q + 4 + ml + kl + 12 + 32 > len) return MH_ERR_TRUNCATED;
         q += 4 + ml + kl + 12 + 32;
-        msg += (v1 ? 4 + ml + kl : kl) + 32;
     }
     if (q + 32 > len) return MH_ERR_TRUNCATED;
     alh = q;
@@ -629,15 +626,15 @@ void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint
     o.start = p;
     while (p < stop && o.R.size() < max_recs) {
         mh_tx_header h;
-        uint64_t first = 0, alh = 0, msg = 0;
+        uint64_t first = 0, alh = 0;
         bool eof = false;
-        const int rc = hop_record(buf, len, p, lim, h, first, alh, msg, eof);
+        const int rc = hop_record(buf, len, p, lim, h, first, alh, eof);
         if (rc != MH_OK || eof) {
             o.rc = rc;
             o.stopped = true;
             break;
         }
-        o.R.push_back(HopRec{p, alh, msg, h.nentries, 0});
+        o.R.push_back(HopRec{p, alh, h.nentries, 0});
         if (o.want_headers) o.H.push_back(h);
         p = alh + 32;
     }
@@ -666,9 +663,9 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
         int ok = 0;
         for (; ok < 3; ok++) {
             mh_tx_header h;
-            uint64_t first, alh, msg;
+            uint64_t first, alh;
             bool eof;
-            if (hop_record(buf, len, p, lim, h, first, alh, msg, eof) != MH_OK) break;
+            if (hop_record(buf, len, p, lim, h, first, alh, eof) != MH_OK) break;
             if (eof) {
                 // the end of the log, or a zero-filled preallocated tail after at
                 // least one record -- not 8 zero bytes inside a record (a zero

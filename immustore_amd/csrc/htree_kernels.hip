@@ -526,7 +526,7 @@ __global__ __launch_bounds__(256) void k_leaves_from_digests(const uint8_t *__re
     if (first >= n) return;
     const int c = (int)min<uint64_t>(LPL, n - first);
     LaneReducer<LPL> red;
-#pragma unroll
+#pragma unroll 1  // one node_hash call site (LaneReducer::push)
     for (int i = 0; i < LPL; i++) {
         if (i < c) {
             uint32_t d[8], leaf[8];
