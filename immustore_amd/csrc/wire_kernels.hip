@@ -30,6 +30,7 @@
 // per round, 3.0 ms (8 per round: 3.7 ms, LDS occupancy; 2: 4.0 ms, flush
 // overhead).
 #include <algorithm>
+#include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
 
@@ -172,19 +173,24 @@ __global__ __launch_bounds__(256) void k_pb_dual_size(const uint8_t *__restrict_
 // One lane writes one message.  Bytes collect in a 32-bit register and leave
 // as dword stores; only the partial words at the two ends of a run (shared
 // with the neighbouring messages / records) are written byte by byte.
+// global-memory pointer types: stores through them are global_* rather than
+// flat_* (a pointer rebuilt from an integer or read from LDS is generic)
+typedef __attribute__((address_space(1))) uint8_t g8;
+typedef __attribute__((address_space(1))) uint32_t g32;
+
 struct ByteWriter {
-    uint32_t *w;       // dword that receives the pending bytes
+    g32 *w;            // dword that receives the pending bytes
     uint32_t acc = 0;  // pending bytes, little-endian
     uint32_t fill;     // bytes already in *w's slot (pending or not ours)
     uint32_t lo;       // first byte of the current word that is ours
     __device__ explicit ByteWriter(uint8_t *p)
-        : w(reinterpret_cast<uint32_t *>((uintptr_t)p & ~(uintptr_t)3)),
+        : w((g32 *)((g8 *)p - ((uintptr_t)p & 3))),
           fill((uint32_t)((uintptr_t)p & 3)), lo((uint32_t)((uintptr_t)p & 3)) {}
     __device__ __forceinline__ void flush_word() {  // fill == 4
         if (lo == 0) {
             *w = acc;
         } else {
-            uint8_t *b = reinterpret_cast<uint8_t *>(w);
+            g8 *b = (g8 *)w;
             for (uint32_t k = lo; k < 4; k++) b[k] = (uint8_t)(acc >> (8 * k));
             lo = 0;
         }
@@ -220,10 +226,10 @@ struct ByteWriter {
         put8((uint32_t)v);
     }
     __device__ __forceinline__ void finish() {  // the trailing partial word
-        uint8_t *b = reinterpret_cast<uint8_t *>(w);
+        g8 *b = (g8 *)w;
         for (uint32_t k = lo; k < fill; k++) b[k] = (uint8_t)(acc >> (8 * k));
     }
-    __device__ __forceinline__ uint8_t *pos() const { return reinterpret_cast<uint8_t *>(w) + fill; }
+    __device__ __forceinline__ uint8_t *pos() const { return (uint8_t *)((g8 *)w + fill); }
 };
 
 // A 34-byte field `tag, 32, d[0..31]` (repeated-bytes term or a header
@@ -232,7 +238,12 @@ struct ByteWriter {
 // and stored as 7-8 dwords plus predicated byte / short stores for the
 // partial words at the two ends (a = 0: -/short, 1: byte+short/short+byte,
 // 2: short/-, 3: byte/byte).
-__device__ __forceinline__ void put_rec34(uint8_t *p, uint32_t tag, const uint32_t d[8]) {
+template <int AS>  // address space of the destination: 0 generic, 1 global
+__device__ __forceinline__ void put_rec34_as(uint8_t *pg, uint32_t tag, const uint32_t d[8]) {
+    typedef __attribute__((address_space(AS))) uint8_t b8;
+    typedef __attribute__((address_space(AS))) uint16_t b16;
+    typedef __attribute__((address_space(AS))) uint32_t b32;
+    b8 *p = (b8 *)pg;
     uint32_t r[10];
     r[0] = (tag & 0xff) | (32u << 8) | (d[0] << 16);
 #pragma unroll
@@ -240,24 +251,28 @@ __device__ __forceinline__ void put_rec34(uint8_t *p, uint32_t tag, const uint32
     r[8] = d[7] >> 16;
     r[9] = 0;
     const uint32_t a = (uint32_t)((uintptr_t)p & 3);
-    uint32_t *w = reinterpret_cast<uint32_t *>(p - a);
+    b32 *w = (b32 *)(p - a);
     uint32_t o[10];
     o[0] = r[0] << (8 * a);
 #pragma unroll
     for (int j = 1; j < 10; j++)
         o[j] = a ? __builtin_amdgcn_alignbyte(r[j], r[j - 1], 4 - a) : r[j];
-    uint8_t *wb = reinterpret_cast<uint8_t *>(w);
+    b8 *wb = (b8 *)w;
     // word 0: ours from byte a
     if (a == 0) w[0] = o[0];
     if (a & 1) wb[a] = (uint8_t)(o[0] >> (8 * a));
-    if (a == 1 || a == 2) *reinterpret_cast<uint16_t *>(wb + 2) = (uint16_t)(o[0] >> 16);
+    if (a == 1 || a == 2) *(b16 *)(wb + 2) = (uint16_t)(o[0] >> 16);
 #pragma unroll
     for (int j = 1; j < 8; j++) w[j] = o[j];
     // word 8: ours up to byte a + 34 - 32
     if (a >= 2) w[8] = o[8];
-    if (a <= 1) *reinterpret_cast<uint16_t *>(wb + 32) = (uint16_t)o[8];
+    if (a <= 1) *(b16 *)(wb + 32) = (uint16_t)o[8];
     if (a == 1) wb[34] = (uint8_t)(o[8] >> 16);
     if (a == 3) wb[36] = (uint8_t)o[9];
+}
+
+__device__ __forceinline__ void put_rec34(uint8_t *p, uint32_t tag, const uint32_t d[8]) {
+    put_rec34_as<0>(p, tag, d);
 }
 
 // 32-byte digest field (tag, length 32, bytes; d 8-byte aligned): the byte
@@ -273,7 +288,7 @@ __device__ __forceinline__ void put_digest(ByteWriter &bw, uint32_t tag, const u
     }
     bw.finish();
     uint8_t *p = bw.pos();
-    put_rec34(p, tag, x);
+    put_rec34_as<1>(p, tag, x);
     bw = ByteWriter(p + 34);
 }
 
@@ -366,7 +381,7 @@ __device__ __forceinline__ void staged_records(uint8_t *rec_base, uint32_t cnt, 
                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ga, sl);
             const uint32_t as = (uint32_t)(gs & 3);
             const uint32_t nd = (as + ls + 3) / 4;
-            uint32_t *gw = reinterpret_cast<uint32_t *>(gs - as);
+            g32 *gw = (g32 *)(uintptr_t)(gs - as);
             const uint32_t *lw = reinterpret_cast<const uint32_t *>(wave_lds + sl * kSlotBytes);
             for (uint32_t d = lane; d < nd; d += 64) {
                 const uint32_t lo = d == 0 ? as : 0;
@@ -375,13 +390,148 @@ __device__ __forceinline__ void staged_records(uint8_t *rec_base, uint32_t cnt, 
                 if (lo == 0 && hi == 4) {
                     gw[d] = v;
                 } else {
-                    uint8_t *gb = reinterpret_cast<uint8_t *>(gw + d);
+                    g8 *gb = (g8 *)(gw + d);
                     for (uint32_t e = lo; e < hi; e++) gb[e] = (uint8_t)(v >> (8 * e));
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();  // every span is out before the slots are rebuilt
     }
+}
+
+// ------------------------------------------------------------ wave-dense term records
+// The records of a wave's 64 messages written record-parallel: each lane
+// walks its own proof (the loop form, proof_walk.hpp) into an LDS index list
+// -- the lists of the wave back to back, at the wave's exclusive prefix of the
+// term counts -- and then the wave writes the flattened records with one
+// lane per 34-byte record, consecutive records on consecutive lanes, two
+// records per lane in flight.  Node indices are 32-bit: the host takes this
+// path only when the tree has fewer than 2^32 nodes (else staged_records).
+// Lists that do not fit kIdxCap go in chunks of whole messages.
+#ifndef MH_PB_IDXCAP
+#define MH_PB_IDXCAP 4096
+#endif
+constexpr uint32_t kIdxCap = MH_PB_IDXCAP;
+#ifndef MH_PB_UNROLL
+#define MH_PB_UNROLL 2
+#endif
+constexpr uint32_t kPbUnroll = MH_PB_UNROLL;  // records per lane in flight
+static_assert(kIdxCap >= 256, "a message's list (<= 130 terms) must fit a chunk");
+struct WaveRecLds {
+    uint32_t idx[kIdxCap];
+    uint32_t pre[65];
+    uint64_t base[64];
+};
+
+// walk(emit) runs the loop-form walk of the calling lane and returns its term
+// count; emit(q, node) gets the terms in walk order (proof position cnt-1-q).
+// Called by the whole wave (blockDim 64); lanes without records pass cnt 0.
+template <class Walk>
+__device__ __forceinline__ void wave_records(uint8_t *rec_base, uint32_t cnt, uint32_t tag,
+                                             Walk &&walk, const uint8_t *__restrict__ nodes,
+                                             WaveRecLds &L, int lane, bool *bad) {
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t excl = incl - cnt;
+    __syncthreads();  // a previous call's records are out of L
+    L.pre[lane] = excl;
+    if (lane == 63) L.pre[64] = incl;
+    L.base[lane] = (uint64_t)(uintptr_t)rec_base;
+    uint32_t m0 = 0;
+    while (m0 < 64) {
+        const uint32_t base0 = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)m0);
+        const uint64_t fit = __ballot(lane >= (int)m0 && incl - base0 <= kIdxCap);
+        const uint32_t m1 = m0 + max(1u, (uint32_t)__popcll(fit));
+        const uint32_t T =
+            min(kIdxCap, (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)(m1 - 1)) - base0);
+        __syncthreads();  // the previous chunk's records are out of L.idx
+        if ((uint32_t)lane >= m0 && (uint32_t)lane < m1 && cnt) {
+            uint32_t *dst = L.idx + (excl - base0);
+            const uint32_t c = walk([&](uint32_t q, uint64_t node) {
+                if (q < cnt) dst[cnt - 1 - q] = (uint32_t)node;
+            });
+            if (c != cnt || cnt > kIdxCap) {  // size pass and writer disagree: never seen
+                for (uint32_t k = 0; k < min(cnt, kIdxCap); k++) dst[k] = 0;
+                *bad = true;
+            }
+        }
+        __syncthreads();
+        uint32_t m = m0;
+        auto locate = [&](uint32_t r) {  // message of flattened record r (m only moves forward)
+            while (m + 1 < m1 && L.pre[m + 1] - base0 <= r) m++;
+            return m;
+        };
+        for (uint32_t r0 = 0; r0 < T; r0 += 64 * kPbUnroll) {
+            uint32_t x[kPbUnroll][8];
+            uint8_t *pr[kPbUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kPbUnroll; u++) {  // kPbUnroll gathers in flight
+                const uint32_t r = r0 + 64 * u + lane;
+                pr[u] = nullptr;
+                if (r < T) {
+                    const uint32_t mr = locate(r);
+                    pr[u] = reinterpret_cast<uint8_t *>(L.base[mr]) + 34ull * (r - (L.pre[mr] - base0));
+                    load_node(nodes + (uint64_t)L.idx[r] * 32, x[u]);
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kPbUnroll; u++)
+                if (pr[u]) put_rec34_as<1>(pr[u], tag, x[u]);  // global stores
+        }
+        m0 = m1;
+    }
+}
+
+// DualProofV2 writer over wave_records: one wave per block, lane per message
+// for the headers (ByteWriter) and the walks.
+__global__ __launch_bounds__(64) void k_pb_dual_write_w(const uint8_t *__restrict__ dlog,
+                                                        uint64_t size, uint64_t n,
+                                                        const MhTxHeader *__restrict__ src,
+                                                        const MhTxHeader *__restrict__ tgt,
+                                                        const uint8_t *__restrict__ md_blob,
+                                                        const uint64_t *__restrict__ off,
+                                                        const uint32_t *__restrict__ cnt,
+                                                        uint8_t *__restrict__ out, uint64_t out_cap,
+                                                        int32_t *__restrict__ status) {
+    __shared__ WaveRecLds L;
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const int lane = threadIdx.x;
+    bool active = p < n && status[p] == MH_OK;
+    if (active && off[p + 1] > out_cap) {
+        status[p] = MH_ERR_BUFFER_TOO_SMALL;
+        active = false;
+    }
+    uint8_t *rec = out;
+    uint32_t ni = 0, nc = 0;
+    uint64_t ii = 1, ij = 1, ci = 1;
+    if (active) {
+        const MhTxHeader &S = src[p], &T = tgt[p];
+        const PbDual d = pb_dual(S, T, md_blob, size);
+        uint8_t *o = out + off[p];
+        ByteWriter bw(o);
+        put_header(bw, 0x0a, S, d.s, md_blob);
+        put_header(bw, 0x12, T, d.t, md_blob);
+        bw.finish();
+        rec = o + framed(d.s.body) + framed(d.t.body);
+        if (d.proofs) {
+            ni = cnt[2 * p];
+            nc = cnt[2 * p + 1];
+            ii = d.ii;
+            ij = d.ij;
+            ci = d.ci;
+        }
+    }
+    if (!__any(ni + nc > 0)) return;  // wave-uniform (one wave per block)
+    bool bad = false;
+    wave_records(rec, ni, 0x1a, [&](auto &&emit) { return ahtree_walk(false, ii, ij, emit); },
+                 dlog, L, lane, &bad);
+    wave_records(rec + 34ull * ni, nc, 0x22,
+                 [&](auto &&emit) { return ahtree_walk(true, ci, ij, emit); }, dlog, L, lane, &bad);
+    if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
 }
 
 // One lane per message: header fields streamed from registers, term records
@@ -494,6 +644,41 @@ __global__ __launch_bounds__(256) void k_pb_incl_write(const uint8_t *__restrict
     if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
 }
 
+__global__ __launch_bounds__(64) void k_pb_incl_write_w(const uint8_t *__restrict__ levels,
+                                                        uint64_t w, uint64_t n,
+                                                        const uint64_t *__restrict__ leaf,
+                                                        const uint64_t *__restrict__ off,
+                                                        const uint32_t *__restrict__ cnt,
+                                                        uint8_t *__restrict__ out, uint64_t out_cap,
+                                                        int32_t *__restrict__ status) {
+    __shared__ WaveRecLds L;
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const int lane = threadIdx.x;
+    bool active = p < n && status[p] == MH_OK;
+    if (active && off[p + 1] > out_cap) {
+        status[p] = MH_ERR_BUFFER_TOO_SMALL;
+        active = false;
+    }
+    uint8_t *rec = out;
+    uint32_t c = 0;
+    uint64_t i = 0;
+    if (active) {
+        i = leaf[p];
+        uint8_t *o = out + off[p];
+        ByteWriter bw(o);
+        if ((uint32_t)i) { bw.put8(0x08); bw.varint(i32v((uint32_t)i)); }
+        if ((uint32_t)w) { bw.put8(0x10); bw.varint(i32v((uint32_t)w)); }
+        bw.finish();
+        rec = o + pb_incl_prefix(i, w);
+        c = cnt[2 * p];
+    }
+    if (!__any(c > 0)) return;
+    bool bad = false;
+    wave_records(rec, c, 0x1a, [&](auto &&emit) { return htree_walk(i, w, emit); }, levels, L,
+                 lane, &bad);
+    if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
+}
+
 // ------------------------------------------------------------ launchers
 size_t pb_scan_temp_bytes(uint64_t n) {
     size_t bytes = 0;
@@ -528,6 +713,13 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }
 
+// MH_PB_STAGED=1 in the environment (read per launch) forces the staged
+// writers, the path of trees with >= 2^32 nodes, so the tests cover both.
+static bool pb_force_staged() {
+    const char *e = getenv("MH_PB_STAGED");
+    return e && e[0] == '1';
+}
+
 hipError_t launch_pb_dual_v2(hipStream_t st, Timer *tm, int phase, const uint8_t *dlog,
                              uint64_t size, uint64_t n, const MhTxHeader *src,
                              const MhTxHeader *tgt, const uint8_t *md_blob, uint8_t *out,
@@ -545,8 +737,12 @@ hipError_t launch_pb_dual_v2(hipStream_t st, Timer *tm, int phase, const uint8_t
     }
     if (phase & 2) {
         TimerScope ts(tm, "pb_dual_write", st);
-        hipLaunchKernelGGL(k_pb_dual_write, dim3(grid_for(n, 256)), dim3(256), 0, st, dlog, size,
-                           n, src, tgt, md_blob, off, cnt, out, out_cap, status);
+        if (ahtree_nodes_upto(size) < (1ull << 32) && !pb_force_staged())  // 32-bit node indices
+            hipLaunchKernelGGL(k_pb_dual_write_w, dim3(grid_for(n, 64)), dim3(64), 0, st, dlog,
+                               size, n, src, tgt, md_blob, off, cnt, out, out_cap, status);
+        else
+            hipLaunchKernelGGL(k_pb_dual_write, dim3(grid_for(n, 256)), dim3(256), 0, st, dlog,
+                               size, n, src, tgt, md_blob, off, cnt, out, out_cap, status);
         if (hipError_t e = hipGetLastError()) return e;
     }
     return hipSuccess;
@@ -568,8 +764,12 @@ hipError_t launch_pb_inclusion(hipStream_t st, Timer *tm, int phase, const uint8
     }
     if (phase & 2) {
         TimerScope ts(tm, "pb_incl_write", st);
-        hipLaunchKernelGGL(k_pb_incl_write, dim3(grid_for(n, 256)), dim3(256), 0, st, levels, w, n,
-                           leaf, off, cnt, out, out_cap, status);
+        if (w < (1ull << 31) && !pb_force_staged())  // < 2^32 level nodes: 32-bit indices
+            hipLaunchKernelGGL(k_pb_incl_write_w, dim3(grid_for(n, 64)), dim3(64), 0, st, levels,
+                               w, n, leaf, off, cnt, out, out_cap, status);
+        else
+            hipLaunchKernelGGL(k_pb_incl_write, dim3(grid_for(n, 256)), dim3(256), 0, st, levels,
+                               w, n, leaf, off, cnt, out, out_cap, status);
         if (hipError_t e = hipGetLastError()) return e;
     }
     return hipSuccess;

@@ -141,6 +141,17 @@ def wire(orc):
     return wire
 
 
+@pytest.fixture(params=["wave", "staged"])
+def writer(request, monkeypatch):
+    """both protobuf record writers: wave-dense (trees below 2^32 nodes, the
+    default) and staged (larger trees; forced with MH_PB_STAGED=1)."""
+    if request.param == "staged":
+        monkeypatch.setenv("MH_PB_STAGED", "1")
+    else:
+        monkeypatch.delenv("MH_PB_STAGED", raising=False)
+    return request.param
+
+
 def _rec_hdr(r, blob):
     return {"id": int(r["id"]), "ts": int(r["ts"]), "bltxid": int(r["bl_tx_id"]),
             "blroot": r["bl_root"].tobytes(), "prevalh": r["prev_alh"].tobytes(),
@@ -148,7 +159,7 @@ def _rec_hdr(r, blob):
             "md": blob[int(r["md_off"]):int(r["md_off"]) + int(r["md_len"])]}
 
 
-def test_dual_proof_v2_pb_fixture_stores(m, ctx, orc, wire, fixtures):
+def test_dual_proof_v2_pb_fixture_stores(m, ctx, orc, wire, fixtures, writer):
     from tx_util import headers_from_fixture
     for name, fx in fixtures.items():
         pay = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
@@ -200,7 +211,7 @@ def _random_headers(rng, n_tx, with_md=True):
     return recs, bytes(blob)
 
 
-def test_dual_proof_v2_pb_random_vs_oracle(m, ctx, orc, wire):
+def test_dual_proof_v2_pb_random_vs_oracle(m, ctx, orc, wire, writer):
     rng = np.random.default_rng(91)
     N_TX = 70000
     pay = rng.integers(0, 256, (N_TX, 32), dtype=np.uint8)
@@ -225,7 +236,7 @@ def test_dual_proof_v2_pb_random_vs_oracle(m, ctx, orc, wire):
     assert (st == 0).sum() > 2900
 
 
-def test_htree_inclusion_proof_pb_vs_oracle(m, ctx, orc, wire):
+def test_htree_inclusion_proof_pb_vs_oracle(m, ctx, orc, wire, writer):
     rng = np.random.default_rng(17)
     for w in [1, 2, 3, 1000, (1 << 18) + 3]:
         d = rng.integers(0, 256, (w, 32), dtype=np.uint8)
@@ -239,7 +250,7 @@ def test_htree_inclusion_proof_pb_vs_oracle(m, ctx, orc, wire):
             assert st[k] == est and msgs[k] == eb, (w, int(i))
 
 
-def test_pb_device_phases_and_capacity(m, ctx, orc, wire):
+def test_pb_device_phases_and_capacity(m, ctx, orc, wire, writer):
     """phase 1 (sizes/offsets) then phase 2 (write) through the device ABI; a
     too-small output marks exactly the messages past the capacity."""
     from immustore_amd import _native as N
