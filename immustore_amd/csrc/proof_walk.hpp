@@ -57,9 +57,10 @@ struct HtreeWalk {
 };
 
 // The same walk as a loop calling emit(q, node): with an empty emit (term
-// counting) the compiler drops the index math entirely.
-template <class F>
-__device__ __forceinline__ uint32_t htree_walk(uint64_t i, uint64_t w, F &&emit) {
+// counting) the compiler drops the index math entirely.  lo(layer) gives
+// level_off(w, layer) (a table when many proofs share one width).
+template <class LO, class F>
+__device__ __forceinline__ uint32_t htree_walk_lo(uint64_t i, uint64_t w, LO &&lo, F &&emit) {
     uint32_t q = 0;
     if (w <= 1) return 0;
     uint64_t m = i, nn = w, offset = 0;
@@ -79,11 +80,16 @@ __device__ __forceinline__ uint32_t htree_walk(uint64_t i, uint64_t w, F &&emit)
             offset += k;
         }
         const int layer = bits_len(r - l);
-        emit(q, level_off(w, layer) + (l >> layer));
+        emit(q, lo(layer) + (l >> layer));
         q++;
         if (nn < 1 || (nn == 1 && m == 0)) break;
     }
     return q;
+}
+
+template <class F>
+__device__ __forceinline__ uint32_t htree_walk(uint64_t i, uint64_t w, F &&emit) {
+    return htree_walk_lo(i, w, [&](int layer) { return level_off(w, layer); }, emit);
 }
 
 __device__ __forceinline__ uint64_t aht_node_index(uint64_t n, int l) {

@@ -652,8 +652,10 @@ __global__ __launch_bounds__(64) void k_pb_incl_write_w(const uint8_t *__restric
                                                         uint8_t *__restrict__ out, uint64_t out_cap,
                                                         int32_t *__restrict__ status) {
     __shared__ WaveRecLds L;
+    __shared__ uint64_t loff[64];  // level_off(w, l): one table per block
     const uint64_t p = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     const int lane = threadIdx.x;
+    loff[lane] = level_off(w, lane);
     bool active = p < n && status[p] == MH_OK;
     if (active && off[p + 1] > out_cap) {
         status[p] = MH_ERR_BUFFER_TOO_SMALL;
@@ -674,8 +676,11 @@ __global__ __launch_bounds__(64) void k_pb_incl_write_w(const uint8_t *__restric
     }
     if (!__any(c > 0)) return;
     bool bad = false;
-    wave_records(rec, c, 0x1a, [&](auto &&emit) { return htree_walk(i, w, emit); }, levels, L,
-                 lane, &bad);
+    wave_records(rec, c, 0x1a,
+                 [&](auto &&emit) {
+                     return htree_walk_lo(i, w, [&](int l) { return loff[l]; }, emit);
+                 },
+                 levels, L, lane, &bad);
     if (bad) status[p] = MH_ERR_ILLEGAL_STATE;
 }
 
