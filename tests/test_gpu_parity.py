@@ -505,3 +505,64 @@ def test_ahtree_proof_batch_vs_oracle(m, ctx, orc):
     _, _, st = t.proof_batch(0, [5, 1, 0], [4, N_ + 1, 0])
     assert list(st) == [2, 5, 5]
     t.close()
+
+
+def _aht_verify_csr(m, ctx, kind, i, j, terms, nt, a, b):
+    """mh_ahtree_verify_batch over device-generated proofs (terms[n, max, 32],
+    nt[n]) as a CSR term list -> ok[n]."""
+    from immustore_amd import _native as N
+    mask = np.arange(terms.shape[1])[None, :] < nt[:, None]
+    flat = np.ascontiguousarray(terms[mask]) if nt.sum() else np.zeros((1, 32), np.uint8)
+    off = np.zeros(len(i) + 1, np.uint64)
+    off[1:] = np.cumsum(nt.astype(np.uint64))
+    ok = np.zeros(len(i), np.uint8)
+    vi = np.ascontiguousarray(i, np.uint64)
+    vj = np.ascontiguousarray(j, np.uint64)
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    N.check(N.load().mh_ahtree_verify_batch(ctx.handle, kind, len(i), vi.ctypes.data,
+                                            vj.ctypes.data, off.ctypes.data, flat.ctypes.data,
+                                            a.ctypes.data, b.ctypes.data, ok.ctypes.data, None))
+    return ok.astype(bool)
+
+
+def test_ahtree_reset_reference_sequence(m, ctx):
+    """The reference's TestReset (embedded/ahtree/ahtree_test.go:759-850) on
+    the device: 32 one-byte appends, ResetSize(0), 1024 appends of byte(i),
+    ResetSize(N+1) -> ErrCannotResetToLargerSize, ResetSize(1024), ResetSize(512);
+    then for every 1 <= i <= j <= 512 the inclusion and consistency proofs
+    verify against RootAt, and VerifyLastInclusion(InclusionProof(i, 512), i,
+    leaf_i, RootAt(i)) holds only for i == 512 (ahtree/verification.go)."""
+    from immustore_amd import _native as N
+    t = m.AHtree(ctx)
+    for i in range(1, 33):
+        t.append(bytes([i]))
+    t.reset_size(0)
+    assert t.size() == 0
+    n = 1024
+    for i in range(1, n + 1):
+        t.append(bytes([i & 0xFF]))  # Go: byte(i)
+    with pytest.raises(m.ErrCannotResetToLargerSize):
+        t.reset_size(n + 1)
+    t.reset_size(n)
+    assert t.size() == n
+    n = 512
+    t.reset_size(n)
+    assert t.size() == n
+    leaf = np.stack([np.frombuffer(H(b"\x00" + bytes([i & 0xFF])), np.uint8) for i in range(n + 1)])
+    root = np.stack([np.zeros(32, np.uint8)] +
+                    [np.frombuffer(t.root_at(k), np.uint8) for k in range(1, n + 1)])
+    I, J = np.triu_indices(n, 0)
+    I = (I + 1).astype(np.uint64)
+    J = (J + 1).astype(np.uint64)
+    terms, nt, st = t.proof_batch(N.MH_AHT_INCLUSION, I, J, max_terms=32)
+    assert (st == 0).all()
+    assert _aht_verify_csr(m, ctx, N.MH_AHT_INCLUSION, I, J, terms, nt, leaf[I], root[J]).all()
+    terms, nt, st = t.proof_batch(N.MH_AHT_CONSISTENCY, I, J, max_terms=32)
+    assert (st == 0).all()
+    assert _aht_verify_csr(m, ctx, N.MH_AHT_CONSISTENCY, I, J, terms, nt, root[I], root[J]).all()
+    K = np.arange(1, n + 1, dtype=np.uint64)
+    terms, nt, st = t.proof_batch(N.MH_AHT_INCLUSION, K, np.full(n, n, np.uint64), max_terms=32)
+    assert (st == 0).all()
+    ok = _aht_verify_csr(m, ctx, N.MH_AHT_LAST_INCLUSION, K, K, terms, nt, leaf[K], root[K])
+    assert list(np.nonzero(ok)[0] + 1) == [n]
