@@ -64,6 +64,9 @@ def parse():
                         "(c3 / c5: one GPU, GPU part from bench_workloads.py)")
     p.add_argument("--entries", type=int, default=None, help="override entries per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--launch-check", action="store_true",
+                   help="only bring up the N-rank process group (gloo, no GPU work) and print "
+                        "its world size: tests the --gpus N launcher on a CPU host")
     p.add_argument("--inflight", type=int, default=3,
                    help="independent builds in flight on separate streams (1 = sequential)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -227,8 +230,50 @@ def secondary_config(a):
     print(json.dumps(out), flush=True)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_ranks(a):
+    """--gpus N > 1 without a launcher (WORLD_SIZE unset): start N ranks under
+    torch.distributed.run as a CHILD process -- before this process touches the
+    GPU -- and exit with its status.  Never runs N > 1 as one silent rank."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(a):
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    if world != a.gpus:
+        raise SystemExit("process group has %d ranks, --gpus %d" % (world, a.gpus))
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world,
+                          "process_group": {"backend": "gloo" if world > 1 else None,
+                                            "world_size": world}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(relaunch_ranks(a))
+    if a.launch_check:
+        return launch_check(a)
     if a.config in ("c3", "c5"):
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("--config c3/c5 here is one GPU; multi-GPU: bench_workloads.py "
@@ -242,7 +287,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world != 1:
+    if a.gpus != world:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
     dist = None
     # one process per GPU; MH_DIST_BACKEND=gloo rehearses several ranks on
@@ -260,6 +305,9 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit("process group has %d ranks, --gpus %d"
+                             % (dist.get_world_size(), a.gpus))
 
     # D builds in flight (--inflight), each on its own HIP stream with its own
     # level buffers: the latency-bound top of one tree overlaps the leaf
@@ -388,6 +436,8 @@ def main():
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
+        "process_group": {"backend": backend if dist else None,
+                          "world_size": dist.get_world_size() if dist else 1},
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),

@@ -117,6 +117,7 @@ extern "C" int mh_ctx_destroy(mh_ctx *c) {
 extern "C" int mh_ctx_synchronize(mh_ctx *c) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         MH_HIP(hipStreamSynchronize(c->stream));
         return MH_OK;
     });
@@ -135,6 +136,7 @@ extern "C" int mh_ctx_set_timing(mh_ctx *c, int enable) {
 extern "C" int mh_ctx_timing(mh_ctx *c, const char *prefix, double *total_ms, uint64_t *launches) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         return c->timer.sum(prefix, total_ms, launches);
     });
 }
@@ -142,6 +144,7 @@ extern "C" int mh_ctx_timing(mh_ctx *c, const char *prefix, double *total_ms, ui
 extern "C" int mh_ctx_timing_reset(mh_ctx *c) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         c->timer.reset();
         return MH_OK;
     });
@@ -158,6 +161,7 @@ extern "C" int mh_dev_alloc(mh_ctx *c, uint64_t bytes, void **dptr) {
 extern "C" int mh_dev_free(mh_ctx *c, void *dptr) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         MH_HIP(hipFree(dptr));
         return MH_OK;
     });
@@ -180,6 +184,7 @@ extern "C" int mh_host_free_pinned(void *hptr) {
 extern "C" int mh_memcpy_h2d(mh_ctx *c, void *dst, const void *src, uint64_t bytes) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (!bytes) return MH_OK;
         MH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
         return MH_OK;
@@ -189,6 +194,7 @@ extern "C" int mh_memcpy_h2d(mh_ctx *c, void *dst, const void *src, uint64_t byt
 extern "C" int mh_memcpy_d2h(mh_ctx *c, void *dst, const void *src, uint64_t bytes) {
     return mh_guard([&]() -> int {
         if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (!bytes) return MH_OK;
         MH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
         return MH_OK;
@@ -198,6 +204,7 @@ extern "C" int mh_memcpy_d2h(mh_ctx *c, void *dst, const void *src, uint64_t byt
 extern "C" int mh_dev_fill_random(mh_ctx *c, void *dptr, uint64_t nbytes, uint64_t seed) {
     return mh_guard([&]() -> int {
         if (!c || (!dptr && nbytes)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (!nbytes) return MH_OK;
         MH_HIP(launch_fill_random(c->stream, (uint8_t *)dptr, nbytes, seed));
         return MH_OK;
@@ -207,6 +214,7 @@ extern "C" int mh_dev_fill_random(mh_ctx *c, void *dptr, uint64_t nbytes, uint64
 extern "C" int mh_dev_fill_keys_be64(mh_ctx *c, void *dptr, uint64_t n, uint64_t first) {
     return mh_guard([&]() -> int {
         if (!c || (!dptr && n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (((uintptr_t)dptr) & 7) return MH_ERR_ILLEGAL_ARGUMENTS;
         MH_HIP(launch_fill_keys_be64(c->stream, (uint8_t *)dptr, n, first));
         return MH_OK;
@@ -275,6 +283,7 @@ extern "C" int mh_dev_htree_build_digests(mh_ctx *c, const uint8_t *digests, uin
                                           uint8_t *levels, uint8_t *root) {
     return mh_guard([&]() -> int {
         if (!c || (n && (!digests || !levels))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (((uintptr_t)digests & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
         g.init(n);
@@ -292,6 +301,7 @@ extern "C" int mh_dev_htree_build_entries_fixed(mh_ctx *c, int version, uint64_t
                                                 uint8_t *hvals_out, uint8_t *levels, uint8_t *root) {
     return mh_guard([&]() -> int {
         if (!c || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (n && (!levels || (!keys && key_len) || (!vals && val_len))) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (((uintptr_t)levels & 15) || ((uintptr_t)hvals_out & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
@@ -332,6 +342,7 @@ extern "C" int mh_dev_htree_build_entries(mh_ctx *c, int version, uint64_t n, co
                                           uint8_t *levels, uint8_t *root) {
     return mh_guard([&]() -> int {
         if (!c || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (n && (!levels || !key_off || !val_off)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
@@ -368,6 +379,7 @@ extern "C" int mh_dev_htree_reduce_nodes(mh_ctx *c, const uint8_t *nodes, uint64
                                          uint8_t *levels, uint8_t *root) {
     return mh_guard([&]() -> int {
         if (!c || (w && (!nodes || !levels))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (((uintptr_t)nodes & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
         g.init(w);
@@ -383,6 +395,7 @@ extern "C" int mh_dev_sha256_batch(mh_ctx *c, const uint8_t *buf, const uint64_t
                                    uint8_t *out) {
     return mh_guard([&]() -> int {
         if (!c || (n && (!off || !out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         MH_HIP(launch_sha256_csr(c->stream, c->tm(), buf, off, n, nullptr, nullptr, out));
         return MH_OK;
     });
@@ -420,6 +433,7 @@ extern "C" int mh_htree_new(mh_ctx *c, uint64_t max_width, mh_htree **out) {
 extern "C" int mh_htree_free(mh_htree *t) {
     return mh_guard([&]() -> int {
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(t->ctx->device));
         hipStreamSynchronize(t->stream);
         hipStreamDestroy(t->stream);
         if (t->pinned) hipHostFree(t->pinned);
@@ -579,6 +593,7 @@ extern "C" int mh_htree_inclusion_proof(mh_htree *t, uint64_t i, uint8_t *terms,
     return mh_guard([&]() -> int {
         // htree.go:121-164: index walk on the host, terms gathered from HBM.
         if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(t->ctx->device));
         *nterms = 0;
         if (i >= t->width) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (t->width == 1) return MH_OK;
@@ -644,6 +659,7 @@ extern "C" int mh_htree_inclusion_proof_batch(mh_htree *t, uint64_t n, const uin
     return mh_guard([&]() -> int {
         if (!t || (n && (!leaf || !terms || !nterms || !status || !max_terms)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(t->ctx->device));
         if (!n) return MH_OK;
         const uint8_t *lv = t->levels.as<uint8_t>();
         const uint64_t w = t->width;
@@ -679,6 +695,7 @@ extern "C" int mh_dev_htree_inclusion_proof_batch(mh_ctx *c, const uint8_t *leve
 extern "C" int mh_htree_levels(mh_htree *t, uint8_t *out, uint64_t cap_nodes) {
     return mh_guard([&]() -> int {
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(t->ctx->device));
         const uint64_t total = mh_htree_levels_len(t->width);
         if (cap_nodes < total || (total && !out)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!total) return MH_OK;
@@ -704,6 +721,7 @@ extern "C" int mh_dev_htree_verify_inclusion_batch(mh_ctx *c, uint64_t np, const
     return mh_guard([&]() -> int {
         if (!c || (np && (!leaf || !width || !term_off || !digests || !roots || !ok)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (!np) return MH_OK;
         MH_HIP(launch_htree_verify(c->stream, c->tm(), np, leaf, width, term_off, terms, digests, roots,
                                    ok));
@@ -756,6 +774,7 @@ extern "C" int mh_dev_ahtree_verify_batch(mh_ctx *c, int kind, uint64_t np, cons
                                           uint8_t *ok, uint8_t *eval_out) {
     return mh_guard([&]() -> int {
         if (!c || kind < 0 || kind > 2) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
         if (np && (!i || !j || !term_off || !a || !b || !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!np) return MH_OK;
         MH_HIP(launch_ahtree_verify(c->stream, c->tm(), kind, np, i, j, term_off, terms, a, b, ok,
@@ -939,6 +958,7 @@ extern "C" int mh_ahtree_new(mh_ctx *c, mh_ahtree **out) {
 extern "C" int mh_ahtree_free(mh_ahtree *t) {
     return mh_guard([&]() -> int {
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(t->ctx->device));
         hipStreamSynchronize(t->stream);
         hipStreamDestroy(t->stream);
         delete t;
@@ -970,6 +990,7 @@ static int aht_append_batch(mh_ahtree *t, const uint8_t *payloads, uint64_t m, u
                             uint64_t p_off0, uint8_t *plog_out, uint8_t *clog_out,
                             uint8_t *roots_out) {
     if (!t || !logs_ok(payloads, m, plen, p_off0)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
     if (!m) return MH_OK;
     hipSetDevice(t->ctx->device);
     int st = aht_reserve(t, t->size + m);
@@ -1025,6 +1046,8 @@ extern "C" int mh_ahtree_append(mh_ahtree *t, const uint8_t *payload, uint64_t p
     return mh_guard([&]() -> int {
         // ahtree.go:246-373 (d == nil -> ErrIllegalArguments, ahtree.go:258-261)
         if (!t || (!payload && plen)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         if (!payload) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (plen > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
         uint8_t root[32];
@@ -1039,6 +1062,7 @@ extern "C" int mh_ahtree_append(mh_ahtree *t, const uint8_t *payload, uint64_t p
 extern "C" int mh_ahtree_size(mh_ahtree *t, uint64_t *size) {
     return mh_guard([&]() -> int {
         if (!t || !size) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
         *size = t->size;
         return MH_OK;
     });
@@ -1056,6 +1080,8 @@ extern "C" int mh_ahtree_root_at(mh_ahtree *t, uint64_t n, uint8_t root[32]) {
     return mh_guard([&]() -> int {
         // ahtree.go:749-771
         if (!t || !root) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         if (n == 0) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (t->size == 0) return MH_ERR_EMPTY_TREE;
         if (n > t->size) return MH_ERR_UNEXISTENT_DATA;
@@ -1067,6 +1093,8 @@ extern "C" int mh_ahtree_root_at(mh_ahtree *t, uint64_t n, uint8_t root[32]) {
 extern "C" int mh_ahtree_root(mh_ahtree *t, uint64_t *n, uint8_t root[32]) {
     return mh_guard([&]() -> int {
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         if (t->size == 0) return MH_ERR_EMPTY_TREE;  // ahtree.go:731-734
         if (n) *n = t->size;
         return mh_ahtree_root_at(t, t->size, root);
@@ -1130,6 +1158,8 @@ extern "C" int mh_ahtree_inclusion_proof(mh_ahtree *t, uint64_t i, uint64_t j, u
                                          uint32_t cap, uint32_t *nterms) {
     return mh_guard([&]() -> int {
         if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         *nterms = 0;
         if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;    // ahtree.go:534-536
         if (j > t->size) return MH_ERR_UNEXISTENT_DATA;  // ahtree.go:538-540
@@ -1144,6 +1174,8 @@ extern "C" int mh_ahtree_consistency_proof(mh_ahtree *t, uint64_t i, uint64_t j,
                                            uint32_t cap, uint32_t *nterms) {
     return mh_guard([&]() -> int {
         if (!t || !nterms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         *nterms = 0;
         if (i > j) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (j > t->size) return MH_ERR_UNEXISTENT_DATA;
@@ -1161,6 +1193,8 @@ extern "C" int mh_ahtree_proof_batch(mh_ahtree *t, int kind, uint64_t n, const u
         if (!t || (kind != MH_AHT_INCLUSION && kind != MH_AHT_CONSISTENCY) ||
             (n && (!i || !j || !terms || !nterms || !status || !max_terms)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         if (!n) return MH_OK;
         const uint8_t *dl = t->dlog.as<uint8_t>();
         const uint64_t size = t->size;
@@ -1195,6 +1229,7 @@ extern "C" int mh_ahtree_reset_size(mh_ahtree *t, uint64_t new_size) {
     return mh_guard([&]() -> int {
         // ahtree.go:375-458 (file-size checks belong to the Go appendables)
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
         if (new_size > t->size) return MH_ERR_CANNOT_RESET_TO_LARGER;
         t->size = new_size;
         return MH_OK;
@@ -1204,6 +1239,8 @@ extern "C" int mh_ahtree_reset_size(mh_ahtree *t, uint64_t new_size) {
 extern "C" int mh_ahtree_dlog(mh_ahtree *t, uint64_t first, uint64_t count, uint8_t *out) {
     return mh_guard([&]() -> int {
         if (!t) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
+        MH_HIP(hipSetDevice(t->ctx->device));
         const uint64_t total = ahtree_nodes_upto(t->size);
         if (first > total || count > total - first) return MH_ERR_UNEXISTENT_DATA;
         if (!count) return MH_OK;
@@ -1218,6 +1255,7 @@ extern "C" int mh_ahtree_dlog(mh_ahtree *t, uint64_t first, uint64_t count, uint
 extern "C" int mh_ahtree_dlog_device(mh_ahtree *t, const uint8_t **dptr) {
     return mh_guard([&]() -> int {
         if (!t || !dptr) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
         *dptr = t->dlog.as<uint8_t>();
         return MH_OK;
     });

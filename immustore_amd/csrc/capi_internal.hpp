@@ -192,6 +192,11 @@ struct mh_ahtree {
     mh_ctx *ctx = nullptr;
     hipStream_t stream = nullptr;
     uint64_t size = 0;
+    // every mh_ahtree_* call holds this for its whole duration, like the Go
+    // AHtree's t.mutex (ahtree.go:60-84): readers (Root, proofs, dLog reads)
+    // may run concurrently with a committer's Append, which can reallocate
+    // the dLog.  Recursive: Append / Root call other locked entry points.
+    std::recursive_mutex mu;
     DevBuf dlog, in, roots, idx, out, ctr;
     DevBuf w_in, w_out;  // wire formats (capi_wire.hip)
 };

@@ -613,6 +613,9 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
         const uint64_t kl = be16p(buf + q + 2 + ml);
         if (kl > lim.max_key_len) return MH_ERR_CORRUPTED_MAX_KEYLEN;
         if (q + 4 + ml + kl + 12 + 32 > len) return MH_ERR_TRUNCATED;
+        // a v0 header cannot carry KV metadata: TxEntryDigest_v1_1 fails the
+        // read with ErrMetadataUnsupported (tx.go:690-693, via readEntry)
+        if (h.version == 0 && ml > 0) return MH_ERR_METADATA_UNSUPPORTED;
         q += 4 + ml + kl + 12 + 32;
     }
     if (q + 32 > len) return MH_ERR_TRUNCATED;

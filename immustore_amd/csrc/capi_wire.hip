@@ -101,6 +101,7 @@ extern "C" int mh_ahtree_dual_proof_v2_pb_batch(mh_ahtree *t, uint64_t n, const 
                                                 uint64_t out_cap, uint64_t *off, int32_t *status) {
     return mh_guard([&]() -> int {
         if (!t || !off || (n && (!src || !tgt || !status))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::recursive_mutex> lk_(t->mu);  // AHtree.mutex (ahtree.go:60-84)
         if (!n) {
             off[0] = 0;
             return MH_OK;

@@ -15,8 +15,13 @@
  *  - digests are 32 raw bytes (Go [sha256.Size]byte); "levels" is the flat
  *    level-major copy of Go's HTree.levels: level l holds ceil(n/2^l) nodes
  *    (including the promoted odd node) starting at node mh_htree_level_offset.
- *  - mh_htree / mh_ahtree handles are not synchronised (like Go's HTree); use
- *    one handle per goroutine.  An mh_ctx may be shared by many handles, and
+ *  - mh_htree handles are not synchronised (like Go's HTree, one per pooled
+ *    Tx, tx.go:70); use one per goroutine.  mh_ahtree handles ARE
+ *    synchronised like Go's AHtree (t.mutex, ahtree.go:60-84): every
+ *    mh_ahtree_* call holds the handle's lock, so readers (root, proofs,
+ *    dLog reads) may run concurrently with appends.  A device pointer from
+ *    mh_ahtree_dlog_device is valid only until the next append that grows
+ *    the dLog.  An mh_ctx may be shared by many handles, and
  *    calls on different handles of one context may run concurrently from
  *    different threads (the context's scratch is locked and used on its own
  *    stream only).

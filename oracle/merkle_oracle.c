@@ -777,6 +777,57 @@ int orc_ahtree_verify_last_inclusion(const uint8_t *terms, uint32_t nterms, uint
     return memcmp(r, root, 32) == 0;
 }
 
+/* Batch of ahtree VerifyInclusion / VerifyConsistency / VerifyLastInclusion
+ * calls (ahtree/verification.go:21-137) over CSR term lists, split over
+ * nthreads host threads; ok[p] = the Go verifier's bool.  The CPU side of the
+ * ahtree half of BASELINE configs[4].  Returns the number verified. */
+typedef struct {
+    int kind;
+    uint64_t lo, hi;
+    const uint64_t *i, *j, *term_off;
+    const uint8_t *terms, *a, *b;
+    uint8_t *ok;
+    uint64_t cnt;
+} aht_vjob;
+
+static void *aht_verify_worker(void *arg) {
+    aht_vjob *J = (aht_vjob *)arg;
+    for (uint64_t p = J->lo; p < J->hi; p++) {
+        const uint8_t *t = J->terms + J->term_off[p] * 32;
+        const uint32_t nt = (uint32_t)(J->term_off[p + 1] - J->term_off[p]);
+        int r;
+        if (J->kind == 0)
+            r = orc_ahtree_verify_inclusion(t, nt, J->i[p], J->j[p], J->a + 32 * p, J->b + 32 * p);
+        else if (J->kind == 1)
+            r = orc_ahtree_verify_consistency(t, nt, J->i[p], J->j[p], J->a + 32 * p, J->b + 32 * p);
+        else
+            r = orc_ahtree_verify_last_inclusion(t, nt, J->i[p], J->a + 32 * p, J->b + 32 * p);
+        J->ok[p] = (uint8_t)r;
+        J->cnt += (uint64_t)r;
+    }
+    return NULL;
+}
+
+uint64_t orc_ahtree_verify_batch(int kind, uint64_t n, const uint64_t *i, const uint64_t *j,
+                                 const uint64_t *term_off, const uint8_t *terms, const uint8_t *a,
+                                 const uint8_t *b, uint8_t *ok, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    aht_vjob jobs[64];
+    pthread_t th[64];
+    for (int t = 0; t < nthreads; t++) {
+        aht_vjob J = {kind, n * t / nthreads, n * (t + 1) / nthreads, i, j, term_off, terms, a, b, ok, 0};
+        jobs[t] = J;
+        pthread_create(&th[t], NULL, aht_verify_worker, &jobs[t]);
+    }
+    uint64_t cnt = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        cnt += jobs[t].cnt;
+    }
+    return cnt;
+}
+
 /* ------------------------------------------------------------ synthetic */
 void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed) {
     /* word w = splitmix64 output number w+1 from state `seed` (little endian) */

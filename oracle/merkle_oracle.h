@@ -55,6 +55,14 @@ uint64_t orc_htree_verify_batch(uint64_t n, const uint64_t *leaf, uint64_t width
                                 const uint8_t *terms, uint32_t nterms_each,
                                 const uint8_t *digests, const uint8_t root[32], uint8_t *ok);
 
+/* n ahtree Verify{Inclusion,Consistency,LastInclusion} calls (kind 0/1/2,
+ * ahtree/verification.go:21-137) over CSR term lists (term_off[n+1], in
+ * 32-byte terms), a / b = leaf / root, iroot / jroot, leaf / root per proof;
+ * nthreads host threads.  Returns how many verify, ok[p] per proof. */
+uint64_t orc_ahtree_verify_batch(int kind, uint64_t n, const uint64_t *i, const uint64_t *j,
+                                 const uint64_t *term_off, const uint8_t *terms, const uint8_t *a,
+                                 const uint8_t *b, uint8_t *ok, int nthreads);
+
 /* Value hash loop (embedded/store/immustore.go:1620-1630) + Tx.BuildHashTree
  * (embedded/store/tx.go:332-355): CSR inputs (offsets have n+1 entries).
  * md / md_off may be NULL (no KV metadata).  hval_override / use_override

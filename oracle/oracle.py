@@ -74,6 +74,9 @@ def lib():
         L.orc_htree_verify_batch.restype = C.c_uint64
         L.orc_htree_verify_batch.argtypes = [C.c_uint64, u64p, C.c_uint64, u8p, C.c_uint32, u8p,
                                              u8p, u8p]
+        L.orc_ahtree_verify_batch.restype = C.c_uint64
+        L.orc_ahtree_verify_batch.argtypes = [C.c_int, C.c_uint64, u64p, u64p, u64p, u8p, u8p,
+                                              u8p, u8p, C.c_int]
         L.orc_verify_linear_proof.argtypes = [C.c_uint64, C.c_uint64, u8p, C.c_uint32, C.c_uint64,
                                               C.c_uint64, u8p, u8p]
         L.orc_verify_linear_advance_proof.argtypes = [C.c_int, u8p, C.c_uint32, u8p, u32p,
@@ -449,4 +452,23 @@ def htree_verify_batch(leaf, width, terms, digests, root):
     ok = np.zeros(max(n, 1), np.uint8)
     c = lib().orc_htree_verify_batch(n, _p(lf, u64p), width, _p(t), D, _p(d), _p(_u8(root)),
                                      _p(ok))
+    return c, ok[:n]
+
+
+def ahtree_verify_batch(kind, i, j, term_off, terms, a, b, nthreads=1):
+    """kind 0/1/2 = VerifyInclusion / VerifyConsistency / VerifyLastInclusion
+    over CSR proofs: term_off (n+1,) u64 in terms, terms (T,32), a/b (n,32).
+    Returns (count verified, ok[n])."""
+    iv = np.ascontiguousarray(i, np.uint64)
+    jv = np.ascontiguousarray(j, np.uint64)
+    to = np.ascontiguousarray(term_off, np.uint64)
+    t = np.ascontiguousarray(terms, np.uint8).reshape(-1, 32)
+    if t.shape[0] == 0:
+        t = np.zeros((1, 32), np.uint8)
+    av = np.ascontiguousarray(a, np.uint8)
+    bv = np.ascontiguousarray(b, np.uint8)
+    n = iv.shape[0]
+    ok = np.zeros(max(n, 1), np.uint8)
+    c = lib().orc_ahtree_verify_batch(kind, n, _p(iv, u64p), _p(jv, u64p), _p(to, u64p), _p(t),
+                                      _p(av), _p(bv), _p(ok), nthreads)
     return c, ok[:n]

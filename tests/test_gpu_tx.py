@@ -125,6 +125,23 @@ def test_txlog_validate_synthetic_vs_oracle(m, ctx, orc):
         assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), cut
 
 
+def test_txlog_validate_v0_entry_with_kv_metadata(m, ctx, orc):
+    """a v0 record whose entry carries KV metadata fails the
+    read with ErrMetadataUnsupported (tx.go:690-693); validation stops there
+    with the records before it validated, as in the oracle."""
+    import struct
+    rng = np.random.default_rng(12)
+    good = _synthetic_txlog(rng, 9, orc, version_mix=False)
+    for md in (b"\x00", b"\x02", b"\x00\x02"):
+        ent = struct.pack(">H", len(md)) + md + struct.pack(">H", 4) + b"keyz"
+        ent += struct.pack(">IQ", 5, 9) + bytes(32)
+        rec = struct.pack(">QQQ", 10, 1, 0) + bytes(64) + struct.pack(">HH", 0, 1) + ent + bytes(32)
+        a = m.txlog_validate(good + rec, ctx=ctx)
+        b = orc.txlog_validate(good + rec)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]) == (6, 9, len(good))
+        assert list(a[5]) == list(b[4]) == [0] * 9 and np.array_equal(a[4], b[3])
+
+
 def test_txlog_validate_message_lengths(m, ctx, orc):
     """Entry-digest messages hashed in place from the raw records
     (k_txe_leaf): every key length 0..140 (all padding remainders, one-, two-

@@ -81,3 +81,20 @@ def test_scan_parallel_hop_matches_sequential(txl, orc):
     assert (a[0], a[1]) == (0, 3)
     same(txl, orc, recs, max_entries=1000)  # MaxTxEntries exceeded in the first record
     same(txl, orc, recs[:len(recs) // 2], max_entries=1 << 20)
+
+
+def test_scan_v0_entry_with_kv_metadata(txl, orc):
+    """A v0 record whose entry carries KV metadata: TxEntryDigest_v1_1 fails
+    the read with ErrMetadataUnsupported (tx.go:690-693 via readEntry,
+    tx.go:582-588); the hop stops before that record."""
+    import struct
+    rng = np.random.default_rng(11)
+    good = _synthetic_txlog(rng, 6, orc, version_mix=False)
+    for md in (b"\x00", b"\x02", b"\x01" + struct.pack(">Q", 7)):
+        ent = struct.pack(">H", len(md)) + md + struct.pack(">H", 3) + b"key"
+        ent += struct.pack(">IQ", 5, 9) + bytes(32)
+        rec = struct.pack(">QQQ", 7, 1, 0) + bytes(64) + struct.pack(">HH", 0, 1) + ent + bytes(32)
+        for buf in (rec, good + rec):
+            a = same(txl, orc, buf)
+            assert a[0] == 6  # MH_ERR_METADATA_UNSUPPORTED
+            assert a[1] == (0 if buf is rec else 6)
