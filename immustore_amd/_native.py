@@ -31,6 +31,9 @@ MH_ERR_CORRUPTED_MAX_KEYLEN = 16
 MH_ERR_CORRUPTED_UNKNOWN_VERSION = 17
 MH_ERR_TRUNCATED = 18
 MH_ERR_BUFFER_TOO_SMALL = 19
+MH_ERR_INVALID_PROOF = 20
+MH_ERR_UNSUPPORTED_TX_VERSION = 21
+MH_ERR_INVALID_PROOF_ENTRY = 22
 
 MH_AHT_INCLUSION = 0
 MH_AHT_CONSISTENCY = 1
@@ -127,6 +130,18 @@ class ErrBufferTooSmall(MerkleError):
     pass
 
 
+class ErrInvalidProof(MerkleError):
+    """store.ErrInvalidProof (immustore.go:114)"""
+
+
+class ErrInvalidProofEntry(ErrInvalidProof):
+    """store.ErrInvalidProof from VerifyDocument's entry check (verification.go:60-76)"""
+
+
+class ErrUnsupportedTxVersion(MerkleError):
+    """store.ErrUnsupportedTxVersion (immustore.go:90)"""
+
+
 class HipError(MerkleError):
     pass
 
@@ -151,6 +166,9 @@ _ERRORS = {
     MH_ERR_CORRUPTED_UNKNOWN_VERSION: ErrCorruptedTxDataUnknownHeaderVersion,
     MH_ERR_TRUNCATED: ErrUnexpectedEOF,
     MH_ERR_BUFFER_TOO_SMALL: ErrBufferTooSmall,
+    MH_ERR_INVALID_PROOF: ErrInvalidProof,
+    MH_ERR_UNSUPPORTED_TX_VERSION: ErrUnsupportedTxVersion,
+    MH_ERR_INVALID_PROOF_ENTRY: ErrInvalidProofEntry,
 }
 
 vp = C.c_void_p
@@ -238,6 +256,12 @@ SIGNATURES = {
     "mh_verify_dual_proof_v2_batch": (i32, [vp, u64, vp, vp, u8p, u64, vp, u8p, vp, u8p, vp, vp,
                                             u8p, u8p, vp]),
     "mh_verify_dual_proof_batch": (i32, [vp, vp, u8p]),
+    "mh_verify_document_batch": (i32, [vp, vp, vp, u8p]),
+    "mh_commit_queue_new": (i32, [vp, i32, u64, u32, u32, C.POINTER(vp)]),
+    "mh_commit_queue_free": (i32, [vp]),
+    "mh_commit_queue_submit": (i32, [vp, u64, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p, u8p,
+                                     u8p]),
+    "mh_commit_queue_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
                                 u8p, vp]),
     "mh_commit_pipe_new": (i32, [vp, u64, C.POINTER(vp)]),

@@ -50,6 +50,10 @@ extern "C" const char *mh_status_string(int st) {
         case MH_ERR_CORRUPTED_MAX_KEYLEN: return "tx data is corrupted: maximum key length exceeded";
         case MH_ERR_CORRUPTED_UNKNOWN_VERSION: return "tx data is corrupted: unknown TX header version";
         case MH_ERR_TRUNCATED: return "unexpected EOF";
+        case MH_ERR_BUFFER_TOO_SMALL: return "output buffer too small";
+        case MH_ERR_INVALID_PROOF: return "invalid proof";
+        case MH_ERR_UNSUPPORTED_TX_VERSION: return "unsupported tx version";
+        case MH_ERR_INVALID_PROOF_ENTRY: return "invalid proof: document entry";
         default: return st < 0 ? hipGetErrorString((hipError_t)(-st)) : "unknown status";
     }
 }

@@ -1,0 +1,253 @@
+// capi_queue.hip -- group commit for the single-transaction precommit path.
+//
+// In the reference every committer hashes its own transaction before taking
+// the store lock: precommit's value-hash loop and Tx.BuildHashTree
+// (immustore.go:1620-1632, the lock is taken at :1689), from up to
+// MaxConcurrency = 30 goroutines at once (options.go:35).  One transaction of
+// a few entries is far too little work for a GPU launch sequence, so the
+// library coalesces them: every committer submits its one transaction and
+// blocks; a worker thread gathers what arrives within a short window (or a
+// full batch), packs it into one pinned arena, runs one mh_precommit_batch
+// over the commit pipe (value hashes, entry digests, one htree per tx -- all
+// on the device) and hands each committer its own hVals, Eh and status.
+//
+// Lock order: q->mu is never held while the device works.
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+
+#include "capi_internal.hpp"
+
+struct mh_commit_queue {
+    mh_ctx *ctx = nullptr;
+    mh_commit_pipe *pipe = nullptr;
+    int version = 1;
+    uint64_t max_width = 0;
+    uint32_t max_txs = 64;
+    uint32_t wait_us = 50;
+
+    struct Req {
+        uint64_t n;
+        const uint8_t *keys, *md, *vals, *ov, *use, *expect;
+        const uint64_t *key_off, *md_off, *val_off;
+        uint8_t *hvals_out, *eh_out;
+        int32_t status = MH_OK;
+        bool done = false;
+    };
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<Req *> pending;
+    bool stop = false;
+    std::thread worker;
+    // packing arenas (pinned: the pipe's copies are then DMA)
+    PinBuf in, out;
+    // counters (mh_commit_queue_stats)
+    uint64_t batches = 0, txs = 0;
+};
+
+namespace {
+
+// One batch: pack, hash on the device, scatter.
+int run_batch(mh_commit_queue *q, std::vector<mh_commit_queue::Req *> &B) {
+    const uint64_t nt = B.size();
+    uint64_t ne = 0, kb = 0, mb = 0, vb = 0;
+    bool any_md = false, any_ov = false;
+    for (auto *r : B) {
+        ne += r->n;
+        if (r->n) {
+            kb += r->key_off[r->n] - r->key_off[0];
+            vb += r->val_off[r->n] - r->val_off[0];
+            if (r->md_off) mb += r->md_off[r->n] - r->md_off[0];
+        }
+        any_md |= r->md_off != nullptr;
+        any_ov |= r->use != nullptr;
+    }
+    Layout L;
+    const uint64_t b_tx = L.add((nt + 1) * 8), b_ko = L.add((ne + 1) * 8),
+                   b_mo = L.add(any_md ? (ne + 1) * 8 : 0), b_vo = L.add((ne + 1) * 8),
+                   b_k = L.add(kb), b_m = L.add(mb), b_v = L.add(vb),
+                   b_ov = L.add(any_ov ? ne * 32 : 0), b_use = L.add(any_ov ? ne : 0);
+    Layout O;
+    const uint64_t o_hv = O.add(ne * 32), o_eh = O.add(nt * 32), o_st = O.add(nt * 4);
+    MH_HIP(q->in.ensure(L.total));
+    MH_HIP(q->out.ensure(O.total));
+    uint8_t *in = q->in.as<uint8_t>(), *out = q->out.as<uint8_t>();
+    uint64_t *tx_off = (uint64_t *)(in + b_tx), *ko = (uint64_t *)(in + b_ko),
+             *mo = any_md ? (uint64_t *)(in + b_mo) : nullptr, *vo = (uint64_t *)(in + b_vo);
+    uint64_t e = 0, kp = 0, mp = 0, vp = 0;
+    tx_off[0] = 0;
+    ko[0] = mo ? (mo[0] = 0) : 0;
+    vo[0] = 0;
+    for (uint64_t t = 0; t < nt; t++) {
+        const mh_commit_queue::Req *r = B[t];
+        for (uint64_t i = 0; i < r->n; i++, e++) {
+            const uint64_t kl = r->key_off[i + 1] - r->key_off[i];
+            const uint64_t vl = r->val_off[i + 1] - r->val_off[i];
+            if (kl) memcpy(in + b_k + kp, r->keys + r->key_off[i], kl);
+            if (vl) memcpy(in + b_v + vp, r->vals + r->val_off[i], vl);
+            kp += kl;
+            vp += vl;
+            ko[e + 1] = kp;
+            vo[e + 1] = vp;
+            if (mo) {
+                const uint64_t ml = r->md_off ? r->md_off[i + 1] - r->md_off[i] : 0;
+                if (ml) memcpy(in + b_m + mp, r->md + r->md_off[i], ml);
+                mp += ml;
+                mo[e + 1] = mp;
+            }
+            if (any_ov) {
+                const bool u = r->use && r->use[i];
+                in[b_use + e] = u ? 1 : 0;
+                if (u) memcpy(in + b_ov + e * 32, r->ov + i * 32, 32);
+            }
+        }
+        tx_off[t + 1] = e;
+    }
+    int32_t *st = (int32_t *)(out + o_st);
+    int rc = mh_precommit_batch(q->pipe, q->version, q->max_width, nt, tx_off, in + b_k, ko,
+                                any_md ? in + b_m : nullptr, mo, in + b_v, vo,
+                                any_ov ? in + b_ov : nullptr, any_ov ? in + b_use : nullptr,
+                                nullptr, out + o_hv, out + o_eh, st);
+    if (rc != MH_OK) return rc;
+    e = 0;
+    for (uint64_t t = 0; t < nt; t++) {
+        mh_commit_queue::Req *r = B[t];
+        int32_t s = st[t];
+        const uint8_t *eh = out + o_eh + t * 32;
+        // ReplicateTx's check, immustore.go:1649-1654
+        if (s == MH_OK && r->expect && memcmp(r->expect, eh, 32)) s = MH_ERR_ILLEGAL_ARGUMENTS;
+        if (r->hvals_out && r->n) memcpy(r->hvals_out, out + o_hv + e * 32, r->n * 32);
+        if (r->eh_out) memcpy(r->eh_out, eh, 32);
+        r->status = s;
+        e += r->n;
+    }
+    return MH_OK;
+}
+
+void worker_loop(mh_commit_queue *q) {
+    hipSetDevice(q->ctx->device);
+    std::vector<mh_commit_queue::Req *> B;
+    for (;;) {
+        std::unique_lock<std::mutex> lk(q->mu);
+        q->cv_work.wait(lk, [&] { return q->stop || !q->pending.empty(); });
+        if (q->pending.empty()) break;  // stop requested, nothing left
+        // gather: until the window closes or a full batch is waiting
+        const auto deadline =
+            std::chrono::steady_clock::now() + std::chrono::microseconds(q->wait_us);
+        while (!q->stop && q->pending.size() < q->max_txs) {
+            if (q->cv_work.wait_until(lk, deadline) == std::cv_status::timeout) break;
+        }
+        B.clear();
+        while (!q->pending.empty() && B.size() < q->max_txs) {
+            B.push_back(q->pending.front());
+            q->pending.pop_front();
+        }
+        lk.unlock();
+        int rc = MH_ERR_ILLEGAL_STATE;
+        try {
+            rc = run_batch(q, B);
+        } catch (const std::bad_alloc &) {
+            rc = MH_ERR_OUT_OF_MEMORY;
+        } catch (...) {
+            rc = MH_ERR_ILLEGAL_STATE;
+        }
+        lk.lock();
+        for (auto *r : B) {
+            if (rc != MH_OK) r->status = rc;
+            r->done = true;
+        }
+        q->batches++;
+        q->txs += B.size();
+        lk.unlock();
+        q->cv_done.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" int mh_commit_queue_new(mh_ctx *c, int version, uint64_t max_width, uint32_t max_txs,
+                                   uint32_t wait_us, mh_commit_queue **out) {
+    return mh_guard([&]() -> int {
+        if (!c || !out || (version != 0 && version != 1)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        *out = nullptr;
+        MH_HIP(hipSetDevice(c->device));
+        mh_commit_queue *q = new mh_commit_queue();
+        q->ctx = c;
+        q->version = version;
+        q->max_width = max_width;
+        q->max_txs = max_txs ? max_txs : 64;
+        q->wait_us = wait_us;
+        int st = mh_commit_pipe_new(c, 0, &q->pipe);
+        if (st != MH_OK) {
+            delete q;
+            return st;
+        }
+        q->worker = std::thread(worker_loop, q);
+        *out = q;
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_commit_queue_free(mh_commit_queue *q) {
+    return mh_guard([&]() -> int {
+        if (!q) return MH_OK;
+        {
+            std::lock_guard<std::mutex> lk(q->mu);
+            q->stop = true;
+        }
+        q->cv_work.notify_all();
+        if (q->worker.joinable()) q->worker.join();  // drains what is pending first
+        mh_commit_pipe_free(q->pipe);
+        delete q;
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_commit_queue_submit(mh_commit_queue *q, uint64_t n, const uint8_t *keys,
+                                      const uint64_t *key_off, const uint8_t *md,
+                                      const uint64_t *md_off, const uint8_t *vals,
+                                      const uint64_t *val_off, const uint8_t *hval_override,
+                                      const uint8_t *use_override, const uint8_t *expect_eh,
+                                      uint8_t *hvals_out, uint8_t *eh_out) {
+    return mh_guard([&]() -> int {
+        if (!q) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n && (!key_off || !val_off)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((md == nullptr) != (md_off == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        for (uint64_t i = 0; i < n; i++)
+            if (key_off[i + 1] < key_off[i] || val_off[i + 1] < val_off[i] ||
+                (md_off && md_off[i + 1] < md_off[i]))
+                return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n && ((key_off[n] > key_off[0] && !keys) || (val_off[n] > val_off[0] && !vals)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        mh_commit_queue::Req r;
+        r.n = n;
+        r.keys = keys;
+        r.key_off = key_off;
+        r.md = md;
+        r.md_off = md_off;
+        r.vals = vals;
+        r.val_off = val_off;
+        r.ov = hval_override;
+        r.use = use_override;
+        r.expect = expect_eh;
+        r.hvals_out = hvals_out;
+        r.eh_out = eh_out;
+        std::unique_lock<std::mutex> lk(q->mu);
+        if (q->stop) return MH_ERR_ILLEGAL_STATE;
+        q->pending.push_back(&r);
+        q->cv_work.notify_one();
+        q->cv_done.wait(lk, [&] { return r.done; });
+        return r.status;
+    });
+}
+
+extern "C" int mh_commit_queue_stats(mh_commit_queue *q, uint64_t *batches, uint64_t *txs) {
+    return mh_guard([&]() -> int {
+        if (!q) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (batches) *batches = q->batches;
+        if (txs) *txs = q->txs;
+        return MH_OK;
+    });
+}

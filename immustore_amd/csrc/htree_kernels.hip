@@ -564,7 +564,7 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
             load_digest(levels + (la.off[l0] + 2 * q) * 32, lft);
             if (2 * q + 1 < la.width[l0]) {
                 load_digest(levels + (la.off[l0] + 2 * q + 1) * 32, rgt);
-                node_hash(lft, rgt, out);
+                node_hash_g(lft, rgt, out);
             } else {
                 copy8(out, lft);
             }
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
                 if (2 * q + 1 < la.width[l - 1]) {
 #pragma unroll
                     for (int j = 0; j < 8; j++) rgt[j] = buf[cur][2 * t + 1][j];
-                    node_hash(lft, rgt, out);
+                    node_hash_g(lft, rgt, out);
                 } else {
                     copy8(out, lft);
                 }

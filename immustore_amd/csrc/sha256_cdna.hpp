@@ -300,4 +300,41 @@ __device__ __forceinline__ void node_hash_tab(const uint32_t l[8], const uint32_
     for (int j = 0; j < 8; j++) out[j] = s.h[j];
 }
 
+// node = SHA256(0x01 || l || r) with the second block's K+W row read from
+// the table in GLOBAL memory (L2-resident): for latency-bound lone waves at
+// the top of a tree, where a workgroup cannot afford the 53 KB LDS copy.  The
+// 12 row loads are issued before the first block, whose ~1400 VALU
+// instructions hide their latency.
+__device__ __forceinline__ void node_hash_g(const uint32_t l[8], const uint32_t r[8],
+                                            uint32_t out[8]) {
+    const uint4 *row = (const uint4 *)(g_node_tab.w + (r[7] & 0xffu) * kNodeTabStride);
+    uint4 kw[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) kw[q] = row[q];
+    uint32_t w[16];
+    w[0] = 0x01000000u | (l[0] >> 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[j] = __builtin_amdgcn_alignbit(l[j - 1], l[j], 8);
+    w[8] = __builtin_amdgcn_alignbit(l[7], r[0], 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[8 + j] = __builtin_amdgcn_alignbit(r[j - 1], r[j], 8);
+    State s;
+    s.init();
+    compress(s, w);
+    const uint32_t r7 = r[7];
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6],
+             h = s.h[7];
+    MH_ROUNDS8(MH_K(0) + ((r7 << 24) | 0x00800000u), MH_K(1), MH_K(2), MH_K(3), MH_K(4), MH_K(5),
+               MH_K(6), MH_K(7));
+    MH_ROUNDS8(MH_K(8), MH_K(9), MH_K(10), MH_K(11), MH_K(12), MH_K(13), MH_K(14),
+               MH_K(15) + 65u * 8u);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint4 x = kw[2 * q], y = kw[2 * q + 1];
+        MH_ROUNDS8(x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w);
+    }
+    out[0] = s.h[0] + a; out[1] = s.h[1] + b; out[2] = s.h[2] + c; out[3] = s.h[3] + d;
+    out[4] = s.h[4] + e; out[5] = s.h[5] + f; out[6] = s.h[6] + g; out[7] = s.h[7] + h;
+}
+
 }  // namespace mh

@@ -7,6 +7,7 @@
   VerifyDualProof (v1, with linear / linear-advance parts)
                                    verification.go:127-235 -> verify_dual_proof_batch
   Tx.readFrom (read-path check)    tx.go:388-630          -> txlog_validate
+  pkg/verification.VerifyDocument  verification.go:37-196 -> verify_document_batch
 
 Headers travel as a numpy structured array of TX_HEADER (the C struct
 mh_tx_header); metadata bytes live in a side blob addressed by md_off.
@@ -195,6 +196,73 @@ def verify_dual_proof_batch(src_hdrs, tgt_hdrs, md_blob, incl, cons, target_bl_t
     ok = np.zeros(n, np.uint8)
     N.check(N.load().mh_verify_dual_proof_batch(_ctx(ctx).handle, C.byref(b), _addr(ok)))
     return ok.astype(bool)
+
+
+class _DocumentBatch(C.Structure):
+    """mirror of mh_document_batch (include/immustore_merkle.h)"""
+    _fields_ = [("n", C.c_uint64), ("doc", C.c_void_p), ("doc_off", C.c_void_p),
+                ("doc_key", C.c_void_p), ("doc_key_off", C.c_void_p), ("tx_hdr", C.c_void_p),
+                ("ent_off", C.c_void_p), ("ekeys", C.c_void_p), ("ekey_off", C.c_void_p),
+                ("emd", C.c_void_p), ("emd_off", C.c_void_p), ("ehval", C.c_void_p),
+                ("src_hdr", C.c_void_p), ("tgt_hdr", C.c_void_p), ("md_blob", C.c_void_p),
+                ("md_blob_len", C.c_uint64), ("incl_off", C.c_void_p),
+                ("incl_terms", C.c_void_p), ("cons_off", C.c_void_p),
+                ("cons_terms", C.c_void_p), ("known_tx_id", C.c_void_p),
+                ("known_alh", C.c_void_p)]
+
+
+def _csr_bytes(items):
+    off = np.zeros(len(items) + 1, np.uint64)
+    for k, b in enumerate(items):
+        off[k + 1] = off[k] + len(b)
+    flat = b"".join(bytes(b) for b in items)
+    return off, (np.frombuffer(flat, np.uint8).copy() if flat else np.zeros(16, np.uint8))
+
+
+def verify_document_batch(docs, ctx: Optional[Context] = None):
+    """pkg/verification.VerifyDocument (verification.go:37-196), hashing part,
+    for many documents.  docs: sequence of dicts with
+      encoded_document (bytes), doc_key (bytes, encodedKeyForDocument),
+      tx_hdr (TX_HEADER record), entries [(key, md_bytes, hvalue), ...],
+      src_hdr, tgt_hdr (TX_HEADER records), incl, cons (term lists),
+      known_tx_id (int, 0 = none), known_alh (32 bytes);
+    plus md_blob under key "md_blob" of the FIRST dict (shared by all headers).
+    -> (status[n] int32, target_alh[n,32])."""
+    n = len(docs)
+    if n == 0:
+        return np.zeros(0, np.int32), np.zeros((0, 32), np.uint8)
+    keep = []
+
+    def k(a):
+        keep.append(a)
+        return _addr(a)
+
+    doff, dbuf = _csr_bytes([d["encoded_document"] for d in docs])
+    koff, kbuf = _csr_bytes([d["doc_key"] for d in docs])
+    txh = _hdrs([d["tx_hdr"] for d in docs])
+    ents = [e for d in docs for e in d["entries"]]
+    ent_off = np.zeros(n + 1, np.uint64)
+    for i, d in enumerate(docs):
+        ent_off[i + 1] = ent_off[i] + len(d["entries"])
+    ekoff, ekbuf = _csr_bytes([e[0] for e in ents])
+    emoff, embuf = _csr_bytes([e[1] for e in ents])
+    ehv = _d32([e[2] for e in ents], len(ents)) if ents else np.zeros((1, 32), np.uint8)
+    sh = _hdrs([d["src_hdr"] for d in docs])
+    th = _hdrs([d["tgt_hdr"] for d in docs])
+    mb, ml = _blob(docs[0].get("md_blob", b""))
+    io, it = _terms_csr([d["incl"] for d in docs])
+    co, ct = _terms_csr([d["cons"] for d in docs])
+    kid = np.array([d.get("known_tx_id", 0) for d in docs], np.uint64)
+    kalh = _d32([d.get("known_alh", bytes(32)) for d in docs], n)
+    b = _DocumentBatch(n, k(dbuf), k(doff), k(kbuf), k(koff), k(txh), k(ent_off), k(ekbuf),
+                       k(ekoff), k(embuf), k(emoff), k(ehv), k(sh), k(th),
+                       k(mb) if mb is not None else None, ml, k(io), k(it), k(co), k(ct), k(kid),
+                       k(kalh))
+    st = np.zeros(n, np.int32)
+    alh = np.zeros((n, 32), np.uint8)
+    N.check(N.load().mh_verify_document_batch(_ctx(ctx).handle, C.byref(b), _addr(st),
+                                              _addr(alh)))
+    return st, alh
 
 
 def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,

@@ -63,6 +63,11 @@ extern "C" {
 #define MH_ERR_CORRUPTED_UNKNOWN_VERSION 17 /* ErrCorruptedTxDataUnknownHeaderVersion immustore.go:74 */
 #define MH_ERR_TRUNCATED 18             /* record cut short (io.ErrUnexpectedEOF from the reader) */
 #define MH_ERR_BUFFER_TOO_SMALL 19      /* output capacity below the encoded size (wire formats) */
+#define MH_ERR_INVALID_PROOF 20         /* store.ErrInvalidProof immustore.go:114 */
+#define MH_ERR_UNSUPPORTED_TX_VERSION 21 /* store.ErrUnsupportedTxVersion immustore.go:90 */
+#define MH_ERR_INVALID_PROOF_ENTRY 22   /* store.ErrInvalidProof from VerifyDocument's entry /
+                                           hash-value check (pkg/verification/verification.go:60-76),
+                                           i.e. raised BEFORE the document decode (:78-110) */
 
 #define MH_MAX_TX_METADATA_LEN 268 /* maxTxMetadataLen tx_metadata.go:36-39 */
 #define MH_MAX_KV_METADATA_LEN 11  /* maxKVMetadataLen kv_metadata.go:41-43 */
@@ -356,6 +361,58 @@ int mh_verify_dual_proof_v2_batch(mh_ctx *ctx, uint64_t n, const mh_tx_header *s
                                   const uint64_t *tgt, const uint8_t *src_alh,
                                   const uint8_t *tgt_alh, int32_t *status);
 
+/* pkg/verification.VerifyDocument (pkg/verification/verification.go:37-196),
+ * the hashing part, for n documents: replaces the per-document Go calls of a
+ * client verifying many ProofDocumentResponses.  The caller keeps what is not
+ * hashing: the document-id lookup and encodedKeyForDocument (:50-58), the
+ * EncodedDocument decode and proto.Equal against the caller's document
+ * (:78-110, which Go runs between the entry check and the htree) and the
+ * signature check of the new state (:199-205).
+ * Document d:
+ *   doc[doc_off[d] .. doc_off[d+1])              proof.EncodedDocument
+ *   doc_key[doc_key_off[d] .. doc_key_off[d+1])  encodedKeyForDocument(...)
+ *   tx_hdr[d]                                    VerifiableTx.Tx.Header (its Eh is checked)
+ *   entries ent_off[d] .. ent_off[d+1] of the flat entry arrays (offsets index
+ *   ekey_off / emd_off / ehval directly): key ekeys[ekey_off[e] .. ekey_off[e+1]),
+ *   KVMetadata.Bytes() emd[emd_off[e] .. emd_off[e+1]) (emd_off may be NULL:
+ *   no metadata), HValue ehval[32 e]
+ *   src_hdr[d], tgt_hdr[d], InclusionProof incl_terms[incl_off[d] .. incl_off[d+1]),
+ *   ConsistencyProof cons_terms[cons_off[d] ..)  VerifiableTx.DualProof (V2)
+ *   known_tx_id[d] (0: no known state), known_alh[32 d]  knownState
+ * Tx metadata of every header lives in md_blob (mh_tx_header.md_off).
+ * status[d]: MH_OK; MH_ERR_INVALID_PROOF_ENTRY (:60-76); MH_ERR_UNSUPPORTED_TX_VERSION
+ * (:118-121); MH_ERR_INVALID_PROOF (Eh :137-139, headers :146-163, known state
+ * :165-183); MH_ERR_ILLEGAL_ARGUMENTS for a header Go cannot hash (its
+ * innerHash panics); or the VerifyDualProofV2 status.  target_alh_out[32 d]
+ * (may be NULL): the new state's TxHash (the target header's Alh) when OK,
+ * zeros otherwise. */
+typedef struct mh_document_batch {
+    uint64_t n;
+    const uint8_t *doc;
+    const uint64_t *doc_off;
+    const uint8_t *doc_key;
+    const uint64_t *doc_key_off;
+    const mh_tx_header *tx_hdr;
+    const uint64_t *ent_off;
+    const uint8_t *ekeys;
+    const uint64_t *ekey_off;
+    const uint8_t *emd;
+    const uint64_t *emd_off;
+    const uint8_t *ehval;
+    const mh_tx_header *src_hdr;
+    const mh_tx_header *tgt_hdr;
+    const uint8_t *md_blob;
+    uint64_t md_blob_len;
+    const uint64_t *incl_off;
+    const uint8_t *incl_terms;
+    const uint64_t *cons_off;
+    const uint8_t *cons_terms;
+    const uint64_t *known_tx_id;
+    const uint8_t *known_alh;
+} mh_document_batch;
+int mh_verify_document_batch(mh_ctx *ctx, const mh_document_batch *batch, int32_t *status,
+                             uint8_t *target_alh_out);
+
 /* VerifyDualProof (verification.go:127-235: v1 proofs with linear and
  * linear-advance parts) for n proofs, all arrays host memory, term lists as
  * CSR (x_off has n + 1 entries, terms x_terms[x_off[p] .. x_off[p+1])).
@@ -454,6 +511,32 @@ int mh_precommit_batch(mh_commit_pipe *p, int version, uint64_t max_width, uint6
                        const uint64_t *val_off, const uint8_t *hval_override,
                        const uint8_t *use_override, const uint8_t *expect_eh, uint8_t *hvals_out,
                        uint8_t *eh_out, int32_t *status);
+
+/* Group commit of single transactions (the concurrent committers of
+ * precommit, immustore.go:1620-1632: each hashes its own tx before taking the
+ * store lock at :1689, up to MaxConcurrency = 30 at once, options.go:35).
+ * mh_commit_queue_submit hashes ONE transaction -- hVal per entry
+ * (immustore.go:1624-1629), entry digests and the htree (tx.go:332-355) --
+ * and blocks until its results are ready; a worker thread coalesces the
+ * transactions submitted within wait_us (or max_txs of them) into one
+ * mh_precommit_batch.  Arguments of submit are those of one tx of
+ * mh_precommit_batch (offsets index the arrays directly; n + 1 of each);
+ * expect_eh (32 bytes, may be NULL) is ReplicateTx's Eh (immustore.go:1649-1654).
+ * Returns the tx's status (MH_OK, MH_ERR_MAX_WIDTH_EXCEEDED,
+ * MH_ERR_METADATA_UNSUPPORTED, MH_ERR_ILLEGAL_ARGUMENTS for an Eh mismatch)
+ * or an error of the batch.  Thread-safe: call submit from any number of
+ * threads. */
+typedef struct mh_commit_queue mh_commit_queue;
+int mh_commit_queue_new(mh_ctx *ctx, int version, uint64_t max_width, uint32_t max_txs,
+                        uint32_t wait_us, mh_commit_queue **out);
+int mh_commit_queue_free(mh_commit_queue *q);
+int mh_commit_queue_submit(mh_commit_queue *q, uint64_t n, const uint8_t *keys,
+                           const uint64_t *key_off, const uint8_t *md, const uint64_t *md_off,
+                           const uint8_t *vals, const uint64_t *val_off,
+                           const uint8_t *hval_override, const uint8_t *use_override,
+                           const uint8_t *expect_eh, uint8_t *hvals_out, uint8_t *eh_out);
+/* batches run and transactions hashed so far */
+int mh_commit_queue_stats(mh_commit_queue *q, uint64_t *batches, uint64_t *txs);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

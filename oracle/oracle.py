@@ -472,3 +472,83 @@ def ahtree_verify_batch(kind, i, j, term_off, terms, a, b, nthreads=1):
     c = lib().orc_ahtree_verify_batch(kind, n, _p(iv, u64p), _p(jv, u64p), _p(to, u64p), _p(t),
                                       _p(av), _p(bv), _p(ok), nthreads)
     return c, ok[:n]
+
+
+# ---------------------------------------------------------------- VerifyDocument
+ERR_ILLEGAL_ARGS = 2
+ERR_INVALID_PROOF = 20
+ERR_UNSUPPORTED_TX_VERSION = 21
+ERR_INVALID_PROOF_ENTRY = 22
+_EMPTY = bytes.fromhex("e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855")
+
+
+def verify_document(d, md_blob=b""):
+    """pkg/verification.VerifyDocument (pkg/verification/verification.go:37-196),
+    the hashing part, restated over the oracle's primitives.  d: the dict of
+    immustore_amd.txlayer.verify_document_batch.  -> (status, target_alh or None).
+    Not restated (the caller's, not hashing): the document-id lookup and
+    encodedKeyForDocument (:50-58), the document decode + proto.Equal
+    (:78-110), the signature check (:199-205)."""
+    doc, key = bytes(d["encoded_document"]), bytes(d["doc_key"])
+    # :60-76 -- the document's entry must exist exactly once with HValue = SHA256(doc)
+    found = 0
+    for ek, _, hv in d["entries"]:
+        if bytes(ek) == key:
+            if bytes(hv) != sha256(doc):
+                return ERR_INVALID_PROOF_ENTRY, None
+            found += 1
+    if found != 1:
+        return ERR_INVALID_PROOF_ENTRY, None
+    tx = np.asarray(d["tx_hdr"], TX_HEADER).reshape(1)[0]
+    ver = int(tx["version"])
+    # :118-121 EntrySpecDigestFor (store/verification.go:244-254)
+    if ver not in (0, 1):
+        return ERR_UNSUPPORTED_TX_VERSION, None
+    digs = []
+    for ek, md, hv in d["entries"]:
+        if ver == 0:
+            # EntrySpecDigest_v0 (store/verification.go:256-262): key || SHA256(Value),
+            # Value nil in VerifyDocument's EntrySpec -> SHA256(nil); md ignored
+            digs.append(sha256(bytes(ek) + _EMPTY))
+        else:
+            # EntrySpecDigest_v1 (:264-302), IsValueTruncated -> HashValue
+            st, dg = entry_digest(1, bytes(ek), bytes(md), bytes(hv))
+            assert st == 0
+            digs.append(dg)
+    root = htree_build(np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))[1] if digs \
+        else _EMPTY
+    if root != bytes(tx["eh"]):  # :137-139
+        return ERR_INVALID_PROOF, None
+    sh = np.asarray(d["src_hdr"], TX_HEADER).reshape(1).copy()
+    th = np.asarray(d["tgt_hdr"], TX_HEADER).reshape(1).copy()
+    x = np.asarray(d["tx_hdr"], TX_HEADER).reshape(1).copy()
+    for h in (sh, th, x):  # a v0 innerHash never reads the metadata (tx.go:258-263)
+        if int(h[0]["version"]) == 0:
+            h[0]["md_len"] = 0
+    src, tgt = int(sh[0]["id"]), int(th[0]["id"])
+    if tgt < src:  # :146-148
+        return ERR_INVALID_PROOF, None
+    s1, _, salh = tx_header_alh(sh[0], md_blob)
+    s2, _, talh = tx_header_alh(th[0], md_blob)
+    if s1 or s2:  # Go's innerHash panics on such a header
+        return ERR_ILLEGAL_ARGS, None
+    tid = int(x[0]["id"])
+    if tid != src and tid != tgt:  # :153-155
+        return ERR_INVALID_PROOF, None
+    s3, _, xalh = tx_header_alh(x[0], md_blob)
+    if s3:
+        return ERR_ILLEGAL_ARGS, None
+    if (tid == src and xalh != salh) or (tid == tgt and xalh != talh):  # :157-163
+        return ERR_INVALID_PROOF, None
+    kid = int(d.get("known_tx_id", 0))
+    ka = bytes(d.get("known_alh", bytes(32)))
+    if kid == 0:
+        if src != 1:  # :165-168
+            return ERR_INVALID_PROOF, None
+    else:
+        if kid != src and kid != tgt:  # :170-172
+            return ERR_INVALID_PROOF, None
+        if (kid == src and ka != salh) or (kid == tgt and ka != talh):  # :174-180
+            return ERR_INVALID_PROOF, None
+    st = verify_dual_proof_v2(sh[0], th[0], md_blob, d["incl"], d["cons"], src, tgt, salh, talh)
+    return st, (talh if st == 0 else None)

@@ -141,3 +141,77 @@ def test_precommit_large_batch_pinned(m, ctx, orc):
         p.close()
     assert (st == 0).all() and (st_o == 0).all()
     assert np.array_equal(eh, eh_o) and np.array_equal(hv, hv_o)
+
+
+def test_commit_queue_30_threads_vs_oracle(m, ctx, orc):
+    """Group commit (mh_commit_queue): 30 threads -- MaxConcurrency
+    (options.go:35) -- each submit single 16-entry transactions
+    (immustore.go:1620-1632) with 1 KiB values, KV metadata, truncated values
+    and ReplicateTx Eh checks mixed in; every tx's hVals, Eh and status equal
+    the oracle's, and the queue really coalesced them into fewer batches."""
+    import threading
+    from immustore_amd.commit import CommitQueue, EntrySpec
+    q = CommitQueue(ctx, version=1, max_width=24, max_txs=64, wait_us=100)
+    rng = np.random.default_rng(30)
+    per_thread = 12
+    txs = []
+    for k in range(30 * per_thread):
+        ne = 16 if k % 7 else int(rng.integers(0, 30))  # some empty / over max_width
+        es = []
+        for e in range(ne):
+            key = b"k/%d/%d" % (k, e)
+            val = bytes(rng.integers(0, 256, 1024 if e % 5 else int(rng.integers(0, 3000)),
+                                     dtype=np.uint8))
+            md = [b"", b"", b"\x00", b"\x01" + bytes(8)][e % 4]
+            hv = orc.sha256(val + b"!") if (k + e) % 11 == 0 else None
+            es.append(EntrySpec(key, val, md, hv))
+        txs.append(es)
+    exp = []
+    for k, es in enumerate(txs):
+        ovs = [e.hash_value for e in es]
+        st, hv, _, root = orc.build_entries(1, [e.key for e in es], [e.md for e in es],
+                                            [e.value for e in es], ovs)
+        if len(es) > 24:
+            st, root = 1, None
+        exp.append((st, hv, root))
+    out = [None] * len(txs)
+
+    def run(t):
+        for k in range(t, len(txs), 30):
+            want = exp[k][2] if (k % 13 == 0 and exp[k][0] == 0) else None
+            if want is not None and k % 26 == 0:
+                want = bytes([want[0] ^ 1]) + want[1:]  # a replicated tx whose Eh differs
+            out[k] = (q.submit(txs[k], expect_eh=want), want)
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(30)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    for k, ((st, hv, eh), want) in enumerate(out):
+        est, ehv, eroot = exp[k]
+        if est == 1:
+            assert st == 1, k  # MH_ERR_MAX_WIDTH_EXCEEDED
+            continue
+        assert np.array_equal(hv, ehv.reshape(-1, 32)), k
+        assert eh == eroot, k
+        if want is not None and want != eroot:
+            assert st == 2, k  # "entries hash (Eh) differs"
+        else:
+            assert st == 0, k
+    batches, n = q.stats()
+    assert n == len(txs) and batches < n
+    q.close()
+
+
+def test_commit_queue_v0_metadata_and_free(m, ctx, orc):
+    from immustore_amd.commit import CommitQueue, EntrySpec
+    q = CommitQueue(ctx, version=0)
+    st, hv, eh = q.submit([EntrySpec(b"a", b"x", b"\x00")])
+    assert st == 6  # MH_ERR_METADATA_UNSUPPORTED (tx.go:691-693)
+    st, hv, eh = q.submit([EntrySpec(b"a", b"x"), EntrySpec(b"bb", b"")])
+    s2, hv2, _, root = orc.build_entries(0, [b"a", b"bb"], [b"", b""], [b"x", b""])
+    assert st == 0 and eh == root and np.array_equal(hv, hv2.reshape(-1, 32))
+    st, hv, eh = q.submit([])
+    assert st == 0 and eh == orc.sha256(b"")
+    q.close()

@@ -566,3 +566,75 @@ def test_ahtree_reset_reference_sequence(m, ctx):
     assert (st == 0).all()
     ok = _aht_verify_csr(m, ctx, N.MH_AHT_LAST_INCLUSION, K, K, terms, nt, leaf[K], root[K])
     assert list(np.nonzero(ok)[0] + 1) == [n]
+
+
+# ------------------------------------------ upper levels (k_entries_fixed + k_reduce)
+@pytest.mark.parametrize("wgl", ["0", "2", "4", "8"])
+def test_entries_fixed_wg_levels_vs_oracle(m, ctx, orc, lpl, wgl):
+    """Every depth of the leaf workgroups' in-LDS subtrees (MH_WG_LEVELS) with
+    the level reduction above them (htree.go:85-110): widths that cut
+    workgroups and 512-node reduce blocks unevenly, and two different data
+    sets built alternately into the SAME level / root buffers (a stale read
+    of the previous build's nodes would show), all vs the oracle."""
+    from immustore_amd import _native as N
+    old = os.environ.get("MH_WG_LEVELS")
+    os.environ["MH_WG_LEVELS"] = wgl
+    try:
+        for n in (257, 513, 1025, 4097, 33000, 131073, 262147, 1 << 19, (1 << 20) + 3):
+            klen, vlen = 8, 64
+            dl = DevBuf(ctx, m.levels_len(n) * 32)
+            dr = DevBuf(ctx, 32)
+            dh = DevBuf(ctx, n * 32)
+            sets = []
+            for seed in (31, 32):
+                keys, vals = _fixed_inputs(orc, n, klen, vlen, seed + n)
+                sets.append((keys, vals, DevBuf.from_host(ctx, keys), DevBuf.from_host(ctx, vals),
+                             orc.build_entries_fixed(1, keys, vals, nthreads=8)))
+            for k in (0, 1, 0, 1):
+                keys, vals, dk, dv, (ohv, olv, oroot) = sets[k]
+                N.check(N.load().mh_dev_htree_build_entries_fixed(
+                    ctx.handle, 1, n, dk.ptr, klen, dv.ptr, vlen, dh.ptr, dl.ptr, dr.ptr))
+                ctx.synchronize()
+                assert dr.to_host().tobytes() == oroot, (n, wgl, k)
+                assert np.array_equal(dl.to_host().reshape(-1, 32), olv), (n, wgl, k)
+                assert np.array_equal(dh.to_host().reshape(-1, 32), ohv), (n, wgl, k)
+    finally:
+        if old is None:
+            del os.environ["MH_WG_LEVELS"]
+        else:
+            os.environ["MH_WG_LEVELS"] = old
+
+
+def test_entries_fixed_concurrent_streams(m, orc):
+    """Three contexts on three streams building different trees at once
+    (the bench's builds in flight): every root and level array matches the
+    oracle."""
+    import torch
+    from immustore_amd import _native as N
+    L = N.load()
+    n, vlen = (1 << 18) + 77, 256
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ctxs = [m.Context(0, s.cuda_stream) for s in streams]
+    try:
+        jobs = []
+        for k, c in enumerate(ctxs):
+            keys, vals = _fixed_inputs(orc, n, 8, vlen, 600 + k)
+            dk = torch.from_numpy(keys.reshape(-1).copy()).cuda()
+            dv = torch.from_numpy(vals.reshape(-1).copy()).cuda()
+            lv = torch.empty(m.levels_len(n) * 32, dtype=torch.uint8, device="cuda")
+            rt = torch.empty(32, dtype=torch.uint8, device="cuda")
+            jobs.append((c, keys, vals, dk, dv, lv, rt))
+        torch.cuda.synchronize()
+        for rep in range(4):
+            for c, keys, vals, dk, dv, lv, rt in jobs:
+                N.check(L.mh_dev_htree_build_entries_fixed(c.handle, 1, n, dk.data_ptr(), 8,
+                                                           dv.data_ptr(), vlen, None,
+                                                           lv.data_ptr(), rt.data_ptr()))
+        torch.cuda.synchronize()
+        for c, keys, vals, dk, dv, lv, rt in jobs:
+            _, olv, oroot = orc.build_entries_fixed(1, keys, vals, nthreads=8)
+            assert rt.cpu().numpy().tobytes() == oroot
+            assert np.array_equal(lv.cpu().numpy().reshape(-1, 32), olv)
+    finally:
+        for c in ctxs:
+            c.close()

@@ -292,3 +292,65 @@ def test_dual_proof_v1_fixture_cases(m, ctx, orc, fixtures):
                                     cols[11], cols[12], ctx)
     assert list(got) == exp
     assert sum(exp) > 400 and not all(exp)
+
+
+def test_verify_document_batch_vs_oracle(m, ctx, orc, fixtures):
+    """pkg/verification.VerifyDocument (verification.go:37-196), hashing part,
+    on the device for every document case built from the Go-written stores
+    (tests/tx_util.document_cases: untampered and 12 tampered variants each)
+    -- per-document status and new-state Alh equal the oracle's."""
+    from immustore_amd import txlayer
+    from tx_util import document_cases
+    docs, blob = document_cases(fixtures, orc)
+    docs[0]["md_blob"] = blob
+    st, alh = txlayer.verify_document_batch(docs, ctx=ctx)
+    for k, d in enumerate(docs):
+        ost, oalh = orc.verify_document(d, blob)
+        assert int(st[k]) == ost, (k, k % 13)
+        assert alh[k].tobytes() == (oalh if ost == 0 else bytes(32)), k
+    assert (st == 0).sum() >= 40
+
+
+def test_verify_document_batch_wide_txs(m, ctx, orc):
+    """Synthetic v1 documents in transactions of up to 700 entries (the
+    htrees take the planned many-tree path), with KV metadata, a trivial
+    DualProofV2 (source = target = the document's tx) and the tx as known
+    state; a third of them with one entry's hValue flipped."""
+    import struct
+    from immustore_amd import txlayer
+    from tx_util import TX_HEADER
+    rng = np.random.default_rng(21)
+    docs = []
+    for k in range(60):
+        ne = int(rng.integers(1, 700)) if k % 4 else int(rng.integers(1, 5))
+        ents = []
+        for e in range(ne):
+            key = b"doc/%d/%d" % (k, e)
+            md = [b"", b"\x00", b"\x02", b"\x01" + struct.pack(">Q", e)][e % 4]
+            ents.append((key, md, bytes(rng.integers(0, 256, 32, dtype=np.uint8))))
+        j = int(rng.integers(0, ne))
+        doc = bytes(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8))
+        ents[j] = (ents[j][0], ents[j][1], orc.sha256(doc))
+        digs = np.frombuffer(b"".join(orc.entry_digest(1, a, b_, c)[1] for a, b_, c in ents),
+                             np.uint8).reshape(-1, 32)
+        eh = orc.htree_build(digs)[1]
+        h = np.zeros(1, TX_HEADER)
+        h["id"], h["bl_tx_id"], h["version"], h["nentries"] = 100 + k, 99 + k, 1, ne
+        h["eh"] = np.frombuffer(eh, np.uint8)
+        h["ts"] = 1_700_000_000 + k
+        alh = orc.tx_header_alh(h[0])[2]
+        if k % 3 == 2:
+            i = (j + 1) % ne
+            ents[i] = (ents[i][0], ents[i][1], bytes([ents[i][2][0] ^ 0x80]) + ents[i][2][1:])
+        docs.append({"encoded_document": doc, "doc_key": ents[j][0], "tx_hdr": h[0],
+                     "entries": ents, "src_hdr": h[0], "tgt_hdr": h[0], "incl": [], "cons": [],
+                     "known_tx_id": 100 + k, "known_alh": alh})
+    st, alh = txlayer.verify_document_batch(docs, ctx=ctx)
+    for k, d in enumerate(docs):
+        ost, oalh = orc.verify_document(d)
+        assert int(st[k]) == ost, k
+        assert alh[k].tobytes() == (oalh if ost == 0 else bytes(32))
+        if k % 3 == 2 and len(d["entries"]) > 1:
+            assert ost in (orc.ERR_INVALID_PROOF, orc.ERR_INVALID_PROOF_ENTRY)
+        elif k % 3 != 2:
+            assert ost == 0

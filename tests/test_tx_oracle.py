@@ -234,3 +234,33 @@ def test_precommit_batch_statuses(orc):
     has_md = np.array([int(b["md_off"][int(to[t + 1])] - b["md_off"][int(to[t])]) > 0
                        for t in range(50)])
     assert ((st4 == 6) == has_md).all()
+
+
+def test_verify_document_oracle_on_go_stores(orc, fixtures):
+    """pkg/verification.VerifyDocument restated (oracle.verify_document) on
+    documents taken from the Go-written stores: every untampered v1 document
+    verifies and yields the target's stored Alh; v0 txs fail the Eh check
+    because EntrySpecDigest_v0 hashes SHA256(Value) of the nil Value
+    (store/verification.go:256-262); every tampered check fails."""
+    from tx_util import document_cases
+    docs, blob = document_cases(fixtures, orc)
+    seen = {}
+    for k, d in enumerate(docs):
+        st, alh = orc.verify_document(d, blob)
+        v = k % 13
+        ver = int(d["src_hdr"]["version"])
+        seen.setdefault((ver, v), set()).add(st)
+        if v == 0:
+            if ver == 1 and (d["known_tx_id"] or int(d["src_hdr"]["id"]) == 1):
+                assert st == 0
+                # new state = target Alh
+                assert alh == orc.tx_header_alh(d["tgt_hdr"], blob)[2]
+            else:  # v0 quirk, or no known state with a source other than tx 1 (:165-168)
+                assert st == orc.ERR_INVALID_PROOF
+        elif v in (1, 2, 3):
+            assert st == orc.ERR_INVALID_PROOF_ENTRY
+        elif v == 11:
+            assert st == orc.ERR_UNSUPPORTED_TX_VERSION
+        elif v in (4, 5, 6, 7, 10) or (v == 12 and d["src_hdr"]["id"] != d["tgt_hdr"]["id"]):
+            assert st != 0
+    assert (1, 0) in seen and (0, 0) in seen

@@ -89,3 +89,81 @@ def _bulk_txlog(rng, ntx):
             ents += struct.pack(">IQ", 10, e) + bytes([k % 256]) * 32
         out += hdr + ents + bytes([7]) * 32
     return bytes(out), starts
+
+
+def document_cases(fixtures, orc, per_store=60, seed=7):
+    """VerifyDocument inputs built from the reference's Go-written stores: the
+    "document" of tx t is a stored value of one of t's entries whose key is
+    unique in t (so SHA256(document) is that entry's stored hVal), proven by a
+    fixture DualProofV2 whose source or target is t, with and without a
+    known state, plus tampered variants of every check
+    (pkg/verification/verification.go:60-194).  -> (docs, md_blob)."""
+    rng = np.random.default_rng(seed)
+    docs = []
+    blob_all = bytearray()
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        recs = recs.copy()
+        recs["md_off"] += len(blob_all)
+        blob_all += blob
+        cases = [c for c in fx["dual_v2"]]
+        rng.shuffle(cases)
+        made = 0
+        for c in cases:
+            if made >= per_store:
+                break
+            s, t = c["src"], c["tgt"]
+            tid = [s, t][int(rng.integers(0, 2))]
+            ents = fx["txs"][tid - 1]["entries"]
+            keys = [e["key"] for e in ents]
+            cand = [e for e in ents if e.get("value") is not None and keys.count(e["key"]) == 1]
+            if not cand:
+                continue
+            e = cand[int(rng.integers(0, len(cand)))]
+            entries = [(bytes.fromhex(x["key"]), bytes.fromhex(x["md"]), bytes.fromhex(x["hval"]))
+                       for x in ents]
+            kid = [0, s, t][made % 3]
+            base = {"encoded_document": bytes.fromhex(e["value"]),
+                    "doc_key": bytes.fromhex(e["key"]), "tx_hdr": recs[tid - 1].copy(),
+                    "entries": entries, "src_hdr": recs[s - 1].copy(), "tgt_hdr": recs[t - 1].copy(),
+                    "incl": [bytes.fromhex(x) for x in c["incl"]],
+                    "cons": [bytes.fromhex(x) for x in c["cons"]],
+                    "known_tx_id": kid, "known_alh": alhs[kid - 1] if kid else bytes(32)}
+            made += 1
+            docs.append(base)
+            for v in range(1, 13):
+                d = dict(base)
+                d["tx_hdr"] = base["tx_hdr"].copy()
+                d["src_hdr"] = base["src_hdr"].copy()
+                d["tgt_hdr"] = base["tgt_hdr"].copy()
+                d["entries"] = list(base["entries"])
+                if v == 1:    # document bytes changed: hVal mismatch (:63-67)
+                    d["encoded_document"] = base["encoded_document"] + b"x"
+                elif v == 2:  # key not in the tx (:74-76)
+                    d["doc_key"] = base["doc_key"] + b"\0"
+                elif v == 3:  # key twice (:74-76)
+                    d["entries"] = d["entries"] + [next(x for x in entries if x[0] == d["doc_key"])]
+                elif v == 4:  # Eh changed (:137-139)
+                    d["tx_hdr"]["eh"][0] ^= 1
+                elif v == 5:  # another entry's hValue changed (:137-139) or the doc's own
+                    i = int(rng.integers(0, len(entries)))
+                    k_, m_, h_ = d["entries"][i]
+                    d["entries"][i] = (k_, m_, bytes([h_[0] ^ 1]) + h_[1:])
+                elif v == 6:  # known state names another tx (:170-172)
+                    d["known_tx_id"] = t + 1
+                    d["known_alh"] = bytes(32)
+                elif v == 7:  # known state with a wrong Alh (:174-180)
+                    d["known_tx_id"] = s
+                    d["known_alh"] = bytes(32)
+                elif v == 8:  # no known state (:165-168)
+                    d["known_tx_id"] = 0
+                elif v == 9 and d["incl"]:  # inclusion term changed
+                    d["incl"] = [bytes([d["incl"][0][0] ^ 1]) + d["incl"][0][1:]] + d["incl"][1:]
+                elif v == 10:  # the tx is neither source nor target (:153-155)
+                    d["tx_hdr"]["id"] = t + 5
+                elif v == 11:  # unsupported version (:118-121)
+                    d["tx_hdr"]["version"] = 2
+                elif v == 12:  # source newer than target (:146-148)
+                    d["src_hdr"], d["tgt_hdr"] = base["tgt_hdr"].copy(), base["src_hdr"].copy()
+                docs.append(d)
+    return docs, bytes(blob_all)
