@@ -34,6 +34,7 @@ MH_ERR_BUFFER_TOO_SMALL = 19
 MH_ERR_INVALID_PROOF = 20
 MH_ERR_UNSUPPORTED_TX_VERSION = 21
 MH_ERR_INVALID_PROOF_ENTRY = 22
+MH_ERR_COLLECTIVE = 23
 
 MH_AHT_INCLUSION = 0
 MH_AHT_CONSISTENCY = 1
@@ -142,6 +143,10 @@ class ErrUnsupportedTxVersion(MerkleError):
     """store.ErrUnsupportedTxVersion (immustore.go:90)"""
 
 
+class ErrCollective(MerkleError):
+    """RCCL unavailable or a collective failed (mh_multi_*)"""
+
+
 class HipError(MerkleError):
     pass
 
@@ -169,6 +174,7 @@ _ERRORS = {
     MH_ERR_INVALID_PROOF: ErrInvalidProof,
     MH_ERR_UNSUPPORTED_TX_VERSION: ErrUnsupportedTxVersion,
     MH_ERR_INVALID_PROOF_ENTRY: ErrInvalidProofEntry,
+    MH_ERR_COLLECTIVE: ErrCollective,
 }
 
 vp = C.c_void_p
@@ -262,6 +268,16 @@ SIGNATURES = {
     "mh_commit_queue_submit": (i32, [vp, u64, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p, u8p,
                                      u8p]),
     "mh_commit_queue_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
+    "mh_multi_create": (i32, [i32, vp, C.POINTER(vp)]),
+    "mh_multi_destroy": (i32, [vp]),
+    "mh_multi_size": (i32, [vp, C.POINTER(i32)]),
+    "mh_multi_ctx": (vp, [vp, i32]),
+    "mh_multi_synchronize": (i32, [vp]),
+    "mh_multi_shard_plan": (i32, [u64, i32, C.POINTER(u64), C.POINTER(u64)]),
+    "mh_multi_htree_build_entries_fixed": (i32, [vp, i32, u64, u8p, u32, u8p, u32, u8p, u8p,
+                                                 u8p]),
+    "mh_multi_dev_htree_build_entries_fixed": (i32, [vp, i32, u64, vp, u32, vp, u32, vp, vp, vp,
+                                                     vp]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
                                 u8p, vp]),
     "mh_commit_pipe_new": (i32, [vp, u64, C.POINTER(vp)]),

@@ -54,6 +54,7 @@ extern "C" const char *mh_status_string(int st) {
         case MH_ERR_INVALID_PROOF: return "invalid proof";
         case MH_ERR_UNSUPPORTED_TX_VERSION: return "unsupported tx version";
         case MH_ERR_INVALID_PROOF_ENTRY: return "invalid proof: document entry";
+        case MH_ERR_COLLECTIVE: return "RCCL collective failed or RCCL not available";
         default: return st < 0 ? hipGetErrorString((hipError_t)(-st)) : "unknown status";
     }
 }

@@ -1,0 +1,353 @@
+// capi_multi.hip -- the multi-GPU htree build behind the C ABI.
+//
+// One process drives K devices -- what a cgo caller (one Go process, the
+// commit path of immustore.go:1620-1632) needs -- with one mh_ctx (HIP
+// stream) per device and an RCCL clique over them (ncclCommInitAll).  The
+// leaves are cut into power-of-two aligned shards of S = 2^k entries; device
+// g builds the subtree over [gS, min((g+1)S, n)) with every level (levels
+// 0..k of the global tree restricted to the shard are exactly the shard's own
+// levels, htree.go:85-110, the right edge included); the G <= K subtree roots
+// are all-gathered (32 bytes per device, RCCL over xGMI) and the top
+// ceil(log2 G) levels are reduced on every device.
+//
+// RCCL is loaded on first use (dlopen of librccl.so.1), so single-device
+// users of the library never need it.
+#include <dlfcn.h>
+
+#include <memory>
+
+#include <rccl/rccl.h>
+
+#include "capi_internal.hpp"
+
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*init_all)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+        r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.ok = r.init_all && r.destroy && r.all_gather && r.group_start && r.group_end;
+    });
+    return r;
+}
+
+#define MH_NCCL(expr)                                      \
+    do {                                                   \
+        if ((expr) != ncclSuccess) return MH_ERR_COLLECTIVE; \
+    } while (0)
+
+uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct mh_multi {
+    int K = 0;
+    std::vector<int> dev;
+    std::vector<mh_ctx *> ctx;
+    std::vector<ncclComm_t> comm;
+    // false when a device is listed more than once (more shards than
+    // devices): RCCL wants one rank per device, so the 32-byte roots are then
+    // gathered with device-to-device copies instead
+    bool use_rccl = true;
+    struct Dev {
+        DevBuf keys, vals, hv, levels, send, recv, top;
+    };
+    std::vector<std::unique_ptr<Dev>> buf;
+    std::mutex mu;  // one build at a time per mh_multi
+};
+
+extern "C" int mh_multi_shard_plan(uint64_t n, int ndev, uint64_t *shard, uint64_t *nshards) {
+    if (ndev < 1 || !shard || !nshards) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (n == 0) {
+        *shard = 1;
+        *nshards = 0;
+        return MH_OK;
+    }
+    const uint64_t S = next_pow2((n + (uint64_t)ndev - 1) / (uint64_t)ndev);
+    *shard = S;
+    *nshards = (n + S - 1) / S;
+    return MH_OK;
+}
+
+extern "C" int mh_multi_create(int ndev, const int *devices, mh_multi **out) {
+    return mh_guard([&]() -> int {
+        if (ndev < 1 || !devices || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
+        *out = nullptr;
+        int have = 0;
+        if (hipGetDeviceCount(&have) != hipSuccess || have < 1) return MH_ERR_NO_DEVICE;
+        for (int d = 0; d < ndev; d++)
+            if (devices[d] < 0 || devices[d] >= have) return MH_ERR_ILLEGAL_ARGUMENTS;
+        bool distinct = true;
+        for (int a = 0; a < ndev; a++)
+            for (int b = a + 1; b < ndev; b++) distinct &= devices[a] != devices[b];
+        const Rccl &R = rccl();
+        if (distinct && !R.ok) return MH_ERR_COLLECTIVE;
+        mh_multi *m = new mh_multi();
+        m->use_rccl = distinct;
+        m->K = ndev;
+        m->dev.assign(devices, devices + ndev);
+        m->ctx.assign(ndev, nullptr);
+        for (int d = 0; d < ndev; d++) m->buf.emplace_back(new mh_multi::Dev());
+        for (int d = 0; d < ndev; d++) {
+            int st = mh_ctx_create(devices[d], nullptr, &m->ctx[d]);
+            if (st != MH_OK) {
+                mh_multi_destroy(m);
+                return st;
+            }
+        }
+        if (!distinct) {
+            *out = m;
+            return MH_OK;
+        }
+        m->comm.assign(ndev, nullptr);
+        if (R.init_all(m->comm.data(), ndev, devices) != ncclSuccess) {
+            m->comm.clear();
+            mh_multi_destroy(m);
+            return MH_ERR_COLLECTIVE;
+        }
+        *out = m;
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_multi_destroy(mh_multi *m) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_OK;
+        for (int d = 0; d < m->K; d++)
+            if (m->ctx[d]) mh_ctx_synchronize(m->ctx[d]);
+        const Rccl &R = rccl();
+        for (ncclComm_t c : m->comm)
+            if (c && R.ok) R.destroy(c);
+        for (int d = 0; d < (int)m->buf.size(); d++) {
+            hipSetDevice(m->dev[d]);
+            m->buf[d].reset();  // frees on the owning device
+        }
+        for (mh_ctx *c : m->ctx)
+            if (c) mh_ctx_destroy(c);
+        delete m;
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_multi_size(mh_multi *m, int *ndev) {
+    if (!m || !ndev) return MH_ERR_ILLEGAL_ARGUMENTS;
+    *ndev = m->K;
+    return MH_OK;
+}
+
+extern "C" mh_ctx *mh_multi_ctx(mh_multi *m, int d) {
+    return (m && d >= 0 && d < m->K) ? m->ctx[d] : nullptr;
+}
+
+extern "C" int mh_multi_synchronize(mh_multi *m) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        for (int d = 0; d < m->K; d++)
+            if (int st = mh_ctx_synchronize(m->ctx[d])) return st;
+        return MH_OK;
+    });
+}
+
+namespace {
+
+// All-gather of one 32-byte root per device (send[d] -> recv[d] = K x 32 B),
+// on each device's context stream.
+int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
+                 const std::vector<uint8_t *> &recv) {
+    if (!m->use_rccl) {
+        // shards sharing devices: wait for every subtree, then copy the roots
+        for (int d = 0; d < m->K; d++)
+            if (int st = mh_ctx_synchronize(m->ctx[d])) return st;
+        for (int d = 0; d < m->K; d++) {
+            MH_HIP(hipSetDevice(m->dev[d]));
+            for (int s = 0; s < m->K; s++)
+                MH_HIP(hipMemcpyAsync(recv[d] + 32 * s, send[s], 32, hipMemcpyDefault,
+                                      m->ctx[d]->stream));
+        }
+        return MH_OK;
+    }
+    const Rccl &R = rccl();
+    MH_NCCL(R.group_start());
+    for (int d = 0; d < m->K; d++) {
+        MH_HIP(hipSetDevice(m->dev[d]));
+        if (R.all_gather(send[d], recv[d], 32, ncclUint8, m->comm[d], m->ctx[d]->stream) !=
+            ncclSuccess) {
+            R.group_end();
+            return MH_ERR_COLLECTIVE;
+        }
+    }
+    MH_NCCL(R.group_end());
+    return MH_OK;
+}
+
+}  // namespace
+
+extern "C" int mh_multi_dev_htree_build_entries_fixed(
+    mh_multi *m, int version, uint64_t n_per_dev, const uint8_t *const *keys, uint32_t key_len,
+    const uint8_t *const *vals, uint32_t val_len, uint8_t *const *hvals_out,
+    uint8_t *const *levels, uint8_t *const *top_levels, uint8_t *const *root) {
+    return mh_guard([&]() -> int {
+        if (!m || (version != 0 && version != 1) || !keys || !vals || !levels || !top_levels ||
+            !root || n_per_dev == 0)
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        const int K = m->K;
+        if (K > 1 && (n_per_dev & (n_per_dev - 1))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(m->mu);
+        // 1. every device: its subtree (levels 0..log2 n_per_dev, root at root[d])
+        for (int d = 0; d < K; d++) {
+            int st = mh_dev_htree_build_entries_fixed(m->ctx[d], version, n_per_dev, keys[d],
+                                                      key_len, vals[d], val_len,
+                                                      hvals_out ? hvals_out[d] : nullptr,
+                                                      levels[d], root[d]);
+            if (st) return st;
+        }
+        // 2. all-gather the K subtree roots (32 B each) over RCCL
+        std::vector<const uint8_t *> send(K);
+        std::vector<uint8_t *> recv(K);
+        for (int d = 0; d < K; d++) {
+            MH_HIP(hipSetDevice(m->dev[d]));
+            MH_HIP(m->buf[d]->recv.ensure(32 * (uint64_t)K));
+            send[d] = root[d];
+            recv[d] = m->buf[d]->recv.as<uint8_t>();
+        }
+        if (int st = gather_roots(m, send, recv)) return st;
+        // 3. every device: the top log2(K) levels over the gathered roots
+        //    (replicated, identical), the global root into root[d]
+        for (int d = 0; d < K; d++) {
+            int st = mh_dev_htree_reduce_nodes(m->ctx[d], recv[d], (uint64_t)K, top_levels[d],
+                                               root[d]);
+            if (st) return st;
+        }
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n,
+                                                  const uint8_t *keys, uint32_t key_len,
+                                                  const uint8_t *vals, uint32_t val_len,
+                                                  uint8_t *hvals_out, uint8_t *levels_out,
+                                                  uint8_t root[32]) {
+    return mh_guard([&]() -> int {
+        if (!m || (version != 0 && version != 1) || !root) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n && ((key_len && !keys) || (val_len && !vals))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) {
+            memcpy(root, kEmptyRoot, 32);  // htree.go:73-77
+            return MH_OK;
+        }
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int K = m->K;
+        uint64_t S = 0, G = 0;
+        mh_multi_shard_plan(n, K, &S, &G);
+        int kS = 0;
+        while ((1ull << kS) < S) kS++;
+        LevelGeom gg;
+        gg.init(n);
+        // 1. shards in, subtree per device (host copies on each device's stream)
+        for (uint64_t g = 0; g < G; g++) {
+            const int d = (int)g;
+            mh_multi::Dev &B = *m->buf[d];
+            const uint64_t lo = g * S, ng = std::min(S, n - lo);
+            MH_HIP(hipSetDevice(m->dev[d]));
+            MH_HIP(B.keys.ensure(ng * key_len + 16));
+            MH_HIP(B.vals.ensure(ng * val_len + 16));
+            MH_HIP(B.hv.ensure(ng * 32));
+            MH_HIP(B.levels.ensure(mh_htree_levels_len(ng) * 32));
+            MH_HIP(B.send.ensure(32));
+            hipStream_t st = m->ctx[d]->stream;
+            if (key_len)
+                MH_HIP(hipMemcpyAsync(B.keys.p, keys + lo * key_len, ng * key_len,
+                                      hipMemcpyHostToDevice, st));
+            if (val_len)
+                MH_HIP(hipMemcpyAsync(B.vals.p, vals + lo * val_len, ng * val_len,
+                                      hipMemcpyHostToDevice, st));
+            int e = mh_dev_htree_build_entries_fixed(m->ctx[d], version, ng, B.keys.as<uint8_t>(),
+                                                     key_len, B.vals.as<uint8_t>(), val_len,
+                                                     B.hv.as<uint8_t>(), B.levels.as<uint8_t>(),
+                                                     B.send.as<uint8_t>());
+            if (e) return e;
+        }
+        // 2. all-gather of the subtree roots (devices without a shard send zeros)
+        std::vector<const uint8_t *> send(K);
+        std::vector<uint8_t *> recv(K);
+        for (int d = 0; d < K; d++) {
+            mh_multi::Dev &B = *m->buf[d];
+            MH_HIP(hipSetDevice(m->dev[d]));
+            if ((uint64_t)d >= G) {
+                MH_HIP(B.send.ensure(32));
+                MH_HIP(hipMemsetAsync(B.send.p, 0, 32, m->ctx[d]->stream));
+            }
+            MH_HIP(B.recv.ensure(32 * (uint64_t)K));
+            send[d] = B.send.as<uint8_t>();
+            recv[d] = B.recv.as<uint8_t>();
+        }
+        if (int st = gather_roots(m, send, recv)) return st;
+        // 3. top levels over the G shard roots on device 0 (global levels kS+1 ..)
+        mh_multi::Dev &B0 = *m->buf[0];
+        MH_HIP(hipSetDevice(m->dev[0]));
+        MH_HIP(B0.top.ensure(mh_htree_levels_len(G) * 32 + 32));
+        uint8_t *d_root = B0.top.as<uint8_t>() + mh_htree_levels_len(G) * 32;
+        if (int e = mh_dev_htree_reduce_nodes(m->ctx[0], recv[0], G, B0.top.as<uint8_t>(), d_root))
+            return e;
+        // 4. results back: hVals and each shard's slice of every level <= kS,
+        //    then the top levels and the root
+        for (uint64_t g = 0; g < G; g++) {
+            const int d = (int)g;
+            mh_multi::Dev &B = *m->buf[d];
+            const uint64_t lo = g * S, ng = std::min(S, n - lo);
+            MH_HIP(hipSetDevice(m->dev[d]));
+            hipStream_t st = m->ctx[d]->stream;
+            if (hvals_out)
+                MH_HIP(hipMemcpyAsync(hvals_out + lo * 32, B.hv.p, ng * 32, hipMemcpyDeviceToHost,
+                                      st));
+            if (levels_out) {
+                // global level l <= kS restricted to this shard = the shard's
+                // level l; above the (short) last shard's own root, that root
+                // is promoted unchanged (htree.go:100-103)
+                LevelGeom lg;
+                lg.init(ng);
+                for (int l = 0; l <= kS && l < gg.nlevels; l++) {
+                    const int ll = std::min(l, lg.nlevels - 1);
+                    MH_HIP(hipMemcpyAsync(levels_out + (gg.off[l] + (lo >> l)) * 32,
+                                          B.levels.as<uint8_t>() + lg.off[ll] * 32,
+                                          (l < lg.nlevels ? lg.width[l] : 1) * 32,
+                                          hipMemcpyDeviceToHost, st));
+                }
+            }
+        }
+        hipStream_t st0 = m->ctx[0]->stream;
+        if (levels_out && G > 1) {
+            LevelGeom tg;
+            tg.init(G);
+            for (int j = 1; j < tg.nlevels; j++)
+                MH_HIP(hipMemcpyAsync(levels_out + gg.off[kS + j] * 32,
+                                      B0.top.as<uint8_t>() + tg.off[j] * 32, tg.width[j] * 32,
+                                      hipMemcpyDeviceToHost, st0));
+        }
+        MH_HIP(hipMemcpyAsync(root, d_root, 32, hipMemcpyDeviceToHost, st0));
+        for (int d = 0; d < K; d++)
+            if (int e = mh_ctx_synchronize(m->ctx[d])) return e;
+        return MH_OK;
+    });
+}

@@ -1,0 +1,75 @@
+"""Multi-GPU htree builds behind the C ABI (mh_multi_*).
+
+One process drives K devices (the shape of a cgo caller: one Go process, the
+commit path of immustore.go:1620-1632): one context (HIP stream) per device,
+an RCCL clique over them inside libimmustore_merkle.so, power-of-two leaf
+shards, one all-gather of the 32-byte subtree roots, the top levels reduced
+on the devices.  bench.py's --gpus N path is the same decomposition with one
+process per GPU over torch.distributed (immustore_amd/sharding.py).
+"""
+import ctypes as C
+from typing import Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .merkle import _addr, levels_len
+
+
+def shard_plan(n: int, ndev: int) -> Tuple[int, int]:
+    """(S, G): shard size (power of two >= ceil(n / ndev)) and shard count."""
+    s, g = C.c_uint64(), C.c_uint64()
+    N.check(N.load().mh_multi_shard_plan(n, ndev, C.byref(s), C.byref(g)))
+    return s.value, g.value
+
+
+class MultiDevice:
+    """mh_multi over the given device ordinals (a device may repeat: more
+    shards than devices, roots gathered by device copies instead of RCCL)."""
+
+    def __init__(self, devices: Sequence[int]):
+        arr = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        N.check(N.load().mh_multi_create(len(devices), arr, C.byref(h)))
+        self.handle = h.value
+        self.devices = list(devices)
+
+    def close(self):
+        if self.handle:
+            N.load().mh_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def ctx_handle(self, d: int):
+        return N.load().mh_multi_ctx(self.handle, d)
+
+    def synchronize(self):
+        N.check(N.load().mh_multi_synchronize(self.handle))
+
+    def build_entries_fixed(self, version: int, keys: np.ndarray, vals: np.ndarray,
+                            want_levels: bool = True):
+        """Host arrays keys (n, klen), vals (n, vlen) -> (hvals, levels, root)."""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        vals = np.ascontiguousarray(vals, np.uint8)
+        n = keys.shape[0]
+        hv = np.zeros((max(n, 1), 32), np.uint8)
+        lv = np.zeros((max(levels_len(n), 1), 32), np.uint8) if want_levels else None
+        root = np.zeros(32, np.uint8)
+        N.check(N.load().mh_multi_htree_build_entries_fixed(
+            self.handle, version, n, _addr(keys), keys.shape[1], _addr(vals), vals.shape[1],
+            _addr(hv), _addr(lv), _addr(root)))
+        return hv[:n], (lv[:levels_len(n)] if want_levels else None), root.tobytes()
+
+    def dev_build_entries_fixed(self, version, n_per_dev, keys, key_len, vals, val_len, levels,
+                                top_levels, roots, hvals=None):
+        """Device pointers per device (sequences of ints) -- asynchronous."""
+        K = len(self.devices)
+        P = C.c_void_p * K
+        N.check(N.load().mh_multi_dev_htree_build_entries_fixed(
+            self.handle, version, n_per_dev, P(*keys), key_len, P(*vals), val_len,
+            P(*hvals) if hvals is not None else None, P(*levels), P(*top_levels), P(*roots)))

@@ -68,6 +68,7 @@ extern "C" {
 #define MH_ERR_INVALID_PROOF_ENTRY 22   /* store.ErrInvalidProof from VerifyDocument's entry /
                                            hash-value check (pkg/verification/verification.go:60-76),
                                            i.e. raised BEFORE the document decode (:78-110) */
+#define MH_ERR_COLLECTIVE 23            /* RCCL unavailable or a collective failed (mh_multi_*) */
 
 #define MH_MAX_TX_METADATA_LEN 268 /* maxTxMetadataLen tx_metadata.go:36-39 */
 #define MH_MAX_KV_METADATA_LEN 11  /* maxKVMetadataLen kv_metadata.go:41-43 */
@@ -537,6 +538,48 @@ int mh_commit_queue_submit(mh_commit_queue *q, uint64_t n, const uint8_t *keys,
                            const uint8_t *expect_eh, uint8_t *hvals_out, uint8_t *eh_out);
 /* batches run and transactions hashed so far */
 int mh_commit_queue_stats(mh_commit_queue *q, uint64_t *batches, uint64_t *txs);
+
+/* ------------------------------------------------------------ multi-GPU
+ * one process (a cgo caller) driving K devices, one mh_ctx
+ * (HIP stream) per device, an RCCL clique over them (ncclCommInitAll; RCCL is
+ * loaded on first use, MH_ERR_COLLECTIVE if it is missing).  The htree leaves
+ * are cut into power-of-two aligned shards of S entries (mh_multi_shard_plan:
+ * S = next power of two >= ceil(n / K), shard g = [gS, min((g+1)S, n)),
+ * G = ceil(n / S) <= K shards); device g builds its shard's subtree with every
+ * level (exactly the global levels 0..log2 S of that range, htree.go:85-110),
+ * the G subtree roots are all-gathered over RCCL (32 bytes per device) and the
+ * top ceil(log2 G) levels are reduced over them.  A device may be listed more
+ * than once (more shards than devices); the roots are then gathered with
+ * device-to-device copies instead of RCCL. */
+typedef struct mh_multi mh_multi;
+int mh_multi_create(int ndev, const int *devices, mh_multi **out);
+int mh_multi_destroy(mh_multi *m);
+int mh_multi_size(mh_multi *m, int *ndev);
+/* the context of device d (for mh_dev_alloc / fills / copies on that device) */
+mh_ctx *mh_multi_ctx(mh_multi *m, int d);
+int mh_multi_synchronize(mh_multi *m);
+int mh_multi_shard_plan(uint64_t n, int ndev, uint64_t *shard, uint64_t *nshards);
+/* Tx.BuildHashTree over n fixed-shape entries (value hash loop
+ * immustore.go:1620-1630 + tx.go:332-355 + htree.go:68-113) across the K
+ * devices, HOST memory in and out (as mh_htree_build_entries with fixed
+ * strides): hvals_out (n x 32, may be NULL), levels_out (the flat level-major
+ * layout, mh_htree_levels_len(n) x 32, may be NULL), root. */
+int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n, const uint8_t *keys,
+                                       uint32_t key_len, const uint8_t *vals, uint32_t val_len,
+                                       uint8_t *hvals_out, uint8_t *levels_out, uint8_t root[32]);
+/* Device-resident variant (BASELINE configs[3]): device d holds entries
+ * [d n_per_dev, (d+1) n_per_dev) of a K * n_per_dev-entry tree (n_per_dev a
+ * power of two when K > 1) in keys[d] / vals[d]; it writes its subtree's levels
+ * to levels[d] (mh_htree_levels_len(n_per_dev) nodes), hVals to hvals_out[d]
+ * (array may be NULL), the top levels over the K gathered roots to
+ * top_levels[d] (mh_htree_levels_len(K) nodes) and the GLOBAL root to root[d]
+ * -- every device ends with the same top levels and root.  Asynchronous on the
+ * devices' context streams (mh_multi_synchronize). */
+int mh_multi_dev_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n_per_dev,
+                                           const uint8_t *const *keys, uint32_t key_len,
+                                           const uint8_t *const *vals, uint32_t val_len,
+                                           uint8_t *const *hvals_out, uint8_t *const *levels,
+                                           uint8_t *const *top_levels, uint8_t *const *root);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

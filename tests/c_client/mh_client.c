@@ -86,6 +86,28 @@ int main(int argc, char **argv) {
     hex("ahtree_cons", pt, pn * 32u);
     printf("empty_root_at %d\n", mh_ahtree_root_at(a, m + 1, at) == MH_ERR_UNEXISTENT_DATA);
     CHECK(mh_ahtree_free(a));
+
+    /* multi-GPU htree over entries: an RCCL clique over
+     * device 0, then device 0 listed three times (three shards, roots
+     * gathered by device copies); entries: key = BE64(k), 64-byte values =
+     * the ahtree payload bytes p[2k .. 2k+2) (m >= 2w required, else skipped) */
+    if (m >= 2 * w) {
+        uint8_t *keys = malloc(w * 8);
+        for (uint64_t k = 0; k < w; k++)
+            for (int b = 0; b < 8; b++) keys[k * 8 + b] = (uint8_t)(k >> (56 - 8 * b));
+        const int one[1] = {0}, three[3] = {0, 0, 0};
+        const int *devs[2] = {one, three};
+        const int nd[2] = {1, 3};
+        for (int v = 0; v < 2; v++) {
+            mh_multi *mm;
+            CHECK(mh_multi_create(nd[v], devs[v], &mm));
+            uint8_t mroot[32];
+            CHECK(mh_multi_htree_build_entries_fixed(mm, 1, w, keys, 8, p, 64, NULL, NULL, mroot));
+            hex(v ? "multi3_root" : "multi1_root", mroot, 32);
+            CHECK(mh_multi_destroy(mm));
+        }
+        free(keys);
+    }
     CHECK(mh_ctx_destroy(ctx));
     free(d);
     free(p);

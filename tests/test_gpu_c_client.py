@@ -34,7 +34,8 @@ def _run(w, m):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,m", [(1000, 777), (1, 3), (2, 4), (4096, 1 << 12), (65537, 100003)])
+@pytest.mark.parametrize("w,m", [(1000, 777), (1, 3), (2, 4), (4096, 1 << 13), (65537, 100003),
+                                 (300, 1000)])
 def test_c_client_matches_oracle(w, m):
     out = _run(w, m)
     d, p = _inputs(w, m)
@@ -57,6 +58,11 @@ def test_c_client_matches_oracle(w, m):
     st, cons = t.consistency_proof(m // 2, m)
     assert st == 0 and out["ahtree_cons"] == cons.tobytes().hex()
     assert out["empty_root_at"] == "1"
+    if m >= 2 * w:
+        # mh_multi_htree_build_entries_fixed (RCCL clique of device 0; three shards)
+        keys = np.frombuffer(np.arange(w, dtype=">u8").tobytes(), np.uint8).reshape(w, 8)
+        _, _, eroot = O.build_entries_fixed(1, keys, p[:2 * w].reshape(w, 64))
+        assert out["multi1_root"] == eroot.hex() and out["multi3_root"] == eroot.hex()
 
 
 def test_c_client_links_and_reports_no_device():
