@@ -55,7 +55,7 @@ SHA_PEAK_GCOMPS = 30.9
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", choices=["c2", "c4", "c3", "c5"], default="c2",
                    help="c2: BASELINE configs[1], 2^20 x 1 KiB per GPU (headline); c4: "
@@ -384,18 +384,24 @@ def main():
         elapsed = float(t.item())
     k_ms0, k_cnt0 = ctxs[0].timing("entries_fixed")
     r_ms0 = ctxs[0].timing("reduce")[0]
-    # isolated launches (outside the timed region): one build at a time on
-    # one stream, for the dominant kernel's exclusive duration
-    iso_ms = None
-    if D > 1:
-        ctxs[0].timing_reset()
-        ctxs[0].set_timing(True)
-        for k in range(5):
-            step(0)
-            torch.cuda.synchronize(dev)
-        ctxs[0].set_timing(False)
-        ims, icnt = ctxs[0].timing("entries_fixed")
-        iso_ms = ims / max(icnt, 1)
+    # isolated launches (outside the timed region): ISO builds back to back on
+    # ONE stream (a single BuildWith chain, i.e. --inflight 1), for the
+    # dominant kernel's exclusive duration and the single-build rate
+    ISO = 10
+    ctxs[0].timing_reset()
+    ctxs[0].set_timing(True)
+    torch.cuda.synchronize(dev)
+    ti0 = time.perf_counter()
+    for k in range(ISO):
+        with torch.cuda.stream(streams[0]):
+            N.check(L.mh_dev_htree_build_entries_fixed(ctxs[0].handle, 1, n, keys.data_ptr(),
+                                                       KEY_LEN, vals.data_ptr(), VAL, None,
+                                                       levels[0].data_ptr(), root[0].data_ptr()))
+    torch.cuda.synchronize(dev)
+    single_ms = (time.perf_counter() - ti0) / ISO * 1e3
+    ctxs[0].set_timing(False)
+    ims, icnt = ctxs[0].timing("entries_fixed")
+    iso_ms = ims / max(icnt, 1)
     # every build's root must be the same tree root (same input each step)
     r0 = root[0].cpu()
     assert all(torch.equal(r0, r.cpu()) for r in root), "in-flight builds disagree"
@@ -403,7 +409,8 @@ def main():
     k_ms = sum(c.timing("entries_fixed")[0] for c in ctxs[1:]) + k_ms0
     k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
     r_ms = sum(c.timing("reduce")[0] for c in ctxs[1:]) + r_ms0
-    kern_ms = k_ms / max(k_cnt, 1)
+    contended_ms = k_ms / max(k_cnt, 1)
+    kern_ms = iso_ms
     lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
     # levels written by one launch of the dominant kernel: the lanes' groups
     # up to level log2(lpl), then each workgroup's subtree 8 levels higher
@@ -463,13 +470,17 @@ def main():
                              "peak_gcomp_per_s": SHA_PEAK_GCOMPS,
                              "frac": round(comp_rate / 1e9 / SHA_PEAK_GCOMPS, 4)},
                      "reduce_ms_per_step": round(r_ms / max(a.steps, 1), 4),
-                     "note": "kernel_ms: mean launch duration over the timed region (builds "
-                             "in flight overlap, so it includes sharing the GPU)",
-                     "isolated_kernel_ms": round(iso_ms, 4) if iso_ms else None,
-                     "isolated_frac": round(alg_bytes / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                     if iso_ms else None,
-                     "isolated_sha_frac": round(comp_rate * kern_ms / iso_ms / 1e9 /
-                                                SHA_PEAK_GCOMPS, 4) if iso_ms else None},
+                     "kernel_ms_source": "isolated launches: %d builds back to back on one "
+                                         "stream after the timed region, HIP events around "
+                                         "each k_entries_fixed launch (achieved / frac / valu / "
+                                         "sha all use this duration)" % ISO,
+                     "contended_kernel_ms": round(contended_ms, 4),
+                     "contended_note": "mean launch duration inside the timed region, where "
+                                       "%d builds in flight share the GPU and stretch each "
+                                       "launch; not the kernel's own time" % D},
+        "single_build": {"builds_in_flight": 1, "ms_per_build": round(single_ms, 4),
+                         "gib_per_s": round(n * VAL / (single_ms * 1e-3) / 2 ** 30, 2),
+                         "note": "one BuildWith at a time (what one Go committer sees)"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.config == "c2":
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)

@@ -21,6 +21,13 @@
                     a 2^24-append ahtree + TxHeader encoding) and 10^6 htree
                     InclusionProof messages over a 2^24-leaf tree; sizes pass,
                     scan, write pass; a sample checked against oracle/wire.py.
+  --workload ragged SURVEY.md 8(a) a1-a4 over ragged EntrySpecs (the general
+                    CSR entry path, mh_dev_htree_build_entries): 2^20 entries,
+                    value length uniform in [0, 4096] (MaxValueLen), keys of
+                    8-64 B, KV metadata of 0-11 B, v1, device resident;
+                    value hashes + entry digests + leaves + all levels; SHA
+                    ceiling fraction of the ragged-message kernel; root and
+                    hVals checked against the oracle.
   --workload commit SURVEY.md 8(f) row 1: ImmuStore.precommit hashing over a
                     batch of 2^16 txs x 16 entries x 1 KiB values (8 B keys,
                     v1) in pinned host memory through mh_precommit_batch: value
@@ -179,7 +186,7 @@ def distributed_main(a):
 
 def make_parser():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire"],
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged"],
                    required=True)
     p.add_argument("--logs", action="store_true",
                    help="c3: also write the pLog / cLog appendable records (8(f) row 4)")
@@ -193,6 +200,9 @@ def make_parser():
     p.add_argument("--proofs", type=int, default=10 ** 6, help="c5 proofs")
     p.add_argument("--depth", type=int, default=24, help="c5 tree depth")
     p.add_argument("--no-ahtree", action="store_true", help="c5: htree proofs only")
+    p.add_argument("--entries", type=int, default=1 << 20, help="ragged entries")
+    p.add_argument("--max-vlen", type=int, default=4096, help="ragged: max value length")
+    p.add_argument("--no-check", action="store_true", help="ragged: skip the oracle check")
     return p
 
 
@@ -273,6 +283,79 @@ def c5_ahtree(a, m, N, L, ctx, dev, sync):
                      "kernel_ms": round(kms, 3), "mean_terms": round(float(cnt.float().mean()), 2),
                      "bitmap_exact": bool((okh == ~tamper).all()),
                      "tampered": int(tamper.sum())}
+    return res
+
+
+def ragged_inputs(n, max_vlen, seed=6):
+    """Host CSR arrays of the ragged workload (seeded): value length uniform
+    in [0, max_vlen], key 8-64 B, KV metadata 0-11 B (embedded/store/
+    options.go:37-39, kv_metadata.go:41-43)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, lo, hi, sd in (("v", 0, max_vlen, seed), ("k", 8, 64, seed + 1), ("m", 0, 11, seed + 2)):
+        ln = rng.integers(lo, hi + 1, n).astype(np.uint64)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum(ln, out=off[1:])
+        out[name] = (orc.fill_random(int(off[-1]) + 16, sd), off)
+    return out
+
+
+def ragged(a, m, N, L, ctx, dev, sync):
+    import numpy as np
+    import torch
+    n = a.entries
+    R = ragged_inputs(n, a.max_vlen)
+    d = {}
+    for name, (buf, off) in R.items():
+        d[name] = (torch.from_numpy(buf).to(dev), torch.from_numpy(off.view(np.int64)).to(dev))
+    nl = m.levels_len(n)
+    lv = torch.empty(nl * 32, dtype=torch.uint8, device=dev)
+    hv = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    root = torch.empty(32, dtype=torch.uint8, device=dev)
+    sync()
+
+    def step():
+        N.check(L.mh_dev_htree_build_entries(ctx.handle, 1, n, d["k"][0].data_ptr(),
+                                             d["k"][1].data_ptr(), d["m"][0].data_ptr(),
+                                             d["m"][1].data_ptr(), d["v"][0].data_ptr(),
+                                             d["v"][1].data_ptr(), None, None, hv.data_ptr(),
+                                             lv.data_ptr(), root.data_ptr()))
+
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t = timed(step, a.steps, a.warmup, sync)
+    ctx.set_timing(False)
+    runs = a.steps + a.warmup
+    tm = {k: round(ctx.timing(k)[0] / runs, 4) for k in ("varlen_sort", "entries_varlen", "reduce")}
+    sha_ms = tm["entries_varlen"]
+    vl = np.diff(R["v"][1]).astype(np.int64)
+    ml = 36 + np.diff(R["k"][1]).astype(np.int64) + np.diff(R["m"][1]).astype(np.int64)
+    comp_val = int(((vl + 72) // 64).sum())
+    comp_dig = int(((ml + 72) // 64).sum())
+    comp_tree = n + 2 * (n - 1)
+    sha_rate = (comp_val + comp_dig + n) / (sha_ms * 1e-3) / 1e9
+    SHA_PEAK = 30.9  # profiles/microbench_r01.txt
+    res = {"metric": "ragged htree build (value hashes + entry digests + all levels), device "
+                     "resident", "entries": n,
+           "value": round(float(vl.sum()) / t / 2 ** 30, 2), "unit": "GiB/s of values",
+           "M_entries_per_s": round(n / t / 1e6, 2), "ms_per_step": round(t * 1e3, 3),
+           "kernel_ms": tm,
+           "compressions": {"values": comp_val, "digests": comp_dig, "tree": comp_tree},
+           "sha": {"kernel": "k_entries_varlen (value blocks + digest blocks + leaf)",
+                   "gcomp_per_s": round(sha_rate, 2), "peak_gcomp_per_s": SHA_PEAK,
+                   "frac": round(sha_rate / SHA_PEAK, 4)},
+           "step_gcomp_per_s": round((comp_val + comp_dig + comp_tree) / t / 1e9, 2),
+           "sorted": os.environ.get("MH_VARLEN_NOSORT") is None}
+    if not a.no_check:
+        sys.path.insert(0, os.path.join(HERE, "oracle"))
+        import oracle as orc
+        st, ohv, _, oroot = orc.build_entries_csr(1, R["k"][0], R["k"][1], R["m"][0], R["m"][1],
+                                                  R["v"][0], R["v"][1], want_levels=False)
+        res["oracle_match"] = bool(st == 0 and root.cpu().numpy().tobytes() == oroot and
+                                   np.array_equal(hv.cpu().numpy().reshape(-1, 32), ohv))
     return res
 
 
@@ -589,6 +672,8 @@ def run_single(a):
                                           "threads, SHA-NI=%s, median of 3 = %.3f s"
                                           % (orc.has_shani(), t_cpu)}}
 
+    elif a.workload == "ragged":
+        out = ragged(a, m, N, L, ctx, dev, sync)
     elif a.workload == "c2e2e":
         n, vlen, klen = 1 << 20, 1024, 8
         hv = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()

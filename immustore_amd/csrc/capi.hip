@@ -270,18 +270,19 @@ static int build_digests(hipStream_t st, Timer *tm, const uint8_t *digests, uint
     return MH_OK;
 }
 
-// General CSR path.  msg_total = sum of digest message lengths (host known).
+// General CSR path (ragged keys / metadata / values, hVal overrides): value
+// hashes, entry digests and leaves in one fused launch (varlen_kernels.hip),
+// then the levels above the leaves.
 static int build_csr(hipStream_t st, Timer *tm, int version, uint64_t n, const uint8_t *keys,
                      const uint64_t *key_off, const uint8_t *md, const uint64_t *md_off,
                      const uint8_t *vals, const uint64_t *val_off, const uint8_t *ov,
-                     const uint8_t *use, uint8_t *hvals, uint64_t *msg_off, uint8_t *msgs,
-                     uint8_t *digests, uint8_t *levels, const LevelGeom &g) {
-    MH_HIP(launch_sha256_csr(st, tm, vals, val_off, n, ov, use, hvals));
-    MH_HIP(launch_msg_offsets(st, tm, version, n, key_off, md_off, msg_off));
-    MH_HIP(launch_digest_assemble(st, tm, version, n, keys, key_off, md, md_off, hvals, msg_off, msgs,
-                                  nullptr));
-    MH_HIP(launch_sha256_csr(st, tm, msgs, msg_off, n, nullptr, nullptr, digests));
-    return build_digests(st, tm, digests, n, levels, g);
+                     const uint8_t *use, uint8_t *hvals, uint8_t *levels, const LevelGeom &g,
+                     DevBuf &sort) {
+    MH_HIP(sort.ensure(sha_varlen_scratch_bytes(n)));
+    MH_HIP(launch_entries_varlen(st, tm, version, n, keys, key_off, md, md_off, vals, val_off, ov,
+                                 use, hvals, levels, true, sort.as<uint8_t>()));
+    MH_HIP(launch_reduce(st, tm, levels, g, 0));
+    return MH_OK;
 }
 
 extern "C" int mh_dev_htree_build_digests(mh_ctx *c, const uint8_t *digests, uint64_t n,
@@ -323,15 +324,8 @@ extern "C" int mh_dev_htree_build_entries_fixed(mh_ctx *c, int version, uint64_t
                 uint64_t *koff = c->s_offs.as<uint64_t>(), *voff = koff + (n + 1);
                 MH_HIP(launch_iota_offsets(c->stream, koff, n, key_len));
                 MH_HIP(launch_iota_offsets(c->stream, voff, n, val_len));
-                uint64_t msg_total = n * ((uint64_t)key_len + (version == 1 ? 36 : 32));
-                MH_HIP(c->s_hvals.ensure(n * 32));
-                MH_HIP(c->s_msgoff.ensure((n + 1) * 8));
-                MH_HIP(c->s_msgs.ensure(msg_total));
-                MH_HIP(c->s_digests.ensure(n * 32));
-                uint8_t *hv = hvals_out ? hvals_out : c->s_hvals.as<uint8_t>();
                 int st = build_csr(c->stream, c->tm(), version, n, keys, koff, nullptr, nullptr, vals,
-                                   voff, nullptr, nullptr, hv, c->s_msgoff.as<uint64_t>(),
-                                   c->s_msgs.as<uint8_t>(), c->s_digests.as<uint8_t>(), levels, g);
+                                   voff, nullptr, nullptr, hvals_out, levels, g, c->s_sort);
                 if (st) return st;
             }
         }
@@ -353,27 +347,18 @@ extern "C" int mh_dev_htree_build_entries(mh_ctx *c, int version, uint64_t n, co
         LevelGeom g;
         g.init(n);
         if (n) {
-            // bounds of the CSR arrays (one small D2H): sizes the message scratch
-            // and rejects v0 + KV metadata up front (tx.go:691-693).
-            uint64_t kb[2], mb[2] = {0, 0};
-            MH_HIP(hipMemcpyAsync(&kb[0], key_off, 8, hipMemcpyDeviceToHost, c->stream));
-            MH_HIP(hipMemcpyAsync(&kb[1], key_off + n, 8, hipMemcpyDeviceToHost, c->stream));
-            if (md_off) {
+            if (version == 0 && md_off) {
+                // v0 + KV metadata is rejected up front (tx.go:691-693): one
+                // small D2H of the metadata bounds
+                uint64_t mb[2] = {0, 0};
                 MH_HIP(hipMemcpyAsync(&mb[0], md_off, 8, hipMemcpyDeviceToHost, c->stream));
                 MH_HIP(hipMemcpyAsync(&mb[1], md_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+                MH_HIP(hipStreamSynchronize(c->stream));
+                if (mb[1] != mb[0]) return MH_ERR_METADATA_UNSUPPORTED;
             }
-            MH_HIP(hipStreamSynchronize(c->stream));
-            if (version == 0 && mb[1] != mb[0]) return MH_ERR_METADATA_UNSUPPORTED;
-            const uint64_t msg_total = (kb[1] - kb[0]) + (mb[1] - mb[0]) + n * (version == 1 ? 36 : 32);
             std::lock_guard<std::mutex> lk(c->mu);
-            MH_HIP(c->s_hvals.ensure(n * 32));
-            MH_HIP(c->s_msgoff.ensure((n + 1) * 8));
-            MH_HIP(c->s_msgs.ensure(msg_total));
-            MH_HIP(c->s_digests.ensure(n * 32));
-            uint8_t *hv = hvals_out ? hvals_out : c->s_hvals.as<uint8_t>();
             int st = build_csr(c->stream, c->tm(), version, n, keys, key_off, md, md_off, vals, val_off,
-                               hval_override, use_override, hv, c->s_msgoff.as<uint64_t>(),
-                               c->s_msgs.as<uint8_t>(), c->s_digests.as<uint8_t>(), levels, g);
+                               hval_override, use_override, hvals_out, levels, g, c->s_sort);
             if (st) return st;
         }
         return write_root(c->stream, g, levels, root);
@@ -401,7 +386,10 @@ extern "C" int mh_dev_sha256_batch(mh_ctx *c, const uint8_t *buf, const uint64_t
     return mh_guard([&]() -> int {
         if (!c || (n && (!off || !out))) return MH_ERR_ILLEGAL_ARGUMENTS;
         MH_HIP(hipSetDevice(c->device));
-        MH_HIP(launch_sha256_csr(c->stream, c->tm(), buf, off, n, nullptr, nullptr, out));
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(c->s_sort.ensure(sha_varlen_scratch_bytes(n)));
+        MH_HIP(launch_sha256_csr(c->stream, c->tm(), buf, off, n, nullptr, nullptr, out,
+                                 c->s_sort.as<uint8_t>()));
         return MH_OK;
     });
 }
@@ -559,14 +547,10 @@ extern "C" int mh_htree_build_entries(mh_htree *t, int version, uint64_t n, cons
                 ovd = t->ov.as<uint8_t>();
                 used = t->use.as<uint8_t>();
             }
-            const uint64_t msg_total = kbytes + md_bytes + n * (version == 1 ? 36 : 32);
-            MH_HIP(t->msgoff.ensure((n + 1) * 8));
-            MH_HIP(t->msgs.ensure(msg_total));
-            MH_HIP(t->digests.ensure(n * 32));
             st = build_csr(t->stream, tm, version, n, t->in_a.as<uint8_t>(), t->off_a.as<uint64_t>(),
                            md_off ? t->in_c.as<uint8_t>() : nullptr, mo_dev, t->in_b.as<uint8_t>(),
-                           t->off_b.as<uint64_t>(), ovd, used, hv_dev, t->msgoff.as<uint64_t>(),
-                           t->msgs.as<uint8_t>(), t->digests.as<uint8_t>(), t->levels.as<uint8_t>(), g);
+                           t->off_b.as<uint64_t>(), ovd, used, hv_dev, t->levels.as<uint8_t>(), g,
+                           t->sort);
             if (st) return st;
         }
     done:

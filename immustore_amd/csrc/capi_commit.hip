@@ -134,12 +134,11 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
     const uint64_t b_ko = L.add((n + 1) * 8), b_mo = L.add(R.md_off ? (n + 1) * 8 : 0),
                    b_vo = L.add((n + 1) * 8);
     const uint64_t b_ov = L.add(R.use ? n * 32 : 0), b_use = L.add(R.use ? n : 0);
-    const uint64_t b_hv = L.add(n * 32), b_go = L.add((n + 1) * 8),
-                   b_msg = L.add(n * (R.version == 1 ? 36 : 32) + kb + (R.version == 1 ? mb : 0) +
-                                 64),
+    const uint64_t b_hv = L.add(n * 32),
                    b_dig = L.add(std::max<uint64_t>(n, 1) * 32), b_eh = L.add(nt * 32),
                    b_lv = L.add(small ? std::max<uint64_t>(n, 1) * 32 : 0),
-                   b_lo = L.add(small ? (nt + 1) * 8 : 0);
+                   b_lo = L.add(small ? (nt + 1) * 8 : 0),
+                   b_sort = L.add(sha_varlen_scratch_bytes(n));
     MH_HIP(s.arena.ensure(L.total));
     const uint64_t idx_bytes = ((small ? (nt + 1) * 8 : plan_index_bytes(P, nt)) + 255) & ~255ull;
     MH_HIP(s.pin.ensure(idx_bytes + n * 32 + nt * 32));
@@ -168,17 +167,13 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
         hipLaunchKernelGGL(k_rebase3, dim3((unsigned)((n + 256) / 256)), dim3(256), 0, st, n, ko, mo,
                            vo, k0, m0, v0);
         MH_HIP(hipGetLastError());
-        // ---- hVal (immustore.go:1624-1629), entry digests (tx.go:690-731)
-        uint8_t *hv = base + b_hv;
-        MH_HIP(launch_sha256_csr(st, tm, base + b_v, vo, n, R.use ? base + b_ov : nullptr,
-                                 R.use ? base + b_use : nullptr, hv));
-        uint64_t *go = (uint64_t *)(base + b_go);
-        MH_HIP(launch_msg_offsets(st, tm, R.version, n, ko, R.version == 1 ? mo : nullptr, go));
-        MH_HIP(launch_digest_assemble(st, tm, R.version, n, base + b_k, ko,
-                                      R.version == 1 ? base + b_m : nullptr,
-                                      R.version == 1 ? mo : nullptr, hv, go, base + b_msg,
-                                      nullptr));
-        MH_HIP(launch_sha256_csr(st, tm, base + b_msg, go, n, nullptr, nullptr, base + b_dig));
+        // ---- hVal (immustore.go:1624-1629) and entry digests (tx.go:690-731)
+        // in one fused launch (varlen_kernels.hip)
+        MH_HIP(launch_entries_varlen(st, tm, R.version, n, base + b_k, ko,
+                                     R.version == 1 ? base + b_m : nullptr,
+                                     R.version == 1 ? mo : nullptr, base + b_v, vo,
+                                     R.use ? base + b_ov : nullptr, R.use ? base + b_use : nullptr,
+                                     base + b_hv, base + b_dig, false, base + b_sort));
     }
     // ---- one htree per tx (tx.go:347 -> htree.go:68-113), Eh = root
     if (small) {

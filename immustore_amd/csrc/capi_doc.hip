@@ -29,7 +29,7 @@ int sha_batch_host(mh_ctx *c, const uint8_t *buf, const std::vector<uint64_t> &o
     hipStream_t st = c->stream;
     Layout L;
     const uint64_t b_buf = L.add(std::max<uint64_t>(bytes, 16)), b_off = L.add((n + 1) * 8),
-                   b_out = L.add(n * 32);
+                   b_out = L.add(n * 32), b_sort = L.add(sha_varlen_scratch_bytes(n));
     MH_HIP(c->s_msgs.ensure(L.total));
     uint8_t *base = c->s_msgs.as<uint8_t>();
     std::vector<uint64_t> rel(n + 1);
@@ -37,7 +37,7 @@ int sha_batch_host(mh_ctx *c, const uint8_t *buf, const std::vector<uint64_t> &o
     if (bytes) MH_HIP(hipMemcpyAsync(base + b_buf, buf + off[0], bytes, hipMemcpyHostToDevice, st));
     MH_HIP(hipMemcpyAsync(base + b_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     MH_HIP(launch_sha256_csr(st, c->tm(), base + b_buf, (const uint64_t *)(base + b_off), n,
-                             nullptr, nullptr, base + b_out));
+                             nullptr, nullptr, base + b_out, base + b_sort));
     MH_HIP(hipMemcpyAsync(out, base + b_out, n * 32, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
     return MH_OK;

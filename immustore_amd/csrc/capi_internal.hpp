@@ -169,6 +169,7 @@ struct mh_ctx {
     EventTimer timer;
     std::mutex mu;  // guards scratch for mh_dev_* calls
     DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs, s_ctr;
+    DevBuf s_sort;        // length-class sort of ragged messages (varlen_kernels.hip)
     DevBuf s_tx, s_tree;  // tx layer (capi_tx.hip)
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
@@ -182,6 +183,7 @@ struct mh_htree {
     uint64_t width = 0;
     uint8_t root[32];
     DevBuf levels, in_a, in_b, in_c, off_a, off_b, off_c, ov, use, hv, msgoff, msgs, digests;
+    DevBuf sort;  // length-class sort of ragged messages
     DevBuf w_in, w_out;  // wire formats (capi_wire.hip)
     void *pinned = nullptr;
     uint64_t pinned_cap = 0;

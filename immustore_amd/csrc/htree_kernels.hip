@@ -600,67 +600,71 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
     }
 }
 
-__global__ __launch_bounds__(256) void k_sha256_csr(const uint8_t *__restrict__ buf,
-                                                    const uint64_t *__restrict__ off, uint64_t n,
-                                                    const uint8_t *__restrict__ override32,
-                                                    const uint8_t *__restrict__ use_override,
-                                                    uint8_t *__restrict__ out32) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (use_override && use_override[i]) {  // EntrySpec.IsValueTruncated
-        reinterpret_cast<uint4 *>(out32 + i * 32)[0] =
-            reinterpret_cast<const uint4 *>(override32 + i * 32)[0];
-        reinterpret_cast<uint4 *>(out32 + i * 32)[1] =
-            reinterpret_cast<const uint4 *>(override32 + i * 32)[1];
-        return;
+// Level reduction with two in-lane levels first: a T-thread workgroup turns
+// 4T nodes of level l0 into levels l0+1, l0+2 (each lane hashes its own 4
+// nodes -> 2 -> 1, every lane busy: three quarters of all the node hashes)
+// and then up to nsteps-2 (<= 8) more levels of its aligned subtree in LDS.
+// Every level is written (htree.go:158 needs them for InclusionProof).
+template <int T>
+__global__ __launch_bounds__(T) void k_reduce4(uint8_t *__restrict__ levels, LevelArgs la, int l0,
+                                               int nsteps) {
+    __shared__ uint32_t buf[2][T][9];
+    const int t = threadIdx.x;
+    const uint64_t q = (uint64_t)blockIdx.x * T + t;  // node of level l0 + 2
+    uint32_t A[8], B[8];
+    if (q < la.width[l0 + 2]) {
+        // k = 0, 1: level l0+1 nodes 2q, 2q+1; k = 2: level l0+2 node q
+#pragma unroll 1
+        for (int k = 0; k < 3; k++) {
+            const int l = k < 2 ? l0 + 1 : l0 + 2;
+            const uint64_t p = k < 2 ? 2 * q + k : q;
+            if (p >= la.width[l]) break;  // k == 1 only: promoted below
+            uint32_t lft[8], rgt[8], out[8];
+            if (k < 2) load_digest(levels + (la.off[l0] + 2 * p) * 32, lft);
+            else copy8(lft, A);
+            const bool pair = 2 * p + 1 < la.width[l - 1];
+            if (pair) {
+                if (k < 2) load_digest(levels + (la.off[l0] + 2 * p + 1) * 32, rgt);
+                else copy8(rgt, B);
+                node_hash_g(lft, rgt, out);
+            } else {
+                copy8(out, lft);
+            }
+            store_digest(levels + (la.off[l] + p) * 32, out);
+            if (k == 0) copy8(A, out);
+            else if (k == 1) copy8(B, out);
+            else copy8(A, out);
+        }
+        // width[l0+1] odd and 2q+1 past it: node q of level l0+2 is the promoted 2q
+        if (2 * q + 1 >= la.width[l0 + 1]) store_digest(levels + (la.off[l0 + 2] + q) * 32, A);
+#pragma unroll
+        for (int j = 0; j < 8; j++) buf[0][t][j] = A[j];
     }
-    uint32_t h[8];
-    sha256_bytes(buf + off[i], off[i + 1] - off[i], -1, h);
-    store_digest(out32 + i * 32, h);
-}
-
-__global__ __launch_bounds__(256) void k_sha256_fixed(const uint8_t *__restrict__ buf,
-                                                      uint64_t stride, uint64_t len, uint64_t n,
-                                                      uint8_t *__restrict__ out32) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t h[8];
-    sha256_bytes(buf + i * stride, len, -1, h);
-    store_digest(out32 + i * 32, h);
-}
-
-// msg_off[i] = (key_off[i]-key_off[0]) + (md_off[i]-md_off[0]) + i*(v1 ? 36 : 32)
-__global__ void k_msg_offsets(int version, uint64_t n, const uint64_t *__restrict__ key_off,
-                              const uint64_t *__restrict__ md_off, uint64_t *__restrict__ msg_off) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
-    uint64_t o = key_off[i] - key_off[0] + i * (version == 1 ? 36u : 32u);
-    if (md_off) o += md_off[i] - md_off[0];
-    msg_off[i] = o;
-}
-
-// Entry digest messages (tx.go:690-731), one lane per entry, byte copies.
-__global__ __launch_bounds__(256) void k_digest_assemble(
-    int version, uint64_t n, const uint8_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
-    const uint8_t *__restrict__ md, const uint64_t *__restrict__ md_off,
-    const uint8_t *__restrict__ hvals, const uint64_t *__restrict__ msg_off,
-    uint8_t *__restrict__ msgs, int *__restrict__ err_flag) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t kl = key_off[i + 1] - key_off[i];
-    const uint64_t ml = md_off ? md_off[i + 1] - md_off[i] : 0;
-    uint8_t *o = msgs + msg_off[i];
-    if (version == 1) {
-        *o++ = (uint8_t)(ml >> 8);
-        *o++ = (uint8_t)ml;
-        for (uint64_t k = 0; k < ml; k++) *o++ = md[md_off[i] + k];
-        *o++ = (uint8_t)(kl >> 8);
-        *o++ = (uint8_t)kl;
-    } else if (ml > 0 && err_flag) {
-        atomicExch(err_flag, MH_ERR_METADATA_UNSUPPORTED);
+    int cur = 0;
+    for (int s = 3; s <= nsteps; s++) {
+        __syncthreads();
+        const int active = T >> (s - 2);
+        const int l = l0 + s;
+        if (t < active) {
+            const uint64_t qq = (uint64_t)blockIdx.x * active + t;
+            if (qq < la.width[l]) {
+                uint32_t lft[8], rgt[8], out[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) lft[j] = buf[cur][2 * t][j];
+                if (2 * qq + 1 < la.width[l - 1]) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) rgt[j] = buf[cur][2 * t + 1][j];
+                    node_hash_g(lft, rgt, out);
+                } else {
+                    copy8(out, lft);
+                }
+                store_digest(levels + (la.off[l] + qq) * 32, out);
+#pragma unroll
+                for (int j = 0; j < 8; j++) buf[cur ^ 1][t][j] = out[j];
+            }
+        }
+        cur ^= 1;
     }
-    for (uint64_t k = 0; k < kl; k++) *o++ = keys[key_off[i] + k];
-    for (int k = 0; k < 32; k++) *o++ = hvals[i * 32 + k];
 }
 
 // ------------------------------------------------------------------ small helpers
@@ -796,6 +800,12 @@ hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const Level
         if (left <= 10 && g.width[cur] <= 1024) {
             hipLaunchKernelGGL(k_reduce<512>, dim3(1), dim3(512), 0, st, levels, la, cur, left);
             cur += left;
+        } else if (left >= 3 && g.width[cur] >= 4 * 256) {
+            // two in-lane levels + up to 8 in LDS per launch
+            const int steps = std::min(10, left);
+            const unsigned grid = grid_for(g.width[cur + 2], 256);
+            hipLaunchKernelGGL(k_reduce4<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);
+            cur += steps;
         } else {
             const int steps = std::min(9, left);
             const unsigned grid = grid_for(g.width[cur + 1], 256);
@@ -803,44 +813,6 @@ hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const Level
             cur += steps;
         }
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
-                             uint64_t n, const uint8_t *override32, const uint8_t *use_override,
-                             uint8_t *out32) {
-    if (!n) return hipSuccess;
-    TimerScope ts(tm, "sha256_csr", st);
-    hipLaunchKernelGGL(k_sha256_csr, dim3(grid_for(n, 256)), dim3(256), 0, st, buf, off, n,
-                       override32, use_override, out32);
-    return hipGetLastError();
-}
-
-hipError_t launch_sha256_fixed(hipStream_t st, Timer *tm, const uint8_t *buf, uint64_t stride,
-                               uint64_t len, uint64_t n, uint8_t *out32) {
-    if (!n) return hipSuccess;
-    TimerScope ts(tm, "sha256_fixed", st);
-    hipLaunchKernelGGL(k_sha256_fixed, dim3(grid_for(n, 256)), dim3(256), 0, st, buf, stride, len,
-                       n, out32);
-    return hipGetLastError();
-}
-
-hipError_t launch_msg_offsets(hipStream_t st, Timer *tm, int version, uint64_t n,
-                              const uint64_t *key_off, const uint64_t *md_off, uint64_t *msg_off) {
-    TimerScope ts(tm, "msg_offsets", st);
-    hipLaunchKernelGGL(k_msg_offsets, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, version, n,
-                       key_off, md_off, msg_off);
-    return hipGetLastError();
-}
-
-hipError_t launch_digest_assemble(hipStream_t st, Timer *tm, int version, uint64_t n,
-                                  const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
-                                  const uint64_t *md_off, const uint8_t *hvals,
-                                  const uint64_t *msg_off, uint8_t *msgs, int *err_flag) {
-    if (!n) return hipSuccess;
-    TimerScope ts(tm, "digest_assemble", st);
-    hipLaunchKernelGGL(k_digest_assemble, dim3(grid_for(n, 256)), dim3(256), 0, st, version, n, keys,
-                       key_off, md, md_off, hvals, msg_off, msgs, err_flag);
     return hipGetLastError();
 }
 

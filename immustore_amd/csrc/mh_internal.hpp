@@ -85,21 +85,23 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
 bool entries_fixed_supported(int version, const uint8_t *keys, uint32_t key_len,
                              const uint8_t *vals, uint32_t val_len);
 
+// SHA-256 of n ragged byte ranges buf[off[i] .. off[i+1]) (varlen_kernels.hip);
+// override32[i] replaces message i where use_override[i] != 0.  scratch
+// (sha_varlen_scratch_bytes(n), device, stream-ordered on st) lets the
+// messages be bucketed by block count first; null hashes them in input order.
+size_t sha_varlen_scratch_bytes(uint64_t n);
 hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
                              uint64_t n, const uint8_t *override32, const uint8_t *use_override,
-                             uint8_t *out32);
-hipError_t launch_sha256_fixed(hipStream_t st, Timer *tm, const uint8_t *buf, uint64_t stride,
-                               uint64_t len, uint64_t n, uint8_t *out32);
-
-// Assemble entry-digest messages (tx.go:690-731) into `msgs` at msg_off.
-// err_flag (device int) is set to MH_ERR_METADATA_UNSUPPORTED for v0 + md.
-hipError_t launch_digest_assemble(hipStream_t st, Timer *tm, int version, uint64_t n,
-                                  const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
-                                  const uint64_t *md_off, const uint8_t *hvals,
-                                  const uint64_t *msg_off, uint8_t *msgs, int *err_flag);
-hipError_t launch_msg_offsets(hipStream_t st, Timer *tm, int version, uint64_t n,
-                              const uint64_t *key_off, const uint64_t *md_off, uint64_t *msg_off);
-
+                             uint8_t *out32, uint8_t *scratch);
+// Fused ragged entries (varlen_kernels.hip): hVal (or override) -> hvals_out
+// (may be null), entry digest (tx.go:690-731) -> out32, or its htree leaf when
+// leaf is set (level 0 of the tree).  scratch as for launch_sha256_csr.
+hipError_t launch_entries_varlen(hipStream_t st, Timer *tm, int version, uint64_t n,
+                                 const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
+                                 const uint64_t *md_off, const uint8_t *vals,
+                                 const uint64_t *val_off, const uint8_t *override32,
+                                 const uint8_t *use_override, uint8_t *hvals_out, uint8_t *out32,
+                                 bool leaf, uint8_t *scratch);
 // Leaves from digests (htree.go:79-83) + in-lane levels up to log2(LPL).
 hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *digests,
                                       uint64_t n, uint8_t *levels, const LevelGeom &g,

@@ -190,6 +190,21 @@ def build_entries(version, keys, mds, vals, overrides=None):
     return st, hv[:n], lv[:levels_len(n)], root.tobytes()
 
 
+def build_entries_csr(version, kb, ko, mb, mo, vb, vo, want_levels=True):
+    """CSR byte arrays (u8) + u64 offsets (n+1 each; mb/mo may be None) ->
+    (status, hvals, levels, root); the array form of build_entries for large
+    ragged batches."""
+    n = len(ko) - 1
+    ko, vo = np.ascontiguousarray(ko, np.uint64), np.ascontiguousarray(vo, np.uint64)
+    mo = None if mo is None else np.ascontiguousarray(mo, np.uint64)
+    hv = np.zeros((max(n, 1), 32), np.uint8)
+    lv = np.zeros((max(levels_len(n), 1), 32), np.uint8) if want_levels else None
+    root = np.zeros(32, np.uint8)
+    st = lib().orc_build_entries(version, n, _p(kb), _p(ko, u64p), _p(mb), _p(mo, u64p), _p(vb),
+                                 _p(vo, u64p), None, None, _p(hv), _p(lv), _p(root))
+    return st, hv[:n], (lv[:levels_len(n)] if want_levels else None), root.tobytes()
+
+
 def precommit_batch(version, tx_off, keys, key_off, vals, val_off, md=None, md_off=None,
                     hval_override=None, use_override=None, expect_eh=None, max_width=0,
                     nthreads=1):

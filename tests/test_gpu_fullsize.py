@@ -259,3 +259,35 @@ def test_c5_ahtree_full_vs_oracle(m, ctx, orc):
         # whose tampered term is unused when i == j
         assert got[~tam].all() and c == int(got.sum())
         assert not got[tam & (iv != jv)].any()
+
+
+def test_ragged_full_size_vs_oracle(m, ctx, orc):
+    """The ragged workload of bench_workloads.py at its size: 2^20 entries,
+    values 0-4096 B, keys 8-64 B, KV metadata 0-11 B, v1 -- every hVal, every
+    level and the root through mh_dev_htree_build_entries."""
+    import sys
+    import torch
+    from immustore_amd import _native as N
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench_workloads import ragged_inputs
+    n = 1 << 20
+    R = ragged_inputs(n, 4096)
+    dev = torch.device("cuda", 0)
+    d = {k: (torch.from_numpy(b).to(dev), torch.from_numpy(o.view(np.int64)).to(dev))
+         for k, (b, o) in R.items()}
+    nl = m.levels_len(n)
+    lv = torch.empty(nl * 32, dtype=torch.uint8, device=dev)
+    hv = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    root = torch.empty(32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    N.check(N.load().mh_dev_htree_build_entries(
+        ctx.handle, 1, n, d["k"][0].data_ptr(), d["k"][1].data_ptr(), d["m"][0].data_ptr(),
+        d["m"][1].data_ptr(), d["v"][0].data_ptr(), d["v"][1].data_ptr(), None, None,
+        hv.data_ptr(), lv.data_ptr(), root.data_ptr()))
+    ctx.synchronize()
+    st, ohv, olv, oroot = orc.build_entries_csr(1, R["k"][0], R["k"][1], R["m"][0], R["m"][1],
+                                                R["v"][0], R["v"][1])
+    assert st == 0
+    assert root.cpu().numpy().tobytes() == oroot
+    assert np.array_equal(hv.cpu().numpy().reshape(n, 32), ohv)
+    assert np.array_equal(lv.cpu().numpy().reshape(nl, 32), olv)

@@ -78,6 +78,49 @@ def test_sha256_batch_any_alignment(m, ctx):
         assert got[i].tobytes() == H(buf[int(cuts[i]):int(cuts[i + 1])].tobytes())
 
 
+def test_sha256_batch_ragged_length_classes(m, ctx):
+    """Many ragged messages (the length-class sorted kernel, n > 256): every
+    length 0..1100 several times over at random alignments, a spread up to
+    4 KiB, and messages past the last length class (> 1023 blocks)."""
+    from immustore_amd import _native as N
+    rng = np.random.default_rng(12)
+    lens = np.concatenate([np.tile(np.arange(0, 1101), 3), rng.integers(0, 4097, 6000),
+                           [65472 - 9, 65472 - 8, 70000, 100000, 0, 0]])
+    rng.shuffle(lens)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    for shift in (0, 1, 3):   # the whole batch starts at every alignment
+        d_buf = DevBuf.from_host(ctx, buf)
+        o = off + np.uint64(shift)
+        d_off = DevBuf.from_host(ctx, o)
+        d_out = DevBuf(ctx, 32 * len(lens))
+        N.check(N.load().mh_dev_sha256_batch(ctx.handle, d_buf.ptr, d_off.ptr, len(lens), d_out.ptr))
+        got = d_out.to_host().reshape(-1, 32)
+        bb = buf.tobytes()
+        for k in range(len(lens)):
+            assert got[k].tobytes() == H(bb[int(o[k]):int(o[k + 1])]), (shift, k, int(lens[k]))
+
+
+def test_entries_ragged_with_overrides_vs_oracle(m, ctx, orc):
+    """General entry path with ragged keys / metadata / values and a share of
+    IsValueTruncated overrides (their hVal taken from the caller)."""
+    rng = np.random.default_rng(13)
+    for n in (257, 3001):
+        keys = [rng.integers(0, 256, int(rng.integers(1, 130)), dtype=np.uint8).tobytes()
+                for _ in range(n)]
+        mds = [rng.integers(0, 256, int(rng.integers(0, 12)), dtype=np.uint8).tobytes()
+               for _ in range(n)]
+        vals = [rng.integers(0, 256, int(rng.integers(0, 4097)), dtype=np.uint8).tobytes()
+                for _ in range(n)]
+        ov = [H(v) if rng.random() < 0.2 else None for v in vals]
+        vals2 = [b"" if o is not None else v for o, v in zip(ov, vals)]
+        eh, hv, lv = m.build_hash_tree(1, keys, vals2, mds, hval_overrides=ov, ctx=ctx)
+        st, ohv, olv, oroot = orc.build_entries(1, keys, mds, vals)
+        assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
+
+
+
 # ------------------------------------------------------------------ htree
 def test_htree_build_with_golden(m, ctx, synthetic, lpl):
     for case in synthetic["htree"]:

@@ -15,7 +15,7 @@ def main():
     p.add_argument("trace")
     p.add_argument("--steps", type=int, required=True)
     p.add_argument("--warmup", type=int, required=True)
-    p.add_argument("--isolated", type=int, default=5)
+    p.add_argument("--isolated", type=int, default=10)
     p.add_argument("--kernel", default="k_entries_fixed")
     a = p.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
