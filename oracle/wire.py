@@ -20,7 +20,11 @@ with the C oracle (oracle.py) the way the Go server does, and serialises it:
 Parity note: the reference holds no Go-marshalled protobuf bytes for these
 messages, so the encoding is pinned by the protobuf wire-format rules as the
 python runtime implements them (protobuf 7.x), and the message CONTENT (terms,
-headers) by the C oracle, itself pinned by the Go-written fixtures.
+headers) by the C oracle, itself pinned by the Go-written fixtures.  The
+declarations below are checked field by field (name, number, type, label,
+message type) against the reference's own compiled descriptor
+(schema.pb.go file_schema_proto_rawDesc, decoded into
+tests/golden/schema_fields.json; tests/test_wire_oracle.py).
 """
 import struct
 

@@ -495,6 +495,34 @@ def synthetic():
     return res
 
 
+SCHEMA_MESSAGES = ("TxMetadata", "TxHeader", "DualProofV2", "InclusionProof")
+
+
+def schema_fields():
+    """(name, number, type, label, type_name) of the proof messages, decoded
+    from the reference's generated descriptor (pkg/api/schema/schema.pb.go,
+    file_schema_proto_rawDesc: the serialised FileDescriptorProto of
+    schema.proto).  Data only: the byte literal is parsed and decoded here,
+    nothing of the Go file is kept but these tuples."""
+    import re
+    from google.protobuf import descriptor_pb2
+    lines = open(os.path.join(REF, "pkg/api/schema/schema.pb.go")).read().split("\n")
+    start = next(k for k, ln in enumerate(lines) if ln.startswith("var file_schema_proto_rawDesc = []byte{"))
+    raw = bytearray()
+    for ln in lines[start + 1:]:
+        if ln.startswith("}"):
+            break
+        raw += bytes(int(x, 16) for x in re.findall(r"0x([0-9a-f]{2})", ln))
+    fdp = descriptor_pb2.FileDescriptorProto.FromString(bytes(raw))
+    out = {"package": fdp.package, "syntax": fdp.syntax, "messages": {}}
+    for m in fdp.message_type:
+        if m.name in SCHEMA_MESSAGES:
+            out["messages"][m.name] = [[f.name, f.number, f.type, f.label, f.type_name]
+                                       for f in m.field]
+    assert set(out["messages"]) == set(SCHEMA_MESSAGES)
+    return out
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("needs /root/reference (build container only)")
@@ -507,6 +535,8 @@ def main():
               "values", fx[name]["n_values"])
     with open(os.path.join(OUT, "immudb_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=0, sort_keys=True)
+    with open(os.path.join(OUT, "schema_fields.json"), "w") as f:
+        json.dump(schema_fields(), f, indent=1, sort_keys=True)
     syn = synthetic()
     with open(os.path.join(OUT, "synthetic.json"), "w") as f:
         json.dump(syn, f, indent=0, sort_keys=True)

@@ -112,3 +112,24 @@ def test_htree_inclusion_proof_pb(orc, wire):
             assert (m.leaf, m.width) == (i, w)
             assert orc.htree_verify_inclusion(i, w, list(m.terms), d[i].tobytes(), root)
         assert wire.htree_inclusion_proof_pb(lv, w, w)[0] == wire.MH_ERR_ILLEGAL_ARGUMENTS
+
+
+def test_wire_descriptor_matches_reference_generated_descriptor():
+    """oracle/wire.py's hand-declared messages == the reference's own compiled
+    descriptor (pkg/api/schema/schema.pb.go file_schema_proto_rawDesc, decoded
+    by tests/golden/make_golden.py into schema_fields.json): every field's
+    name, number, type, label and message type."""
+    import json
+    import os
+    import wire
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "schema_fields.json")))
+    assert ref["package"] == "immudb.schema" and ref["syntax"] == "proto3"
+    for name, fields in ref["messages"].items():
+        from google.protobuf import descriptor_pb2
+        d = wire.MSG[name].DESCRIPTOR
+        assert d.full_name == "immudb.schema." + name
+        dp = descriptor_pb2.DescriptorProto()
+        d.CopyToProto(dp)
+        got = [[f.name, f.number, f.type, f.label, f.type_name] for f in dp.field]
+        assert got == fields, name
+    assert set(ref["messages"]) == set(wire.MSG)
