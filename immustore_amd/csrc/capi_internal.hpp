@@ -172,6 +172,7 @@ struct mh_ctx {
     DevBuf s_sort;        // length-class sort of ragged messages (varlen_kernels.hip)
     DevBuf s_tx, s_tree;  // tx layer (capi_tx.hip)
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
+    DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
 };

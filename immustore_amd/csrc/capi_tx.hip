@@ -554,8 +554,20 @@ struct HopRec {
     uint32_t nent, pad;
 };
 
+// A record whose metadata is valid but not in the canonical form Go hashes
+// (the reader re-serialises parsed metadata: KVMetadata.Bytes() in the entry
+// digest, TxMetadata.Bytes() in the inner hash): the canonical bytes the
+// device hashes instead.  kind 0: entry `entry` of the record, bytes = the
+// whole entry record with canonical KV metadata; kind 1: the tx metadata.
+struct HopPatch {
+    uint64_t rec;  // index into HopOut::R
+    uint32_t kind, entry;
+    std::vector<uint8_t> bytes;
+};
+
 struct HopOut {
     std::vector<HopRec> R;
+    std::vector<HopPatch> P;
     std::vector<mh_tx_header> H;  // want_headers only
     bool want_headers = false;
     uint64_t start = 0, end = 0;  // first record parsed / where parsing stopped
@@ -569,10 +581,89 @@ struct HopLimits {
 
 inline uint64_t be16p(const uint8_t *q) { return (uint64_t)((uint32_t)q[0] << 8 | q[1]); }
 
+// KVMetadata.unsafeReadFrom + Bytes() (kv_metadata.go:207-256): deleted(0),
+// expiresAt(1, 8 bytes), nonIndexable(2); unknown codes and a short expiresAt
+// are ErrCorruptedData; a repeated attribute replaces the earlier one; Bytes()
+// writes the attributes in code order.
+int kv_md_canonical(const uint8_t *md, uint64_t ml, uint8_t out[MH_MAX_KV_METADATA_LEN],
+                    uint64_t *ol) {
+    if (ml > MH_MAX_KV_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+    bool has[3] = {false, false, false};
+    const uint8_t *exp = nullptr;
+    for (uint64_t i = 0; i < ml;) {
+        const uint8_t code = md[i++];
+        if (code == 1) {
+            if (ml - i < 8) return MH_ERR_CORRUPTED_DATA;
+            exp = md + i;
+            i += 8;
+        } else if (code > 2) {
+            return MH_ERR_CORRUPTED_DATA;
+        }
+        has[code] = true;
+    }
+    uint64_t o = 0;
+    if (has[0]) out[o++] = 0;
+    if (has[1]) {
+        out[o++] = 1;
+        memcpy(out + o, exp, 8);
+        o += 8;
+    }
+    if (has[2]) out[o++] = 2;
+    *ol = o;
+    return MH_OK;
+}
+
+// TxMetadata.ReadFrom + Bytes() (tx_metadata.go:145-193): truncatedUptoTx(0,
+// 8 bytes), extra(1, BE16 length + up to 256 bytes).  An extra running past
+// the metadata (Go indexes past the slice) or longer than 256 bytes (Bytes()
+// slices past its array) panics in Go: corrupted data here.
+int tx_md_canonical(const uint8_t *md, uint64_t ml, uint8_t out[MH_MAX_TX_METADATA_LEN],
+                    uint64_t *ol) {
+    if (ml > MH_MAX_TX_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+    const uint8_t *trunc = nullptr, *extra = nullptr;
+    uint64_t el = 0;
+    for (uint64_t i = 0; i < ml;) {
+        const uint8_t code = md[i++];
+        if (code == 0) {
+            if (ml - i < 8) return MH_ERR_CORRUPTED_DATA;
+            trunc = md + i;
+            i += 8;
+        } else if (code == 1) {
+            if (ml - i < 2) return MH_ERR_CORRUPTED_DATA;
+            el = be16p(md + i);
+            i += 2;
+            if (ml - i < el || el > 256) return MH_ERR_CORRUPTED_DATA;
+            extra = md + i;
+            i += el;
+        } else {
+            return MH_ERR_CORRUPTED_DATA;
+        }
+    }
+    uint64_t o = 0;
+    if (trunc) {
+        out[o++] = 0;
+        memcpy(out + o, trunc, 8);
+        o += 8;
+    }
+    if (extra) {
+        out[o++] = 1;
+        out[o++] = (uint8_t)(el >> 8);
+        out[o++] = (uint8_t)el;
+        memcpy(out + o, extra, el);
+        o += el;
+    }
+    *ol = o;
+    return MH_OK;
+}
+
 // Parse the record at p.  Returns MH_OK and fills h / first / alh, or
 // the structural error; *eof for an id-0 tail or a buffer too short for an id.
+// Checks follow the reader's order (tx.go:419-588): lengths are read before
+// the metadata they announce is parsed.  patches (may be null): where to note
+// non-canonical metadata of this record (index rec).
 int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &lim,
-               mh_tx_header &h, uint64_t &first, uint64_t &alh, bool &eof) {
+               mh_tx_header &h, uint64_t &first, uint64_t &alh, bool &eof,
+               std::vector<HopPatch> *patches = nullptr, uint64_t rec = 0) {
     eof = false;
     if (p + 8 > len) { eof = true; return MH_OK; }
     memset(&h, 0, sizeof h);
@@ -585,6 +676,7 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
     memcpy(h.prev_alh, buf + p + 56, 32);
     h.version = (uint32_t)be16p(buf + p + 88);
     uint64_t q = p + 90;
+    uint8_t canon[MH_MAX_TX_METADATA_LEN];
     if (h.version == 0) {
         if (q + 2 > len) return MH_ERR_TRUNCATED;
         h.nentries = (uint32_t)be16p(buf + q);
@@ -594,6 +686,11 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
         h.md_len = (uint32_t)be16p(buf + q);
         q += 2;
         if (h.md_len > MH_MAX_TX_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+        if (q + h.md_len > len) return MH_ERR_TRUNCATED;
+        uint64_t cl = 0;
+        if (tx_md_canonical(buf + q, h.md_len, canon, &cl)) return MH_ERR_CORRUPTED_DATA;
+        if (patches && (cl != h.md_len || memcmp(canon, buf + q, cl)))
+            patches->push_back(HopPatch{rec, 1, 0, std::vector<uint8_t>(canon, canon + cl)});
         if (q + h.md_len + 4 > len) return MH_ERR_TRUNCATED;
         if (q > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
         h.md_off = (uint32_t)q;
@@ -608,7 +705,9 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
     for (uint32_t e = 0; e < h.nentries; e++) {
         if (q + 2 > len) return MH_ERR_TRUNCATED;
         const uint64_t ml = be16p(buf + q);
-        if (ml > MH_MAX_KV_METADATA_LEN) return MH_ERR_CORRUPTED_DATA;
+        if (q + 2 + ml > len) return MH_ERR_TRUNCATED;
+        uint64_t cml = 0;
+        if (ml && kv_md_canonical(buf + q + 2, ml, canon, &cml)) return MH_ERR_CORRUPTED_DATA;
         if (q + 2 + ml + 2 > len) return MH_ERR_TRUNCATED;
         const uint64_t kl = be16p(buf + q + 2 + ml);
         if (kl > lim.max_key_len) return MH_ERR_CORRUPTED_MAX_KEYLEN;
@@ -616,6 +715,15 @@ int hop_record(const uint8_t *buf, uint64_t len, uint64_t p, const HopLimits &li
         // a v0 header cannot carry KV metadata: TxEntryDigest_v1_1 fails the
         // read with ErrMetadataUnsupported (tx.go:690-693, via readEntry)
         if (h.version == 0 && ml > 0) return MH_ERR_METADATA_UNSUPPORTED;
+        if (patches && ml && (cml != ml || memcmp(canon, buf + q + 2, cml))) {
+            // the entry record re-serialised with canonical metadata
+            std::vector<uint8_t> r(4 + cml + kl + 12 + 32);
+            r[0] = (uint8_t)(cml >> 8);
+            r[1] = (uint8_t)cml;
+            memcpy(r.data() + 2, canon, cml);
+            memcpy(r.data() + 2 + cml, buf + q + 2 + ml, 2 + kl + 12 + 32);
+            patches->push_back(HopPatch{rec, 0, e, std::move(r)});
+        }
         q += 4 + ml + kl + 12 + 32;
     }
     if (q + 32 > len) return MH_ERR_TRUNCATED;
@@ -631,8 +739,10 @@ void hop_range(const uint8_t *buf, uint64_t len, uint64_t p, uint64_t stop, uint
         mh_tx_header h;
         uint64_t first = 0, alh = 0;
         bool eof = false;
-        const int rc = hop_record(buf, len, p, lim, h, first, alh, eof);
+        const size_t np = o.P.size();
+        const int rc = hop_record(buf, len, p, lim, h, first, alh, eof, &o.P, o.R.size());
         if (rc != MH_OK || eof) {
+            o.P.resize(np);  // patches of a record that did not parse
             o.rc = rc;
             o.stopped = true;
             break;
@@ -740,6 +850,11 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
         }
         const uint64_t room = max_txs - out.R.size();
         const uint64_t take = std::min<uint64_t>(room, o->R.size());
+        for (HopPatch &pt : o->P)
+            if (pt.rec < take) {
+                pt.rec += out.R.size();
+                out.P.push_back(std::move(pt));
+            }
         out.R.insert(out.R.end(), o->R.begin(), o->R.begin() + take);
         if (want_headers) out.H.insert(out.H.end(), o->H.begin(), o->H.begin() + take);
         if (take < o->R.size()) {         // max_txs reached inside this chunk
@@ -841,6 +956,49 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             E += r.nent;
             wmax = std::max<uint64_t>(wmax, r.nent);
         }
+        // ---- metadata that parses but is not in canonical form (a log not
+        // written by immudb): Go hashes KVMetadata.Bytes() / TxMetadata.Bytes(),
+        // so the canonical entry records / tx metadata go after the log bytes
+        // on the device and the entry index / headers point at them.
+        std::vector<uint64_t> patch;  // [ne idx][ne off][nh idx][nh off | len << 32]
+        uint64_t npe = 0, nph = 0;
+        if (!hop.P.empty()) {
+            std::vector<uint64_t> first_leaf(ntx);
+            for (uint64_t k = 0, acc = 0; k < ntx; k++) {
+                first_leaf[k] = acc;
+                acc += hop.R[k].nent;
+            }
+            uint64_t side = 0;
+            for (const HopPatch &pt : hop.P) {
+                side += pt.bytes.size();
+                (pt.kind == 0 ? npe : nph)++;
+            }
+            if (len + side > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
+            std::vector<uint8_t> sbuf;
+            sbuf.reserve(side);
+            patch.resize(2 * (npe + nph));
+            uint64_t ie = 0, ih = 0;
+            for (const HopPatch &pt : hop.P) {
+                const uint64_t off = len + sbuf.size();
+                if (pt.kind == 0) {
+                    patch[ie] = first_leaf[pt.rec] + pt.entry;
+                    patch[npe + ie++] = off;
+                } else {
+                    patch[2 * npe + ih] = pt.rec;
+                    patch[2 * npe + nph + ih++] = off | ((uint64_t)pt.bytes.size() << 32);
+                }
+                sbuf.insert(sbuf.end(), pt.bytes.begin(), pt.bytes.end());
+            }
+            MH_HIP(c->s_txpatch.ensure(len + side + patch.size() * 8));
+            uint8_t *nb = c->s_txpatch.as<uint8_t>();
+            MH_HIP(hipMemcpyAsync(nb, dbuf, len, hipMemcpyDeviceToDevice, st));
+            MH_HIP(hipMemcpyAsync(nb + len, sbuf.data(), side, hipMemcpyHostToDevice, st));
+            MH_HIP(hipMemcpyAsync(nb + ((len + side + 7) & ~7ull), patch.data(), patch.size() * 8,
+                                  hipMemcpyHostToDevice, st));
+            MH_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
+            dbuf = nb;
+            patch.assign(1, (len + side + 7) & ~7ull);  // device offset of the patch lists
+        }
         // ---- device: headers, entry index, digests, trees, Alh
         // small trees (every tx here: a handful of entries) get their roots one
         // lane per tree; a batch with a wide tx goes through the host tree plan
@@ -890,6 +1048,11 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
                                 (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
                                 (uint64_t *)(base + b_rec), base + b_ver));
+        if (npe + nph) {
+            const uint64_t *pl = reinterpret_cast<const uint64_t *>(dbuf + patch[0]);
+            MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
+                                      pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
+        }
         MH_HIP(launch_txe_leaf(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec), base + b_ver,
                                small, base + b_lv));
         // one htree per tx (tx.go:617-621)

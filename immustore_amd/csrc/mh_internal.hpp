@@ -187,6 +187,11 @@ hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const 
 // headers + first-entry offsets of tx records from the raw log (md_off relative to buf)
 hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                                   const uint64_t *rec_off, MhTxHeader *hdrs, uint64_t *ent_start);
+// non-canonical metadata of a tx log: rec_off[e_idx[k]] = e_off[k];
+// hdrs[h_idx[k]].md_off / md_len = low / high 32 bits of h_val[k]
+hipError_t launch_txlog_patch(hipStream_t st, uint64_t ne, const uint64_t *e_idx,
+                              const uint64_t *e_off, uint64_t *rec_off, uint64_t nh,
+                              const uint64_t *h_idx, const uint64_t *h_val, MhTxHeader *hdrs);
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
 hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                             const MhTxHeader *hdrs, const uint64_t *ent_start,

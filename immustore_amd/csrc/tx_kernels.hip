@@ -318,6 +318,28 @@ hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8
     return hipGetLastError();
 }
 
+__global__ void k_txlog_patch(uint64_t ne, const uint64_t *__restrict__ e_idx,
+                              const uint64_t *__restrict__ e_off, uint64_t *__restrict__ rec_off,
+                              uint64_t nh, const uint64_t *__restrict__ h_idx,
+                              const uint64_t *__restrict__ h_val, MhTxHeader *__restrict__ hdrs) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ne) rec_off[e_idx[t]] = e_off[t];
+    if (t < nh) {
+        hdrs[h_idx[t]].md_off = (uint32_t)h_val[t];
+        hdrs[h_idx[t]].md_len = (uint32_t)(h_val[t] >> 32);
+    }
+}
+
+hipError_t launch_txlog_patch(hipStream_t st, uint64_t ne, const uint64_t *e_idx,
+                              const uint64_t *e_off, uint64_t *rec_off, uint64_t nh,
+                              const uint64_t *h_idx, const uint64_t *h_val, MhTxHeader *hdrs) {
+    const uint64_t n = std::max(ne, nh);
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_txlog_patch, dim3(grid_for(n, 256)), dim3(256), 0, st, ne, e_idx, e_off,
+                       rec_off, nh, h_idx, h_val, hdrs);
+    return hipGetLastError();
+}
+
 __device__ __constant__ static const uint8_t kEmptyRootDev[32] = {
     0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
     0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};

@@ -462,9 +462,14 @@ int mh_verify_dual_proof_batch(mh_ctx *ctx, const mh_dual_proof_batch *b, uint8_
  * (Eh) and Alh and compares it with the stored one: status[k] = MH_OK or
  * MH_ERR_CORRUPTED_DATA ("ALH mismatch", tx.go:625).  Optional outputs
  * (capacity max_txs): hdrs (md_off relative to buf, eh = rebuilt Eh) and
- * alh (recomputed).  KV / tx metadata are hashed as stored; the reference
- * re-serializes its parsed attributes, which gives the same bytes for every
- * record it writes. */
+ * alh (recomputed).  KV / tx metadata are parsed as the reader parses them
+ * (KVMetadata.unsafeReadFrom kv_metadata.go:221-256, TxMetadata.ReadFrom
+ * tx_metadata.go:159-193): unknown attribute codes, short payloads and an
+ * extra running past the metadata stop the parse with MH_ERR_CORRUPTED_DATA;
+ * valid metadata is hashed in its re-serialized form (Bytes(), attributes in
+ * code order, a repeated attribute's last value), as Go hashes it -- records
+ * whose stored metadata is not already in that form (never written by immudb)
+ * are hashed from canonical copies placed after the log on the device. */
 /* The record structure alone (host only, no hashing, no device): the same
  * parse as mh_txlog_validate (readHeader / readEntry limits and errors,
  * tx.go:419-603) returning the headers (eh zero) and the offset of each

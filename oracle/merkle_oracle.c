@@ -990,6 +990,91 @@ static uint64_t be(const uint8_t *b, int n) {
     return v;
 }
 
+/* KVMetadata.unsafeReadFrom (kv_metadata.go:221-256) then Bytes()
+ * (kv_metadata.go:207-219): attributes deleted(0, no payload),
+ * expiresAt(1, BE64), nonIndexable(2, no payload); an unknown code or a short
+ * expiresAt is ErrCorruptedData; a repeated attribute overwrites the earlier one
+ * (map), and the digest is taken over the re-serialised bytes in code order. */
+static int kvmd_canonical(const uint8_t *md, uint64_t ml, uint8_t out[11], uint64_t *outl) {
+    int have[3] = {0, 0, 0};
+    uint8_t exp[8];
+    if (ml > 11) return ERR_CORRUPTED_DATA;
+    uint64_t i = 0;
+    while (i < ml) {
+        const uint8_t code = md[i++];
+        if (code == 0) {
+            have[0] = 1;
+        } else if (code == 1) {
+            if (ml - i < 8) return ERR_CORRUPTED_DATA;
+            memcpy(exp, md + i, 8);
+            i += 8;
+            have[1] = 1;
+        } else if (code == 2) {
+            have[2] = 1;
+        } else {
+            return ERR_CORRUPTED_DATA;
+        }
+    }
+    uint64_t o = 0;
+    if (have[0]) out[o++] = 0;
+    if (have[1]) {
+        out[o++] = 1;
+        memcpy(out + o, exp, 8);
+        o += 8;
+    }
+    if (have[2]) out[o++] = 2;
+    *outl = o;
+    return OK;
+}
+
+/* TxMetadata.ReadFrom (tx_metadata.go:159-193) then Bytes() (:145-157):
+ * truncatedUptoTx(0, BE64), extra(1, BE16 length + bytes, <= 256 bytes).  An
+ * extra whose length runs past the metadata makes Go's parse index past the
+ * slice (a panic), and one longer than 256 bytes panics in Bytes(): both are
+ * corrupted data here. */
+static int txmd_canonical(const uint8_t *md, uint64_t ml, uint8_t out[268], uint64_t *outl) {
+    int have0 = 0, have1 = 0;
+    uint8_t trunc[8];
+    const uint8_t *extra = NULL;
+    uint64_t el = 0;
+    if (ml > 268) return ERR_CORRUPTED_DATA;
+    uint64_t i = 0;
+    while (i < ml) {
+        const uint8_t code = md[i++];
+        if (code == 0) {
+            if (ml - i < 8) return ERR_CORRUPTED_DATA;
+            memcpy(trunc, md + i, 8);
+            i += 8;
+            have0 = 1;
+        } else if (code == 1) {
+            if (ml - i < 2) return ERR_CORRUPTED_DATA;
+            el = be(md + i, 2);
+            i += 2;
+            if (ml - i < el || el > 256) return ERR_CORRUPTED_DATA;
+            extra = md + i;
+            i += el;
+            have1 = 1;
+        } else {
+            return ERR_CORRUPTED_DATA;
+        }
+    }
+    uint64_t o = 0;
+    if (have0) {
+        out[o++] = 0;
+        memcpy(out + o, trunc, 8);
+        o += 8;
+    }
+    if (have1) {
+        out[o++] = 1;
+        out[o++] = (uint8_t)(el >> 8);
+        out[o++] = (uint8_t)el;
+        memcpy(out + o, extra, el);
+        o += el;
+    }
+    *outl = o;
+    return OK;
+}
+
 int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries,
                        uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                        uint64_t *consumed_out, uint8_t *alh_out, int32_t *status_out) {
@@ -1021,7 +1106,14 @@ int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries,
             h.md_len = (uint32_t)be(buf + p - 2, 2);
             if (h.md_len > 268) { rc = ERR_CORRUPTED_DATA; p = p0; break; }
             if (!rd(len, &p, h.md_len)) { rc = ERR_TRUNCATED; p = p0; break; }
-            memcpy(txmd, buf + p - h.md_len, h.md_len);
+            /* TxMetadata.ReadFrom, then Alh over Bytes() (tx.go:483-501, 300-319) */
+            uint64_t cl = 0;
+            if (txmd_canonical(buf + p - h.md_len, h.md_len, txmd, &cl)) {
+                rc = ERR_CORRUPTED_DATA;
+                p = p0;
+                break;
+            }
+            h.md_len = (uint32_t)cl;
             if (!rd(len, &p, 4)) { rc = ERR_TRUNCATED; p = p0; break; }
             h.nentries = (uint32_t)be(buf + p - 4, 4);
         } else {
@@ -1036,13 +1128,18 @@ int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries,
             uint64_t q = p;
             if (!rd(len, &p, 2)) { bad = ERR_TRUNCATED; break; }
             const uint64_t ml = be(buf + q, 2);
-            if (ml > 11) { bad = ERR_CORRUPTED_DATA; break; } /* maxKVMetadataLen */
-            if (!rd(len, &p, ml + 2)) { bad = ERR_TRUNCATED; break; }
+            if (!rd(len, &p, ml)) { bad = ERR_TRUNCATED; break; }
+            /* KVMetadata.unsafeReadFrom (maxKVMetadataLen 11), digest over Bytes() */
+            uint8_t cmd[11];
+            uint64_t cml = 0;
+            if (ml && kvmd_canonical(buf + q + 2, ml, cmd, &cml)) { bad = ERR_CORRUPTED_DATA; break; }
+            if (!rd(len, &p, 2)) { bad = ERR_TRUNCATED; break; }
             const uint64_t kl = be(buf + p - 2, 2);
             if (kl > max_key_len) { bad = ERR_CORRUPTED_MAX_KEYLEN; break; }
             if (!rd(len, &p, kl + 4 + 8 + 32)) { bad = ERR_TRUNCATED; break; }
-            const uint8_t *md = buf + q + 2, *key = buf + q + 4 + ml, *hv = buf + p - 32;
-            int st = orc_entry_digest((int)h.version, key, kl, md, ml, hv, digs + 32 * (size_t)e);
+            const uint8_t *key = buf + q + 4 + ml, *hv = buf + p - 32;
+            int st = orc_entry_digest((int)h.version, key, kl, cml ? cmd : NULL, cml, hv,
+                                      digs + 32 * (size_t)e);
             if (st) { bad = st; break; }
         }
         if (bad) { rc = bad; p = p0; break; }

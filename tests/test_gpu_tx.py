@@ -354,3 +354,22 @@ def test_verify_document_batch_wide_txs(m, ctx, orc):
             assert ost in (orc.ERR_INVALID_PROOF, orc.ERR_INVALID_PROOF_ENTRY)
         elif k % 3 != 2:
             assert ost == 0
+
+
+def test_txlog_validate_metadata_parse_vs_oracle(m, ctx, orc):
+    """Metadata as the reader parses it: valid non-canonical
+    KV / tx metadata is hashed in its re-serialised form (Go hashes Bytes()):
+    the device hashes canonical entry records / tx metadata placed after the
+    log; invalid metadata stops the read with ErrCorruptedData.  Also a
+    > 8 MiB log of such records (the multi-threaded hop merges the patches)."""
+    from tx_util import metadata_logs
+    logs = metadata_logs(orc)
+    big = b"".join(raw for name, raw in logs if name == "noncanonical_sealed_canonical") * 4200
+    assert len(big) > (8 << 20)
+    for name, raw in logs + [("big", big)]:
+        rc, n, used, hdrs, alh, sts = m.txlog_validate(raw, ctx=ctx)
+        o = orc.txlog_validate(raw)
+        assert (rc, n, used) == (o[0], o[1], o[2]), name
+        assert np.array_equal(alh, o[3][:n]) and np.array_equal(sts, o[4][:n]), name
+    rc, n, _, _, _, sts = m.txlog_validate(big, ctx=ctx)
+    assert rc == 0 and n == 42000 and not sts.any()

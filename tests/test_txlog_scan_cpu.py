@@ -98,3 +98,30 @@ def test_scan_v0_entry_with_kv_metadata(txl, orc):
             a = same(txl, orc, buf)
             assert a[0] == 6  # MH_ERR_METADATA_UNSUPPORTED
             assert a[1] == (0 if buf is rec else 6)
+
+
+def test_scan_metadata_parse(txl, orc):
+    """KV / tx metadata parsed as the reader does (kv_metadata.go:221-256,
+    tx_metadata.go:159-193): unknown attribute codes, short payloads and an
+    extra running past the metadata stop the read with ErrCorruptedData;
+    valid non-canonical metadata parses."""
+    from tx_util import metadata_logs
+    for name, raw in metadata_logs(orc):
+        a = same(txl, orc, raw)
+        if name.startswith("bad"):
+            assert (a[0], a[1]) == (14, 1), name
+        else:
+            assert (a[0], a[1]) == (0, 10), name
+
+
+def test_oracle_metadata_canonical_hashing(orc):
+    """Go hashes the re-serialised metadata: a log sealed over the canonical
+    bytes validates, the same log sealed over the raw non-canonical bytes gives
+    an ALH mismatch on exactly the non-canonical records."""
+    from tx_util import metadata_logs
+    logs = dict(metadata_logs(orc))
+    rc, n, _, _, sts = orc.txlog_validate(logs["noncanonical_sealed_canonical"])
+    assert rc == 0 and n == 10 and not np.any(sts)
+    rc, n, _, _, sts = orc.txlog_validate(logs["noncanonical_sealed_raw"])
+    assert rc == 0 and n == 10
+    assert list(sts) == [0] + [14] * 8 + [0]

@@ -32,6 +32,20 @@ def inner_hashes(orc, recs, blob):
     return [orc.tx_header_alh(recs[k], blob)[1] for k in range(len(recs))]
 
 
+def _txmd(rng, kind):
+    """TxMetadata.Bytes() (tx_metadata.go:145-157): none, truncatedUptoTx,
+    extra (short), or both attributes at the 268-byte maximum."""
+    rb = lambda n: bytes(rng.integers(0, 256, n, dtype=np.uint8))  # noqa: E731
+    trunc = b"\x00" + rb(8)
+    if kind == 2:
+        return trunc
+    if kind == 3:
+        return b"\x01" + struct.pack(">H", 5) + rb(5)
+    if kind == 4:
+        return trunc + b"\x01" + struct.pack(">H", 256) + rb(256)
+    return b""
+
+
 def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True, key_len=None):
     """Tx records in the immustore.go:1812-1924 layout with a valid Alh chain
     (the stored alh of each record is the oracle's Alh over its own fields)."""
@@ -40,7 +54,7 @@ def _synthetic_txlog(rng, ntx, orc, max_entries=40, version_mix=True, key_len=No
     for k in range(ntx):
         ver = int(rng.integers(0, 2)) if version_mix else 1
         ne = int(rng.integers(0, max_entries + 1)) if k % 5 else int(rng.integers(1, 3))
-        txmd = b"" if ver == 0 else bytes(rng.integers(0, 256, [0, 0, 3, 268][k % 4], dtype=np.uint8))
+        txmd = b"" if ver == 0 else _txmd(rng, k % 5)
         ents, digs = bytearray(), []
         for e in range(ne):
             md = b"" if ver == 0 else [b"", b"\x00", b"\x01" + struct.pack(">Q", e), b"\x02",
@@ -167,3 +181,71 @@ def document_cases(fixtures, orc, per_store=60, seed=7):
                     d["src_hdr"], d["tgt_hdr"] = base["tgt_hdr"].copy(), base["src_hdr"].copy()
                 docs.append(d)
     return docs, bytes(blob_all)
+
+
+def md_record(orc, txid, prev, ver, txmd_raw, txmd_hash, entries, seal_raw=False):
+    """One tx record whose metadata is stored as given (txmd_raw, and per
+    entry md_raw) while the Alh is sealed over txmd_hash / md_hash (what Go
+    hashes: the re-serialised Bytes(), tx.go:300-319, 703-731), or over the raw
+    bytes when seal_raw.  entries: [(md_raw, md_hash, key, hval)].
+    -> (record bytes, alh)"""
+    digs = []
+    ents = bytearray()
+    for md_raw, md_hash, key, hv in entries:
+        digs.append(orc.entry_digest(ver, key, md_raw if seal_raw else md_hash, hv)[1])
+        ents += struct.pack(">H", len(md_raw)) + md_raw + struct.pack(">H", len(key)) + key
+        ents += struct.pack(">IQ", 3, 77) + hv
+    ne = len(entries)
+    eh = orc.htree_build(np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))[1] if ne \
+        else orc.sha256(b"")
+    st, inner = orc.tx_inner_hash(1000 + txid, ver, txmd_raw if seal_raw else txmd_hash, ne, eh,
+                                  0, bytes(32))
+    assert st == 0
+    alh = orc.tx_alh(txid, prev, inner)
+    hdr = struct.pack(">QQQ", txid, 1000 + txid, 0) + bytes(32) + prev + struct.pack(">H", ver)
+    hdr += struct.pack(">H", ne) if ver == 0 else struct.pack(">H", len(txmd_raw)) + txmd_raw + \
+        struct.pack(">I", ne)
+    return bytes(hdr + ents + alh), alh
+
+
+def metadata_logs(orc):
+    """Tx logs exercising the metadata parse of the reader: valid but
+    non-canonical KV / tx metadata (Go re-serialises it before hashing),
+    the same sealed over the raw bytes (an ALH mismatch in Go), and every
+    ErrCorruptedData case of KVMetadata.unsafeReadFrom / TxMetadata.ReadFrom.
+    -> list of (name, log bytes)"""
+    exp = lambda v: b"\x01" + struct.pack(">Q", v)  # noqa: E731
+    trunc = lambda v: b"\x00" + struct.pack(">Q", v)  # noqa: E731
+    extra = lambda b: b"\x01" + struct.pack(">H", len(b)) + b  # noqa: E731
+    key, hv = b"key-1", bytes(range(32))
+    noncanon_kv = [(b"\x02\x00", b"\x00\x02"), (b"\x00\x00", b"\x00"), (exp(9) + b"\x00", b"\x00" + exp(9)),
+                   (b"\x02" + exp(7) + b"\x00", b"\x00" + exp(7) + b"\x02"), (b"\x02\x02\x02", b"\x02")]
+    noncanon_tx = [(extra(b"xyz") + trunc(4), trunc(4) + extra(b"xyz")),
+                   (trunc(1) + trunc(2), trunc(2)), (extra(b"a") + extra(b"bc"), extra(b"bc"))]
+    bad_kv = [b"\x03", b"\x01" + bytes(4), b"\x00\x07", bytes([0x01]) + bytes(8) + b"\x09"]
+    bad_tx = [b"\x05", trunc(1)[:5], b"\x01\x00", extra(b"abc")[:4], b"\x01" + struct.pack(">H", 257)
+              + bytes(257)]
+    logs = []
+
+    def chain(recs):
+        out, prev = bytearray(), orc.sha256(b"")
+        for k, (txmd_raw, txmd_hash, ents, seal_raw) in enumerate(recs):
+            r, prev = md_record(orc, k + 1, prev, 1, txmd_raw, txmd_hash, ents, seal_raw)
+            out += r
+        return bytes(out)
+
+    good = (b"", b"", [(b"\x00", b"\x00", key, hv)], False)
+    for seal_raw in (False, True):
+        recs = [good]
+        for raw, canon in noncanon_kv:
+            recs.append((b"", b"", [(b"", b"", b"k0", hv), (raw, canon, key, hv)], seal_raw))
+        for raw, canon in noncanon_tx:
+            recs.append((raw, canon, [(b"\x02", b"\x02", key, hv)], seal_raw))
+        recs.append(good)
+        logs.append(("noncanonical_sealed_%s" % ("raw" if seal_raw else "canonical"), chain(recs)))
+    for k, md in enumerate(bad_kv):
+        logs.append(("bad_kv_%d" % k, chain([good, (b"", b"", [(b"", b"", b"a", hv), (md, md, key, hv)],
+                                                      True), good])))
+    for k, md in enumerate(bad_tx):
+        logs.append(("bad_tx_%d" % k, chain([good, (md, md, [], True), good])))
+    return logs
