@@ -390,12 +390,81 @@ __global__ __launch_bounds__(256) void k_small_roots(uint64_t ntrees,
     d[1] = src[1];
 }
 
+// The same roots with one WAVE per tree (width <= 64): lane k holds node k of
+// the current level in LDS, every level's nodes are hashed at once, so a tree
+// costs ceil(log2 w) node-hash latencies instead of w - 1 -- for the small
+// batches of a group commit, where the lane-per-tree kernel is one lone
+// wave walking each tree serially.
+__global__ __launch_bounds__(256) void k_small_roots_wave(uint64_t ntrees,
+                                                          const uint64_t *__restrict__ leaf_off,
+                                                          const uint8_t *__restrict__ nodes,
+                                                          uint8_t *__restrict__ roots) {
+    __shared__ uint32_t lvl[4][64][9];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + wv;
+    if (t >= ntrees) return;  // wave-uniform
+    const uint8_t *lv = nodes + (leaf_off[t] - leaf_off[0]) * 32;
+    uint64_t w = leaf_off[t + 1] - leaf_off[t];
+    if (w == 0) {
+        if (lane < 2)
+            reinterpret_cast<uint4 *>(roots + t * 32)[lane] =
+                reinterpret_cast<const uint4 *>(kEmptyRootDev)[lane];
+        return;
+    }
+    uint32_t(*L)[9] = lvl[wv];
+    if ((uint64_t)lane < w) {
+        uint32_t d[8];
+        load_digest(lv + 32 * lane, d);
+#pragma unroll
+        for (int j = 0; j < 8; j++) L[lane][j] = d[j];
+    }
+    while (w > 1) {  // htree.go:85-110, level by level
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t half = w / 2;
+        uint32_t a[8], b[8], h[8];
+        const bool hash = (uint64_t)lane < half, promote = (w & 1) && (uint64_t)lane == half;
+        if (hash || promote) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = L[promote ? w - 1 : 2 * lane][j];
+        }
+        if (hash) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) b[j] = L[2 * lane + 1][j];
+            node_hash_g(a, b, h);
+        } else {
+            copy8(h, a);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (hash || promote) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) L[lane][j] = h[j];
+        }
+        w = (w + 1) / 2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        uint32_t r[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) r[j] = L[0][j];
+        store_digest(roots + t * 32, r);
+    }
+}
+
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
                               uint8_t *nodes, uint8_t *roots) {
     if (!ntrees) return hipSuccess;
     TimerScope ts(tm, "small_roots", st);
-    hipLaunchKernelGGL(k_small_roots, dim3(grid_for(ntrees, 256)), dim3(256), kNodeTabBytes, st,
-                       ntrees, leaf_off, nodes, roots);
+    if (ntrees <= 2048) {
+        // few trees: latency-bound, a wave per tree
+        hipLaunchKernelGGL(k_small_roots_wave, dim3(grid_for(ntrees, 4)), dim3(256), 0, st, ntrees,
+                           leaf_off, nodes, roots);
+    } else {
+        hipLaunchKernelGGL(k_small_roots, dim3(grid_for(ntrees, 256)), dim3(256), kNodeTabBytes, st,
+                           ntrees, leaf_off, nodes, roots);
+    }
     return hipGetLastError();
 }
 

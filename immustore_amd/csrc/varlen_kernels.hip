@@ -450,7 +450,8 @@ static const uint32_t *nb_sort(hipStream_t st, Timer *tm, const uint64_t *off, c
                                uint64_t n, uint8_t *scratch, hipError_t *err) {
     static const bool nosort = getenv("MH_VARLEN_NOSORT") != nullptr;
     *err = hipSuccess;
-    if (!scratch || nosort || n <= 256 || n >= 0xffffffffull) return nullptr;
+    // below ~16K messages the four sort launches cost more than the divergence
+    if (!scratch || nosort || n < 16384 || n >= 0xffffffffull) return nullptr;
     TimerScope ts(tm, "varlen_sort", st);
     uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *cursor = hist + kNbBuckets;
