@@ -55,7 +55,7 @@ SHA_PEAK_GCOMPS = 30.9
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", choices=["c2", "c4", "c3", "c5"], default="c2",
                    help="c2: BASELINE configs[1], 2^20 x 1 KiB per GPU (headline); c4: "

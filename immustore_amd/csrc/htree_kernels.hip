@@ -800,8 +800,11 @@ hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const Level
         if (left <= 10 && g.width[cur] <= 1024) {
             hipLaunchKernelGGL(k_reduce<512>, dim3(1), dim3(512), 0, st, levels, la, cur, left);
             cur += left;
-        } else if (left >= 3 && g.width[cur] >= 4 * 256) {
-            // two in-lane levels + up to 8 in LDS per launch
+        } else if (left >= 3 && g.width[cur] >= (uint64_t)4 * 256 * 256) {
+            // throughput regime (>= 256 workgroups): two in-lane levels + up
+            // to 8 in LDS per launch.  Narrower levels are latency-bound, where
+            // one node per lane (k_reduce) is one node-hash latency per level
+            // instead of three for the in-lane pair.
             const int steps = std::min(10, left);
             const unsigned grid = grid_for(g.width[cur + 2], 256);
             hipLaunchKernelGGL(k_reduce4<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);

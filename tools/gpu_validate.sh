@@ -25,6 +25,6 @@ cd /tmp && export TMPDIR=/tmp
 # the default bench command (same steps / warmup / builds in flight) under the profiler
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1; rc=$?
 grep '^{"metric"' "$GRAFT_REPO_ROOT/gpurun_out/prof.log" > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json"
-python3 "$GRAFT_REPO_ROOT/tools/prof_summary.py" "$GRAFT_REPO_ROOT/gpurun_out/prof/run_kernel_trace.csv" --steps 200 --warmup 3 | tee "$GRAFT_REPO_ROOT/gpurun_out/prof_summary.json"
+python3 "$GRAFT_REPO_ROOT/tools/prof_summary.py" "$GRAFT_REPO_ROOT/gpurun_out/prof/run_kernel_trace.csv" --steps 2000 --warmup 3 | tee "$GRAFT_REPO_ROOT/gpurun_out/prof_summary.json"
 find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*"
 exit $rc
