@@ -142,8 +142,8 @@ struct MsgWalk {
     const uint32_t *qlast;  // dword holding the last byte
     uint32_t sel;           // v_perm selector of p's alignment
     uint64_t L;
-    uint32_t dn[17];        // prefetched window of the next block
-    bool pre;
+    uint32_t d[17];         // window of the current block (loaded one block ahead)
+    bool pre;               // d already holds this block's window
 
     __device__ __forceinline__ void init(const uint8_t *p, uint64_t len) {
         const uint32_t al = (uint32_t)((uintptr_t)p & 3);
@@ -156,40 +156,37 @@ struct MsgWalk {
 
     // Message words of block b for the lanes with `on`.  fast (wave-uniform):
     // every active lane has >= 2 more blocks after b, so its 68-byte window
-    // and the next one lie inside the message; otherwise the general form
-    // (clamped loads, byte masks, 0x80, bit length in the last block nb-1).
+    // and the next one lie inside the message; the words are taken from d and
+    // the same registers then receive the next block's window, which lands
+    // under this block's compression.  Otherwise the general form (clamped
+    // loads, byte masks, 0x80, bit length in the last block nb-1).
     __device__ __forceinline__ void block(uint32_t b, uint32_t nb, bool on, bool fast,
                                           uint32_t w[16]) {
-        uint32_t d[17];
         if (fast) {
-            if (pre) {
-#pragma unroll
-                for (int j = 0; j < 17; j++) d[j] = dn[j];
-            } else if (on) {
-                load_window(q + 16 * (uint64_t)b, d);
-            }
-            pre = on && b + 3 < nb;
-            if (pre) load_window(q + 16 * (uint64_t)(b + 1), dn);
+            if (!pre && on) load_window(q + 16 * (uint64_t)b, d);
 #pragma unroll
             for (int j = 0; j < 16; j++) w[j] = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
+            pre = on && b + 3 < nb;
+            if (pre) load_window(q + 16 * (uint64_t)(b + 1), d);
             return;
         }
         pre = false;
+        uint32_t x[17];
 #pragma unroll
-        for (int j = 0; j < 17; j++) d[j] = 0;
+        for (int j = 0; j < 17; j++) x[j] = 0;
         if (on && L) {
             const uint32_t *qb = q + 16 * (uint64_t)b;
 #pragma unroll
-            for (int j = 0; j < 17; j++) d[j] = *(qb + j <= qlast ? qb + j : qlast);
+            for (int j = 0; j < 17; j++) x[j] = *(qb + j <= qlast ? qb + j : qlast);
         }
         const int r = clamp_rel((int64_t)L - 64 * (int64_t)b);  // data bytes left at block start
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            uint32_t x = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
+            uint32_t y = __builtin_amdgcn_perm(x[j + 1], x[j], sel);
             const int v = r - 4 * j;  // valid bytes in this word
-            x &= hi_mask(v);
-            if (v >= 0 && v < 4) x |= 0x80u << (24 - 8 * v);
-            w[j] = x;
+            y &= hi_mask(v);
+            if (v >= 0 && v < 4) y |= 0x80u << (24 - 8 * v);
+            w[j] = y;
         }
         if (b + 1 == nb) {
             const uint64_t bits = L * 8;
@@ -265,15 +262,16 @@ __device__ __forceinline__ uint32_t seg_word(const uint32_t d[17], int j, uint32
     return x & hi_mask(re - 4 * j) & ~hi_mask(rs - 4 * j);
 }
 
-// 17-dword window of a segment at byte address a (may start before / run past
+// ND-dword window of a segment at byte address a (may start before / run past
 // the segment: loads are clamped to [lo, hi], the bytes masked later)
+template <int ND = 17>
 __device__ __forceinline__ void seg_window(const uint8_t *a, const uint32_t *lo, const uint32_t *hi,
                                            uint32_t d[17], uint32_t *sel) {
     const uint32_t al = (uint32_t)((uintptr_t)a & 3);
     const uint32_t *q = reinterpret_cast<const uint32_t *>(a - al);
     *sel = 0x00010203u + al * 0x01010101u;
 #pragma unroll
-    for (int j = 0; j < 17; j++) {
+    for (int j = 0; j < ND; j++) {
         const uint32_t *x = q + j;
         d[j] = *(x < lo ? lo : (x > hi ? hi : x));
     }
@@ -284,6 +282,25 @@ __device__ __forceinline__ uint32_t be16_word(uint32_t x, int rel) {
     if (rel < -1 || rel > 3) return 0u;
     const uint64_t t = (uint64_t)((x & 0xffffu) << 16) << 8;
     return (uint32_t)(t >> (8 * rel + 8));
+}
+
+// OR the v1 digest-message prefix (BE16 ml | md | BE16 kl, message bytes
+// [0, 4 + ml)) into 4 words x[0..3] that start at message byte p0.
+__device__ __forceinline__ void prefix_words4(uint32_t x[4], const uint8_t *mp, uint64_t ml,
+                                              uint64_t kl, int64_t p0) {
+    const int r0 = clamp_rel(-p0), r_kl = clamp_rel(2 + (int64_t)ml - p0);
+    if (ml) {
+        const uint32_t *m_lo = reinterpret_cast<const uint32_t *>((uintptr_t)mp & ~(uintptr_t)3);
+        const uint32_t *m_hi =
+            reinterpret_cast<const uint32_t *>((uintptr_t)(mp + ml - 1) & ~(uintptr_t)3);
+        uint32_t d[17], sel;
+        seg_window<5>(mp + (p0 - 2), m_lo, m_hi, d, &sel);
+#pragma unroll
+        for (int j = 0; j < 4; j++) x[j] |= seg_word(d, j, sel, r0 + 2, r_kl);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        x[j] |= be16_word((uint32_t)ml, r0 - 4 * j) | be16_word((uint32_t)kl, r_kl - 4 * j);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_entries_varlen(
@@ -367,23 +384,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
                     for (int j = 0; j < 16; j++) x[j] |= seg_word(d, j, sel, r_key, r_hv);
                 }
-                // v1 prefix: BE16 ml | md | BE16 kl  at [0, s_key)
+                // v1 prefix: BE16 ml | md | BE16 kl  at [0, s_key): in block 0
+                // only, and within its first 4 words whenever every digest lane
+                // of the wave has s_key <= 16 (KV metadata <= 11 bytes, always
+                // for immudb's attributes)
                 if (version == 1 && p0 < s_key) {
-                    const int r0 = clamp_rel(-p0), r_kl = clamp_rel(2 + (int64_t)ml - p0);
-                    if (ml) {
-                        const uint32_t *m_lo =
-                            reinterpret_cast<const uint32_t *>((uintptr_t)mp & ~(uintptr_t)3);
-                        const uint32_t *m_hi = reinterpret_cast<const uint32_t *>(
-                            (uintptr_t)(mp + ml - 1) & ~(uintptr_t)3);
-                        uint32_t d[17], sel;
-                        seg_window(mp + (p0 - 2), m_lo, m_hi, d, &sel);
+                    prefix_words4(x, mp, ml, kl, p0);
+                    if (__ballot(s_key > p0 + 16)) {  // metadata longer than 12 bytes
 #pragma unroll
-                        for (int j = 0; j < 16; j++) x[j] |= seg_word(d, j, sel, r0 + 2, r_kl);
+                        for (int c = 1; c < 4; c++) prefix_words4(x + 4 * c, mp, ml, kl, p0 + 16 * c);
                     }
-#pragma unroll
-                    for (int j = 0; j < 16; j++)
-                        x[j] |= be16_word((uint32_t)ml, r0 - 4 * j) |
-                                be16_word((uint32_t)kl, r_kl - 4 * j);
                 }
                 // hVal bytes [s_hv, s_hv + 32): window over the zero-padded slot
                 {

@@ -271,6 +271,23 @@ def test_entries_csr_random_vs_oracle(m, ctx, orc):
         assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
 
 
+def test_entries_long_metadata_vs_oracle(m, ctx, orc):
+    """Metadata longer than immudb's attributes (> 12 bytes: the digest
+    prefix then spans more than the first 4 message words, and more than one
+    block for the longest) through the general path, next to short ones."""
+    rng = np.random.default_rng(21)
+    for n in (5, 300, 2000):
+        keys = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes()
+                for _ in range(n)]
+        mds = [rng.integers(0, 256, int(rng.choice([0, 3, 11, 13, 17, 40, 61, 62, 70, 130])),
+                            dtype=np.uint8).tobytes() for _ in range(n)]
+        vals = [rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+                for _ in range(n)]
+        eh, hv, lv = m.build_hash_tree(1, keys, vals, mds, ctx=ctx)
+        st, ohv, olv, oroot = orc.build_entries(1, keys, mds, vals)
+        assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
+
+
 def test_go_fixtures_alh_chain_on_gpu(m, ctx, orc, fixtures):
     """Eh computed on the GPU -> innerHash/Alh (oracle) == Alh stored by Go."""
     for name, fx in fixtures.items():
