@@ -71,7 +71,7 @@ def parse():
                    help="independent builds in flight on separate streams (1 = sequential)")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU work of the cpu_baseline sample")
-    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
+    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r02.json"),
                    help="PMC-derived HBM bytes per launch of the dominant kernel (or missing)")
     return p.parse_args()
 
