@@ -414,7 +414,7 @@ def main():
     lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
     # levels written by one launch of the dominant kernel: the lanes' groups
     # up to level log2(lpl), then each workgroup's subtree 8 levels higher
-    wgl = int(os.environ.get("MH_WG_LEVELS", "4"))  # default of launch_entries_fixed
+    wgl = int(os.environ.get("MH_WG_LEVELS", "2"))  # default of launch_entries_fixed
     top = min({1: 0, 2: 1, 4: 2}[lpl] + wgl, max(m.levels_len(n) and (n - 1).bit_length(), 0))
     widths = [-(-n // (1 << l)) for l in range(top + 1)]
     nodes_written = sum(widths)

@@ -15,6 +15,7 @@
 #include <dlfcn.h>
 
 #include <memory>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -172,6 +173,36 @@ extern "C" int mh_multi_synchronize(mh_multi *m) {
 
 namespace {
 
+// fn(d) for d in [0, n) on n threads (this one included): each device's host
+// copies go over its own PCIe link at once, and a pageable copy, which holds
+// the issuing thread until it is staged, never serialises the devices.
+// Returns the first non-zero status.
+template <class F>
+int per_device(int n, F &&fn) {
+    std::vector<int> st(n, MH_OK);
+    std::vector<std::thread> th;
+    auto run = [&](int d) {
+        try {
+            st[d] = fn(d);
+        } catch (const std::bad_alloc &) {
+            st[d] = MH_ERR_OUT_OF_MEMORY;
+        } catch (...) {
+            st[d] = MH_ERR_ILLEGAL_STATE;
+        }
+    };
+    int d = 1;
+    try {
+        for (; d < n; d++) th.emplace_back(run, d);
+    } catch (...) {  // no thread: the rest run here
+    }
+    run(0);
+    for (int k = d; k < n; k++) run(k);
+    for (auto &t : th) t.join();
+    for (int k = 0; k < n; k++)
+        if (st[k]) return st[k];
+    return MH_OK;
+}
+
 // All-gather of one 32-byte root per device (send[d] -> recv[d] = K x 32 B),
 // on each device's context stream.
 int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
@@ -264,30 +295,32 @@ extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint
         while ((1ull << kS) < S) kS++;
         LevelGeom gg;
         gg.init(n);
-        // 1. shards in, subtree per device (host copies on each device's stream)
-        for (uint64_t g = 0; g < G; g++) {
-            const int d = (int)g;
-            mh_multi::Dev &B = *m->buf[d];
-            const uint64_t lo = g * S, ng = std::min(S, n - lo);
-            MH_HIP(hipSetDevice(m->dev[d]));
-            MH_HIP(B.keys.ensure(ng * key_len + 16));
-            MH_HIP(B.vals.ensure(ng * val_len + 16));
-            MH_HIP(B.hv.ensure(ng * 32));
-            MH_HIP(B.levels.ensure(mh_htree_levels_len(ng) * 32));
-            MH_HIP(B.send.ensure(32));
-            hipStream_t st = m->ctx[d]->stream;
-            if (key_len)
-                MH_HIP(hipMemcpyAsync(B.keys.p, keys + lo * key_len, ng * key_len,
-                                      hipMemcpyHostToDevice, st));
-            if (val_len)
-                MH_HIP(hipMemcpyAsync(B.vals.p, vals + lo * val_len, ng * val_len,
-                                      hipMemcpyHostToDevice, st));
-            int e = mh_dev_htree_build_entries_fixed(m->ctx[d], version, ng, B.keys.as<uint8_t>(),
-                                                     key_len, B.vals.as<uint8_t>(), val_len,
-                                                     B.hv.as<uint8_t>(), B.levels.as<uint8_t>(),
-                                                     B.send.as<uint8_t>());
-            if (e) return e;
-        }
+        // 1. shards in, subtree per device (host copies on each device's stream,
+        //    every device from its own thread)
+        if (int e = per_device((int)G, [&](int d) -> int {
+                const uint64_t g = (uint64_t)d;
+                mh_multi::Dev &B = *m->buf[d];
+                const uint64_t lo = g * S, ng = std::min(S, n - lo);
+                MH_HIP(hipSetDevice(m->dev[d]));
+                MH_HIP(B.keys.ensure(ng * key_len + 16));
+                MH_HIP(B.vals.ensure(ng * val_len + 16));
+                MH_HIP(B.hv.ensure(ng * 32));
+                MH_HIP(B.levels.ensure(mh_htree_levels_len(ng) * 32));
+                MH_HIP(B.send.ensure(32));
+                hipStream_t st = m->ctx[d]->stream;
+                if (key_len)
+                    MH_HIP(hipMemcpyAsync(B.keys.p, keys + lo * key_len, ng * key_len,
+                                          hipMemcpyHostToDevice, st));
+                if (val_len)
+                    MH_HIP(hipMemcpyAsync(B.vals.p, vals + lo * val_len, ng * val_len,
+                                          hipMemcpyHostToDevice, st));
+                return mh_dev_htree_build_entries_fixed(m->ctx[d], version, ng,
+                                                        B.keys.as<uint8_t>(), key_len,
+                                                        B.vals.as<uint8_t>(), val_len,
+                                                        B.hv.as<uint8_t>(), B.levels.as<uint8_t>(),
+                                                        B.send.as<uint8_t>());
+            }))
+            return e;
         // 2. all-gather of the subtree roots (devices without a shard send zeros)
         std::vector<const uint8_t *> send(K);
         std::vector<uint8_t *> recv(K);
@@ -310,32 +343,34 @@ extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint
         uint8_t *d_root = B0.top.as<uint8_t>() + mh_htree_levels_len(G) * 32;
         if (int e = mh_dev_htree_reduce_nodes(m->ctx[0], recv[0], G, B0.top.as<uint8_t>(), d_root))
             return e;
-        // 4. results back: hVals and each shard's slice of every level <= kS,
-        //    then the top levels and the root
-        for (uint64_t g = 0; g < G; g++) {
-            const int d = (int)g;
-            mh_multi::Dev &B = *m->buf[d];
-            const uint64_t lo = g * S, ng = std::min(S, n - lo);
-            MH_HIP(hipSetDevice(m->dev[d]));
-            hipStream_t st = m->ctx[d]->stream;
-            if (hvals_out)
-                MH_HIP(hipMemcpyAsync(hvals_out + lo * 32, B.hv.p, ng * 32, hipMemcpyDeviceToHost,
-                                      st));
-            if (levels_out) {
-                // global level l <= kS restricted to this shard = the shard's
-                // level l; above the (short) last shard's own root, that root
-                // is promoted unchanged (htree.go:100-103)
-                LevelGeom lg;
-                lg.init(ng);
-                for (int l = 0; l <= kS && l < gg.nlevels; l++) {
-                    const int ll = std::min(l, lg.nlevels - 1);
-                    MH_HIP(hipMemcpyAsync(levels_out + (gg.off[l] + (lo >> l)) * 32,
-                                          B.levels.as<uint8_t>() + lg.off[ll] * 32,
-                                          (l < lg.nlevels ? lg.width[l] : 1) * 32,
+        // 4. results back: hVals and each shard's slice of every level <= kS
+        //    (every device from its own thread), then the top levels and the root
+        if (int e = per_device((int)G, [&](int d) -> int {
+                const uint64_t g = (uint64_t)d;
+                mh_multi::Dev &B = *m->buf[d];
+                const uint64_t lo = g * S, ng = std::min(S, n - lo);
+                MH_HIP(hipSetDevice(m->dev[d]));
+                hipStream_t st = m->ctx[d]->stream;
+                if (hvals_out)
+                    MH_HIP(hipMemcpyAsync(hvals_out + lo * 32, B.hv.p, ng * 32,
                                           hipMemcpyDeviceToHost, st));
+                if (levels_out) {
+                    // global level l <= kS restricted to this shard = the shard's
+                    // level l; above the (short) last shard's own root, that root
+                    // is promoted unchanged (htree.go:100-103)
+                    LevelGeom lg;
+                    lg.init(ng);
+                    for (int l = 0; l <= kS && l < gg.nlevels; l++) {
+                        const int ll = std::min(l, lg.nlevels - 1);
+                        MH_HIP(hipMemcpyAsync(levels_out + (gg.off[l] + (lo >> l)) * 32,
+                                              B.levels.as<uint8_t>() + lg.off[ll] * 32,
+                                              (l < lg.nlevels ? lg.width[l] : 1) * 32,
+                                              hipMemcpyDeviceToHost, st));
+                    }
                 }
-            }
-        }
+                return MH_OK;
+            }))
+            return e;
         hipStream_t st0 = m->ctx[0]->stream;
         if (levels_out && G > 1) {
             LevelGeom tg;

@@ -744,10 +744,11 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
     const size_t lds = (kFixedThreads / 64) * kWaveLds + 256;
     // levels each leaf workgroup reduces in LDS after its lanes (0..8); 0
     // leaves the whole upper tree to k_reduce, which a concurrent build on
-    // another stream can overlap (MH_WG_LEVELS overrides).  4 measured best
-    // with builds in flight (profiles/ab_inflight_wgl_r01.txt): deeper
+    // another stream can overlap (MH_WG_LEVELS overrides).  2 measured best
+    // with builds in flight at 1000-2000 steps (round-2 sweep in
+    // profiles/ab_wg_levels_r02.txt; 4 in round 1's 20-step A/B): deeper
     // in-kernel subtrees idle most lanes at the end of the leaf kernel.
-    int wgl = 4;
+    int wgl = 2;
     if (const char *e = getenv("MH_WG_LEVELS")) wgl = std::max(0, std::min(8, atoi(e)));
     {
         TimerScope ts(tm, "entries_fixed", st);
