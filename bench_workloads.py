@@ -28,6 +28,13 @@
                     value hashes + entry digests + leaves + all levels; SHA
                     ceiling fraction of the ragged-message kernel; root and
                     hVals checked against the oracle.
+  --workload document  pkg/verification.VerifyDocument (verification.go:37-196, the
+                    package configs[4] names) over a batch: 8192 documents, each in its
+                    own v1 transaction of 64 entries (KV metadata on some), a trivial
+                    DualProofV2 (source = target = the tx) and the tx as known state,
+                    inputs in pinned host memory as a cgo caller hands them over;
+                    mh_verify_document_batch end to end; every status / Alh checked
+                    against the oracle on a sample.
   --workload commit SURVEY.md 8(f) row 1: ImmuStore.precommit hashing over a
                     batch of 2^16 txs x 16 entries x 1 KiB values (8 B keys,
                     v1) in pinned host memory through mh_precommit_batch: value
@@ -186,7 +193,7 @@ def distributed_main(a):
 
 def make_parser():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged"],
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged", "document"],
                    required=True)
     p.add_argument("--logs", action="store_true",
                    help="c3: also write the pLog / cLog appendable records (8(f) row 4)")
@@ -203,6 +210,8 @@ def make_parser():
     p.add_argument("--entries", type=int, default=1 << 20, help="ragged entries")
     p.add_argument("--max-vlen", type=int, default=4096, help="ragged: max value length")
     p.add_argument("--no-check", action="store_true", help="ragged: skip the oracle check")
+    p.add_argument("--docs", type=int, default=8192, help="document: documents")
+    p.add_argument("--doc-entries", type=int, default=64, help="document: entries per tx")
     return p
 
 
@@ -357,6 +366,108 @@ def ragged(a, m, N, L, ctx, dev, sync):
         res["oracle_match"] = bool(st == 0 and root.cpu().numpy().tobytes() == oroot and
                                    np.array_equal(hv.cpu().numpy().reshape(-1, 32), ohv))
     return res
+
+
+def document_batch(ndocs, width, seed=31):
+    """Synthetic VerifyDocument inputs: document k is the value of entry 0 of
+    its own v1 tx of `width` entries (keys doc/<k>/<e>, KV metadata on three
+    entries of four), the tx's Eh / Alh sealed by the oracle (EntrySpec
+    digests with the stored HValues, htree, innerHash, Alh), a trivial
+    DualProofV2 (source = target = the tx) and the tx as known state."""
+    import hashlib
+    import struct
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(seed)
+    mds = [b"", b"\x00", b"\x02", b"\x01" + struct.pack(">Q", 1_800_000_000)]
+    ml = np.array([len(mds[e % 4]) for e in range(width)], np.uint64)
+    mo = np.zeros(width + 1, np.uint64)
+    np.cumsum(ml, out=mo[1:])
+    mb = np.frombuffer(b"".join(mds[e % 4] for e in range(width)) + bytes(8), np.uint8)
+    docs = []
+    for k in range(ndocs):
+        keys = [b"doc/%08d/%04d" % (k, e) for e in range(width)]
+        kb = np.frombuffer(b"".join(keys) + bytes(8), np.uint8)
+        ko = np.arange(width + 1, dtype=np.uint64) * len(keys[0])
+        doc = rng.integers(0, 256, int(rng.integers(64, 1024)), dtype=np.uint8).tobytes()
+        hv = rng.integers(0, 256, (width, 32), dtype=np.uint8)
+        hv[0] = np.frombuffer(hashlib.sha256(doc).digest(), np.uint8)
+        st, _, _, eh = orc.build_entries_csr(1, kb, ko, mb, mo, np.zeros(8, np.uint8),
+                                             np.zeros(width + 1, np.uint64), want_levels=False,
+                                             ov=hv, use=np.ones(width, np.uint8))
+        assert st == 0
+        h = np.zeros(1, TX_HEADER)
+        h["id"], h["bl_tx_id"], h["version"], h["nentries"] = 100 + k, 99 + k, 1, width
+        h["eh"] = np.frombuffer(eh, np.uint8)
+        h["ts"] = 1_700_000_000 + k
+        alh = orc.tx_header_alh(h[0])[2]
+        ents = [(keys[e], mds[e % 4], hv[e].tobytes()) for e in range(width)]
+        docs.append({"encoded_document": doc, "doc_key": keys[0], "tx_hdr": h[0], "entries": ents,
+                     "src_hdr": h[0], "tgt_hdr": h[0], "incl": [], "cons": [],
+                     "known_tx_id": 100 + k, "known_alh": alh})
+    return docs
+
+
+def document(a, ctx):
+    import concurrent.futures as cf
+    import numpy as np
+    from immustore_amd import txlayer
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    docs = document_batch(a.docs, a.doc_entries)
+    b, keep = txlayer.pack_document_batch(docs, pinned=True)
+    n = len(docs)
+    res = {}
+
+    def step():
+        res["out"] = txlayer.call_document_batch(b, n, ctx)
+
+    t = timed(step, a.steps, a.warmup, lambda: None)
+    st, alh = res["out"]
+    sample = range(0, n, max(1, n // 256))
+    ok = all(int(st[k]) == 0 and alh[k].tobytes() == orc.verify_document(docs[k])[1]
+             for k in sample)
+    # CPU baseline: the oracle's hashing of the same documents on 16 host
+    # threads -- EntrySpec digests + one htree per tx (orc_precommit_batch with
+    # every HValue as the hVal override: the same digests and trees) plus
+    # SHA256(document); innerHash / Alh (4 compressions per doc) left out.
+    # Packed outside the timed region, as the device batch is.
+    W = a.doc_entries
+    kb = np.frombuffer(b"".join(e[0] for d in docs for e in d["entries"]) + bytes(8), np.uint8)
+    ko = np.zeros(n * W + 1, np.uint64)
+    np.cumsum([len(e[0]) for d in docs for e in d["entries"]], out=ko[1:])
+    mbb = np.frombuffer(b"".join(e[1] for d in docs for e in d["entries"]) + bytes(8), np.uint8)
+    mo_ = np.zeros(n * W + 1, np.uint64)
+    np.cumsum([len(e[1]) for d in docs for e in d["entries"]], out=mo_[1:])
+    hv = np.frombuffer(b"".join(e[2] for d in docs for e in d["entries"]), np.uint8)
+    txo = np.arange(n + 1, dtype=np.uint64) * W
+    dbs = np.frombuffer(b"".join(d["encoded_document"] for d in docs), np.uint8)
+    dof = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(d["encoded_document"]) for d in docs], out=dof[1:])
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(2) as ex:
+        f = ex.submit(orc.precommit_batch, 1, txo, kb, ko, np.zeros(8, np.uint8),
+                      np.zeros(n * W + 1, np.uint64), mbb, mo_, hv, np.ones(n * W, np.uint8),
+                      None, 0, 16)
+        # SHA256(document) beside it: the documents' bytes once, one core
+        orc.precommit_batch(0, np.arange(n + 1, dtype=np.uint64), np.zeros(8, np.uint8),
+                            np.zeros(n + 1, np.uint64), dbs, dof, nthreads=1)
+        _, ehs, sts = f.result()
+    tc = time.perf_counter() - t0
+    roots = [ehs[k].tobytes() for k in range(n)]
+    assert all(r == bytes(docs[k]["tx_hdr"]["eh"]) for k, r in enumerate(roots))
+    return {"metric": "VerifyDocument batch (hashing part), documents in host memory", "docs": n,
+            "entries_per_doc": a.doc_entries, "value": round(n / t / 1e3, 1),
+            "unit": "K documents/s", "ms_per_step": round(t * 1e3, 3),
+            "all_valid": bool((st == 0).all()), "sample_matches_oracle": bool(ok),
+            "cpu_baseline": {"kind": "port", "cores": 16, "value": round(n / tc / 1e3, 1),
+                             "unit": "K documents/s",
+                             "sample": "the whole batch once: oracle orc_precommit_batch over "
+                                       "the docs' txs with the HValues as overrides (EntrySpec "
+                                       "digests + htree, 16 threads) beside SHA256 of every "
+                                       "document (1 thread)"}}
 
 
 def run_single(a):
@@ -674,6 +785,8 @@ def run_single(a):
 
     elif a.workload == "ragged":
         out = ragged(a, m, N, L, ctx, dev, sync)
+    elif a.workload == "document":
+        out = document(a, ctx)
     elif a.workload == "c2e2e":
         n, vlen, klen = 1 << 20, 1024, 8
         hv = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()

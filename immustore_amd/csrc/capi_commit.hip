@@ -126,7 +126,7 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
     for (uint64_t k = 0; k < nt; k++) wmax = std::max(wmax, loff[k + 1] - loff[k]);
     // small trees (every tx of the chunk <= kSmallTreeMax entries): one lane
     // per tree on the device, no host tree plan
-    const bool small = wmax <= kSmallTreeMax;
+    const bool small = small_roots_fit(nt, wmax);
     TreePlan P;
     if (!small) P.build(nt, loff.data());
     Layout L;

@@ -12,40 +12,48 @@
 //   4. checks the tx / source / target headers and the known state against
 //      the headers' Alh values (:141-183);
 //   5. runs VerifyDualProofV2 (:185-194).
-// Steps 1, 3, 4 and 5 run here: SHA-256 of the documents, the entry-spec
-// digests and the per-document htrees, the header Alh values and the dual
-// proofs all on the device (capi_tx.hip's batch entry points); the host packs
-// messages and combines verdicts in the reference's order.
+// Steps 1, 3, 4 and 5 run here: SHA-256 of the documents and the entry
+// search, the entry-spec digests (fused entry kernel, HValues as hVal
+// overrides) and the per-document htrees, the header Alh values and the dual
+// proofs all on the device; the caller's arrays go up as they are and the host
+// combines verdicts in the reference's order.
 #include "capi_internal.hpp"
 
 namespace {
 
-// SHA-256 of n host byte ranges buf[off[i] .. off[i+1]) on the device.
-int sha_batch_host(mh_ctx *c, const uint8_t *buf, const std::vector<uint64_t> &off, uint8_t *out) {
-    const uint64_t n = off.size() - 1;
-    if (!n) return MH_OK;
-    const uint64_t bytes = off[n] - off[0];
-    std::lock_guard<std::mutex> lk(c->mu);
-    hipStream_t st = c->stream;
-    Layout L;
-    const uint64_t b_buf = L.add(std::max<uint64_t>(bytes, 16)), b_off = L.add((n + 1) * 8),
-                   b_out = L.add(n * 32), b_sort = L.add(sha_varlen_scratch_bytes(n));
-    MH_HIP(c->s_msgs.ensure(L.total));
-    uint8_t *base = c->s_msgs.as<uint8_t>();
-    std::vector<uint64_t> rel(n + 1);
-    for (uint64_t i = 0; i <= n; i++) rel[i] = off[i] - off[0];
-    if (bytes) MH_HIP(hipMemcpyAsync(base + b_buf, buf + off[0], bytes, hipMemcpyHostToDevice, st));
-    MH_HIP(hipMemcpyAsync(base + b_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    MH_HIP(launch_sha256_csr(st, c->tm(), base + b_buf, (const uint64_t *)(base + b_off), n,
-                             nullptr, nullptr, base + b_out, base + b_sort));
-    MH_HIP(hipMemcpyAsync(out, base + b_out, n * 32, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
-    return MH_OK;
-}
-
-inline void put16(std::vector<uint8_t> &v, uint64_t x) {
-    v.push_back((uint8_t)(x >> 8));
-    v.push_back((uint8_t)x);
+// VerifyDocument :60-76 per document (one lane): among the tx's entries
+// [ent_off[d], ent_off[d+1]) exactly one has the document's encoded key, and
+// its HValue is SHA256(EncodedDocument) -- a match whose HValue differs ends
+// the search at once (:63-67).  Key / offset arrays are the caller's
+// (unrebased offsets, base pointers shifted by the caller's first offset).
+__global__ __launch_bounds__(256) void k_doc_find(uint64_t n, const uint64_t *__restrict__ ent_off,
+                                                  const uint8_t *__restrict__ dkeys,
+                                                  const uint64_t *__restrict__ dkey_off,
+                                                  const uint8_t *__restrict__ ekeys,
+                                                  const uint64_t *__restrict__ ekey_off,
+                                                  const uint8_t *__restrict__ ehval,
+                                                  const uint8_t *__restrict__ hdoc,
+                                                  int32_t *__restrict__ status) {
+    const uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n) return;
+    const uint8_t *k = dkeys + dkey_off[d];
+    const uint64_t kl = dkey_off[d + 1] - dkey_off[d];
+    int found = 0;
+    for (uint64_t e = ent_off[d]; e < ent_off[d + 1]; e++) {
+        if (ekey_off[e + 1] - ekey_off[e] != kl) continue;
+        const uint8_t *q = ekeys + ekey_off[e];
+        bool eq = true;
+        for (uint64_t j = 0; j < kl && eq; j++) eq = q[j] == k[j];
+        if (!eq) continue;
+        bool same = true;
+        for (int j = 0; j < 32 && same; j++) same = ehval[32 * (e - ent_off[0]) + j] == hdoc[32 * d + j];
+        if (!same) {
+            found = -1;
+            break;
+        }
+        found++;
+    }
+    status[d] = found == 1 ? MH_OK : MH_ERR_INVALID_PROOF_ENTRY;
 }
 
 }  // namespace
@@ -74,66 +82,109 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
         for (uint64_t d = 0; d < n; d++) status[d] = MH_OK;
         const uint64_t e0 = B->ent_off[0];
 
-        // ---- 1. SHA256(EncodedDocument) vs the HValue of the document's entry (:60-76)
-        std::vector<uint64_t> doff(B->doc_off, B->doc_off + n + 1);
-        std::vector<uint8_t> hdoc(n * 32);
-        if (int e = sha_batch_host(c, B->doc, doff, hdoc.data())) return e;
-        for (uint64_t d = 0; d < n; d++) {
-            const uint8_t *k = B->doc_key + B->doc_key_off[d];
-            const uint64_t kl = B->doc_key_off[d + 1] - B->doc_key_off[d];
-            int found = 0;
-            for (uint64_t e = B->ent_off[d]; e < B->ent_off[d + 1]; e++) {
-                const uint64_t el = B->ekey_off[e + 1] - B->ekey_off[e];
-                if (el != kl || (kl && memcmp(B->ekeys + B->ekey_off[e], k, kl))) continue;
-                if (memcmp(B->ehval + 32 * e, &hdoc[32 * d], 32)) {
-                    found = -1;  // hash mismatch: returned at once (:63-67)
-                    break;
+        // ---- 1 + 3 on the device, one upload of the caller's arrays as they
+        // are (offsets unrebased: the device base pointers are shifted instead)
+        //  1. SHA256(EncodedDocument) vs the HValue of the document's entry (:60-76)
+        //  3. htree over EntrySpecDigestFor(version), IsValueTruncated (:112-139):
+        //     the fused entry kernel (k_entries_varlen) takes each entry's HValue
+        //     as the hVal override and the digest version per entry, one htree
+        //     per document.
+        //     v1: EntrySpecDigest_v1 (store/verification.go:264-302) =
+        //         SHA256(BE16 mdLen || md || BE16 kLen || key || HashValue)
+        //     v0: EntrySpecDigest_v0 (:256-262) = SHA256(key || SHA256(Value));
+        //         VerifyDocument leaves Value nil, so SHA256(Value) = SHA256(nil)
+        //         whatever the entry's HValue (and its metadata is not hashed).
+        //     Only a batch that mixes v0 and v1 documents stages per-entry
+        //     versions and hVals.
+        std::vector<uint8_t> roots(n * 32);
+        {
+            bool any_v0 = false;
+            for (uint64_t d = 0; d < n && !any_v0; d++) any_v0 = B->tx_hdr[d].version == 0;
+            std::vector<uint64_t> leaf_off(n + 1);
+            for (uint64_t d = 0; d <= n; d++) leaf_off[d] = B->ent_off[d] - e0;
+            std::vector<uint8_t> ov, ver;
+            if (any_v0 && E) {
+                ov.resize(E * 32);
+                ver.resize(E);
+                for (uint64_t d = 0; d < n; d++) {
+                    const uint8_t v = B->tx_hdr[d].version == 0 ? 0 : 1;
+                    for (uint64_t e = B->ent_off[d]; e < B->ent_off[d + 1]; e++) {
+                        ver[e - e0] = v;
+                        memcpy(&ov[32 * (e - e0)], v ? B->ehval + 32 * e : kEmptyRoot, 32);
+                    }
                 }
-                found++;
             }
-            if (found != 1) status[d] = MH_ERR_INVALID_PROOF_ENTRY;
-        }
-
-        // ---- 3. htree over EntrySpecDigestFor(version), IsValueTruncated (:112-139)
-        //   v1: EntrySpecDigest_v1 (store/verification.go:264-302) =
-        //       SHA256(BE16 mdLen || md || BE16 kLen || key || HashValue)
-        //   v0: EntrySpecDigest_v0 (:256-262) = SHA256(key || SHA256(Value));
-        //       VerifyDocument leaves Value nil, so SHA256(Value) = SHA256(nil)
-        //       whatever the entry's HValue (and its metadata is not hashed).
-        std::vector<uint8_t> msg;
-        std::vector<uint64_t> moff(1, 0);
-        std::vector<uint64_t> leaf_off(n + 1, 0);
-        for (uint64_t d = 0; d < n; d++) {
-            const uint32_t ver = B->tx_hdr[d].version;
-            if (status[d] == MH_OK && ver > 1) status[d] = MH_ERR_UNSUPPORTED_TX_VERSION;
-            const bool hash = status[d] == MH_OK;
-            for (uint64_t e = B->ent_off[d]; hash && e < B->ent_off[d + 1]; e++) {
-                const uint8_t *key = B->ekeys ? B->ekeys + B->ekey_off[e] : nullptr;
-                const uint64_t kl = B->ekey_off[e + 1] - B->ekey_off[e];
-                if (ver == 1) {
-                    const uint64_t ml = B->emd_off ? B->emd_off[e + 1] - B->emd_off[e] : 0;
-                    put16(msg, ml);
-                    if (ml) msg.insert(msg.end(), B->emd + B->emd_off[e], B->emd + B->emd_off[e] + ml);
-                    put16(msg, kl);
-                    if (kl) msg.insert(msg.end(), key, key + kl);
-                    msg.insert(msg.end(), B->ehval + 32 * e, B->ehval + 32 * e + 32);
-                } else {
-                    if (kl) msg.insert(msg.end(), key, key + kl);
-                    msg.insert(msg.end(), kEmptyRoot, kEmptyRoot + 32);
+            const uint64_t k0 = E ? B->ekey_off[e0] : 0, kb = E ? B->ekey_off[e0 + E] - k0 : 0;
+            const bool has_md = B->emd_off != nullptr;
+            const uint64_t m0 = (has_md && E) ? B->emd_off[e0] : 0,
+                           mb = (has_md && E) ? B->emd_off[e0 + E] - m0 : 0;
+            const uint64_t dc0 = B->doc_off[0], dcb = B->doc_off[n] - dc0;
+            const uint64_t dk0 = B->doc_key_off[0], dkb = B->doc_key_off[n] - dk0;
+            std::lock_guard<std::mutex> lk(c->mu);
+            hipStream_t st = c->stream;
+            Layout L;
+            const uint64_t b_k = L.add(std::max<uint64_t>(kb, 16)), b_m = L.add(mb),
+                           b_ko = L.add((E + 1) * 8), b_mo = L.add(has_md ? (E + 1) * 8 : 0),
+                           b_hv = L.add(E * 32), b_ov = L.add(any_v0 ? E * 32 : 0),
+                           b_ver = L.add(any_v0 ? E : 0), b_dig = L.add(std::max<uint64_t>(E, 1) * 32),
+                           b_r = L.add(n * 32), b_doc = L.add(std::max<uint64_t>(dcb, 16)),
+                           b_doff = L.add((n + 1) * 8), b_dk = L.add(std::max<uint64_t>(dkb, 16)),
+                           b_dko = L.add((n + 1) * 8), b_eo = L.add((n + 1) * 8),
+                           b_hdoc = L.add(n * 32), b_st = L.add(n * 4),
+                           b_sort = L.add(sha_varlen_scratch_bytes(n));
+            MH_HIP(c->s_msgs.ensure(L.total));
+            uint8_t *base = c->s_msgs.as<uint8_t>();
+            auto up = [&](uint64_t off, const void *src, uint64_t bytes) -> hipError_t {
+                return bytes ? hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, st)
+                             : hipSuccess;
+            };
+            MH_HIP(up(b_doc, B->doc + dc0, dcb));
+            MH_HIP(up(b_doff, B->doc_off, (n + 1) * 8));
+            MH_HIP(up(b_dk, B->doc_key + dk0, dkb));
+            MH_HIP(up(b_dko, B->doc_key_off, (n + 1) * 8));
+            MH_HIP(up(b_eo, B->ent_off, (n + 1) * 8));
+            if (E) {
+                MH_HIP(up(b_k, B->ekeys + k0, kb));
+                MH_HIP(up(b_m, B->emd + m0, mb));
+                MH_HIP(up(b_ko, B->ekey_off + e0, (E + 1) * 8));
+                if (has_md) MH_HIP(up(b_mo, B->emd_off + e0, (E + 1) * 8));
+                MH_HIP(up(b_hv, B->ehval + 32 * e0, E * 32));
+                if (any_v0) {
+                    MH_HIP(up(b_ov, ov.data(), E * 32));
+                    MH_HIP(up(b_ver, ver.data(), E));
                 }
-                moff.push_back(msg.size());
             }
-            leaf_off[d + 1] = moff.size() - 1;
+            // 1.
+            MH_HIP(launch_sha256_csr(st, c->tm(), base + b_doc - dc0, (const uint64_t *)(base + b_doff),
+                                     n, nullptr, nullptr, base + b_hdoc, base + b_sort));
+            hipLaunchKernelGGL(k_doc_find, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                               (const uint64_t *)(base + b_eo), base + b_dk - dk0,
+                               (const uint64_t *)(base + b_dko), base + b_k - k0,
+                               (const uint64_t *)(base + b_ko) - e0, base + b_hv, base + b_hdoc,
+                               (int32_t *)(base + b_st));
+            MH_HIP(hipGetLastError());
+            // 3.
+            if (E)
+                MH_HIP(launch_entries_varlen(st, c->tm(), 1, E, base + b_k - k0,
+                                             (const uint64_t *)(base + b_ko),
+                                             has_md ? base + b_m - m0 : nullptr,
+                                             has_md ? (const uint64_t *)(base + b_mo) : nullptr,
+                                             nullptr, nullptr, any_v0 ? base + b_ov : base + b_hv,
+                                             nullptr, nullptr, base + b_dig, false, nullptr,
+                                             any_v0 ? base + b_ver : nullptr));
+            if (int e = build_many_dev(c, st, n, leaf_off.data(), base + b_dig, base + b_r,
+                                       c->s_digests, c->s_offs))
+                return e;
+            MH_HIP(hipMemcpyAsync(roots.data(), base + b_r, n * 32, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(status, base + b_st, n * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipStreamSynchronize(st));
         }
-        (void)e0;
-        const uint64_t nd = moff.size() - 1;
-        std::vector<uint8_t> digs(std::max<uint64_t>(nd, 1) * 32), roots(n * 32);
-        if (nd)
-            if (int e = sha_batch_host(c, msg.data(), moff, digs.data())) return e;
-        if (int e = mh_htree_build_many(c, n, leaf_off.data(), digs.data(), roots.data())) return e;
-        for (uint64_t d = 0; d < n; d++)
+        for (uint64_t d = 0; d < n; d++) {
+            if (status[d] == MH_OK && B->tx_hdr[d].version > 1)
+                status[d] = MH_ERR_UNSUPPORTED_TX_VERSION;  // :118-121
             if (status[d] == MH_OK && memcmp(&roots[32 * d], B->tx_hdr[d].eh, 32))
-                status[d] = MH_ERR_INVALID_PROOF;
+                status[d] = MH_ERR_INVALID_PROOF;  // :137-139
+        }
 
         // ---- 4. headers and known state (:141-183)
         // Alh of the tx, source and target headers; a header that cannot be

@@ -280,6 +280,9 @@ inline uint64_t plan_index_bytes(const TreePlan &P, uint64_t ntrees) {
 }
 
 // Leaves + levels + roots of a planned batch (capi_tx.hip).
+// roots of many htrees over device digests (capi_tx.hip)
+int build_many_dev(mh_ctx *c, hipStream_t st, uint64_t ntrees, const uint64_t *leaf_off,
+                   const uint8_t *d_dig, uint8_t *d_roots, DevBuf &s_lv, DevBuf &s_lo);
 int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,
                   const uint8_t *d_digests, uint8_t *d_roots);
 int run_tree_plan_on(DevBuf &scratch, hipStream_t st, Timer *tm, const TreePlan &P, uint64_t ntrees,

@@ -116,6 +116,32 @@ extern "C" int mh_dev_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hd
 }
 
 // ------------------------------------------------------------------ a3 x many
+// Roots of many htrees over device digests d_dig (leaf_off: host, ntrees + 1,
+// rebased so leaf_off[0] is d_dig's first digest) into device d_roots, on st;
+// scratch: two device buffers of the caller (the small-tree leaves + offsets).
+int build_many_dev(mh_ctx *c, hipStream_t st, uint64_t ntrees, const uint64_t *leaf_off,
+                   const uint8_t *d_dig, uint8_t *d_roots, DevBuf &s_lv, DevBuf &s_lo) {
+    const uint64_t E = leaf_off[ntrees] - leaf_off[0];
+    uint64_t wmax = 0;
+    for (uint64_t t = 0; t < ntrees; t++) wmax = std::max(wmax, leaf_off[t + 1] - leaf_off[t]);
+    if (small_roots_fit(ntrees, wmax)) {  // one lane (or wave) per tree, no host plan
+        MH_HIP(s_lv.ensure(std::max<uint64_t>(E, 1) * 32));
+        MH_HIP(s_lo.ensure((ntrees + 1) * 8));
+        MH_HIP(hipMemcpyAsync(s_lo.p, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(launch_leaf_for(st, c->tm(), E, d_dig, s_lv.as<uint8_t>()));  // htree.go:79-83
+        MH_HIP(launch_small_roots(st, c->tm(), ntrees, s_lo.as<uint64_t>(), s_lv.as<uint8_t>(),
+                                  d_roots));
+        // leaf_off is the caller's host memory: done with it before returning
+        MH_HIP(hipStreamSynchronize(st));
+    } else {
+        TreePlan P;
+        P.build(ntrees, leaf_off);
+        if (int e = run_tree_plan(c, st, P, ntrees, E, d_dig, d_roots)) return e;
+        MH_HIP(hipStreamSynchronize(st));  // the plan's host vectors go out of scope
+    }
+    return MH_OK;
+}
+
 extern "C" int mh_htree_build_many(mh_ctx *c, uint64_t ntrees, const uint64_t *leaf_off,
                                    const uint8_t *digests, uint8_t *roots) {
     return mh_guard([&]() -> int {
@@ -125,29 +151,19 @@ extern "C" int mh_htree_build_many(mh_ctx *c, uint64_t ntrees, const uint64_t *l
             if (leaf_off[t + 1] < leaf_off[t]) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t E = leaf_off[ntrees] - leaf_off[0];
         if (E && !digests) return MH_ERR_ILLEGAL_ARGUMENTS;
-        uint64_t wmax = 0;
-        for (uint64_t t = 0; t < ntrees; t++) wmax = std::max(wmax, leaf_off[t + 1] - leaf_off[t]);
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         hipStream_t st = c->stream;
         Layout L;
-        const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
-                       b_lo = L.add((ntrees + 1) * 8), b_r = L.add(ntrees * 32);
+        const uint64_t b_d = L.add(std::max<uint64_t>(E, 1) * 32), b_r = L.add(ntrees * 32);
         MH_HIP(c->s_tx.ensure(L.total));
         uint8_t *base = c->s_tx.as<uint8_t>();
         if (E)
             MH_HIP(hipMemcpyAsync(base + b_d, digests + leaf_off[0] * 32, E * 32,
                                   hipMemcpyHostToDevice, st));
-        if (wmax <= kSmallTreeMax) {  // one lane per tree, no host plan
-            MH_HIP(hipMemcpyAsync(base + b_lo, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
-            MH_HIP(launch_leaf_for(st, c->tm(), E, base + b_d, base + b_lv));  // htree.go:79-83
-            MH_HIP(launch_small_roots(st, c->tm(), ntrees, (const uint64_t *)(base + b_lo),
-                                      base + b_lv, base + b_r));
-        } else {
-            TreePlan P;
-            P.build(ntrees, leaf_off);
-            if (int e = run_tree_plan(c, st, P, ntrees, E, base + b_d, base + b_r)) return e;
-        }
+        if (int e = build_many_dev(c, st, ntrees, leaf_off, base + b_d, base + b_r, c->s_digests,
+                                   c->s_offs))
+            return e;
         MH_HIP(hipMemcpyAsync(roots, base + b_r, ntrees * 32, hipMemcpyDeviceToHost, st));
         MH_HIP(hipStreamSynchronize(st));
         return MH_OK;
@@ -1002,7 +1018,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // ---- device: headers, entry index, digests, trees, Alh
         // small trees (every tx here: a handful of entries) get their roots one
         // lane per tree; a batch with a wide tx goes through the host tree plan
-        const bool small = wmax <= kSmallTreeMax;
+        const bool small = small_roots_fit(ntx, wmax);
         Layout L;
         const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
                        b_lv = L.add(std::max<uint64_t>(E, 1) * 32),

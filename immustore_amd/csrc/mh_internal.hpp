@@ -96,12 +96,15 @@ hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, cons
 // Fused ragged entries (varlen_kernels.hip): hVal (or override) -> hvals_out
 // (may be null), entry digest (tx.go:690-731) -> out32, or its htree leaf when
 // leaf is set (level 0 of the tree).  scratch as for launch_sha256_csr.
+// ver_e (device, n bytes, may be null): per-entry digest version instead of
+// `version` (a v0 entry's metadata is then not hashed).  override32 with a
+// null use_override overrides every entry (val_off / vals may be null).
 hipError_t launch_entries_varlen(hipStream_t st, Timer *tm, int version, uint64_t n,
                                  const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
                                  const uint64_t *md_off, const uint8_t *vals,
                                  const uint64_t *val_off, const uint8_t *override32,
                                  const uint8_t *use_override, uint8_t *hvals_out, uint8_t *out32,
-                                 bool leaf, uint8_t *scratch);
+                                 bool leaf, uint8_t *scratch, const uint8_t *ver_e = nullptr);
 // Leaves from digests (htree.go:79-83) + in-lane levels up to log2(LPL).
 hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *digests,
                                       uint64_t n, uint8_t *levels, const LevelGeom &g,
@@ -182,6 +185,14 @@ hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uin
 // roots of many htrees (widths leaf_off[t+1]-leaf_off[t], small), one lane
 // each, in place over nodes = their leaf hashes back to back
 constexpr uint64_t kSmallTreeMax = 64;
+// launch_small_roots is the right tool when a tree's serial chain is short
+// (one lane walks <= 15 node hashes) or there are few trees (a wave per tree,
+// level by level); many trees of 17..64 leaves go level-parallel through the
+// host tree plan instead (k_seg_level: every node of a level at once) --
+// e.g. 8192 trees of 64 leaves: 0.29 ms one lane per tree vs ~0.07 ms.
+inline bool small_roots_fit(uint64_t ntrees, uint64_t wmax) {
+    return wmax <= kSmallTreeMax && (wmax <= 16 || ntrees <= 2048);
+}
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
                               uint8_t *nodes, uint8_t *roots);
 // headers + first-entry offsets of tx records from the raw log (md_off relative to buf)

@@ -309,22 +309,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const uint8_t *__restrict__ vals, const uint64_t *__restrict__ val_off,
     const uint32_t *__restrict__ perm, const uint8_t *__restrict__ override32,
     const uint8_t *__restrict__ use_override, uint8_t *__restrict__ hvals_out,
-    uint8_t *__restrict__ out32, int want_leaf) {
+    uint8_t *__restrict__ out32, int want_leaf, const uint8_t *__restrict__ ver_e) {
     __shared__ uint32_t hv_lds[256 * kHvSlot];
     uint32_t *slot = hv_lds + threadIdx.x * kHvSlot;
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool valid = g < n;
     const uint64_t gc = valid ? g : n - 1;
     const uint64_t i = perm ? (uint64_t)perm[gc] : gc;
-    const bool ovr = use_override && use_override[i];
-    const uint64_t vo = val_off[i];
-    const uint64_t L = val_off[i + 1] - vo;
+    // override32 without use_override: every entry takes its hVal from the
+    // caller (val_off may then be null)
+    const bool ovr = override32 && (!use_override || use_override[i]);
+    // digest version: the launch's, or per entry (documents of several txs)
+    const int ver = ver_e ? (int)ver_e[i] : version;
+    const uint64_t vo = ovr ? 0 : val_off[i];
+    const uint64_t L = ovr ? 0 : val_off[i + 1] - vo;
     const uint64_t ko = key_off[i];
     const uint64_t kl = key_off[i + 1] - ko;
-    const uint64_t mo = (version == 1 && md_off) ? md_off[i] : 0;
-    const uint64_t ml = (version == 1 && md_off) ? md_off[i + 1] - mo : 0;
+    const uint64_t mo = (ver == 1 && md_off) ? md_off[i] : 0;
+    const uint64_t ml = (ver == 1 && md_off) ? md_off[i + 1] - mo : 0;
     // digest message layout (tx.go:703-731 v1, :690-701 v0)
-    const int64_t s_key = version == 1 ? (int64_t)(4 + ml) : 0;
+    const int64_t s_key = ver == 1 ? (int64_t)(4 + ml) : 0;
     const int64_t s_hv = s_key + (int64_t)kl;
     const int64_t ld = s_hv + 32;
     const uint32_t nbv = ovr ? 0u : (uint32_t)((L + 72) >> 6);
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                 // only, and within its first 4 words whenever every digest lane
                 // of the wave has s_key <= 16 (KV metadata <= 11 bytes, always
                 // for immudb's attributes)
-                if (version == 1 && p0 < s_key) {
+                if (ver == 1 && p0 < s_key) {
                     prefix_words4(x, mp, ml, kl, p0);
                     if (__ballot(s_key > p0 + 16)) {  // metadata longer than 12 bytes
 #pragma unroll
@@ -494,15 +498,18 @@ hipError_t launch_entries_varlen(hipStream_t st, Timer *tm, int version, uint64_
                                  const uint64_t *md_off, const uint8_t *vals,
                                  const uint64_t *val_off, const uint8_t *override32,
                                  const uint8_t *use_override, uint8_t *hvals_out, uint8_t *out32,
-                                 bool leaf, uint8_t *scratch) {
+                                 bool leaf, uint8_t *scratch, const uint8_t *ver_e) {
     if (!n) return hipSuccess;
-    hipError_t e;
-    const uint32_t *perm = nb_sort(st, tm, val_off, use_override, n, scratch, &e);
+    hipError_t e = hipSuccess;
+    // every hVal overridden: no value blocks, nothing to sort by
+    const uint32_t *perm = (override32 && !use_override)
+                               ? nullptr
+                               : nb_sort(st, tm, val_off, use_override, n, scratch, &e);
     if (e != hipSuccess) return e;
     TimerScope ts(tm, "entries_varlen", st);
     hipLaunchKernelGGL(k_entries_varlen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        version, n, keys, key_off, md, md_off, vals, val_off, perm, override32,
-                       use_override, hvals_out, out32, leaf ? 1 : 0);
+                       use_override, hvals_out, out32, leaf ? 1 : 0, ver_e);
     return hipGetLastError();
 }
 

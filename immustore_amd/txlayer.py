@@ -231,9 +231,48 @@ def verify_document_batch(docs, ctx: Optional[Context] = None):
     n = len(docs)
     if n == 0:
         return np.zeros(0, np.int32), np.zeros((0, 32), np.uint8)
+    b, keep = pack_document_batch(docs)
+    return call_document_batch(b, n, ctx)
+
+
+def call_document_batch(b, n, ctx: Optional[Context] = None):
+    """mh_verify_document_batch over a batch packed by pack_document_batch."""
+    st = np.zeros(n, np.int32)
+    alh = np.zeros((n, 32), np.uint8)
+    N.check(N.load().mh_verify_document_batch(_ctx(ctx).handle, C.byref(b), _addr(st),
+                                              _addr(alh)))
+    return st, alh
+
+
+class _Pinned:
+    """A numpy array in pinned host memory (mh_host_alloc_pinned)."""
+
+    def __init__(self, a):
+        a = np.ascontiguousarray(a)
+        self.p = C.c_void_p()
+        N.check(N.load().mh_host_alloc_pinned(max(a.nbytes, 1), C.byref(self.p)))
+        buf = (C.c_uint8 * max(a.nbytes, 1)).from_address(self.p.value)
+        self.a = np.frombuffer(buf, np.uint8, count=a.nbytes).view(a.dtype).reshape(a.shape)
+        self.a[...] = a
+
+    def __del__(self):
+        if self.p:
+            N.load().mh_host_free_pinned(self.p)
+            self.p = None
+
+
+def pack_document_batch(docs, pinned: bool = False):
+    """The mh_document_batch of verify_document_batch's docs -> (struct, the
+    arrays it points into, to be kept alive while it is used).  pinned: the
+    arrays in pinned host memory, as a cgo shim's packing arena would be."""
+    n = len(docs)
     keep = []
 
     def k(a):
+        if pinned:
+            a = _Pinned(a)
+            keep.append(a)
+            return a.a.ctypes.data
         keep.append(a)
         return _addr(a)
 
@@ -258,11 +297,7 @@ def verify_document_batch(docs, ctx: Optional[Context] = None):
                        k(ekoff), k(embuf), k(emoff), k(ehv), k(sh), k(th),
                        k(mb) if mb is not None else None, ml, k(io), k(it), k(co), k(ct), k(kid),
                        k(kalh))
-    st = np.zeros(n, np.int32)
-    alh = np.zeros((n, 32), np.uint8)
-    N.check(N.load().mh_verify_document_batch(_ctx(ctx).handle, C.byref(b), _addr(st),
-                                              _addr(alh)))
-    return st, alh
+    return b, keep
 
 
 def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,

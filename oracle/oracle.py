@@ -190,18 +190,21 @@ def build_entries(version, keys, mds, vals, overrides=None):
     return st, hv[:n], lv[:levels_len(n)], root.tobytes()
 
 
-def build_entries_csr(version, kb, ko, mb, mo, vb, vo, want_levels=True):
+def build_entries_csr(version, kb, ko, mb, mo, vb, vo, want_levels=True, ov=None, use=None):
     """CSR byte arrays (u8) + u64 offsets (n+1 each; mb/mo may be None) ->
     (status, hvals, levels, root); the array form of build_entries for large
-    ragged batches."""
+    ragged batches.  ov (n x 32) / use (n, u8): IsValueTruncated hVal
+    overrides."""
     n = len(ko) - 1
     ko, vo = np.ascontiguousarray(ko, np.uint64), np.ascontiguousarray(vo, np.uint64)
     mo = None if mo is None else np.ascontiguousarray(mo, np.uint64)
     hv = np.zeros((max(n, 1), 32), np.uint8)
     lv = np.zeros((max(levels_len(n), 1), 32), np.uint8) if want_levels else None
     root = np.zeros(32, np.uint8)
+    ov = None if ov is None else np.ascontiguousarray(ov, np.uint8)
+    use = None if use is None else np.ascontiguousarray(use, np.uint8)
     st = lib().orc_build_entries(version, n, _p(kb), _p(ko, u64p), _p(mb), _p(mo, u64p), _p(vb),
-                                 _p(vo, u64p), None, None, _p(hv), _p(lv), _p(root))
+                                 _p(vo, u64p), _p(ov), _p(use), _p(hv), _p(lv), _p(root))
     return st, hv[:n], (lv[:levels_len(n)] if want_levels else None), root.tobytes()
 
 
