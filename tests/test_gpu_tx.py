@@ -84,6 +84,15 @@ def test_htree_build_many_vs_oracle(m, ctx, orc):
     roots = m.htree_build_many(small, ctx)
     for t, r in zip(small, roots):
         assert r.tobytes() == orc.htree_build(t)[1]
+    # every shape class of the many-tree dispatch (small_roots_fit): few trees
+    # up to 64 wide (a wave per tree), many trees up to 16 wide (a lane per
+    # tree), many trees of 17..64 (level-parallel through the plan)
+    for count, lo, hi in ((2048, 1, 65), (3000, 1, 17), (3000, 17, 65), (2049, 60, 65)):
+        ts = [rng.integers(0, 256, (int(w), 32), dtype=np.uint8)
+              for w in rng.integers(lo, hi, count)]
+        roots = m.htree_build_many(ts, ctx)
+        for t, r in zip(ts, roots):
+            assert r.tobytes() == orc.htree_build(t)[1], (count, lo, hi, len(t))
 
 
 def test_txlog_validate_fixture_stores(m, ctx, fixtures):
