@@ -490,6 +490,10 @@ extern "C" int mh_htree_build_entries(mh_htree *t, int version, uint64_t n, cons
         if (n && (!key_off || !val_off)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (n > t->max_width) return MH_ERR_MAX_WIDTH_EXCEEDED;
+        for (uint64_t i = 0; i < n; i++)
+            if (key_off[i + 1] < key_off[i] || val_off[i + 1] < val_off[i] ||
+                (md_off && md_off[i + 1] < md_off[i]))
+                return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t md_bytes = md_off && n ? md_off[n] - md_off[0] : 0;
         if (version == 0 && md_bytes) return MH_ERR_METADATA_UNSUPPORTED;  // tx.go:691-693
         if (n == 0) return finish_build(t, 0);

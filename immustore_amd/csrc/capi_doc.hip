@@ -78,6 +78,10 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
             if (B->doc_off[d + 1] < B->doc_off[d] || B->doc_key_off[d + 1] < B->doc_key_off[d] ||
                 B->ent_off[d + 1] < B->ent_off[d])
                 return MH_ERR_ILLEGAL_ARGUMENTS;
+        for (uint64_t e = B->ent_off[0]; e < B->ent_off[n]; e++)
+            if (B->ekey_off[e + 1] < B->ekey_off[e] ||
+                (B->emd_off && B->emd_off[e + 1] < B->emd_off[e]))
+                return MH_ERR_ILLEGAL_ARGUMENTS;
         MH_HIP(hipSetDevice(c->device));
         for (uint64_t d = 0; d < n; d++) status[d] = MH_OK;
         const uint64_t e0 = B->ent_off[0];

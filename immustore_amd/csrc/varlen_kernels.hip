@@ -32,7 +32,7 @@ constexpr int kNbChunk = 256 * 16;   // entries per workgroup of the sort passes
 // entries hashed from an override count 0 (no compression)
 __device__ __forceinline__ uint32_t nb_key(const uint64_t *off, const uint8_t *use, uint64_t i) {
     if (use && use[i]) return 0;
-    const uint64_t nb = (off[i + 1] - off[i] + 72) >> 6;
+    const uint64_t nb = ((off[i + 1] >= off[i] ? off[i + 1] - off[i] : 0) + 72) >> 6;
     return (uint32_t)(nb < (uint64_t)kNbBuckets ? nb : (uint64_t)kNbBuckets - 1);
 }
 
@@ -211,7 +211,9 @@ __global__ __launch_bounds__(256) void k_sha_varlen(const uint8_t *__restrict__ 
     const uint64_t i = perm ? (uint64_t)perm[gc] : gc;
     const bool ovr = use_override && use_override[i];
     const uint64_t o0 = off[i];
-    const uint64_t L = off[i + 1] - o0;
+    // offsets that run backwards (a caller bug) hash as empty messages rather
+    // than send the lane through a wrapped-around length
+    const uint64_t L = off[i + 1] >= o0 ? off[i + 1] - o0 : 0;
     const uint32_t nb = (valid && !ovr) ? (uint32_t)((L + 72) >> 6) : 0u;
     const uint32_t nbmax = wave_max_u32(nb);
     MsgWalk mw;
@@ -321,12 +323,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const bool ovr = override32 && (!use_override || use_override[i]);
     // digest version: the launch's, or per entry (documents of several txs)
     const int ver = ver_e ? (int)ver_e[i] : version;
+    // offsets that run backwards (a caller bug) read as empty ranges rather
+    // than send the lane through a wrapped-around length
+    auto span = [](const uint64_t *o, uint64_t k) { return o[k + 1] >= o[k] ? o[k + 1] - o[k] : 0; };
     const uint64_t vo = ovr ? 0 : val_off[i];
-    const uint64_t L = ovr ? 0 : val_off[i + 1] - vo;
+    const uint64_t L = ovr ? 0 : span(val_off, i);
     const uint64_t ko = key_off[i];
-    const uint64_t kl = key_off[i + 1] - ko;
+    const uint64_t kl = span(key_off, i);
     const uint64_t mo = (ver == 1 && md_off) ? md_off[i] : 0;
-    const uint64_t ml = (ver == 1 && md_off) ? md_off[i + 1] - mo : 0;
+    const uint64_t ml = (ver == 1 && md_off) ? span(md_off, i) : 0;
     // digest message layout (tx.go:703-731 v1, :690-701 v0)
     const int64_t s_key = ver == 1 ? (int64_t)(4 + ml) : 0;
     const int64_t s_hv = s_key + (int64_t)kl;

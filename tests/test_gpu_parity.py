@@ -102,6 +102,32 @@ def test_sha256_batch_ragged_length_classes(m, ctx):
             assert got[k].tobytes() == H(bb[int(o[k]):int(o[k + 1])]), (shift, k, int(lens[k]))
 
 
+def test_csr_offsets_running_backwards(m, ctx):
+    """Caller bugs never reach the device as wrapped-around lengths: host CSR
+    offsets that run backwards are MH_ERR_ILLEGAL_ARGUMENTS; device CSR ones
+    (checked nowhere on the host) hash the bad range as an empty message."""
+    from immustore_amd import _native as N
+    L = N.load()
+    buf = np.arange(64, dtype=np.uint8)
+    off = np.array([0, 10, 5, 20], np.uint64)
+    d_buf, d_off, d_out = DevBuf.from_host(ctx, buf), DevBuf.from_host(ctx, off), DevBuf(ctx, 96)
+    N.check(L.mh_dev_sha256_batch(ctx.handle, d_buf.ptr, d_off.ptr, 3, d_out.ptr))
+    got = d_out.to_host().reshape(3, 32)
+    assert got[0].tobytes() == H(buf[0:10].tobytes())
+    assert got[1].tobytes() == H(b"")
+    assert got[2].tobytes() == H(buf[5:20].tobytes())
+    t = m.HTree(8, ctx)
+    keys = np.frombuffer(b"abcdefgh", np.uint8).copy()
+    ko = np.array([0, 4, 2, 8], np.uint64)   # entry 1 runs backwards
+    vo = np.array([0, 1, 2, 3], np.uint64)
+    vals = np.zeros(8, np.uint8)
+    hv = np.zeros((3, 32), np.uint8)
+    st = L.mh_htree_build_entries(t.handle, 1, 3, keys.ctypes.data, ko.ctypes.data, None, None,
+                                  vals.ctypes.data, vo.ctypes.data, None, None, hv.ctypes.data)
+    assert st == N.MH_ERR_ILLEGAL_ARGUMENTS
+    t.close()
+
+
 def test_entries_ragged_with_overrides_vs_oracle(m, ctx, orc):
     """General entry path with ragged keys / metadata / values and a share of
     IsValueTruncated overrides (their hVal taken from the caller)."""
