@@ -731,6 +731,7 @@ extern "C" int mh_htree_verify_inclusion_batch(mh_ctx *c, uint64_t np, const uin
         if (!c || (np && (!leaf || !width || !term_off || !digests || !roots || !ok)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!np) return MH_OK;
+        if (!monotonic(term_off, np)) return MH_ERR_ILLEGAL_ARGUMENTS;
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         const uint64_t nterms = term_off[np] - term_off[0];
@@ -784,6 +785,7 @@ extern "C" int mh_ahtree_verify_batch(mh_ctx *c, int kind, uint64_t np, const ui
         if (!c || kind < 0 || kind > 2) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (np && (!i || !j || !term_off || !a || !b || !ok)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!np) return MH_OK;
+        if (!monotonic(term_off, np)) return MH_ERR_ILLEGAL_ARGUMENTS;
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         const uint64_t nterms = term_off[np] - term_off[0];

@@ -34,6 +34,14 @@ inline int mh_guard(F &&f) noexcept {
         if (e_ != hipSuccess) return -(int)e_;              \
     } while (0)
 
+// CSR offsets off[0..n] never run backwards (checked before a host wrapper
+// rebases them and sizes the device copies from off[n] - off[0])
+inline bool monotonic(const uint64_t *off, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) return false;
+    return true;
+}
+
 static const uint8_t kEmptyRoot[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14,
                                        0x9a, 0xfb, 0xf4, 0xc8, 0x99, 0x6f, 0xb9, 0x24,
                                        0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b, 0x93, 0x4c,

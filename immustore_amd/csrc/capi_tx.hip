@@ -181,6 +181,7 @@ extern "C" int mh_verify_linear_proof_batch(mh_ctx *c, uint64_t n, const uint64_
                          !tgt_alh || !ok)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!n) return MH_OK;
+        if (!monotonic(term_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t nterms = term_off[n] - term_off[0];
         if (nterms && !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
         std::lock_guard<std::mutex> lk(c->mu);
@@ -226,6 +227,7 @@ extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_
                          !tgt_alh || !status)))
             return MH_ERR_ILLEGAL_ARGUMENTS;
         if (!n) return MH_OK;
+        if (!monotonic(incl_off, n) || !monotonic(cons_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
         if ((ni && !incl_terms) || (nc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
         // verification.go:305-316: argument checks on the host, headers that
@@ -344,6 +346,10 @@ extern "C" int mh_verify_dual_proof_batch(mh_ctx *c, const mh_dual_proof_batch *
             !B->src || !B->tgt || !B->src_alh || !B->tgt_alh)
             return MH_ERR_ILLEGAL_ARGUMENTS;
         const mh_tx_header *sh = B->src_hdr, *th = B->tgt_hdr;
+        if (!monotonic(B->incl_off, n) || !monotonic(B->cons_off, n) ||
+            !monotonic(B->last_off, n) || !monotonic(B->linear_off, n) ||
+            !monotonic(B->advance_off, n) || !monotonic(B->advance_incl_first, n))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t ni = B->incl_off[n] - B->incl_off[0], nc = B->cons_off[n] - B->cons_off[0],
                        nl = B->last_off[n] - B->last_off[0], nlin = B->linear_off[n] - B->linear_off[0],
                        nadv = B->advance_off[n] - B->advance_off[0],

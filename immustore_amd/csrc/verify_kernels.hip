@@ -37,7 +37,8 @@ __global__ __launch_bounds__(512) void k_htree_verify(uint64_t np, const uint64_
     load_digest(digests + p * 32, d);
     leaf_hash(d, calc);
     uint64_t i = leaf[p], r = width[p] - 1;
-    const uint64_t t0 = term_off[p], t1 = term_off[p + 1];
+    // offsets running backwards (device CSR, unchecked by the host): no terms
+    const uint64_t t0 = term_off[p], t1 = max(term_off[p + 1], t0);
     for (uint64_t t = t0; t < t1; t++) {
         uint32_t term[8], l[8], rr[8];
         load_digest(terms + t * 32, term);
@@ -76,7 +77,8 @@ __global__ __launch_bounds__(512) void k_ahtree_verify(int kind, uint64_t np,
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
          p += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t i = vi[p], j = vj[p];
-        const uint64_t t0 = term_off[p], t1 = term_off[p + 1], len = t1 - t0;
+        // offsets running backwards (device CSR, unchecked by the host): no terms
+        const uint64_t t0 = term_off[p], t1 = max(term_off[p + 1], t0), len = t1 - t0;
         uint32_t c[8], cj[8];
         // verification.go:22-24 / :59-61: argument checks shared by inclusion
         // and consistency; last inclusion only needs i != 0 (:112-114)
