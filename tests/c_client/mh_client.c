@@ -108,6 +108,63 @@ int main(int argc, char **argv) {
         }
         free(keys);
     }
+    /* ragged entries (value hash loop + Tx.BuildHashTree, immustore.go:1620-1630,
+     * tx.go:332-355) through mh_htree_build_entries: CSR keys / KV metadata /
+     * values of varying length, every 5th entry with an IsValueTruncated hVal
+     * override; v1 (with metadata) and v0 (without).  Entry e (ne = w):
+     *   key   len 1 + (7e mod 40),  byte j = (13e + 5j + 1) & 0xff
+     *   md    e%4: none | 00 | 02 | 01 BE64(e)
+     *   value len (37e mod 700),    byte j = (3e + 11j) & 0xff
+     *   ovr   e%5==0: byte j = (e + j) & 0xff */
+    {
+        const uint64_t ne = w;
+        uint64_t *ko = malloc((ne + 1) * 8), *mo = malloc((ne + 1) * 8), *vo = malloc((ne + 1) * 8);
+        ko[0] = mo[0] = vo[0] = 0;
+        for (uint64_t e = 0; e < ne; e++) {
+            ko[e + 1] = ko[e] + 1 + (7 * e) % 40;
+            mo[e + 1] = mo[e] + (e % 4 == 0 ? 0 : e % 4 == 3 ? 9 : 1);
+            vo[e + 1] = vo[e] + (37 * e) % 700;
+        }
+        uint8_t *kb = malloc(ko[ne] + 1), *mb = malloc(mo[ne] + 1), *vb = malloc(vo[ne] + 1);
+        uint8_t *ov = malloc(ne * 32), *use = malloc(ne), *hv = malloc(ne * 32);
+        for (uint64_t e = 0; e < ne; e++) {
+            for (uint64_t j = 0; j < ko[e + 1] - ko[e]; j++) kb[ko[e] + j] = (uint8_t)(13 * e + 5 * j + 1);
+            for (uint64_t j = 0; j < vo[e + 1] - vo[e]; j++) vb[vo[e] + j] = (uint8_t)(3 * e + 11 * j);
+            uint8_t *m = mb + mo[e];
+            if (e % 4 == 1) m[0] = 0x00;
+            if (e % 4 == 2) m[0] = 0x02;
+            if (e % 4 == 3) {
+                m[0] = 0x01;
+                for (int b = 0; b < 8; b++) m[1 + b] = (uint8_t)(e >> (56 - 8 * b));
+            }
+            for (int j = 0; j < 32; j++) ov[e * 32 + j] = (uint8_t)(e + j);
+            use[e] = e % 5 == 0;
+        }
+        mh_htree *et;
+        CHECK(mh_htree_new(ctx, ne, &et));
+        uint8_t er[32];
+        CHECK(mh_htree_build_entries(et, 1, ne, kb, ko, mb, mo, vb, vo, ov, use, hv));
+        CHECK(mh_htree_root(et, er));
+        hex("entries_v1_root", er, 32);
+        hex("entries_v1_hval_mid", hv + (ne / 2) * 32, 32);
+        hex("entries_v1_hval_last", hv + (ne - 1) * 32, 32);
+        CHECK(mh_htree_build_entries(et, 0, ne, kb, ko, NULL, NULL, vb, vo, NULL, NULL, NULL));
+        CHECK(mh_htree_root(et, er));
+        hex("entries_v0_root", er, 32);
+        printf("entries_v0_md_rejected %d\n",
+               mh_htree_build_entries(et, 0, ne, kb, ko, mb, mo, vb, vo, NULL, NULL, NULL) ==
+                   (mo[ne] ? MH_ERR_METADATA_UNSUPPORTED : MH_OK));
+        if (ne >= 2) {
+            const uint64_t save = vo[1];
+            vo[1] = vo[2] + 1; /* offsets running backwards */
+            printf("entries_backwards_rejected %d\n",
+                   mh_htree_build_entries(et, 1, ne, kb, ko, mb, mo, vb, vo, NULL, NULL, NULL) ==
+                       MH_ERR_ILLEGAL_ARGUMENTS);
+            vo[1] = save;
+        }
+        CHECK(mh_htree_free(et));
+        free(ko); free(mo); free(vo); free(kb); free(mb); free(vb); free(ov); free(use); free(hv);
+    }
     CHECK(mh_ctx_destroy(ctx));
     free(d);
     free(p);

@@ -33,6 +33,55 @@ def _run(w, m):
     return out
 
 
+def _entries(ne):
+    """The ragged CSR batch mh_client.c builds (see the comment there)."""
+    e = np.arange(ne, dtype=np.int64)
+
+    def csr(lens, a, b, c):
+        # byte j of entry e = (a e + b j + c) & 0xff
+        off = np.zeros(ne + 1, np.uint64)
+        off[1:] = np.cumsum(lens)
+        ent = np.repeat(e, lens)
+        j = np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1].astype(np.int64), lens)
+        return np.append(((a * ent + b * j + c) & 0xFF).astype(np.uint8), np.uint8(0)), off
+
+    ms = [[b"", b"\x00", b"\x02", b"\x01" + int(x).to_bytes(8, "big")][x % 4] for x in range(ne)]
+    mo = np.zeros(ne + 1, np.uint64)
+    mo[1:] = np.cumsum([len(x) for x in ms])
+    md = (np.frombuffer(b"".join(ms) + b"\0", np.uint8), mo)
+    return csr(1 + (7 * e) % 40, 13, 5, 1), md, csr((37 * e) % 700, 3, 11, 0), *_ovr(ne)
+
+
+def _ovr(ne):
+    ov = ((np.arange(ne)[:, None] + np.arange(32)[None, :]) & 0xFF).astype(np.uint8)
+    use = (np.arange(ne) % 5 == 0).astype(np.uint8)
+    return ov, use
+
+
+def _check_entries(out, ne):
+    (kb, ko), (mb, mo), (vb, vo), ov, use = _entries(ne)
+    st, hv, _, root = O.build_entries_csr(1, kb, ko, mb, mo, vb, vo, False, ov, use)
+    assert st == 0
+    assert out["entries_v1_root"] == root.hex()
+    assert out["entries_v1_hval_mid"] == hv[ne // 2].tobytes().hex()
+    assert out["entries_v1_hval_last"] == hv[ne - 1].tobytes().hex()
+    st, _, _, root0 = O.build_entries_csr(0, kb, ko, None, None, vb, vo, False)
+    assert st == 0 and out["entries_v0_root"] == root0.hex()
+    assert out["entries_v0_md_rejected"] == "1"
+    if ne >= 2:
+        assert out["entries_backwards_rejected"] == "1"
+
+
+def test_c_client_entries_inputs_pin_oracle():
+    """CPU: the oracle side of the C-client entries check is self-consistent
+    (the overridden entries' hVals are the override bytes)."""
+    (kb, ko), (mb, mo), (vb, vo), ov, use = _entries(64)
+    st, hv, _, _ = O.build_entries_csr(1, kb, ko, mb, mo, vb, vo, False, ov, use)
+    assert st == 0
+    assert (hv[use == 1] == ov[use == 1]).all()
+    assert int(mo[-1]) == 16 * 0 + 16 * 1 + 16 * 1 + 16 * 9
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,m", [(1000, 777), (1, 3), (2, 4), (4096, 1 << 13), (65537, 100003),
                                  (300, 1000)])
@@ -58,6 +107,7 @@ def test_c_client_matches_oracle(w, m):
     st, cons = t.consistency_proof(m // 2, m)
     assert st == 0 and out["ahtree_cons"] == cons.tobytes().hex()
     assert out["empty_root_at"] == "1"
+    _check_entries(out, w)
     if m >= 2 * w:
         # mh_multi_htree_build_entries_fixed (RCCL clique of device 0; three shards)
         keys = np.frombuffer(np.arange(w, dtype=">u8").tobytes(), np.uint8).reshape(w, 8)
