@@ -1,0 +1,139 @@
+/* txlog_fuzz.c -- mutation fuzzing of the tx-log record hop (mh_txlog_scan,
+ * the host parse of mh_txlog_validate: tx.go:419-603, kv_metadata.go:207-256,
+ * tx_metadata.go:159-193) against the oracle's sequential parse
+ * (orc_txlog_validate), both built with AddressSanitizer (host code only:
+ * tools/asan/Makefile).  Test infrastructure: the oracle is the checker.
+ *
+ * Every mutant lives in a malloc of exactly its length, so a read one byte
+ * past the record run is reported by ASan.  Mutations: bit flips, bytes set
+ * to 0x00 / 0xff, BE16 / BE32 length fields overwritten with extreme values,
+ * truncation, a splice of another part of the log, a record repeated.
+ * For each mutant: (status, ntx, consumed) of the two parses must agree.
+ *
+ * usage: txlog_fuzz <iterations per file> <seed> <log file>...
+ * prints one line per file; exit 1 on any mismatch. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "immustore_merkle.h"
+
+int orc_txlog_validate(const uint8_t *buf, uint64_t len, uint32_t max_entries, uint32_t max_key_len,
+                       uint64_t max_txs, uint64_t *ntx_out, uint64_t *consumed_out,
+                       uint8_t *alh_out, int32_t *status_out);
+
+static uint64_t S;
+static uint64_t rnd(void) {
+    uint64_t z = (S += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint8_t *load(const char *path, uint64_t *len) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    uint8_t *b = malloc(n ? (size_t)n : 1);
+    if (n && fread(b, 1, (size_t)n, f) != (size_t)n) n = 0;
+    fclose(f);
+    *len = (uint64_t)n;
+    return b;
+}
+
+/* one mutant of src into a fresh exact-size buffer */
+static uint8_t *mutate(const uint8_t *src, uint64_t len, uint64_t *out_len) {
+    uint64_t n = len;
+    uint8_t *b = malloc(n ? n : 1);
+    memcpy(b, src, n);
+    const int k = 1 + (int)(rnd() % 4);
+    for (int m = 0; m < k && n; m++) {
+        const uint64_t p = rnd() % n;
+        switch (rnd() % 7) {
+        case 0: b[p] ^= (uint8_t)(1u << (rnd() % 8)); break;
+        case 1: b[p] = 0xff; break;
+        case 2: b[p] = 0x00; break;
+        case 3: /* a BE16 length field at an extreme */
+            if (p + 2 <= n) {
+                static const uint16_t v[] = {0, 1, 11, 12, 255, 256, 257, 1024, 1025, 0xffff};
+                const uint16_t x = v[rnd() % 10];
+                b[p] = (uint8_t)(x >> 8);
+                b[p + 1] = (uint8_t)x;
+            }
+            break;
+        case 4: /* a BE32 field at an extreme */
+            if (p + 4 <= n) {
+                static const uint32_t v[] = {0, 1, 1023, 1024, 1025, 0x10000, 0x7fffffff, 0xffffffff};
+                const uint32_t x = v[rnd() % 8];
+                for (int j = 0; j < 4; j++) b[p + j] = (uint8_t)(x >> (24 - 8 * j));
+            }
+            break;
+        case 5: /* truncate */
+            n = p;
+            break;
+        case 6: { /* splice: copy a run from elsewhere in the log over p */
+            const uint64_t q = rnd() % n, l = 1 + rnd() % 256;
+            for (uint64_t j = 0; j < l && p + j < n && q + j < n; j++) b[p + j] = src[q + j < len ? q + j : 0];
+            break;
+        }
+        }
+    }
+    uint8_t *e = malloc(n ? n : 1); /* exact size: ASan sees any over-read */
+    memcpy(e, b, n);
+    free(b);
+    *out_len = n;
+    return e;
+}
+
+static int check(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_t mt, long *bad) {
+    const uint64_t cap = n / 90 + 1 < mt ? n / 90 + 1 : mt;
+    mh_tx_header *h = malloc(sizeof(mh_tx_header) * (cap ? cap : 1));
+    uint64_t *ao = malloc(8 * (cap ? cap : 1));
+    uint8_t *alh = malloc(32 * (cap ? cap : 1));
+    int32_t *sts = malloc(4 * (cap ? cap : 1));
+    uint64_t n1 = 0, c1 = 0, n2 = 0, c2 = 0;
+    const int r1 = mh_txlog_scan(b, n, me, mk, cap, &n1, &c1, h, ao);
+    const int r2 = orc_txlog_validate(b, n, me, mk, cap, &n2, &c2, alh, sts);
+    const int ok = r1 == r2 && n1 == n2 && c1 == c2;
+    if (!ok && (*bad)++ < 5)
+        fprintf(stderr, "mismatch len %llu: scan (%d, %llu, %llu) oracle (%d, %llu, %llu)\n",
+                (unsigned long long)n, r1, (unsigned long long)n1, (unsigned long long)c1, r2,
+                (unsigned long long)n2, (unsigned long long)c2);
+    free(h); free(ao); free(alh); free(sts);
+    return ok;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) return 2;
+    const long iters = atol(argv[1]);
+    S = strtoull(argv[2], 0, 10);
+    long bad = 0;
+    for (int a = 3; a < argc; a++) {
+        uint64_t len = 0;
+        uint8_t *src = load(argv[a], &len);
+        if (!src) {
+            fprintf(stderr, "cannot read %s\n", argv[a]);
+            return 2;
+        }
+        long agree = 0, accepted = 0;
+        check(src, len, 1024, 1024, 1ull << 40, &bad);
+        /* large logs: fewer mutants (each parse is ~ms) */
+        const long it = len > (4u << 20) ? iters / 50 + 1 : iters;
+        for (long i = 0; i < it; i++) {
+            uint64_t n;
+            uint8_t *m = mutate(src, len, &n);
+            const uint32_t me = (rnd() & 3) ? 1024 : (uint32_t)(rnd() % 40);
+            const uint32_t mk = (rnd() & 3) ? 1024 : (uint32_t)(rnd() % 70);
+            agree += check(m, n, me, mk, 1ull << 40, &bad);
+            uint64_t nt = 0, c = 0;
+            if (mh_txlog_scan(m, n, me, mk, n / 90 + 1, &nt, &c, NULL, NULL) == MH_OK && nt) accepted++;
+            free(m);
+        }
+        printf("%s: %ld mutants, %ld agree, %ld parsed >= 1 record\n", argv[a], it, agree, accepted);
+        free(src);
+    }
+    return bad ? 1 : 0;
+}
