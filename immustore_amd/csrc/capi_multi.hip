@@ -1,4 +1,5 @@
-// capi_multi.hip -- the multi-GPU htree build behind the C ABI.
+// capi_multi.hip -- the multi-GPU htree build and ahtree batch append behind
+// the C ABI.
 //
 // One process drives K devices -- what a cgo caller (one Go process, the
 // commit path of immustore.go:1620-1632) needs -- with one mh_ctx (HIP
@@ -73,7 +74,7 @@ struct mh_multi {
     // gathered with device-to-device copies instead
     bool use_rccl = true;
     struct Dev {
-        DevBuf keys, vals, hv, levels, send, recv, top;
+        DevBuf keys, vals, hv, levels, send, recv, top, dlog;
     };
     std::vector<std::unique_ptr<Dev>> buf;
     std::mutex mu;  // one build at a time per mh_multi
@@ -383,6 +384,143 @@ extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint
         MH_HIP(hipMemcpyAsync(root, d_root, 32, hipMemcpyDeviceToHost, st0));
         for (int d = 0; d < K; d++)
             if (int e = mh_ctx_synchronize(m->ctx[d])) return e;
+        return MH_OK;
+    });
+}
+
+// ============================================================================
+// Sharded ahtree batch append (C3 at scale; ahtree.go:246-373 over K devices).
+// A batch of `total` appends to an EMPTY tree is cut into K ranges of S = 2^k
+// appends (the smallest S with K*S >= total); device d appends (dS, dS + m_d]
+// into its own globally indexed dLog: the leaves, the perfect nodes of levels
+// <= k and every spine node below level k lie inside its range; only the
+// nodes above level k need the other ranges, and they are built from the
+// complete shards' roots, all-gathered once (32 B per device, RCCL).  The
+// phases are the ones mh_dev_ahtree_append_local / put_shard_roots /
+// append_spine expose to torch.distributed ranks.
+// ============================================================================
+namespace {
+
+int ahtree_shard_bits(uint64_t total, int K) {
+    int k = 0;
+    while ((uint64_t)K * (1ull << k) < total) k++;
+    return k;
+}
+
+// phases 2-3 once every device has run phase 1 into dlog[d]: shard roots
+// all-gathered, the nodes above shard level, then each device's spine
+int ahtree_multi_finish(mh_multi *m, uint64_t total, int k, uint8_t *const *dlog,
+                        uint8_t *const *roots_out) {
+    const int K = m->K;
+    const uint64_t S = 1ull << k;
+    std::vector<const uint8_t *> send(K);
+    std::vector<uint8_t *> recv(K);
+    for (int d = 0; d < K; d++) {
+        mh_multi::Dev &B = *m->buf[d];
+        MH_HIP(hipSetDevice(m->dev[d]));
+        const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
+        if (md == S) {
+            send[d] = dlog[d] + 32 * mh_ahtree_node_index(n0 + S, k);
+        } else {  // a short or empty last range has no shard root: zeros, unused
+            MH_HIP(B.send.ensure(32));
+            MH_HIP(hipMemsetAsync(B.send.p, 0, 32, m->ctx[d]->stream));
+            send[d] = B.send.as<uint8_t>();
+        }
+        MH_HIP(B.recv.ensure(32 * (uint64_t)K));
+        recv[d] = B.recv.as<uint8_t>();
+    }
+    if (int st = gather_roots(m, send, recv)) return st;
+    const uint64_t complete = std::min<uint64_t>(total / S, (uint64_t)K);
+    for (int d = 0; d < K; d++) {
+        const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
+        if (!md) continue;
+        if (int st = mh_dev_ahtree_put_shard_roots(m->ctx[d], dlog[d], k, complete, recv[d]))
+            return st;
+        if (int st = mh_dev_ahtree_append_spine(m->ctx[d], dlog[d], n0, md,
+                                                roots_out ? roots_out[d] : nullptr))
+            return st;
+    }
+    return MH_OK;
+}
+
+}  // namespace
+
+extern "C" int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t total,
+                                                const uint8_t *const *payloads, uint32_t plen,
+                                                uint8_t *const *dlog, uint8_t *const *roots_out) {
+    return mh_guard([&]() -> int {
+        if (!m || !dlog || (total && !payloads)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (total == 0) return MH_OK;
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int K = m->K;
+        const int k = ahtree_shard_bits(total, K);
+        const uint64_t S = 1ull << k;
+        for (int d = 0; d < K; d++) {
+            const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
+            if (!md) continue;
+            if (!dlog[d] || (plen && !payloads[d])) return MH_ERR_ILLEGAL_ARGUMENTS;
+            if (int st = mh_dev_ahtree_append_local(m->ctx[d], dlog[d], n0, payloads[d], md, plen,
+                                                    k))
+                return st;
+        }
+        return ahtree_multi_finish(m, total, k, dlog, roots_out);
+    });
+}
+
+extern "C" int mh_multi_ahtree_append_batch(mh_multi *m, const uint8_t *payloads, uint64_t total,
+                                            uint32_t plen, uint8_t *dlog_out, uint8_t root[32]) {
+    return mh_guard([&]() -> int {
+        if (!m || !root || (total && plen && !payloads)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (total == 0) return MH_ERR_UNEXISTENT_DATA;  // RootAt(0) of an empty tree
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int K = m->K;
+        const int k = ahtree_shard_bits(total, K);
+        const uint64_t S = 1ull << k;
+        const uint64_t nd = mh_ahtree_nodes_upto(total);
+        int last = 0;  // device of the last append: its final root is RootAt(total)
+        for (int d = 0; d < K; d++)
+            if ((uint64_t)d * S < total) last = d;
+        std::vector<uint8_t *> dl(K, nullptr), ro(K, nullptr);
+        // 1. payload ranges in, leaves + perfect nodes up to shard level (every
+        //    device from its own thread: each range crosses its own PCIe link)
+        if (int e = per_device(K, [&](int d) -> int {
+                const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
+                if (!md) return MH_OK;
+                mh_multi::Dev &B = *m->buf[d];
+                MH_HIP(hipSetDevice(m->dev[d]));
+                MH_HIP(B.dlog.ensure(nd * 32));
+                MH_HIP(B.vals.ensure(md * plen + 16));
+                if (d == last) MH_HIP(B.hv.ensure(md * 32));
+                dl[d] = B.dlog.as<uint8_t>();
+                if (d == last) ro[d] = B.hv.as<uint8_t>();
+                hipStream_t st = m->ctx[d]->stream;
+                if (plen)
+                    MH_HIP(hipMemcpyAsync(B.vals.p, payloads + n0 * plen, md * plen,
+                                          hipMemcpyHostToDevice, st));
+                return mh_dev_ahtree_append_local(m->ctx[d], dl[d], n0, B.vals.as<uint8_t>(), md,
+                                                  plen, k);
+            }))
+            return e;
+        // 2-3. shard roots exchanged, nodes above shard level, spines
+        if (int st = ahtree_multi_finish(m, total, k, dl.data(), ro.data())) return st;
+        // 4. every device's own dLog range back (ranges tile [0, nodesUpto(total)))
+        if (int e = per_device(K, [&](int d) -> int {
+                const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
+                if (!md) return MH_OK;
+                MH_HIP(hipSetDevice(m->dev[d]));
+                hipStream_t st = m->ctx[d]->stream;
+                if (dlog_out) {
+                    const uint64_t lo = mh_ahtree_node_index(n0 + 1, 0);
+                    const uint64_t hi = mh_ahtree_nodes_upto(n0 + md);
+                    MH_HIP(hipMemcpyAsync(dlog_out + lo * 32, dl[d] + lo * 32, (hi - lo) * 32,
+                                          hipMemcpyDeviceToHost, st));
+                }
+                if (d == last)
+                    MH_HIP(hipMemcpyAsync(root, ro[d] + (md - 1) * 32, 32, hipMemcpyDeviceToHost,
+                                          st));
+                return mh_ctx_synchronize(m->ctx[d]);
+            }))
+            return e;
         return MH_OK;
     });
 }

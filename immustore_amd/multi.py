@@ -73,3 +73,24 @@ class MultiDevice:
         N.check(N.load().mh_multi_dev_htree_build_entries_fixed(
             self.handle, version, n_per_dev, P(*keys), key_len, P(*vals), val_len,
             P(*hvals) if hvals is not None else None, P(*levels), P(*top_levels), P(*roots)))
+
+    def ahtree_append_batch(self, payloads, want_dlog: bool = True):
+        """AppendBatch of the rows of `payloads` (m, plen) to an empty ahtree
+        across the devices -> (dlog (nodesUpto(m), 32) or None, RootAt(m))."""
+        p = np.ascontiguousarray(payloads, np.uint8)
+        m, plen = p.shape
+        L = N.load()
+        dl = np.zeros((max(L.mh_ahtree_nodes_upto(m), 1), 32), np.uint8) if want_dlog else None
+        root = np.zeros(32, np.uint8)
+        N.check(L.mh_multi_ahtree_append_batch(self.handle, _addr(p), m, plen, _addr(dl),
+                                                _addr(root)))
+        return (dl[:L.mh_ahtree_nodes_upto(m)] if want_dlog else None), root.tobytes()
+
+    def dev_ahtree_append_batch(self, total, payloads, plen, dlogs, roots_out=None):
+        """Device pointers per device (sequences of ints; None entries for devices
+        with no appends) -- asynchronous."""
+        K = len(self.devices)
+        P = C.c_void_p * K
+        N.check(N.load().mh_multi_dev_ahtree_append_batch(
+            self.handle, total, P(*payloads), plen, P(*dlogs),
+            P(*roots_out) if roots_out is not None else None))

@@ -585,6 +585,28 @@ int mh_multi_dev_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n_
                                            const uint8_t *const *vals, uint32_t val_len,
                                            uint8_t *const *hvals_out, uint8_t *const *levels,
                                            uint8_t *const *top_levels, uint8_t *const *root);
+/* ahtree AppendBatch of `total` payloads (plen bytes each) to an EMPTY tree
+ * across the K devices (ahtree.go:246-373; BASELINE configs[2] at scale): S =
+ * 2^k is the smallest power of two with K*S >= total and device d appends
+ * (dS, min((d+1)S, total)] -- its leaves, perfect nodes of levels <= k and the
+ * spine nodes below level k all lie inside its own range -- then the complete
+ * shards' roots are all-gathered over RCCL (32 B per device) and every device
+ * builds the nodes above level k from them and finishes its spine (the three
+ * phases of mh_dev_ahtree_append_local / _put_shard_roots / _append_spine).
+ * Device variant: payloads[d] holds device d's appends, dlog[d] is device
+ * memory for mh_ahtree_nodes_upto(total) digests indexed like the global dLog
+ * (device d fills its range [mh_ahtree_node_index(dS + 1, 0),
+ * mh_ahtree_nodes_upto(dS + m_d)) and the nodes above level k), roots_out
+ * (may be NULL, or hold NULL entries) receives device d's m_d roots (RootAt
+ * after each of its appends).  Asynchronous on the devices' context streams.
+ * Host variant: payloads and dlog_out (nodesUpto(total) x 32 bytes, the
+ * tree/NNNNNNNN.sha stream, may be NULL) in host memory, root = RootAt(total);
+ * total == 0 -> MH_ERR_UNEXISTENT_DATA (ahtree.go:727-745). */
+int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t total, const uint8_t *const *payloads,
+                                     uint32_t plen, uint8_t *const *dlog,
+                                     uint8_t *const *roots_out);
+int mh_multi_ahtree_append_batch(mh_multi *m, const uint8_t *payloads, uint64_t total,
+                                 uint32_t plen, uint8_t *dlog_out, uint8_t root[32]);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

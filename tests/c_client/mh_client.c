@@ -3,8 +3,8 @@
  * shim of INTEGRATION.md calls it (no Python, no torch): build an htree over
  * digests (htree.New / BuildWith / Root / InclusionProof + VerifyInclusion),
  * append a batch to an ahtree (Append / RootAt / InclusionProof /
- * ConsistencyProof), and print the results as hex for the test to compare
- * with the oracle.  Input digests / payloads: SHA-256-free deterministic
+ * ConsistencyProof) on one device and across devices (mh_multi_*), and
+ * print the results as hex for the test to compare with the oracle.  Input digests / payloads: SHA-256-free deterministic
  * bytes (x[k] = (k * 131 + 7) & 0xff), so the test can rebuild them.
  *
  * usage: mh_client <width> <appends>
@@ -85,7 +85,33 @@ int main(int argc, char **argv) {
     CHECK(mh_ahtree_consistency_proof(a, m / 2, m, pt, 128, &pn));
     hex("ahtree_cons", pt, pn * 32u);
     printf("empty_root_at %d\n", mh_ahtree_root_at(a, m + 1, at) == MH_ERR_UNEXISTENT_DATA);
+    const uint64_t nd = mh_ahtree_nodes_upto(m);
+    uint8_t *dl1 = malloc(nd * 32), *dl2 = malloc(nd * 32);
+    CHECK(mh_ahtree_dlog(a, 0, nd, dl1));
     CHECK(mh_ahtree_free(a));
+
+    /* multi-GPU ahtree AppendBatch (SURVEY.md 8(e), C3 at scale): device 0 as an
+     * RCCL clique of one, then listed three times; dLog and RootAt(m) must
+     * equal the single-device append above */
+    {
+        const int one[1] = {0}, three[3] = {0, 0, 0};
+        const int *devs[2] = {one, three};
+        const int ndv[2] = {1, 3};
+        for (int v = 0; v < 2; v++) {
+            mh_multi *mm;
+            CHECK(mh_multi_create(ndv[v], devs[v], &mm));
+            uint8_t mr[32];
+            memset(dl2, 0, nd * 32);
+            CHECK(mh_multi_ahtree_append_batch(mm, p, m, 32, dl2, mr));
+            printf("%s %d\n", v ? "multi3_ahtree_root_equal" : "multi1_ahtree_root_equal",
+                   memcmp(mr, r, 32) == 0);
+            printf("%s %d\n", v ? "multi3_ahtree_dlog_equal" : "multi1_ahtree_dlog_equal",
+                   memcmp(dl1, dl2, nd * 32) == 0);
+            CHECK(mh_multi_destroy(mm));
+        }
+    }
+    free(dl1);
+    free(dl2);
 
     /* multi-GPU htree over entries: an RCCL clique over
      * device 0, then device 0 listed three times (three shards, roots

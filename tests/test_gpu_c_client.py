@@ -107,6 +107,9 @@ def test_c_client_matches_oracle(w, m):
     st, cons = t.consistency_proof(m // 2, m)
     assert st == 0 and out["ahtree_cons"] == cons.tobytes().hex()
     assert out["empty_root_at"] == "1"
+    for k in ("multi1_ahtree_root_equal", "multi1_ahtree_dlog_equal", "multi3_ahtree_root_equal",
+              "multi3_ahtree_dlog_equal"):
+        assert out[k] == "1", k
     _check_entries(out, w)
     if m >= 2 * w:
         # mh_multi_htree_build_entries_fixed (RCCL clique of device 0; three shards)

@@ -102,3 +102,82 @@ def test_multi_device_resident_vs_oracle(m, orc, devices, n_per_dev):
         N.check(0)
     finally:
         md.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+def test_multi_ahtree_append_vs_oracle(m, orc, devices):
+    """mh_multi_ahtree_append_batch: the whole dLog (tree/*.sha stream) and
+    RootAt(m) equal the oracle's single AppendBatch (ahtree.go:246-373,
+    :727-771) -- ranges of 2^k appends per device, the shard roots exchanged
+    (RCCL for [0], device copies when the device repeats)."""
+    from immustore_amd import _native as N
+    from immustore_amd.multi import MultiDevice
+    md = MultiDevice(devices)
+    try:
+        for total in (1, 2, 3, 5, 8, 9, 1000, 4096, 70001, (1 << 17) + 5):
+            pay = orc.fill_random(32 * total, total).reshape(total, 32)
+            dl, root = md.ahtree_append_batch(pay)
+            o = orc.AHtree(total)
+            o.append_batch(pay)
+            assert dl.tobytes() == o.dlog_bytes(), (devices, total)
+            assert root == bytes(o.root_at(total)[1]), (devices, total)
+        # other payload sizes (the leaf kernel's per-lane byte path)
+        for plen in (0, 1, 100):
+            pay = orc.fill_random(plen * 777 + 1, plen)[:plen * 777].reshape(777, plen)
+            dl, root = md.ahtree_append_batch(pay)
+            o = orc.AHtree(777)
+            o.append_batch(pay)
+            assert dl.tobytes() == o.dlog_bytes() and root == bytes(o.root_at(777)[1]), plen
+        with pytest.raises(N.MerkleError):
+            md.ahtree_append_batch(np.zeros((0, 32), np.uint8))
+    finally:
+        md.close()
+
+
+@pytest.mark.parametrize("devices,total", [([0], 1 << 14), ([0, 0, 0, 0], 1 << 16),
+                                           ([0, 0, 0, 0], 3 * (1 << 14) + 5)])
+def test_multi_dev_ahtree_append_vs_oracle(m, orc, devices, total):
+    """Device-resident ranges (the configs[2]-at-scale shape): device d fills
+    its range of a globally indexed dLog byte-identically to one device's
+    append; its roots_out are RootAt after each of its appends."""
+    import torch
+    from immustore_amd import _native as N
+    from immustore_amd.multi import MultiDevice
+    L = N.load()
+    K = len(devices)
+    k = 0
+    while K * (1 << k) < total:
+        k += 1
+    S = 1 << k
+    pay = orc.fill_random(32 * total, 5).reshape(total, 32)
+    nd = L.mh_ahtree_nodes_upto(total)
+    o = orc.AHtree(total)
+    o.append_batch(pay)
+    ref = np.frombuffer(o.dlog_bytes(), np.uint8).reshape(-1, 32)
+    md = MultiDevice(devices)
+    try:
+        spans = [(min(d * S, total), min(S, max(total - d * S, 0))) for d in range(K)]
+        dp = [torch.from_numpy(pay[n0:n0 + c].reshape(-1).copy()).cuda() if c else None
+              for n0, c in spans]
+        dl = [torch.empty(nd * 32, dtype=torch.uint8, device="cuda") if c else None
+              for _, c in spans]
+        ro = [torch.empty(c * 32, dtype=torch.uint8, device="cuda") if c else None
+              for _, c in spans]
+        torch.cuda.synchronize()
+        ptr = lambda ts: [t.data_ptr() if t is not None else None for t in ts]  # noqa: E731
+        md.dev_ahtree_append_batch(total, ptr(dp), 32, ptr(dl), ptr(ro))
+        md.synchronize()
+        covered = 0
+        for d, (n0, c) in enumerate(spans):
+            if not c:
+                continue
+            lo, hi = L.mh_ahtree_node_index(n0 + 1, 0), L.mh_ahtree_nodes_upto(n0 + c)
+            got = dl[d].cpu().numpy().reshape(-1, 32)
+            assert np.array_equal(got[lo:hi], ref[lo:hi]), d
+            covered += hi - lo
+            r = ro[d].cpu().numpy().reshape(-1, 32)
+            for j in (0, c // 2, c - 1):
+                assert r[j].tobytes() == bytes(o.root_at(n0 + j + 1)[1]), (d, j)
+        assert covered == nd
+    finally:
+        md.close()
