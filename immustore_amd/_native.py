@@ -278,6 +278,8 @@ SIGNATURES = {
                                                  u8p]),
     "mh_multi_dev_htree_build_entries_fixed": (i32, [vp, i32, u64, vp, u32, vp, u32, vp, vp, vp,
                                                      vp]),
+    "mh_multi_htree_build_entries": (i32, [vp, i32, u64, u8p, vp, u8p, vp, u8p, vp, u8p,
+                                           u8p, u8p, u8p, u8p]),
     "mh_multi_dev_ahtree_append_batch": (i32, [vp, u64, vp, u32, vp, vp]),
     "mh_multi_ahtree_append_batch": (i32, [vp, u8p, u64, u32, u8p, u8p]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,

@@ -74,7 +74,7 @@ struct mh_multi {
     // gathered with device-to-device copies instead
     bool use_rccl = true;
     struct Dev {
-        DevBuf keys, vals, hv, levels, send, recv, top, dlog;
+        DevBuf keys, vals, hv, levels, send, recv, top, dlog, ovr;
     };
     std::vector<std::unique_ptr<Dev>> buf;
     std::mutex mu;  // one build at a time per mh_multi
@@ -276,6 +276,88 @@ extern "C" int mh_multi_dev_htree_build_entries_fixed(
     });
 }
 
+namespace {
+
+// Steps 2-4 of a host-memory multi build once every shard's subtree is built
+// on its device (B.hv, B.levels, B.send = subtree root): all-gather of the
+// subtree roots (devices without a shard send zeros), the top levels over the
+// G roots on device 0 (global levels kS+1 ..), then the results back -- hVals
+// and each shard's slice of every level <= kS from every device's own
+// thread, the top levels and the root from device 0.
+int multi_htree_finish(mh_multi *m, uint64_t n, uint64_t S, uint64_t G, int kS,
+                       uint8_t *hvals_out, uint8_t *levels_out, uint8_t root[32]) {
+    const int K = m->K;
+    LevelGeom gg;
+    gg.init(n);
+    std::vector<const uint8_t *> send(K);
+    std::vector<uint8_t *> recv(K);
+    for (int d = 0; d < K; d++) {
+        mh_multi::Dev &B = *m->buf[d];
+        MH_HIP(hipSetDevice(m->dev[d]));
+        if ((uint64_t)d >= G) {
+            MH_HIP(B.send.ensure(32));
+            MH_HIP(hipMemsetAsync(B.send.p, 0, 32, m->ctx[d]->stream));
+        }
+        MH_HIP(B.recv.ensure(32 * (uint64_t)K));
+        send[d] = B.send.as<uint8_t>();
+        recv[d] = B.recv.as<uint8_t>();
+    }
+    if (int st = gather_roots(m, send, recv)) return st;
+    mh_multi::Dev &B0 = *m->buf[0];
+    MH_HIP(hipSetDevice(m->dev[0]));
+    MH_HIP(B0.top.ensure(mh_htree_levels_len(G) * 32 + 32));
+    uint8_t *d_root = B0.top.as<uint8_t>() + mh_htree_levels_len(G) * 32;
+    if (int e = mh_dev_htree_reduce_nodes(m->ctx[0], recv[0], G, B0.top.as<uint8_t>(), d_root))
+        return e;
+    if (int e = per_device((int)G, [&](int d) -> int {
+            const uint64_t g = (uint64_t)d;
+            mh_multi::Dev &B = *m->buf[d];
+            const uint64_t lo = g * S, ng = std::min(S, n - lo);
+            MH_HIP(hipSetDevice(m->dev[d]));
+            hipStream_t st = m->ctx[d]->stream;
+            if (hvals_out)
+                MH_HIP(hipMemcpyAsync(hvals_out + lo * 32, B.hv.p, ng * 32,
+                                      hipMemcpyDeviceToHost, st));
+            if (levels_out) {
+                // global level l <= kS restricted to this shard = the shard's
+                // level l; above the (short) last shard's own root, that root
+                // is promoted unchanged (htree.go:100-103)
+                LevelGeom lg;
+                lg.init(ng);
+                for (int l = 0; l <= kS && l < gg.nlevels; l++) {
+                    const int ll = std::min(l, lg.nlevels - 1);
+                    MH_HIP(hipMemcpyAsync(levels_out + (gg.off[l] + (lo >> l)) * 32,
+                                          B.levels.as<uint8_t>() + lg.off[ll] * 32,
+                                          (l < lg.nlevels ? lg.width[l] : 1) * 32,
+                                          hipMemcpyDeviceToHost, st));
+                }
+            }
+            return MH_OK;
+        }))
+        return e;
+    hipStream_t st0 = m->ctx[0]->stream;
+    if (levels_out && G > 1) {
+        LevelGeom tg;
+        tg.init(G);
+        for (int j = 1; j < tg.nlevels; j++)
+            MH_HIP(hipMemcpyAsync(levels_out + gg.off[kS + j] * 32,
+                                  B0.top.as<uint8_t>() + tg.off[j] * 32, tg.width[j] * 32,
+                                  hipMemcpyDeviceToHost, st0));
+    }
+    MH_HIP(hipMemcpyAsync(root, d_root, 32, hipMemcpyDeviceToHost, st0));
+    for (int d = 0; d < K; d++)
+        if (int e = mh_ctx_synchronize(m->ctx[d])) return e;
+    return MH_OK;
+}
+
+int log2_exact(uint64_t S) {
+    int k = 0;
+    while ((1ull << k) < S) k++;
+    return k;
+}
+
+}  // namespace
+
 extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n,
                                                   const uint8_t *keys, uint32_t key_len,
                                                   const uint8_t *vals, uint32_t val_len,
@@ -289,13 +371,8 @@ extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint
             return MH_OK;
         }
         std::lock_guard<std::mutex> lk(m->mu);
-        const int K = m->K;
         uint64_t S = 0, G = 0;
-        mh_multi_shard_plan(n, K, &S, &G);
-        int kS = 0;
-        while ((1ull << kS) < S) kS++;
-        LevelGeom gg;
-        gg.init(n);
+        mh_multi_shard_plan(n, m->K, &S, &G);
         // 1. shards in, subtree per device (host copies on each device's stream,
         //    every device from its own thread)
         if (int e = per_device((int)G, [&](int d) -> int {
@@ -322,69 +399,85 @@ extern "C" int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint
                                                         B.send.as<uint8_t>());
             }))
             return e;
-        // 2. all-gather of the subtree roots (devices without a shard send zeros)
-        std::vector<const uint8_t *> send(K);
-        std::vector<uint8_t *> recv(K);
-        for (int d = 0; d < K; d++) {
-            mh_multi::Dev &B = *m->buf[d];
-            MH_HIP(hipSetDevice(m->dev[d]));
-            if ((uint64_t)d >= G) {
-                MH_HIP(B.send.ensure(32));
-                MH_HIP(hipMemsetAsync(B.send.p, 0, 32, m->ctx[d]->stream));
-            }
-            MH_HIP(B.recv.ensure(32 * (uint64_t)K));
-            send[d] = B.send.as<uint8_t>();
-            recv[d] = B.recv.as<uint8_t>();
+        return multi_htree_finish(m, n, S, G, log2_exact(S), hvals_out, levels_out, root);
+    });
+}
+
+extern "C" int mh_multi_htree_build_entries(mh_multi *m, int version, uint64_t n,
+                                            const uint8_t *keys, const uint64_t *key_off,
+                                            const uint8_t *md, const uint64_t *md_off,
+                                            const uint8_t *vals, const uint64_t *val_off,
+                                            const uint8_t *hval_override,
+                                            const uint8_t *use_override, uint8_t *hvals_out,
+                                            uint8_t *levels_out, uint8_t root[32]) {
+    return mh_guard([&]() -> int {
+        if (!m || (version != 0 && version != 1) || !root) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((hval_override == nullptr) != (use_override == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((md == nullptr) != (md_off == nullptr)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) {
+            memcpy(root, kEmptyRoot, 32);  // htree.go:73-77
+            return MH_OK;
         }
-        if (int st = gather_roots(m, send, recv)) return st;
-        // 3. top levels over the G shard roots on device 0 (global levels kS+1 ..)
-        mh_multi::Dev &B0 = *m->buf[0];
-        MH_HIP(hipSetDevice(m->dev[0]));
-        MH_HIP(B0.top.ensure(mh_htree_levels_len(G) * 32 + 32));
-        uint8_t *d_root = B0.top.as<uint8_t>() + mh_htree_levels_len(G) * 32;
-        if (int e = mh_dev_htree_reduce_nodes(m->ctx[0], recv[0], G, B0.top.as<uint8_t>(), d_root))
-            return e;
-        // 4. results back: hVals and each shard's slice of every level <= kS
-        //    (every device from its own thread), then the top levels and the root
+        if (!key_off || !val_off || !keys || !vals) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(key_off, n) || !monotonic(val_off, n) || (md_off && !monotonic(md_off, n)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (version == 0 && md_off && md_off[n] != md_off[0])
+            return MH_ERR_METADATA_UNSUPPORTED;  // tx.go:691-693
+        std::lock_guard<std::mutex> lk(m->mu);
+        uint64_t S = 0, G = 0;
+        mh_multi_shard_plan(n, m->K, &S, &G);
+        // 1. each shard's CSR slices in (bytes [off[lo], off[hi]) and the
+        //    offsets [lo, hi] unchanged, read through base pointers shifted by
+        //    off[lo]), subtree per device, every device from its own thread
         if (int e = per_device((int)G, [&](int d) -> int {
                 const uint64_t g = (uint64_t)d;
                 mh_multi::Dev &B = *m->buf[d];
-                const uint64_t lo = g * S, ng = std::min(S, n - lo);
+                const uint64_t lo = g * S, ng = std::min(S, n - lo), hi = lo + ng;
+                const uint64_t kb = key_off[hi] - key_off[lo], vb = val_off[hi] - val_off[lo];
+                // v0 never has metadata (checked above): no md arrays for it
+                const bool use_md = md_off && version == 1;
+                const uint64_t mb = use_md ? md_off[hi] - md_off[lo] : 0;
+                const uint64_t offb = (ng + 1) * 8;
+                auto pad8 = [](uint64_t x) { return (x + 16 + 7) & ~7ull; };
                 MH_HIP(hipSetDevice(m->dev[d]));
+                // keys | key offsets | md | md offsets  in B.keys; vals | val offsets in B.vals
+                MH_HIP(B.keys.ensure(pad8(kb) + offb + (use_md ? pad8(mb) + offb : 0)));
+                MH_HIP(B.vals.ensure(pad8(vb) + offb));
+                MH_HIP(B.hv.ensure(ng * 32));
+                MH_HIP(B.levels.ensure(mh_htree_levels_len(ng) * 32));
+                MH_HIP(B.send.ensure(32));
+                if (hval_override) MH_HIP(B.ovr.ensure(ng * 33 + 16));
                 hipStream_t st = m->ctx[d]->stream;
-                if (hvals_out)
-                    MH_HIP(hipMemcpyAsync(hvals_out + lo * 32, B.hv.p, ng * 32,
-                                          hipMemcpyDeviceToHost, st));
-                if (levels_out) {
-                    // global level l <= kS restricted to this shard = the shard's
-                    // level l; above the (short) last shard's own root, that root
-                    // is promoted unchanged (htree.go:100-103)
-                    LevelGeom lg;
-                    lg.init(ng);
-                    for (int l = 0; l <= kS && l < gg.nlevels; l++) {
-                        const int ll = std::min(l, lg.nlevels - 1);
-                        MH_HIP(hipMemcpyAsync(levels_out + (gg.off[l] + (lo >> l)) * 32,
-                                              B.levels.as<uint8_t>() + lg.off[ll] * 32,
-                                              (l < lg.nlevels ? lg.width[l] : 1) * 32,
-                                              hipMemcpyDeviceToHost, st));
-                    }
+                uint8_t *kd = B.keys.as<uint8_t>();
+                uint64_t *kod = reinterpret_cast<uint64_t *>(kd + pad8(kb));
+                uint8_t *mdd = reinterpret_cast<uint8_t *>(kod + ng + 1);
+                uint64_t *mod = reinterpret_cast<uint64_t *>(mdd + pad8(mb));
+                uint8_t *vd = B.vals.as<uint8_t>();
+                uint64_t *vod = reinterpret_cast<uint64_t *>(vd + pad8(vb));
+                if (kb) MH_HIP(hipMemcpyAsync(kd, keys + key_off[lo], kb, hipMemcpyHostToDevice, st));
+                MH_HIP(hipMemcpyAsync(kod, key_off + lo, offb, hipMemcpyHostToDevice, st));
+                if (vb) MH_HIP(hipMemcpyAsync(vd, vals + val_off[lo], vb, hipMemcpyHostToDevice, st));
+                MH_HIP(hipMemcpyAsync(vod, val_off + lo, offb, hipMemcpyHostToDevice, st));
+                if (use_md) {
+                    if (mb) MH_HIP(hipMemcpyAsync(mdd, md + md_off[lo], mb, hipMemcpyHostToDevice, st));
+                    MH_HIP(hipMemcpyAsync(mod, md_off + lo, offb, hipMemcpyHostToDevice, st));
                 }
-                return MH_OK;
+                uint8_t *ovd = nullptr, *used = nullptr;
+                if (hval_override) {
+                    ovd = B.ovr.as<uint8_t>();
+                    used = ovd + ng * 32;
+                    MH_HIP(hipMemcpyAsync(ovd, hval_override + lo * 32, ng * 32,
+                                          hipMemcpyHostToDevice, st));
+                    MH_HIP(hipMemcpyAsync(used, use_override + lo, ng, hipMemcpyHostToDevice, st));
+                }
+                return mh_dev_htree_build_entries(
+                    m->ctx[d], version, ng, kd - key_off[lo], kod,
+                    use_md ? mdd - md_off[lo] : nullptr, use_md ? mod : nullptr, vd - val_off[lo],
+                    vod, ovd, used, B.hv.as<uint8_t>(), B.levels.as<uint8_t>(),
+                    B.send.as<uint8_t>());
             }))
             return e;
-        hipStream_t st0 = m->ctx[0]->stream;
-        if (levels_out && G > 1) {
-            LevelGeom tg;
-            tg.init(G);
-            for (int j = 1; j < tg.nlevels; j++)
-                MH_HIP(hipMemcpyAsync(levels_out + gg.off[kS + j] * 32,
-                                      B0.top.as<uint8_t>() + tg.off[j] * 32, tg.width[j] * 32,
-                                      hipMemcpyDeviceToHost, st0));
-        }
-        MH_HIP(hipMemcpyAsync(root, d_root, 32, hipMemcpyDeviceToHost, st0));
-        for (int d = 0; d < K; d++)
-            if (int e = mh_ctx_synchronize(m->ctx[d])) return e;
-        return MH_OK;
+        return multi_htree_finish(m, n, S, G, log2_exact(S), hvals_out, levels_out, root);
     });
 }
 

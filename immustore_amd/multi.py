@@ -94,3 +94,23 @@ class MultiDevice:
         N.check(N.load().mh_multi_dev_ahtree_append_batch(
             self.handle, total, P(*payloads), plen, P(*dlogs),
             P(*roots_out) if roots_out is not None else None))
+
+    def build_entries(self, version, kb, ko, mb, mo, vb, vo, ov=None, use=None,
+                      want_levels: bool = True):
+        """CSR host arrays (as mh_htree_build_entries; mb/mo and ov/use may be
+        None) -> (hvals, levels, root)."""
+        n = len(ko) - 1
+        ko = np.ascontiguousarray(ko, np.uint64)
+        vo = np.ascontiguousarray(vo, np.uint64)
+        mo = None if mo is None else np.ascontiguousarray(mo, np.uint64)
+        kb, vb = np.ascontiguousarray(kb, np.uint8), np.ascontiguousarray(vb, np.uint8)
+        mb = None if mb is None else np.ascontiguousarray(mb, np.uint8)
+        ov = None if ov is None else np.ascontiguousarray(ov, np.uint8)
+        use = None if use is None else np.ascontiguousarray(use, np.uint8)
+        hv = np.zeros((max(n, 1), 32), np.uint8)
+        lv = np.zeros((max(levels_len(n), 1), 32), np.uint8) if want_levels else None
+        root = np.zeros(32, np.uint8)
+        N.check(N.load().mh_multi_htree_build_entries(
+            self.handle, version, n, _addr(kb), _addr(ko), _addr(mb), _addr(mo), _addr(vb),
+            _addr(vo), _addr(ov), _addr(use), _addr(hv), _addr(lv), _addr(root)))
+        return hv[:n], (lv[:levels_len(n)] if want_levels else None), root.tobytes()

@@ -572,6 +572,15 @@ int mh_multi_shard_plan(uint64_t n, int ndev, uint64_t *shard, uint64_t *nshards
 int mh_multi_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n, const uint8_t *keys,
                                        uint32_t key_len, const uint8_t *vals, uint32_t val_len,
                                        uint8_t *hvals_out, uint8_t *levels_out, uint8_t root[32]);
+/* The general (CSR) form of the same build (mh_htree_build_entries' inputs:
+ * ragged keys / KV metadata / values, IsValueTruncated overrides), host
+ * memory in and out: each shard's byte ranges and offsets go to its device. */
+int mh_multi_htree_build_entries(mh_multi *m, int version, uint64_t n, const uint8_t *keys,
+                                 const uint64_t *key_off, const uint8_t *md,
+                                 const uint64_t *md_off, const uint8_t *vals,
+                                 const uint64_t *val_off, const uint8_t *hval_override,
+                                 const uint8_t *use_override, uint8_t *hvals_out,
+                                 uint8_t *levels_out, uint8_t root[32]);
 /* Device-resident variant (BASELINE configs[3]): device d holds entries
  * [d n_per_dev, (d+1) n_per_dev) of a K * n_per_dev-entry tree (n_per_dev a
  * power of two when K > 1) in keys[d] / vals[d]; it writes its subtree's levels

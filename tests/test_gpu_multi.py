@@ -181,3 +181,52 @@ def test_multi_dev_ahtree_append_vs_oracle(m, orc, devices, total):
         assert covered == nd
     finally:
         md.close()
+
+
+def _ragged(orc, n, seed, md=True):
+    rng = np.random.default_rng(seed)
+    out = []
+    for lo, hi in ((8, 64), (0, 11), (0, 3000)):
+        ln = rng.integers(lo, hi + 1, n).astype(np.uint64)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum(ln, out=off[1:])
+        off += np.uint64(rng.integers(0, 5))  # offsets need not start at 0
+        out.append((orc.fill_random(int(off[-1]) + 16, seed + len(out)), off))
+    (kb, ko), (mb, mo), (vb, vo) = out
+    return kb, ko, (mb if md else None), (mo if md else None), vb, vo
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+def test_multi_ragged_build_vs_oracle(m, orc, devices):
+    """mh_multi_htree_build_entries: ragged CSR entries (key 8-64 B, KV
+    metadata 0-11 B, value 0-3000 B, offsets not starting at 0), some with
+    IsValueTruncated overrides, v1 and v0, sharded over the devices: hVals,
+    every level and the root equal the oracle's single build (immustore.go:
+    1620-1630, tx.go:332-355, htree.go:68-113)."""
+    from immustore_amd import _native as N
+    from immustore_amd.multi import MultiDevice
+    md = MultiDevice(devices)
+    try:
+        for n in (1, 2, 3, 1000, 20001):
+            kb, ko, mb, mo, vb, vo = _ragged(orc, n, n)
+            rng = np.random.default_rng(n)
+            ov = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+            use = (rng.random(n) < 0.2).astype(np.uint8)
+            for version, mdd, ovv in ((1, True, False), (1, True, True), (0, False, True)):
+                args = (kb, ko, mb if mdd else None, mo if mdd else None, vb, vo)
+                hv, lv, root = md.build_entries(version, *args, ov=ov if ovv else None,
+                                                use=use if ovv else None)
+                st, ohv, olv, oroot = orc.build_entries_csr(version, *args,
+                                                            ov=ov if ovv else None,
+                                                            use=use if ovv else None)
+                assert st == 0
+                assert root == oroot, (devices, n, version)
+                assert np.array_equal(lv, olv) and np.array_equal(hv, ohv), (devices, n, version)
+        # v0 with KV metadata: ErrMetadataUnsupported (tx.go:691-693)
+        kb, ko, mb, mo, vb, vo = _ragged(orc, 100, 3)
+        with pytest.raises(N.MerkleError):
+            md.build_entries(0, kb, ko, mb, mo, vb, vo)
+        _, _, root = md.build_entries(1, kb, ko[:1], None, None, vb, vo[:1])
+        assert root == orc.sha256(b"")
+    finally:
+        md.close()
