@@ -10,17 +10,22 @@
 // full batch), packs it into one pinned arena, runs one mh_precommit_batch
 // over the commit pipe (value hashes, entry digests, one htree per tx -- all
 // on the device) and hands each committer its own hVals, Eh and status.
+// Two workers, each with its own pipe (HIP streams) and arenas, take turns:
+// while one batch is packed, hashed and scattered, the other worker gathers
+// the next one, so the host work of one batch runs under the device work of
+// the other (MH_QUEUE_WORKERS = 1..8 overrides the count).
 //
 // Lock order: q->mu is never held while the device works.
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
+#include <memory>
 
 #include "capi_internal.hpp"
 
 struct mh_commit_queue {
     mh_ctx *ctx = nullptr;
-    mh_commit_pipe *pipe = nullptr;
     int version = 1;
     uint64_t max_width = 0;
     uint32_t max_txs = 64;
@@ -38,9 +43,13 @@ struct mh_commit_queue {
     std::condition_variable cv_work, cv_done;
     std::deque<Req *> pending;
     bool stop = false;
-    std::thread worker;
-    // packing arenas (pinned: the pipe's copies are then DMA)
-    PinBuf in, out;
+    bool gathering = false;  // one worker at a time collects the next batch
+    struct Worker {
+        mh_commit_pipe *pipe = nullptr;
+        PinBuf in, out;  // packing arenas (pinned: the pipe's copies are then DMA)
+        std::thread th;
+    };
+    std::vector<std::unique_ptr<Worker>> workers;
     // counters (mh_commit_queue_stats)
     uint64_t batches = 0, txs = 0;
 };
@@ -48,7 +57,8 @@ struct mh_commit_queue {
 namespace {
 
 // One batch: pack, hash on the device, scatter.
-int run_batch(mh_commit_queue *q, std::vector<mh_commit_queue::Req *> &B) {
+int run_batch(mh_commit_queue *q, mh_commit_queue::Worker &W,
+              std::vector<mh_commit_queue::Req *> &B) {
     const uint64_t nt = B.size();
     uint64_t ne = 0, kb = 0, mb = 0, vb = 0;
     bool any_md = false, any_ov = false;
@@ -69,9 +79,9 @@ int run_batch(mh_commit_queue *q, std::vector<mh_commit_queue::Req *> &B) {
                    b_ov = L.add(any_ov ? ne * 32 : 0), b_use = L.add(any_ov ? ne : 0);
     Layout O;
     const uint64_t o_hv = O.add(ne * 32), o_eh = O.add(nt * 32), o_st = O.add(nt * 4);
-    MH_HIP(q->in.ensure(L.total));
-    MH_HIP(q->out.ensure(O.total));
-    uint8_t *in = q->in.as<uint8_t>(), *out = q->out.as<uint8_t>();
+    MH_HIP(W.in.ensure(L.total));
+    MH_HIP(W.out.ensure(O.total));
+    uint8_t *in = W.in.as<uint8_t>(), *out = W.out.as<uint8_t>();
     uint64_t *tx_off = (uint64_t *)(in + b_tx), *ko = (uint64_t *)(in + b_ko),
              *mo = any_md ? (uint64_t *)(in + b_mo) : nullptr, *vo = (uint64_t *)(in + b_vo);
     uint64_t e = 0, kp = 0, mp = 0, vp = 0;
@@ -104,7 +114,7 @@ int run_batch(mh_commit_queue *q, std::vector<mh_commit_queue::Req *> &B) {
         tx_off[t + 1] = e;
     }
     int32_t *st = (int32_t *)(out + o_st);
-    int rc = mh_precommit_batch(q->pipe, q->version, q->max_width, nt, tx_off, in + b_k, ko,
+    int rc = mh_precommit_batch(W.pipe, q->version, q->max_width, nt, tx_off, in + b_k, ko,
                                 any_md ? in + b_m : nullptr, mo, in + b_v, vo,
                                 any_ov ? in + b_ov : nullptr, any_ov ? in + b_use : nullptr,
                                 nullptr, out + o_hv, out + o_eh, st);
@@ -124,14 +134,18 @@ int run_batch(mh_commit_queue *q, std::vector<mh_commit_queue::Req *> &B) {
     return MH_OK;
 }
 
-void worker_loop(mh_commit_queue *q) {
+void worker_loop(mh_commit_queue *q, mh_commit_queue::Worker *W) {
     hipSetDevice(q->ctx->device);
     std::vector<mh_commit_queue::Req *> B;
     for (;;) {
         std::unique_lock<std::mutex> lk(q->mu);
-        q->cv_work.wait(lk, [&] { return q->stop || !q->pending.empty(); });
-        if (q->pending.empty()) break;  // stop requested, nothing left
+        q->cv_work.wait(lk, [&] { return q->stop || (!q->gathering && !q->pending.empty()); });
+        if (q->pending.empty()) {
+            if (q->stop) break;  // stop requested, nothing left
+            continue;
+        }
         // gather: until the window closes or a full batch is waiting
+        q->gathering = true;
         const auto deadline =
             std::chrono::steady_clock::now() + std::chrono::microseconds(q->wait_us);
         while (!q->stop && q->pending.size() < q->max_txs) {
@@ -142,10 +156,12 @@ void worker_loop(mh_commit_queue *q) {
             B.push_back(q->pending.front());
             q->pending.pop_front();
         }
+        q->gathering = false;
         lk.unlock();
+        q->cv_work.notify_all();  // another worker may gather the next batch now
         int rc = MH_ERR_ILLEGAL_STATE;
         try {
-            rc = run_batch(q, B);
+            rc = run_batch(q, *W, B);
         } catch (const std::bad_alloc &) {
             rc = MH_ERR_OUT_OF_MEMORY;
         } catch (...) {
@@ -163,6 +179,14 @@ void worker_loop(mh_commit_queue *q) {
     }
 }
 
+int queue_workers() {
+    if (const char *e = getenv("MH_QUEUE_WORKERS")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 8) return v;
+    }
+    return 2;
+}
+
 }  // namespace
 
 extern "C" int mh_commit_queue_new(mh_ctx *c, int version, uint64_t max_width, uint32_t max_txs,
@@ -177,12 +201,18 @@ extern "C" int mh_commit_queue_new(mh_ctx *c, int version, uint64_t max_width, u
         q->max_width = max_width;
         q->max_txs = max_txs ? max_txs : 64;
         q->wait_us = wait_us;
-        int st = mh_commit_pipe_new(c, 0, &q->pipe);
-        if (st != MH_OK) {
-            delete q;
-            return st;
+        const int nw = queue_workers();
+        for (int k = 0; k < nw; k++) {
+            q->workers.emplace_back(new mh_commit_queue::Worker());
+            int st = mh_commit_pipe_new(c, 0, &q->workers.back()->pipe);
+            if (st != MH_OK) {
+                for (auto &w : q->workers)
+                    if (w->pipe) mh_commit_pipe_free(w->pipe);
+                delete q;
+                return st;
+            }
         }
-        q->worker = std::thread(worker_loop, q);
+        for (auto &w : q->workers) w->th = std::thread(worker_loop, q, w.get());
         *out = q;
         return MH_OK;
     });
@@ -196,8 +226,9 @@ extern "C" int mh_commit_queue_free(mh_commit_queue *q) {
             q->stop = true;
         }
         q->cv_work.notify_all();
-        if (q->worker.joinable()) q->worker.join();  // drains what is pending first
-        mh_commit_pipe_free(q->pipe);
+        for (auto &w : q->workers)
+            if (w->th.joinable()) w->th.join();  // the workers drain what is pending first
+        for (auto &w : q->workers) mh_commit_pipe_free(w->pipe);
         delete q;
         return MH_OK;
     });
@@ -236,7 +267,8 @@ extern "C" int mh_commit_queue_submit(mh_commit_queue *q, uint64_t n, const uint
         std::unique_lock<std::mutex> lk(q->mu);
         if (q->stop) return MH_ERR_ILLEGAL_STATE;
         q->pending.push_back(&r);
-        q->cv_work.notify_one();
+        // all: the worker gathering a batch must see it, not only an idle one
+        q->cv_work.notify_all();
         q->cv_done.wait(lk, [&] { return r.done; });
         return r.status;
     });
