@@ -250,6 +250,9 @@ SIGNATURES = {
     "mh_ahtree_proof_batch": (i32, [vp, i32, u64, vp, vp, u8p, u32, vp, vp]),
     "mh_dev_ahtree_proof_batch": (i32, [vp, i32, u8p, u64, u64, vp, vp, u8p, u32, vp, vp]),
     "mh_ahtree_node_index": (u64, [u64, i32]),
+    "mh_ahtree_log_header": (i32, [u64, C.c_int64, i32, i32, u8p, u64, C.POINTER(u64)]),
+    "mh_appendable_metadata": (i32, [u32, vp, vp, vp, u8p, u64, C.POINTER(u64)]),
+    "mh_multiapp_segments": (i32, [u64, u64, u64, u64, vp, u32, C.POINTER(u32)]),
     "mh_dev_ahtree_append_local": (i32, [vp, u8p, u64, u8p, u64, u32, i32]),
     "mh_dev_ahtree_put_shard_roots": (i32, [vp, u8p, i32, u64, u8p]),
     "mh_dev_ahtree_append_spine": (i32, [vp, u8p, u64, u64, u8p]),

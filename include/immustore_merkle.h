@@ -273,6 +273,30 @@ int mh_dev_ahtree_append_batch_logs(mh_ctx *ctx, uint8_t *dlog, uint64_t n0,
 int mh_dev_ahtree_log_records(mh_ctx *ctx, const uint8_t *payloads, uint64_t m, uint32_t plen,
                               uint64_t p_off0, uint8_t *plog, uint8_t *clog);
 uint64_t mh_ahtree_nodes_upto(uint64_t n); /* ahtree.go:492-511 */
+/* The appendable framing around those streams, host
+ * code.  An ahtree's data/ tree/ commit/ logs are multiapps
+ * (ahtree.go:106-140): file id holds logical bytes [id*file_size,
+ * (id+1)*file_size) (multi_app.go:208-214, named "%08d.<dat|sha|di>") behind
+ * a singleapp header BE32 len(m) || m (single_app.go:116-171), m =
+ * appendable.Metadata.Bytes() (metadata.go:33-80) of { COMPRESSION_FORMAT,
+ * COMPRESSION_LEVEL, PREALLOC_SIZE (omitted when prealloc_size < 0, as in
+ * files written before it existed), WRAPPED_METADATA = { FILE_SIZE,
+ * WRAPPED_METADATA = { VERSION: 1 } } }; Go writes each level's entries in
+ * map order, any order reads back the same -- here in the order shown.
+ * *len = the header size; MH_ERR_BUFFER_TOO_SMALL when out is NULL or cap is
+ * below it. */
+int mh_ahtree_log_header(uint64_t file_size, int64_t prealloc_size, int32_t compression_format,
+                         int32_t compression_level, uint8_t *out, uint64_t cap, uint64_t *len);
+/* appendable.Metadata.Bytes() of n (key, value) pairs in the given order. */
+int mh_appendable_metadata(uint32_t n, const char *const *keys, const uint8_t *const *vals,
+                           const uint64_t *val_len, uint8_t *out, uint64_t cap, uint64_t *len);
+/* Logical log bytes [off, off+n) split at file boundaries: segment k =
+ * seg[4k .. 4k+3] = (file id, byte position in that file = header_len + off
+ * within the file, offset in the source range, length).  *nseg = the count
+ * (seg may be NULL to ask for it); MH_ERR_BUFFER_TOO_SMALL if cap < *nseg. */
+int mh_multiapp_segments(uint64_t off, uint64_t n, uint64_t file_size, uint64_t header_len,
+                         uint64_t *seg, uint32_t cap, uint32_t *nseg);
+
 /* dLog index of node(n, level) = nodesUntil(n) + level (ahtree.go:460-462). */
 uint64_t mh_ahtree_node_index(uint64_t n, int level);
 

@@ -270,6 +270,15 @@ def read_appendable(path):
     return b[4 + ml:]
 
 
+def appendable_header(path):
+    """The singleapp header bytes of a Go-written appendable file (BE32 len ||
+    appendable.Metadata bytes, single_app.go:116-171) -- data, kept to pin
+    the header writer."""
+    b = open(path, "rb").read()
+    ml = struct.unpack(">I", b[:4])[0]
+    return b[:4 + ml]
+
+
 def parse_txlog(raw):
     """tx record layout: embedded/store/immustore.go:1812-1924."""
     txs, p = [], 0
@@ -401,7 +410,10 @@ def fixture_store(root):
                        for k in range(a0 + 1, a1)]
                 c["lap"] = {"terms": lt, "incl": ips}
             dual1.append(c)
-    return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(),
+    headers = {rel: appendable_header(os.path.join(root, rel)).hex()
+               for rel in ("aht/data/00000000.dat", "aht/tree/00000000.sha",
+                           "aht/commit/00000000.di")}
+    return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(), "app_headers": headers,
         "aht_plog": pl.hex(), "aht_clog": clog.hex(), "n_values": sum(
         1 for t in txs for e in t["entries"] if "value" in e), "txlog": raw.hex(),
         "dual_v2": dual, "linear": linear, "dual_v1": dual1}
