@@ -314,6 +314,40 @@ def test_entries_long_metadata_vs_oracle(m, ctx, orc):
         assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
 
 
+def test_entries_max_sizes_vs_oracle(m, ctx, orc):
+    """The reference's limits (options.go:37-39: MaxKeyLen 1024, MaxValueLen
+    4096; KV metadata <= 11 bytes, kv_metadata.go) and the block boundaries of
+    the digest message around them (v1: 4 + ml + kl + 32 bytes, v0: kl + 32):
+    keys of 0..1024 bytes at every class edge, next to empty and 4096-byte
+    values, v1 and v0, some IsValueTruncated."""
+    rng = np.random.default_rng(77)
+    kls = [0, 1, 7, 8, 19, 20, 23, 24, 55, 56, 63, 64, 87, 88, 119, 120, 500, 1000, 1015, 1016,
+           1023, 1024]
+    vls = [0, 1, 55, 56, 63, 64, 119, 120, 4031, 4032, 4095, 4096]
+    keys, mds, vals = [], [], []
+    for kl in kls:
+        for vl in vls:
+            keys.append(rng.integers(0, 256, kl, dtype=np.uint8).tobytes())
+            mds.append(rng.integers(0, 256, int(rng.choice([0, 1, 9, 11])), dtype=np.uint8).tobytes())
+            vals.append(rng.integers(0, 256, vl, dtype=np.uint8).tobytes())
+    eh, hv, lv = m.build_hash_tree(1, keys, vals, mds, ctx=ctx)
+    st, ohv, olv, oroot = orc.build_entries(1, keys, mds, vals)
+    assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
+    eh, hv, lv = m.build_hash_tree(0, keys, vals, ctx=ctx)
+    st, ohv, olv, oroot = orc.build_entries(0, keys, [b""] * len(keys), vals)
+    assert st == 0 and eh == oroot and np.array_equal(lv, olv)
+    ov = [H(v) if k % 3 == 0 else None for k, v in enumerate(vals)]
+    vals2 = [b"" if o is not None else v for o, v in zip(ov, vals)]
+    eh, hv, lv = m.build_hash_tree(1, keys, vals2, mds, hval_overrides=ov, ctx=ctx)
+    st, ohv, olv, oroot = orc.build_entries(1, keys, mds, vals)
+    assert st == 0 and eh == oroot and np.array_equal(hv, ohv)
+    # 64 copies: past the 16384 entries where the length-class sort starts
+    K, M, V = keys * 64, mds * 64, vals * 64
+    eh, hv, lv = m.build_hash_tree(1, K, V, M, ctx=ctx)
+    st, ohv, olv, oroot = orc.build_entries(1, K, M, V)
+    assert st == 0 and eh == oroot and np.array_equal(hv, ohv) and np.array_equal(lv, olv)
+
+
 def test_go_fixtures_alh_chain_on_gpu(m, ctx, orc, fixtures):
     """Eh computed on the GPU -> innerHash/Alh (oracle) == Alh stored by Go."""
     for name, fx in fixtures.items():
