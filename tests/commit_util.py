@@ -59,13 +59,14 @@ def fixture_batch(fx, truncate_every=0):
 
 
 def random_batch(rng, ntx, version=1, max_entries=40, vlens=(0, 1, 55, 56, 64, 100, 1024, 3000),
-                 md_prob=0.2, trunc_prob=0.1, empty_prob=0.05):
+                 md_prob=0.2, trunc_prob=0.1, empty_prob=0.05, klens=None):
     txs = []
     for _ in range(ntx):
         n = 0 if rng.random() < empty_prob else int(rng.integers(1, max_entries + 1))
         es = []
         for _ in range(n):
-            key = rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8).tobytes()
+            kl = int(rng.choice(klens)) if klens is not None else int(rng.integers(1, 64))
+            key = rng.integers(0, 256, kl, dtype=np.uint8).tobytes()
             md = b""
             if version == 1 and rng.random() < md_prob:
                 md = rng.integers(0, 256, int(rng.integers(1, 12)), dtype=np.uint8).tobytes()

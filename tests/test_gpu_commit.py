@@ -65,7 +65,7 @@ def test_precommit_random_vs_oracle(m, ctx, orc, version, chunk):
         p.close()
 
 
-@pytest.mark.parametrize("max_entries", [64, 65, 300])
+@pytest.mark.parametrize("max_entries", [64, 65, 300, 1024])
 def test_precommit_tree_paths_vs_oracle(m, ctx, orc, max_entries):
     """Chunks whose widest tx has <= 64 entries get one-lane-per-tree roots,
     wider ones the host tree plan (both within one batch when chunks differ)."""
@@ -80,6 +80,25 @@ def test_precommit_tree_paths_vs_oracle(m, ctx, orc, max_entries):
             p.close()
         assert np.array_equal(st, st_o) and np.array_equal(eh, eh_o)
         assert np.array_equal(hv, hv_o)
+
+
+def test_precommit_max_sizes_vs_oracle(m, ctx, orc):
+    """The reference's limits (options.go:35-39): MaxTxEntries 1024 entries in
+    one tx, keys up to MaxKeyLen 1024 and values up to MaxValueLen 4096 bytes,
+    KV metadata up to 11 bytes, truncated values among them."""
+    rng = np.random.default_rng(1024)
+    b = random_batch(rng, 24, version=1, max_entries=1024, md_prob=0.5, trunc_prob=0.2,
+                     vlens=(0, 1, 63, 64, 4031, 4032, 4095, 4096),
+                     klens=(1, 55, 56, 119, 120, 1000, 1023, 1024))
+    hv_o, eh_o, st_o = orc.precommit_batch(1, **b)
+    assert (st_o == 0).all()
+    p = m.CommitPipe(ctx)
+    try:
+        hv, eh, st = p.precommit_csr(1, **b)
+        assert np.array_equal(st, st_o) and np.array_equal(eh, eh_o)
+        assert np.array_equal(hv, hv_o)
+    finally:
+        p.close()
 
 
 def test_precommit_statuses_vs_oracle(m, ctx, orc):

@@ -166,7 +166,7 @@ def test_txlog_validate_message_lengths(m, ctx, orc):
     assert np.array_equal(alh, o[3]) and list(sts) == [0] * 200
 
 
-@pytest.mark.parametrize("max_entries", [64, 65, 300])
+@pytest.mark.parametrize("max_entries", [64, 65, 300, 1024])
 def test_txlog_validate_tree_paths(m, ctx, orc, max_entries):
     """Batches whose widest tx has <= 64 entries take the one-lane-per-tree
     root kernel, wider ones the host tree plan: both agree with the oracle."""
