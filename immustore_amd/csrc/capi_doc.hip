@@ -76,7 +76,8 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
             return MH_ERR_ILLEGAL_ARGUMENTS;
         for (uint64_t d = 0; d < n; d++)
             if (B->doc_off[d + 1] < B->doc_off[d] || B->doc_key_off[d + 1] < B->doc_key_off[d] ||
-                B->ent_off[d + 1] < B->ent_off[d])
+                B->ent_off[d + 1] < B->ent_off[d] || B->incl_off[d + 1] < B->incl_off[d] ||
+                B->cons_off[d + 1] < B->cons_off[d])
                 return MH_ERR_ILLEGAL_ARGUMENTS;
         for (uint64_t e = B->ent_off[0]; e < B->ent_off[n]; e++)
             if (B->ekey_off[e + 1] < B->ekey_off[e] ||

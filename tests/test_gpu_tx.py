@@ -320,6 +320,32 @@ def test_verify_document_batch_vs_oracle(m, ctx, orc, fixtures):
     assert (st == 0).sum() >= 40
 
 
+def test_verify_document_batch_offsets_running_backwards(m, ctx, orc, fixtures):
+    """Offsets that run backwards (document, key, entry and proof-term CSR)
+    are rejected with ErrIllegalArguments before anything is read through
+    them; restored, the same batch verifies."""
+    import ctypes as C
+    from immustore_amd import _native as N
+    from immustore_amd import txlayer
+    from tx_util import document_cases
+    docs, blob = document_cases(fixtures, orc)
+    docs = docs[:13]
+    docs[0]["md_blob"] = blob
+    b, keep = txlayer.pack_document_batch(docs)
+    n = len(docs)
+    st0, _ = txlayer.call_document_batch(b, n, ctx)
+    for field in ("doc_off", "doc_key_off", "ent_off", "incl_off", "cons_off"):
+        off = (C.c_uint64 * (n + 1)).from_address(getattr(b, field))
+        saved = list(off)
+        off[1] = off[2] + 5
+        with pytest.raises(N.MerkleError):
+            txlayer.call_document_batch(b, n, ctx)
+        for i, v in enumerate(saved):
+            off[i] = v
+    st1, _ = txlayer.call_document_batch(b, n, ctx)
+    assert np.array_equal(st0, st1)
+
+
 def test_verify_document_batch_wide_txs(m, ctx, orc):
     """Synthetic v1 documents in transactions of up to 700 entries (the
     htrees take the planned many-tree path), with KV metadata, a trivial
