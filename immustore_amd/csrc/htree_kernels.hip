@@ -197,6 +197,13 @@ struct Log2 {
 constexpr int kFixedThreads = 256;
 constexpr int kWaveLds = 8192;
 
+// Workgroup timeline probe points of k_entries_fixed (0: start, 3: first value
+// block hashed, 1: leaf phase done, 2: end); empty in the library, defined by
+// tools/wg_trace.hip.
+#ifndef MH_WG_PROBE
+#define MH_WG_PROBE(point)
+#endif
+
 // Issue the LDS-DMA of one unit (2 blocks = 8 x 1 KiB, or 1 block = 4 x 1 KiB)
 // for the wave's 64 lane-slots.  Address = wave-uniform base (SGPRs) + a
 // 32-bit per-lane offset; slot entries past the end of the batch are clamped
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
         }
     }
     __syncthreads();
+    MH_WG_PROBE(0);
     char *lds = smem + wave * kWaveLds;
     const uint64_t wave_slot0 = ((uint64_t)blockIdx.x * (kFixedThreads / 64) + wave) * 64;
     const uint64_t first = (wave_slot0 + lane) * LPL;
@@ -336,6 +344,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
                                   lane);
                 }
                 if (on) compress(s, w);
+                if (b == 0 && i == 0) MH_WG_PROBE(3);
             }
             b = 0;
             if (rem) {
@@ -480,6 +489,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     // The workgroup's 256 lane-group nodes (level L0 = log2 LPL) are reduced
     // in LDS to up to 8 more levels (htree.go:85-110), writing every level.
     constexpr int L0 = LPL == 4 ? 2 : (LPL == 2 ? 1 : 0);
+    MH_WG_PROBE(1);
     if (wg_levels == 0) return;  // launch-uniform
     const int t = threadIdx.x;
     uint32_t(*buf)[kFixedThreads][9] = reinterpret_cast<uint32_t(*)[kFixedThreads][9]>(smem);
@@ -512,6 +522,7 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
         }
         cur ^= 1;
     }
+    MH_WG_PROBE(2);
 }
 
 // ============================================================================
