@@ -9,21 +9,21 @@ the multi-threaded hop (bit flips, extreme BE16 / BE32 length fields,
 truncation, splices).  Each mutant sits in an allocation of its exact length;
 the library's host code and the oracle are both built with ASan (host only,
 tools/asan/Makefile), and the two parses must agree on (status, ntx,
-consumed) for every mutant."""
+consumed) for every mutant.  (tools/gpu_fuzz.sh runs the same fuzzer on a GPU
+box with the device path, mh_txlog_validate, compared in full:
+profiles/fuzz_txlog_device_r02.log.)"""
 import os
 import shutil
 import subprocess
+import sys
 
-import numpy as np
 import pytest
-
-from tx_util import _bulk_txlog, _synthetic_txlog, metadata_logs
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FUZZ = os.path.join(ROOT, "build", "asan", "txlog_fuzz")
 
 
-def test_txlog_hop_fuzz_asan(tmp_path, orc, fixtures):
+def test_txlog_hop_fuzz_asan(tmp_path):
     import torch
     if torch.cuda.is_available():
         pytest.skip("host-sanitizer run: CPU container only")
@@ -31,19 +31,10 @@ def test_txlog_hop_fuzz_asan(tmp_path, orc, fixtures):
         pytest.skip("hipcc not available")
     subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "tools", "asan")], check=True,
                    timeout=600)
-    files = []
-
-    def put(name, raw):
-        p = tmp_path / name
-        p.write_bytes(raw)
-        files.append(str(p))
-
-    for name, fx in fixtures.items():
-        put(f"fx_{name}.log", bytes.fromhex(fx["txlog"]))
-    put("synthetic.log", _synthetic_txlog(np.random.default_rng(5), 60, orc))
-    for name, raw in metadata_logs(orc):
-        put(f"md_{name}.log", raw)
-    put("bulk.log", _bulk_txlog(np.random.default_rng(78), 9000)[0])
+    sys.path.insert(0, os.path.join(ROOT, "tools", "asan"))
+    import make_corpus
+    make_corpus.main(str(tmp_path))
+    files = sorted(str(p) for p in tmp_path.glob("*.log"))
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=86")
     r = subprocess.run([FUZZ, "1500", "20261016"] + files, capture_output=True, text=True,
                        timeout=600, env=env)

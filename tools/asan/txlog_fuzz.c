@@ -10,6 +10,13 @@
  * truncation, a splice of another part of the log, a record repeated.
  * For each mutant: (status, ntx, consumed) of the two parses must agree.
  *
+ * With MH_FUZZ_DEVICE=1 (on a GPU box) every mutant also goes through
+ * mh_txlog_validate -- the device path: raw records to the device, headers,
+ * entry digests, trees and Alh rebuilt there, the canonical-metadata side
+ * area -- and its status, record count, consumed bytes, Alh values and
+ * per-tx statuses must equal the oracle's.  The host code around it still
+ * runs under ASan (the device code is built as usual).
+ *
  * usage: txlog_fuzz <iterations per file> <seed> <log file>...
  * prints one line per file; exit 1 on any mismatch. */
 #include <stdint.h>
@@ -88,6 +95,27 @@ static uint8_t *mutate(const uint8_t *src, uint64_t len, uint64_t *out_len) {
     return e;
 }
 
+static mh_ctx *CTX;  /* MH_FUZZ_DEVICE=1: mh_txlog_validate as well */
+
+static int check_device(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_t cap,
+                        int r2, uint64_t n2, uint64_t c2, const uint8_t *alh2,
+                        const int32_t *sts2, long *bad) {
+    const uint64_t k = cap ? cap : 1;
+    mh_tx_header *h = malloc(sizeof(mh_tx_header) * k);
+    uint8_t *alh = malloc(32 * k);
+    int32_t *sts = malloc(4 * k);
+    uint64_t n1 = 0, c1 = 0;
+    const int r1 = mh_txlog_validate(CTX, b, n, me, mk, cap, &n1, &c1, h, alh, sts);
+    int ok = r1 == r2 && n1 == n2 && c1 == c2;
+    if (ok && n1) ok = !memcmp(alh, alh2, 32 * n1) && !memcmp(sts, sts2, 4 * n1);
+    if (!ok && (*bad)++ < 5)
+        fprintf(stderr, "device mismatch len %llu: validate (%d, %llu, %llu) oracle (%d, %llu, %llu)\n",
+                (unsigned long long)n, r1, (unsigned long long)n1, (unsigned long long)c1, r2,
+                (unsigned long long)n2, (unsigned long long)c2);
+    free(h); free(alh); free(sts);
+    return ok;
+}
+
 static int check(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_t mt, long *bad) {
     const uint64_t cap = n / 90 + 1 < mt ? n / 90 + 1 : mt;
     mh_tx_header *h = malloc(sizeof(mh_tx_header) * (cap ? cap : 1));
@@ -97,11 +125,12 @@ static int check(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_
     uint64_t n1 = 0, c1 = 0, n2 = 0, c2 = 0;
     const int r1 = mh_txlog_scan(b, n, me, mk, cap, &n1, &c1, h, ao);
     const int r2 = orc_txlog_validate(b, n, me, mk, cap, &n2, &c2, alh, sts);
-    const int ok = r1 == r2 && n1 == n2 && c1 == c2;
+    int ok = r1 == r2 && n1 == n2 && c1 == c2;
     if (!ok && (*bad)++ < 5)
         fprintf(stderr, "mismatch len %llu: scan (%d, %llu, %llu) oracle (%d, %llu, %llu)\n",
                 (unsigned long long)n, r1, (unsigned long long)n1, (unsigned long long)c1, r2,
                 (unsigned long long)n2, (unsigned long long)c2);
+    if (CTX) ok &= check_device(b, n, me, mk, cap, r2, n2, c2, alh, sts, bad);
     free(h); free(ao); free(alh); free(sts);
     return ok;
 }
@@ -110,6 +139,11 @@ int main(int argc, char **argv) {
     if (argc < 4) return 2;
     const long iters = atol(argv[1]);
     S = strtoull(argv[2], 0, 10);
+    const char *dev = getenv("MH_FUZZ_DEVICE");
+    if (dev && dev[0] == '1' && mh_ctx_create(0, NULL, &CTX) != MH_OK) {
+        fprintf(stderr, "MH_FUZZ_DEVICE=1 but no device context\n");
+        return 2;
+    }
     long bad = 0;
     for (int a = 3; a < argc; a++) {
         uint64_t len = 0;
@@ -132,8 +166,11 @@ int main(int argc, char **argv) {
             if (mh_txlog_scan(m, n, me, mk, n / 90 + 1, &nt, &c, NULL, NULL) == MH_OK && nt) accepted++;
             free(m);
         }
-        printf("%s: %ld mutants, %ld agree, %ld parsed >= 1 record\n", argv[a], it, agree, accepted);
+        printf("%s: %ld mutants, %ld agree, %ld parsed >= 1 record%s\n", argv[a], it, agree,
+               accepted, CTX ? " (device validate too)" : "");
+        fflush(stdout);
         free(src);
     }
+    if (CTX) mh_ctx_destroy(CTX);
     return bad ? 1 : 0;
 }
