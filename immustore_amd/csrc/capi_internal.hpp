@@ -182,6 +182,7 @@ struct mh_ctx {
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
+    PinBuf p_stage;       // host-built arrays of one call, staged for a single upload
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
 };
 
@@ -289,6 +290,17 @@ inline uint64_t plan_index_bytes(const TreePlan &P, uint64_t ntrees) {
 
 // Leaves + levels + roots of a planned batch (capi_tx.hip).
 // roots of many htrees over device digests (capi_tx.hip)
+// innerHash / Alh of checked headers (capi_tx.hip); c->mu held by the caller.
+int tx_alh_core(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs, const uint8_t *md_blob,
+                uint64_t md_blob_len, uint8_t *inner_out, uint8_t *alh_out);
+// VerifyDualProofV2 over checked arguments (capi_tx.hip); alh_checked skips
+// the header Alh pass when the caller has matched them already; c->mu held.
+int dual_proof_v2_core(mh_ctx *c, uint64_t n, const mh_tx_header *sh, const mh_tx_header *th,
+                       const uint8_t *md_blob, uint64_t md_blob_len, const uint64_t *incl_off,
+                       const uint8_t *incl_terms, const uint64_t *cons_off,
+                       const uint8_t *cons_terms, const uint64_t *src, const uint64_t *tgt,
+                       const uint8_t *src_alh, const uint8_t *tgt_alh, int32_t *status,
+                       bool alh_checked);
 int build_many_dev(mh_ctx *c, hipStream_t st, uint64_t ntrees, const uint64_t *leaf_off,
                    const uint8_t *d_dig, uint8_t *d_roots, DevBuf &s_lv, DevBuf &s_lo);
 int run_tree_plan(mh_ctx *c, hipStream_t st, const TreePlan &P, uint64_t ntrees, uint64_t nleaves,

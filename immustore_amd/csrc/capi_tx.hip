@@ -74,6 +74,28 @@ int run_tree_plan_on(DevBuf &scratch, hipStream_t st, Timer *tm, const TreePlan 
 
 
 // ------------------------------------------------------------------ a7
+// innerHash / Alh of n checked headers (tx.go:249-319); c->mu held by the
+// caller.  From pinned host memory the header copy is one DMA.
+int tx_alh_core(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs, const uint8_t *md_blob,
+                uint64_t md_blob_len, uint8_t *inner_out, uint8_t *alh_out) {
+    MH_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    Layout L;
+    const uint64_t b_h = L.add(n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
+                   b_s = L.add(n * kTxInnerStride), b_in = L.add(n * 32), b_a = L.add(n * 32);
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base + b_h, hdrs, n * sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
+    if (md_blob && md_blob_len)
+        MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_tx_alh(st, c->tm(), n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
+                         base + b_s, nullptr, nullptr, base + b_in, base + b_a, nullptr));
+    if (inner_out) MH_HIP(hipMemcpyAsync(inner_out, base + b_in, n * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(alh_out, base + b_a, n * 32, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
 extern "C" int mh_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
                                const uint8_t *md_blob, uint64_t md_blob_len, uint8_t *inner_out,
                                uint8_t *alh_out) {
@@ -83,22 +105,7 @@ extern "C" int mh_tx_alh_batch(mh_ctx *c, uint64_t n, const mh_tx_header *hdrs,
         for (uint64_t k = 0; k < n; k++)
             if (int e = check_header(hdrs[k], md_blob_len, md_blob != nullptr)) return e;
         std::lock_guard<std::mutex> lk(c->mu);
-        hipSetDevice(c->device);
-        hipStream_t st = c->stream;
-        Layout L;
-        const uint64_t b_h = L.add(n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
-                       b_s = L.add(n * kTxInnerStride), b_in = L.add(n * 32), b_a = L.add(n * 32);
-        MH_HIP(c->s_tx.ensure(L.total));
-        uint8_t *base = c->s_tx.as<uint8_t>();
-        MH_HIP(hipMemcpyAsync(base + b_h, hdrs, n * sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
-        if (md_blob && md_blob_len)
-            MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
-        MH_HIP(launch_tx_alh(st, c->tm(), n, (const MhTxHeader *)(base + b_h), base + b_md, nullptr,
-                             base + b_s, nullptr, nullptr, base + b_in, base + b_a, nullptr));
-        if (inner_out) MH_HIP(hipMemcpyAsync(inner_out, base + b_in, n * 32, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipMemcpyAsync(alh_out, base + b_a, n * 32, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipStreamSynchronize(st));
-        return MH_OK;
+        return tx_alh_core(c, n, hdrs, md_blob, md_blob_len, inner_out, alh_out);
     });
 }
 
@@ -215,6 +222,113 @@ extern "C" int mh_verify_linear_proof_batch(mh_ctx *c, uint64_t n, const uint64_
     });
 }
 
+// VerifyDualProofV2 (verification.go:305-372) over n proofs whose arguments
+// have been checked (offsets monotonic, term arrays present).  The host-built
+// arrays are written straight into one pinned staging area laid out like
+// their device copies and go up in ONE copy; the results come back the same
+// way.  alh_checked: the caller has already matched both headers' Alh with
+// src_alh / tgt_alh and rejected unhashable headers (the VerifyDocument batch,
+// which hashes every header once) -- the Alh pass (:318-326) is skipped.
+// c->mu held by the caller (c->p_stage, c->s_tx).
+int dual_proof_v2_core(mh_ctx *c, uint64_t n, const mh_tx_header *sh, const mh_tx_header *th,
+                       const uint8_t *md_blob, uint64_t md_blob_len, const uint64_t *incl_off,
+                       const uint8_t *incl_terms, const uint64_t *cons_off,
+                       const uint8_t *cons_terms, const uint64_t *src, const uint64_t *tgt,
+                       const uint8_t *src_alh, const uint8_t *tgt_alh, int32_t *status,
+                       bool alh_checked) {
+    const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
+    const uint64_t nh = alh_checked ? 0 : 2 * n;  // headers hashed here
+    // host-built inputs first (one contiguous upload), then device-only data
+    Layout L;
+    const uint64_t b_h = L.add(nh * sizeof(mh_tx_header)), b_x = L.add(2 * n * 32),
+                   b_sbl = L.add(n * 32), b_tbl = L.add(n * 32), b_sel = L.add(n),
+                   b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
+                   b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8);
+    const uint64_t up_bytes = L.total;
+    const uint64_t b_st = L.add(2 * n * 4), b_oki = L.add(n), b_okc = L.add(n);  // results
+    const uint64_t res0 = b_st, res_bytes = L.total - b_st;
+    const uint64_t b_md = L.add(alh_checked ? 0 : md_blob_len), b_s = L.add(nh * kTxInnerStride),
+                   b_leaf = L.add(n * 32), b_ca = L.add(n * 32), b_it = L.add(ni * 32),
+                   b_ct = L.add(nc * 32);
+    MH_HIP(c->p_stage.ensure(L.total));
+    uint8_t *hp = c->p_stage.as<uint8_t>();
+    mh_tx_header *hh = reinterpret_cast<mh_tx_header *>(hp + b_h);
+    uint8_t *x = hp + b_x, *sbl = hp + b_sbl, *tbl = hp + b_tbl, *sel = hp + b_sel;
+    uint64_t *ii = reinterpret_cast<uint64_t *>(hp + b_ii), *ij = reinterpret_cast<uint64_t *>(hp + b_ij),
+             *ci = reinterpret_cast<uint64_t *>(hp + b_ci), *io = reinterpret_cast<uint64_t *>(hp + b_io),
+             *co = reinterpret_cast<uint64_t *>(hp + b_co);
+    for (uint64_t p = 0; p < n; p++) {
+        if (!alh_checked) {
+            hh[p] = sh[p];
+            hh[n + p] = th[p];
+            if (status[p] != MH_OK) {  // keep the kernel's reads inside md_blob; result unused
+                hh[p].version = hh[n + p].version = 1;
+                hh[p].md_len = hh[n + p].md_len = 0;
+            }
+        }
+        memcpy(x + p * 32, src_alh + p * 32, 32);
+        memcpy(x + (n + p) * 32, tgt_alh + p * 32, 32);
+        ii[p] = src[p];  // verification.go:342-348
+        ij[p] = th[p].bl_tx_id;
+        sel[p] = src[p] == 1;  // :354-370
+        ci[p] = src[p] == 1 ? src[p] : sh[p].bl_tx_id;
+        memcpy(sbl + p * 32, sh[p].bl_root, 32);
+        memcpy(tbl + p * 32, th[p].bl_root, 32);
+    }
+    for (uint64_t p = 0; p <= n; p++) {
+        io[p] = incl_off[p] - incl_off[0];
+        co[p] = cons_off[p] - cons_off[0];
+    }
+    MH_HIP(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    MH_HIP(c->s_tx.ensure(L.total));
+    uint8_t *base = c->s_tx.as<uint8_t>();
+    MH_HIP(hipMemcpyAsync(base, hp, up_bytes, hipMemcpyHostToDevice, st));
+    if (ni) MH_HIP(hipMemcpyAsync(base + b_it, incl_terms + incl_off[0] * 32, ni * 32,
+                                  hipMemcpyHostToDevice, st));
+    if (nc) MH_HIP(hipMemcpyAsync(base + b_ct, cons_terms + cons_off[0] * 32, nc * 32,
+                                  hipMemcpyHostToDevice, st));
+    if (!alh_checked) {
+        if (md_blob && md_blob_len)
+            MH_HIP(hipMemcpyAsync(base + b_md, md_blob, md_blob_len, hipMemcpyHostToDevice, st));
+        // Alh of both headers vs the given ones (verification.go:318-326)
+        MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, (const MhTxHeader *)(base + b_h), base + b_md,
+                             nullptr, base + b_s, base + b_x, nullptr, nullptr, nullptr,
+                             (int32_t *)(base + b_st)));
+    } else {
+        MH_HIP(hipMemsetAsync(base + b_st, 0, 2 * n * 4, st));  // every Alh matched (MH_OK)
+    }
+    // leafFor(sourceAlh) (verification.go:346), then the two ahtree proofs
+    MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
+    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
+                                (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
+                                base + b_it, base + b_leaf, base + b_tbl, base + b_oki, nullptr));
+    MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
+    MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
+                                (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
+                                (const uint64_t *)(base + b_co), base + b_ct, base + b_ca,
+                                base + b_tbl, base + b_okc, nullptr));
+    MH_HIP(hipMemcpyAsync(hp + res0, base + res0, res_bytes, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    const int32_t *ast = reinterpret_cast<const int32_t *>(hp + b_st);
+    const uint8_t *oki = hp + b_oki, *okc = hp + b_okc;
+    for (uint64_t p = 0; p < n; p++) {
+        if (status[p] != MH_OK) continue;
+        if (ast[p] != MH_OK || ast[n + p] != MH_OK) {
+            status[p] = MH_ERR_ILLEGAL_ARGUMENTS;
+        } else if (sh[p].id - 1 != sh[p].bl_tx_id || th[p].id - 1 != th[p].bl_tx_id) {
+            status[p] = MH_ERR_UNEXPECTED_LINKING;  // :328-330
+        } else if (src[p] == tgt[p]) {
+            status[p] = MH_OK;  // :332-334
+        } else if (!oki[p]) {
+            status[p] = MH_ERR_INCLUSION_NOT_VALID;
+        } else if (!okc[p]) {
+            status[p] = MH_ERR_CONSISTENCY_NOT_VALID;
+        }
+    }
+    return MH_OK;
+}
+
 extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_header *sh,
                                              const mh_tx_header *th, const uint8_t *md_blob,
                                              uint64_t md_blob_len, const uint64_t *incl_off,
@@ -232,8 +346,6 @@ extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_
         if ((ni && !incl_terms) || (nc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
         // verification.go:305-316: argument checks on the host, headers that
         // cannot be hashed (unknown version, bad md) fail as ErrIllegalArguments
-        std::vector<mh_tx_header> hh(2 * n);
-        std::vector<uint8_t> expect(2 * n * 32);
         for (uint64_t p = 0; p < n; p++) {
             int32_t s = MH_OK;
             if (sh[p].id == 0 || sh[p].id != src[p] || th[p].id != tgt[p])
@@ -244,94 +356,10 @@ extern "C" int mh_verify_dual_proof_v2_batch(mh_ctx *c, uint64_t n, const mh_tx_
                      check_header(th[p], md_blob_len, md_blob != nullptr))
                 s = MH_ERR_ILLEGAL_ARGUMENTS;
             status[p] = s;
-            hh[p] = sh[p];
-            hh[n + p] = th[p];
-            if (s != MH_OK) {  // keep the kernel's reads inside md_blob; result unused
-                hh[p].version = hh[n + p].version = 1;
-                hh[p].md_len = hh[n + p].md_len = 0;
-            }
-            memcpy(&expect[p * 32], src_alh + p * 32, 32);
-            memcpy(&expect[(n + p) * 32], tgt_alh + p * 32, 32);
-        }
-        std::vector<uint64_t> io(n + 1), co(n + 1), ii(n), ij(n), ci(n);
-        std::vector<uint8_t> sel(n), sbl(n * 32), tbl(n * 32);
-        for (uint64_t p = 0; p <= n; p++) {
-            io[p] = incl_off[p] - incl_off[0];
-            co[p] = cons_off[p] - cons_off[0];
-        }
-        for (uint64_t p = 0; p < n; p++) {
-            ii[p] = src[p];                                    // verification.go:342-348
-            ij[p] = th[p].bl_tx_id;
-            sel[p] = src[p] == 1;                              // :354-370
-            ci[p] = src[p] == 1 ? src[p] : sh[p].bl_tx_id;
-            memcpy(&sbl[p * 32], sh[p].bl_root, 32);
-            memcpy(&tbl[p * 32], th[p].bl_root, 32);
         }
         std::lock_guard<std::mutex> lk(c->mu);
-        hipSetDevice(c->device);
-        hipStream_t st = c->stream;
-        Layout L;
-        const uint64_t b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(md_blob_len),
-                       b_s = L.add(2 * n * kTxInnerStride), b_x = L.add(2 * n * 32),
-                       b_st = L.add(2 * n * 4), b_leaf = L.add(n * 32), b_sbl = L.add(n * 32),
-                       b_tbl = L.add(n * 32), b_ca = L.add(n * 32), b_sel = L.add(n),
-                       b_ii = L.add(n * 8), b_ij = L.add(n * 8), b_ci = L.add(n * 8),
-                       b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8), b_it = L.add(ni * 32),
-                       b_ct = L.add(nc * 32), b_oki = L.add(n), b_okc = L.add(n);
-        MH_HIP(c->s_tx.ensure(L.total));
-        uint8_t *base = c->s_tx.as<uint8_t>();
-        auto h2d = [&](uint64_t off, const void *p, uint64_t bytes) -> hipError_t {
-            return bytes ? hipMemcpyAsync(base + off, p, bytes, hipMemcpyHostToDevice, st)
-                         : hipSuccess;
-        };
-        MH_HIP(h2d(b_h, hh.data(), 2 * n * sizeof(mh_tx_header)));
-        if (md_blob) MH_HIP(h2d(b_md, md_blob, md_blob_len));
-        MH_HIP(h2d(b_x, expect.data(), 2 * n * 32));
-        MH_HIP(h2d(b_sbl, sbl.data(), n * 32));
-        MH_HIP(h2d(b_tbl, tbl.data(), n * 32));
-        MH_HIP(h2d(b_sel, sel.data(), n));
-        MH_HIP(h2d(b_ii, ii.data(), n * 8));
-        MH_HIP(h2d(b_ij, ij.data(), n * 8));
-        MH_HIP(h2d(b_ci, ci.data(), n * 8));
-        MH_HIP(h2d(b_io, io.data(), (n + 1) * 8));
-        MH_HIP(h2d(b_co, co.data(), (n + 1) * 8));
-        if (ni) MH_HIP(h2d(b_it, incl_terms + incl_off[0] * 32, ni * 32));
-        if (nc) MH_HIP(h2d(b_ct, cons_terms + cons_off[0] * 32, nc * 32));
-        // Alh of both headers vs the given ones (verification.go:318-326)
-        MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, (const MhTxHeader *)(base + b_h), base + b_md,
-                             nullptr, base + b_s, base + b_x, nullptr, nullptr, nullptr,
-                             (int32_t *)(base + b_st)));
-        // leafFor(sourceAlh) (verification.go:346), then the two ahtree proofs
-        MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
-        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
-                                    (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
-                                    base + b_it, base + b_leaf, base + b_tbl, base + b_oki, nullptr));
-        MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
-        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
-                                    (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
-                                    (const uint64_t *)(base + b_co), base + b_ct, base + b_ca,
-                                    base + b_tbl, base + b_okc, nullptr));
-        std::vector<int32_t> ast(2 * n);
-        std::vector<uint8_t> oki(n), okc(n);
-        MH_HIP(hipMemcpyAsync(ast.data(), base + b_st, 2 * n * 4, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipMemcpyAsync(oki.data(), base + b_oki, n, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipMemcpyAsync(okc.data(), base + b_okc, n, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipStreamSynchronize(st));
-        for (uint64_t p = 0; p < n; p++) {
-            if (status[p] != MH_OK) continue;
-            if (ast[p] != MH_OK || ast[n + p] != MH_OK) {
-                status[p] = MH_ERR_ILLEGAL_ARGUMENTS;
-            } else if (sh[p].id - 1 != sh[p].bl_tx_id || th[p].id - 1 != th[p].bl_tx_id) {
-                status[p] = MH_ERR_UNEXPECTED_LINKING;  // :328-330
-            } else if (src[p] == tgt[p]) {
-                status[p] = MH_OK;  // :332-334
-            } else if (!oki[p]) {
-                status[p] = MH_ERR_INCLUSION_NOT_VALID;
-            } else if (!okc[p]) {
-                status[p] = MH_ERR_CONSISTENCY_NOT_VALID;
-            }
-        }
-        return MH_OK;
+        return dual_proof_v2_core(c, n, sh, th, md_blob, md_blob_len, incl_off, incl_terms,
+                                  cons_off, cons_terms, src, tgt, src_alh, tgt_alh, status, false);
     });
 }
 
