@@ -20,7 +20,9 @@
                     the device -- 10^6 DualProofV2 (ImmuStore.DualProofV2 over
                     a 2^24-append ahtree + TxHeader encoding) and 10^6 htree
                     InclusionProof messages over a 2^24-leaf tree; sizes pass,
-                    scan, write pass; a sample checked against oracle/wire.py.
+                    scan, write pass; a sample checked against oracle/wire.py;
+                    then the same 10^6 DualProofV2 messages decoded back
+                    (mh_dual_proof_v2_pb_decode_batch, host buffers).
   --workload ragged SURVEY.md 8(a) a1-a4 over ragged EntrySpecs (the general
                     CSR entry path, mh_dev_htree_build_entries): 2^20 entries,
                     value length uniform in [0, 4096] (MaxValueLen), keys of
@@ -931,6 +933,32 @@ def run_single(a):
         for k in [int(x) for x in rng.integers(0, P, 300)]:
             ok &= WR.htree_inclusion_proof_pb(lv_h, W, int(leaf_h[k])) == (
                 0, oi[offs2[k]:offs2[k + 1]].tobytes())
+        # the client side: the same messages decoded (mh_dual_proof_v2_pb_decode_batch,
+        # host buffers in and out: H2D of the messages, D2H of headers + terms)
+        msgs_h = ob
+        n_dec = P
+        dsh, dth = np.zeros(n_dec, TX_HEADER), np.zeros(n_dec, TX_HEADER)
+        dmd = np.zeros(2 * n_dec * 268, np.uint8)
+        dio, dco = np.zeros(n_dec + 1, np.uint64), np.zeros(n_dec + 1, np.uint64)
+        dst = np.zeros(n_dec, np.int32)
+        moff = offs.astype(np.uint64)
+        A = lambda x: x.ctypes.data  # noqa: E731
+        rc = L.mh_dual_proof_v2_pb_decode_batch(ctx.handle, n_dec, A(msgs_h), A(moff), A(dsh), A(dth),
+                                                A(dmd), A(dio), None, 0, A(dco), None, 0, A(dst))
+        assert rc == 19, rc
+        dit = np.zeros((int(dio[n_dec]), 32), np.uint8)
+        dct = np.zeros((int(dco[n_dec]), 32), np.uint8)
+
+        def step_decode():
+            N.check(L.mh_dual_proof_v2_pb_decode_batch(
+                ctx.handle, n_dec, A(msgs_h), A(moff), A(dsh), A(dth), A(dmd), A(dio), A(dit),
+                dit.shape[0], A(dco), A(dct), dct.shape[0], A(dst)))
+
+        tdec = timed(step_decode, max(1, a.steps // 2), 1, sync)
+        ok &= bool((dst == 0).all())
+        for k in [int(x) for x in rng.integers(0, P, 300)]:
+            ok &= dsh[k].tobytes()[:128] == hs_h[k].tobytes()[:128]
+            ok &= dth[k].tobytes()[:128] == ht_h[k].tobytes()[:128]
         out = {"metric": "DualProofV2 protobuf messages built on the device, 10^6 x (2^24 tree)",
                "value": round(P / td / 1e6, 3), "unit": "M messages/s",
                "ms_per_step": round(td * 1e3, 3), "bytes_out": total,
@@ -940,6 +968,11 @@ def run_single(a):
                                       "ms_per_step": round(ti * 1e3, 3), "bytes_out": total2,
                                       "out_GBps": round(total2 / ti / 1e9, 1),
                                       "kernel_ms": {k: round(v, 3) for k, v in ki.items()}},
+               "decode_dual_proof_v2_pb": {
+                   "M_messages_per_s": round(n_dec / tdec / 1e6, 3), "ms_per_step": round(tdec * 1e3, 3),
+                   "bytes_in": int(moff[-1]), "in_GBps": round(int(moff[-1]) / tdec / 1e9, 2),
+                   "note": "host buffers (pageable): H2D of the messages, D2H of the headers, "
+                           "the packed metadata and the terms"},
                "sample_vs_oracle": bool(ok)}
 
     out["workload"] = a.workload

@@ -1,0 +1,388 @@
+// pb_decode.hip -- DualProofV2 protobuf messages decoded on the device
+// (the FromProto side of database_protoconv.go): what a
+// client / auditor does with every VerifiableTxV2 answer before
+// VerifyDualProofV2, for a batch of messages at once.
+//
+//   DualProofV2FromProto  database_protoconv.go:226-233   schema.proto:437-445
+//   TxHeaderFromProto     :235-247                        schema.proto:349-378
+//   TxMetadataFromProto   :249-262 (-> TxMetadata.Bytes(), tx_metadata.go:145-157)
+//   DigestFromProto / DigestsFromProto  :293-305 (copy of up to 32 bytes)
+//
+// proto3 wire format as protobuf-go's Unmarshal reads it: fields in any
+// order; a scalar or bytes field seen twice keeps the last value; an embedded
+// message seen twice is merged (its fields read in turn into the same value);
+// a known field with an unexpected wire type, and unknown fields (groups
+// included), are skipped; int32 values are the low 32 bits of the varint.
+// Malformed bytes (truncation, an over-long varint, wire type 6 / 7, field
+// number 0, an unmatched end group) -> MH_ERR_CORRUPTED_DATA.  A message
+// without a source or target header -> MH_ERR_ILLEGAL_ARGUMENTS (Go's
+// TxHeaderFromProto dereferences the nil header).
+//
+// One lane per message, two passes: the first validates and counts the
+// inclusion / consistency terms and the canonical metadata bytes, the offsets
+// are scanned (hipcub), the second writes the headers, the terms and the
+// metadata (packed: only the bytes that exist travel back to the host).
+#include <hipcub/hipcub.hpp>
+
+#include "capi_internal.hpp"
+
+namespace {
+
+constexpr uint32_t kMdSlot = MH_MAX_TX_METADATA_LEN;  // metadata bytes per header
+constexpr uint32_t kMaxExtra = 256;                    // maxExtraLen, tx_metadata.go
+
+struct PbIn {
+    const uint8_t *p, *end;
+    __device__ bool varint(uint64_t &v) {
+        v = 0;
+        for (int i = 0; i < 10; i++) {
+            if (p >= end) return false;
+            const uint8_t b = *p++;
+            if (i == 9 && b > 1) return false;  // beyond 64 bits (protowire)
+            v |= (uint64_t)(b & 0x7f) << (7 * i);
+            if (!(b & 0x80)) return true;
+        }
+        return false;
+    }
+    __device__ bool bytes(const uint8_t *&q, uint64_t &len) {
+        if (!varint(len) || len > (uint64_t)(end - p)) return false;
+        q = p;
+        p += len;
+        return true;
+    }
+    __device__ bool skip(uint64_t n) {
+        if (n > (uint64_t)(end - p)) return false;
+        p += n;
+        return true;
+    }
+    __device__ bool key(uint32_t &field, uint32_t &wt) {
+        uint64_t k;
+        if (!varint(k)) return false;
+        field = (uint32_t)(k >> 3);
+        wt = (uint32_t)(k & 7);
+        return (k >> 3) != 0 && (k >> 3) < (1ull << 29);
+    }
+    // the value of an unknown (or mistyped) field; a group to its end
+    __device__ __forceinline__ bool skip_value(uint32_t field, uint32_t wt) {
+        uint64_t v;
+        const uint8_t *q;
+        switch (wt) {
+        case 0: return varint(v);
+        case 1: return skip(8);
+        case 2: return bytes(q, v);
+        case 5: return skip(4);
+        case 3: return (p = skip_group(p, end, field)) != nullptr;
+        default: return false;  // 4: an end group with no start; 6, 7
+        }
+    }
+    // groups (deprecated, seen only as unknown fields) out of line, the reader
+    // passed by value (a reference would pin the caller's reader to scratch):
+    // -> the position after the group, nullptr if malformed
+    static __device__ __noinline__ const uint8_t *skip_group(const uint8_t *p, const uint8_t *end,
+                                                             uint32_t field) {
+        PbIn in{p, end};
+        return in.group_end(field) ? in.p : nullptr;
+    }
+    __device__ bool group_end(uint32_t field) {
+        uint32_t stack[32];
+        int depth = 0;
+        uint32_t wt = 3;
+        for (;;) {
+            uint64_t v;
+            const uint8_t *q;
+            switch (wt) {
+            case 0: if (!varint(v)) return false; break;
+            case 1: if (!skip(8)) return false; break;
+            case 2: if (!bytes(q, v)) return false; break;
+            case 5: if (!skip(4)) return false; break;
+            case 3:
+                if (depth == 32) return false;
+                stack[depth++] = field;
+                break;
+            case 4:
+                if (depth == 0 || stack[depth - 1] != field) return false;
+                depth--;
+                break;
+            default: return false;
+            }
+            if (depth == 0) return true;
+            if (!key(field, wt)) return false;
+        }
+    }
+};
+
+// DigestFromProto: the first min(len, 32) bytes, zero padded, into an 8-byte
+// aligned destination.  The usual 32-byte case reads nine aligned dwords and
+// funnel-shifts them (v_alignbyte) instead of 32 byte loads; the read may run
+// up to 3 bytes past the term, inside the padded message area.
+__device__ __forceinline__ void digest_from(const uint8_t *q, uint64_t len, uint8_t *d) {
+    uint32_t o[8];
+    if (len >= 32) {
+        const uint32_t *a = (const uint32_t *)((uintptr_t)q & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)((uintptr_t)q & 3);
+        uint32_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) w[i] = a[i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            uint32_t v = 0;
+            for (int j = 0; j < 4; j++)
+                if ((uint64_t)(4 * i + j) < len) v |= (uint32_t)q[4 * i + j] << (8 * j);
+            o[i] = v;
+        }
+    }
+    uint2 *dd = (uint2 *)d;
+#pragma unroll
+    for (int i = 0; i < 4; i++) dd[i] = make_uint2(o[2 * i], o[2 * i + 1]);
+}
+
+struct MdState {
+    bool present = false;
+    uint64_t trunc = 0;
+    const uint8_t *extra = nullptr;
+    uint64_t extra_len = 0;
+};
+
+// TxMetadata fields into md (merged)
+__device__ __forceinline__ bool parse_md(const uint8_t *q, uint64_t len, MdState &md) {
+    PbIn in{q, q + len};
+    md.present = true;
+    while (in.p < in.end) {
+        uint32_t f, wt;
+        if (!in.key(f, wt)) return false;
+        if (f == 1 && wt == 0) {
+            if (!in.varint(md.trunc)) return false;
+        } else if (f == 2 && wt == 2) {
+            if (!in.bytes(md.extra, md.extra_len)) return false;
+        } else if (!in.skip_value(f, wt)) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// TxHeader fields (merged); WRITE: stored straight into the output header h
+// (zeroed by the caller), else only validated.  md receives the metadata.
+template <bool WRITE>
+__device__ __forceinline__ bool parse_header(const uint8_t *q, uint64_t len, mh_tx_header *h,
+                                             MdState &md) {
+    PbIn in{q, q + len};
+    while (in.p < in.end) {
+        uint32_t f, wt;
+        if (!in.key(f, wt)) return false;
+        uint64_t v;
+        const uint8_t *b;
+        uint64_t bl;
+        if (wt == 0 && (f == 1 || f == 3 || f == 4 || f == 6 || f == 8)) {
+            if (!in.varint(v)) return false;
+            if (WRITE) {
+                if (f == 1) h->id = v;
+                else if (f == 3) h->ts = (int64_t)v;
+                else if (f == 4) h->nentries = (uint32_t)v;  // int32: the low 32 bits
+                else if (f == 6) h->bl_tx_id = v;
+                else h->version = (uint32_t)v;
+            }
+        } else if (wt == 2 && (f == 2 || f == 5 || f == 7)) {
+            if (!in.bytes(b, bl)) return false;
+            if (WRITE) digest_from(b, bl, f == 2 ? h->prev_alh : (f == 5 ? h->eh : h->bl_root));
+        } else if (wt == 2 && f == 9) {
+            if (!in.bytes(b, bl) || !parse_md(b, bl, md)) return false;
+        } else if (!in.skip_value(f, wt)) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// TxMetadataFromProto + Bytes(): truncatedUptoTx (code 0, BE64) when > 0,
+// then extra (code 1, BE16 length) when 1..256 bytes (WithExtra rejects
+// longer data, and the call's error is ignored)
+__device__ __forceinline__ uint32_t md_len(const MdState &md) {
+    if (!md.present) return 0;
+    return (md.trunc > 0 ? 9u : 0u) +
+           (md.extra_len > 0 && md.extra_len <= kMaxExtra ? 3u + (uint32_t)md.extra_len : 0u);
+}
+
+__device__ void md_write(const MdState &md, uint8_t *out) {
+    uint32_t k = 0;
+    if (!md.present) return;
+    if (md.trunc > 0) {
+        out[k++] = 0;
+        for (int j = 7; j >= 0; j--) out[k++] = (uint8_t)(md.trunc >> (8 * j));
+    }
+    if (md.extra_len > 0 && md.extra_len <= kMaxExtra) {
+        out[k++] = 1;
+        out[k++] = (uint8_t)(md.extra_len >> 8);
+        out[k++] = (uint8_t)md.extra_len;
+        for (uint64_t j = 0; j < md.extra_len; j++) out[k++] = md.extra[j];
+    }
+}
+
+// One DualProofV2 message per lane.  WRITE = false: validate, count the
+// inclusion / consistency terms and the canonical metadata bytes of the two
+// headers; WRITE = true: headers, terms and metadata at the scanned offsets.
+// The two headers live in separate variables (no dynamically indexed local
+// arrays: those would go to scratch).
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_pbd_dual(uint64_t n, const uint8_t *__restrict__ msgs,
+                                                  const uint64_t *__restrict__ msg_off,
+                                                  uint64_t *__restrict__ cnt_i, uint64_t *__restrict__ cnt_c,
+                                                  uint64_t *__restrict__ cnt_m,
+                                                  const uint64_t *__restrict__ incl_off,
+                                                  const uint64_t *__restrict__ cons_off,
+                                                  const uint64_t *__restrict__ md_off,
+                                                  uint8_t *__restrict__ incl_terms,
+                                                  uint8_t *__restrict__ cons_terms,
+                                                  mh_tx_header *__restrict__ src_hdr,
+                                                  mh_tx_header *__restrict__ tgt_hdr,
+                                                  uint8_t *__restrict__ md_blob,
+                                                  int32_t *__restrict__ status) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t o0 = msg_off[p], o1 = msg_off[p + 1] >= o0 ? msg_off[p + 1] : o0;
+    mh_tx_header *hs = WRITE ? src_hdr + p : nullptr, *ht = WRITE ? tgt_hdr + p : nullptr;
+    // the write pass re-reads only what the first pass accepted: a malformed
+    // message was given no term or metadata slots and decodes to zero headers
+    const bool corrupt = WRITE && status[p] == MH_ERR_CORRUPTED_DATA;
+    if (WRITE) {
+        *hs = mh_tx_header{};
+        *ht = mh_tx_header{};
+    }
+    PbIn in{msgs + o0, corrupt ? msgs + o0 : msgs + o1};
+    MdState ms, mt;
+    bool have_s = false, have_t = false;
+    uint64_t ki = 0, kc = 0;
+    uint8_t *ti = WRITE ? incl_terms + 32 * incl_off[p] : nullptr;
+    uint8_t *tc = WRITE ? cons_terms + 32 * cons_off[p] : nullptr;
+    bool ok = true;
+    while (ok && in.p < in.end) {
+        uint32_t f, wt;
+        if (!in.key(f, wt)) {
+            ok = false;
+            break;
+        }
+        const uint8_t *b;
+        uint64_t bl;
+        if (wt == 2 && f == 1) {
+            ok = in.bytes(b, bl) && parse_header<WRITE>(b, bl, hs, ms);
+            have_s = true;
+        } else if (wt == 2 && f == 2) {
+            ok = in.bytes(b, bl) && parse_header<WRITE>(b, bl, ht, mt);
+            have_t = true;
+        } else if (wt == 2 && f == 3) {
+            ok = in.bytes(b, bl);
+            if (WRITE) digest_from(b, bl, ti + 32 * ki);
+            ki++;
+        } else if (wt == 2 && f == 4) {
+            ok = in.bytes(b, bl);
+            if (WRITE) digest_from(b, bl, tc + 32 * kc);
+            kc++;
+        } else {
+            ok = in.skip_value(f, wt);
+        }
+    }
+    if (!WRITE) {
+        const int32_t st = !ok ? MH_ERR_CORRUPTED_DATA
+                               : (!have_s || !have_t) ? MH_ERR_ILLEGAL_ARGUMENTS : MH_OK;
+        status[p] = st;
+        // a malformed message contributes no terms and no metadata
+        cnt_i[p] = ok ? ki : 0;
+        cnt_c[p] = ok ? kc : 0;
+        cnt_m[p] = ok ? md_len(ms) + md_len(mt) : 0;
+        return;
+    }
+    const uint64_t m0 = md_off[p];
+    const uint32_t ls = corrupt ? 0u : md_len(ms), lt = corrupt ? 0u : md_len(mt);
+    hs->md_off = (uint32_t)m0;
+    hs->md_len = ls;
+    ht->md_off = (uint32_t)(m0 + ls);
+    ht->md_len = lt;
+    if (ls) md_write(ms, md_blob + m0);
+    if (lt) md_write(mt, md_blob + m0 + ls);
+}
+
+}  // namespace
+
+extern "C" int mh_dual_proof_v2_pb_decode_batch(
+    mh_ctx *c, uint64_t n, const uint8_t *msgs, const uint64_t *msg_off, mh_tx_header *src_hdr,
+    mh_tx_header *tgt_hdr, uint8_t *md_blob, uint64_t *incl_off, uint8_t *incl_terms,
+    uint64_t incl_cap, uint64_t *cons_off, uint8_t *cons_terms, uint64_t cons_cap,
+    int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!msg_off || !src_hdr || !tgt_hdr || !md_blob || !incl_off || !cons_off ||
+                         !status)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) {
+            if (incl_off) incl_off[0] = 0;
+            if (cons_off) cons_off[0] = 0;
+            return MH_OK;
+        }
+        if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
+        if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        size_t scan_bytes = 0;
+        MH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (int)n, st));
+        Layout L;
+        const uint64_t b_msg = L.add(mb + 16), b_off = L.add((n + 1) * 8), b_ni = L.add(n * 8),
+                       b_nc = L.add(n * 8), b_nm = L.add(n * 8), b_io = L.add((n + 1) * 8),
+                       b_co = L.add((n + 1) * 8), b_mo = L.add((n + 1) * 8), b_st = L.add(n * 4),
+                       b_scan = L.add(scan_bytes), b_h = L.add(2 * n * sizeof(mh_tx_header)),
+                       b_md = L.add(2 * n * (uint64_t)kMdSlot);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        if (mb) MH_HIP(hipMemcpyAsync(base + b_msg, msgs + m0, mb, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_off, msg_off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const unsigned grid = (unsigned)((n + 255) / 256);
+        const uint8_t *dmsg = base + b_msg - m0;
+        uint64_t *io = (uint64_t *)(base + b_io), *co = (uint64_t *)(base + b_co),
+                 *mo = (uint64_t *)(base + b_mo);
+        hipLaunchKernelGGL(k_pbd_dual<false>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), (uint64_t *)(base + b_ni),
+                           (uint64_t *)(base + b_nc), (uint64_t *)(base + b_nm), nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        const uint64_t cnt[3] = {b_ni, b_nc, b_nm};
+        uint64_t *outs[3] = {io, co, mo};
+        for (int k = 0; k < 3; k++) {
+            MH_HIP(hipMemsetAsync(outs[k], 0, 8, st));
+            size_t sb = scan_bytes;
+            MH_HIP(hipcub::DeviceScan::InclusiveSum(base + b_scan, sb,
+                                                    (const uint64_t *)(base + cnt[k]), outs[k] + 1,
+                                                    (int)n, st));
+        }
+        uint64_t md_total = 0;
+        MH_HIP(hipMemcpyAsync(incl_off, io, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(cons_off, co, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(&md_total, mo + n, 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(status, base + b_st, n * 4, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        const uint64_t ti = incl_off[n], tc = cons_off[n];
+        if (ti > incl_cap || tc > cons_cap) return MH_ERR_BUFFER_TOO_SMALL;
+        if ((ti && !incl_terms) || (tc && !cons_terms)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        DevBuf &tb = c->s_tree;
+        MH_HIP(tb.ensure(std::max<uint64_t>(ti + tc, 1) * 32));
+        uint8_t *dti = tb.as<uint8_t>(), *dtc = dti + ti * 32;
+        hipLaunchKernelGGL(k_pbd_dual<true>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), nullptr, nullptr, nullptr, io, co, mo,
+                           dti, dtc, (mh_tx_header *)(base + b_h),
+                           (mh_tx_header *)(base + b_h) + n, base + b_md, (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        MH_HIP(hipMemcpyAsync(src_hdr, base + b_h, n * sizeof(mh_tx_header), hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(tgt_hdr, base + b_h + n * sizeof(mh_tx_header),
+                              n * sizeof(mh_tx_header), hipMemcpyDeviceToHost, st));
+        if (md_total) MH_HIP(hipMemcpyAsync(md_blob, base + b_md, md_total, hipMemcpyDeviceToHost, st));
+        if (ti) MH_HIP(hipMemcpyAsync(incl_terms, dti, ti * 32, hipMemcpyDeviceToHost, st));
+        if (tc) MH_HIP(hipMemcpyAsync(cons_terms, dtc, tc * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
+}

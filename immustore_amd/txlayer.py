@@ -357,3 +357,34 @@ def txlog_scan(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
         N.check(rc)
     k = ntx.value
     return rc, k, used.value, hd[:k], ao[:k]
+
+
+def decode_dual_proof_v2_pb(msgs, ctx: Optional[Context] = None):
+    """DualProofV2FromProto (database_protoconv.go:226-262) over many encoded
+    DualProofV2 messages, on the device -> (status[n], src TX_HEADER[n],
+    tgt TX_HEADER[n], md_blob, incl_off, incl_terms, cons_off, cons_terms);
+    the outputs are mh_verify_dual_proof_v2_batch's arguments."""
+    n = len(msgs)
+    off = np.zeros(n + 1, np.uint64)
+    if n:
+        off[1:] = np.cumsum([len(x) for x in msgs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+    sh = np.zeros(max(n, 1), TX_HEADER)
+    th = np.zeros(max(n, 1), TX_HEADER)
+    md = np.zeros(max(2 * n * 268, 1), np.uint8)
+    io = np.zeros(n + 1, np.uint64)
+    co = np.zeros(n + 1, np.uint64)
+    st = np.zeros(max(n, 1), np.int32)
+    L = N.load()
+    h = _ctx(ctx).handle
+    rc = L.mh_dual_proof_v2_pb_decode_batch(h, n, _addr(buf), _addr(off), _addr(sh), _addr(th),
+                                            _addr(md), _addr(io), None, 0, _addr(co), None, 0,
+                                            _addr(st))
+    if rc not in (0, 19):  # MH_ERR_BUFFER_TOO_SMALL: the size query
+        N.check(rc)
+    it = np.zeros((max(int(io[n]), 1), 32), np.uint8)
+    ct = np.zeros((max(int(co[n]), 1), 32), np.uint8)
+    N.check(L.mh_dual_proof_v2_pb_decode_batch(h, n, _addr(buf), _addr(off), _addr(sh), _addr(th),
+                                               _addr(md), _addr(io), _addr(it), int(io[n]),
+                                               _addr(co), _addr(ct), int(co[n]), _addr(st)))
+    return st[:n], sh[:n], th[:n], md.tobytes(), io, it[:int(io[n])], co, ct[:int(co[n])]

@@ -653,6 +653,28 @@ int mh_multi_ahtree_append_batch(mh_multi *m, const uint8_t *payloads, uint64_t 
  * status are filled and MH_ERR_BUFFER_TOO_SMALL is returned (call again with
  * a buffer of off[n] bytes). */
 
+/* The other direction, on the device: DualProofV2FromProto
+ * (database_protoconv.go:226-262, TxHeaderFromProto, TxMetadataFromProto,
+ * DigestsFromProto :293-305) over n DualProofV2 messages, message p =
+ * msgs[msg_off[p] .. msg_off[p+1]), read as protobuf-go's Unmarshal does
+ * (any field order, last scalar wins, repeated headers merged, unknown and
+ * mistyped fields skipped).  Outputs are the arguments of
+ * mh_verify_dual_proof_v2_batch: src_hdr / tgt_hdr (n each), md_blob (room for
+ * 2n x MH_MAX_TX_METADATA_LEN bytes; the canonical TxMetadata.Bytes() of
+ * every header packed in message order, source before target, located by each
+ * header's md_off / md_len), incl_off / cons_off (n + 1 each) and the
+ * terms (32 bytes each, DigestFromProto: shorter terms zero-padded, longer
+ * truncated).  status[p]: MH_OK, MH_ERR_CORRUPTED_DATA (not a valid encoding;
+ * no terms), MH_ERR_ILLEGAL_ARGUMENTS (a header missing: Go dereferences the
+ * nil header).  If incl_cap / cons_cap (terms) are below incl_off[n] /
+ * cons_off[n], only the offsets and statuses are written and
+ * MH_ERR_BUFFER_TOO_SMALL is returned.  n <= 8 013 008 (32-bit md_off). */
+int mh_dual_proof_v2_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msgs,
+                                     const uint64_t *msg_off, mh_tx_header *src_hdr,
+                                     mh_tx_header *tgt_hdr, uint8_t *md_blob, uint64_t *incl_off,
+                                     uint8_t *incl_terms, uint64_t incl_cap, uint64_t *cons_off,
+                                     uint8_t *cons_terms, uint64_t cons_cap, int32_t *status);
+
 /* InclusionProof messages (schema.proto:534-540, InclusionProofToProto
  * database_protoconv.go:115-121) of (*HTree).InclusionProof(leaf[p])
  * (htree.go:121-164) over the tree's last build; status[p] MH_OK or

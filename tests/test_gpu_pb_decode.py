@@ -1,0 +1,373 @@
+"""DualProofV2 protobuf messages decoded on the device
+(mh_dual_proof_v2_pb_decode_batch: DualProofV2FromProto, TxHeaderFromProto,
+TxMetadataFromProto, DigestsFromProto, database_protoconv.go:226-305) against
+the protobuf runtime's own parse of the same bytes (oracle/wire.py's
+descriptors of schema.proto), then fed to VerifyDualProofV2."""
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MAX_EXTRA = 256
+
+
+@pytest.fixture(scope="module")
+def m():
+    import torch  # noqa: F401
+    import immustore_amd as m
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return m
+
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def wire(orc):
+    import wire
+    return wire
+
+
+def d32(b):
+    return (bytes(b) + bytes(32))[:32]
+
+
+def _go_varints_ok(b, kind="top"):
+    """protobuf-go rejects a 10-byte varint whose last byte is above 1
+    (protowire.ConsumeVarint: errCodeOverflow); the upb runtime behind python
+    protobuf drops the excess bits instead.  This walk applies Go's rule to
+    every varint the decoder reads (keys, scalars, lengths, unknown fields
+    and groups, inside the headers and their metadata); all else is left to
+    the protobuf runtime's parse."""
+    def varint(i):
+        v = 0
+        for k in range(10):
+            if i >= len(b):
+                raise IndexError
+            c = b[i]
+            i += 1
+            if k == 9 and c > 1:
+                raise OverflowError
+            v |= (c & 0x7f) << (7 * k)
+            if not c & 0x80:
+                return v, i
+        raise OverflowError
+    try:
+        i, groups = 0, []
+        while i < len(b):
+            key, i = varint(i)
+            f, wt = key >> 3, key & 7
+            if wt == 0:
+                _, i = varint(i)
+            elif wt == 1:
+                i += 8
+            elif wt == 5:
+                i += 4
+            elif wt == 2:
+                ln, i = varint(i)
+                sub, i = b[i:i + ln], i + ln
+                nested = {"top": {1: "hdr", 2: "hdr"}, "hdr": {9: "md"}}.get(kind, {})
+                if not groups and f in nested and not _go_varints_ok(sub, nested[f]):
+                    return False
+            elif wt == 3:
+                groups.append(f)
+            elif wt == 4 and groups:
+                groups.pop()
+            if i > len(b):
+                return True  # truncated: the runtime's parse rejects it too
+        return True
+    except OverflowError:
+        return False
+    except IndexError:
+        return True
+
+
+def expect(wire, raw):
+    """What DualProofV2FromProto gives for `raw` per the protobuf runtime:
+    (status, src, tgt, incl, cons); src / tgt = dict of header fields and the
+    metadata's Bytes()."""
+    from google.protobuf.message import DecodeError
+    if not _go_varints_ok(raw):
+        return 14, None, None, [], []
+    try:
+        mm = wire.MSG["DualProofV2"].FromString(raw)
+    except DecodeError:
+        return 14, None, None, [], []
+    if not (mm.HasField("sourceTxHeader") and mm.HasField("targetTxHeader")):
+        return 2, None, None, [d32(x) for x in mm.inclusionProof], [d32(x) for x in mm.consistencyProof]
+
+    def hdr(h):
+        md = b""
+        if h.HasField("metadata"):
+            if h.metadata.truncatedTxID > 0:
+                md += b"\x00" + struct.pack(">Q", h.metadata.truncatedTxID)
+            if 0 < len(h.metadata.extra) <= MAX_EXTRA:
+                md += b"\x01" + struct.pack(">H", len(h.metadata.extra)) + h.metadata.extra
+        return {"id": h.id, "ts": h.ts, "bl_tx_id": h.blTxId, "bl_root": d32(h.blRoot),
+                "prev_alh": d32(h.prevAlh), "eh": d32(h.eH), "version": h.version & 0xFFFFFFFF,
+                "nentries": h.nentries & 0xFFFFFFFF, "md": md}
+    return (0, hdr(mm.sourceTxHeader), hdr(mm.targetTxHeader),
+            [d32(x) for x in mm.inclusionProof], [d32(x) for x in mm.consistencyProof])
+
+
+def got_hdr(r, md, k):
+    off, ln = int(r["md_off"]), int(r["md_len"])
+    return {"id": int(r["id"]), "ts": int(r["ts"]), "bl_tx_id": int(r["bl_tx_id"]),
+            "bl_root": r["bl_root"].tobytes(), "prev_alh": r["prev_alh"].tobytes(),
+            "eh": r["eh"].tobytes(), "version": int(r["version"]), "nentries": int(r["nentries"]),
+            "md": md[off:off + ln]}
+
+
+def check(wire, raws, out):
+    st, sh, th, md, io, it, co, ct = out
+    # metadata packed in message order, source before target
+    ends = [0]
+    for k in range(len(raws)):
+        assert int(sh[k]["md_off"]) == ends[-1], k
+        assert int(th[k]["md_off"]) == int(sh[k]["md_off"]) + int(sh[k]["md_len"]), k
+        ends.append(int(th[k]["md_off"]) + int(th[k]["md_len"]))
+    for k, raw in enumerate(raws):
+        est, es, et, ei, ec = expect(wire, raw)
+        assert int(st[k]) == est, (k, raw.hex())
+        if est == 14:
+            assert io[k + 1] == io[k] and co[k + 1] == co[k]
+            continue
+        assert [x.tobytes() for x in it[int(io[k]):int(io[k + 1])]] == ei, k
+        assert [x.tobytes() for x in ct[int(co[k]):int(co[k + 1])]] == ec, k
+        if est == 0:
+            assert got_hdr(sh[k], md, 2 * k) == es, k
+            assert got_hdr(th[k], md, 2 * k + 1) == et, k
+
+
+def tag(f, wt):
+    """a field key as its varint bytes"""
+    v, out = f << 3 | wt, bytearray()
+    while v >= 0x80:
+        out.append(v & 0x7f | 0x80)
+        v >>= 7
+    return bytes(out + bytes([v]))
+
+
+def random_msg(wire, rng):
+    """A DualProofV2 message with random field values, the protobuf runtime's
+    bytes, optionally with extra wire-level twists (unknown fields, a header
+    split in two occurrences, fields out of order)."""
+    M = wire.MSG
+
+    def header():
+        h = M["TxHeader"]()
+        for f, v in (("id", int(rng.integers(0, 1 << 62))), ("ts", int(rng.integers(-(1 << 40), 1 << 40))),
+                     ("blTxId", int(rng.integers(0, 1 << 40))),
+                     ("version", int(rng.choice([0, 1, 2, -1]))),
+                     ("nentries", int(rng.integers(-(1 << 31), 1 << 31)))):
+            if rng.random() < 0.85:
+                setattr(h, f, v)
+        for f in ("prevAlh", "eH", "blRoot"):
+            if rng.random() < 0.9:
+                setattr(h, f, bytes(rng.integers(0, 256, int(rng.choice([32, 32, 32, 0, 5, 40])),
+                                                 dtype=np.uint8)))
+        if rng.random() < 0.5:
+            md = M["TxMetadata"]()
+            if rng.random() < 0.6:
+                md.truncatedTxID = int(rng.integers(0, 1 << 50))
+            if rng.random() < 0.6:
+                md.extra = bytes(rng.integers(0, 256, int(rng.choice([0, 1, 100, 256, 257])),
+                                              dtype=np.uint8))
+            h.metadata.CopyFrom(md)
+        return h
+
+    mm = M["DualProofV2"]()
+    if rng.random() < 0.95:
+        mm.sourceTxHeader.CopyFrom(header())
+    if rng.random() < 0.95:
+        mm.targetTxHeader.CopyFrom(header())
+    for _ in range(int(rng.integers(0, 30))):
+        mm.inclusionProof.append(bytes(rng.integers(0, 256, int(rng.choice([32, 32, 31, 33, 0])),
+                                                    dtype=np.uint8)))
+    for _ in range(int(rng.integers(0, 30))):
+        mm.consistencyProof.append(bytes(rng.integers(0, 256, 32, dtype=np.uint8)))
+    raw = mm.SerializeToString()
+    r = rng.random()
+    if r < 0.15:
+        # unknown fields: varint, fixed64, bytes, fixed32, a group (fields 50-54)
+        raw += tag(50, 0) + bytes([0x96, 0x01]) + tag(51, 1) + bytes(8) + \
+            tag(52, 2) + bytes([3, 1, 2, 3]) + tag(53, 5) + bytes(4) + \
+            tag(54, 3) + tag(1, 0) + bytes([7]) + tag(54, 4)
+    elif r < 0.3 and mm.HasField("sourceTxHeader"):
+        # a second source header occurrence: merged into the first
+        h2 = M["TxHeader"](id=int(rng.integers(1, 1 << 30)), blRoot=bytes(range(32)))
+        b = h2.SerializeToString()
+        raw += tag(1, 2) + bytes([len(b)]) + b
+    elif r < 0.4:
+        # a known field with the wrong wire type (skipped as unknown)
+        raw = bytes([3 << 3 | 0, 5]) + raw
+    return raw
+
+
+def test_decode_random_messages_vs_protobuf(m, ctx, wire):
+    from immustore_amd import txlayer
+    rng = np.random.default_rng(2024)
+    raws = [random_msg(wire, rng) for _ in range(3000)]
+    raws += [b"", bytes([1 << 3 | 2, 0, 2 << 3 | 2, 0])]  # empty message; two empty headers
+    check(wire, raws, txlayer.decode_dual_proof_v2_pb(raws, ctx=ctx))
+
+
+def test_decode_corrupted_messages_vs_protobuf(m, ctx, wire):
+    """Truncations and byte flips: the status is CORRUPTED exactly when the
+    protobuf runtime rejects the bytes, else the fields agree."""
+    from immustore_amd import txlayer
+    rng = np.random.default_rng(7)
+    base = [random_msg(wire, rng) for _ in range(400)]
+    raws = []
+    for raw in base:
+        if not raw:
+            continue
+        b = bytearray(raw)
+        if rng.random() < 0.5:
+            raws.append(bytes(b[:int(rng.integers(0, len(b)))]))
+        else:
+            for _ in range(int(rng.integers(1, 4))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            raws.append(bytes(b))
+    raws += [bytes([0x80] * 11), bytes([0x07]), bytes([1 << 3 | 2, 200]), bytes([0, 0]),
+             tag(54, 3) + tag(1, 0) + bytes([7]), tag(54, 4), tag(1 << 29, 0) + bytes([1]), tag((1 << 29) - 1, 0) + bytes([1]),
+             tag(7, 6), tag(2, 2) + bytes([0x80] * 9 + [2])]
+    check(wire, raws, txlayer.decode_dual_proof_v2_pb(raws, ctx=ctx))
+
+
+def _canonical_md(b):
+    """TxMetadata.ReadFrom then Bytes() (tx_metadata.go:145-193): a zero
+    truncated id and an empty extra are not written back"""
+    out, i = b"", 0
+    while i < len(b):
+        if b[i] == 0:
+            v = int.from_bytes(b[i + 1:i + 9], "big")
+            out += b[i:i + 9] if v else b""
+            i += 9
+        else:
+            ln = int.from_bytes(b[i + 1:i + 3], "big")
+            out += b[i:i + 3 + ln] if ln else b""
+            i += 3 + ln
+    return out
+
+
+def _same_hdr(a, b, md, blob):
+    for f in ("id", "ts", "bl_tx_id", "version", "nentries"):
+        assert int(a[f]) == int(b[f]), f
+    for f in ("bl_root", "prev_alh", "eh"):
+        assert a[f].tobytes() == b[f].tobytes(), f
+    assert md[int(a["md_off"]):int(a["md_off"]) + int(a["md_len"])] == \
+        _canonical_md(blob[int(b["md_off"]):int(b["md_off"]) + int(b["md_len"])])
+
+
+def test_decode_device_encoded_random_headers(m, ctx, wire):
+    """Round trip at scale: 3000 DualProofV2 messages written on the device
+    (mh_ahtree_dual_proof_v2_pb_batch) from a 70 000-leaf tree and random
+    headers with every metadata shape decode to the headers and proof terms
+    they were written from."""
+    from immustore_amd import txlayer
+    from test_gpu_formats import _random_headers
+    rng = np.random.default_rng(91)
+    N_TX = 70000
+    t = m.AHtree(ctx)
+    t.append_batch(rng.integers(0, 256, (N_TX, 32), dtype=np.uint8))
+    recs, blob = _random_headers(rng, N_TX + 10)
+    tgt = rng.integers(1, N_TX + 1, 3000)
+    src = np.array([int(rng.integers(1, x + 1)) for x in tgt])
+    s, g = recs[src - 1].copy(), recs[tgt - 1].copy()
+    msgs, st = t.dual_proof_v2_pb_batch(s, g, blob)
+    assert (st == 0).all()
+    out = txlayer.decode_dual_proof_v2_pb(msgs, ctx=ctx)
+    dst, sh, th, md, io, it, co, ct = out
+    assert (dst == 0).all()
+    for k in range(len(msgs)):
+        _same_hdr(sh[k], s[k], md, blob)
+        _same_hdr(th[k], g[k], md, blob)
+    check(wire, msgs, out)  # and the terms, against the protobuf runtime
+
+
+def test_decode_then_verify_fixture_stores(m, ctx, orc, fixtures):
+    """Real immudb stores (the golden fixtures): DualProofV2 messages written on
+    the device, decoded on the device, then VerifyDualProofV2 over the decoded
+    arrays gives the oracle's verdict on the fixture's own proof (0 for every
+    proof the store emits), and a flipped term is rejected."""
+    from immustore_amd import txlayer
+    from tx_util import headers_from_fixture
+    n_ok = 0
+    for name, fx in fixtures.items():
+        pay = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
+        t = m.AHtree(ctx)
+        t.append_batch(pay)
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        cases = [(c["src"], c["tgt"]) for c in fx["dual_v2"] if c["src"] <= c["tgt"]]
+        S = np.array([a for a, _ in cases], np.uint64)
+        T = np.array([b for _, b in cases], np.uint64)
+        msgs, st = t.dual_proof_v2_pb_batch(recs[S.astype(int) - 1], recs[T.astype(int) - 1], blob)
+        assert (st == 0).all(), name
+        dst, sh, th, md, io, it, co, ct = txlayer.decode_dual_proof_v2_pb(msgs, ctx=ctx)
+        assert (dst == 0).all(), name
+        incl = [it[int(io[k]):int(io[k + 1])] for k in range(len(msgs))]
+        cons = [ct[int(co[k]):int(co[k + 1])] for k in range(len(msgs))]
+        sa = [alhs[int(x) - 1] for x in S]
+        ta = [alhs[int(x) - 1] for x in T]
+        vs = txlayer.verify_dual_proof_v2_batch(sh, th, md, incl, cons, S, T, sa, ta, ctx=ctx)
+        exp = [orc.verify_dual_proof_v2(sh[k], th[k], md, [x.tobytes() for x in incl[k]],
+                                        [x.tobytes() for x in cons[k]], int(S[k]), int(T[k]),
+                                        sa[k], ta[k]) for k in range(len(msgs))]
+        assert list(vs) == exp == [0] * len(msgs), name
+        n_ok += len(msgs)
+        flip = [k for k in range(len(msgs)) if len(incl[k])]
+        if flip:
+            k = flip[0]
+            incl[k] = incl[k].copy()
+            incl[k][0, 0] ^= 1
+            vs = txlayer.verify_dual_proof_v2_batch(sh, th, md, incl, cons, S, T, sa, ta, ctx=ctx)
+            assert vs[k] != 0 and (np.delete(vs, k) == 0).all(), name
+    assert n_ok > 10
+
+
+def test_decode_capacity_and_arguments(m, ctx, wire):
+    """The C-ABI's two phases: short term capacity -> BUFFER_TOO_SMALL with
+    the offsets and statuses filled (the size query), then the write; bad
+    offsets -> ILLEGAL_ARGUMENTS; n = 0 -> OK."""
+    from immustore_amd import _native as N
+    from immustore_amd.merkle import _addr
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(5)
+    raws = [random_msg(wire, rng) for _ in range(50)]
+    n = len(raws)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in raws])
+    buf = np.frombuffer(b"".join(raws), np.uint8).copy()
+    sh, th = np.zeros(n, TX_HEADER), np.zeros(n, TX_HEADER)
+    md = np.zeros(2 * n * 268, np.uint8)
+    io, co = np.zeros(n + 1, np.uint64), np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.int32)
+    L, h = N.load(), ctx.handle
+
+    def call(it, icap, ct, ccap, o=off):
+        return L.mh_dual_proof_v2_pb_decode_batch(h, n, _addr(buf), _addr(o), _addr(sh), _addr(th),
+                                                  _addr(md), _addr(io), _addr(it), icap, _addr(co),
+                                                  _addr(ct), ccap, _addr(st))
+    assert call(None, 0, None, 0) == 19
+    ti, tc = int(io[n]), int(co[n])
+    exp = [sum(1 for _ in wire.MSG["DualProofV2"].FromString(r).inclusionProof) for r in raws]
+    assert list(np.diff(io)) == exp and ti > 0 and tc > 0
+    it, ct = np.zeros((ti, 32), np.uint8), np.zeros((tc, 32), np.uint8)
+    assert call(it, ti - 1, ct, tc) == 19
+    assert call(it, ti, ct, tc - 1) == 19
+    assert call(it, ti, ct, tc) == 0
+    check(wire, raws, (st, sh, th, md.tobytes(), io, it, co, ct))
+    bad = off.copy()
+    bad[3], bad[4] = bad[4], bad[3]
+    if bad[3] != bad[4]:
+        assert call(it, ti, ct, tc, bad) == 2
+    assert L.mh_dual_proof_v2_pb_decode_batch(h, 0, None, _addr(off), None, None, None, _addr(io),
+                                              None, 0, _addr(co), None, 0, None) == 0
