@@ -11,6 +11,7 @@ from ._native import (MerkleError, ErrMaxWidthExceeded, ErrIllegalArguments, Err
                       ErrEmptyTree, ErrUnexistentData, ErrMetadataUnsupported,
                       ErrCannotResetToLargerSize, ErrNoDevice, ErrOutOfMemory, HipError)
 from .merkle import (Context, default_context, device_count, HTree, InclusionProof,
+                     decode_inclusion_proof_pb,
                      verify_inclusion, verify_inclusion_batch, VerifyInclusion, AHtree,
                      nodes_upto, levels_len, level_offset, ahtree_verify_inclusion,
                      ahtree_eval_inclusion, ahtree_verify_consistency, ahtree_eval_consistency,

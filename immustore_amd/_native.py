@@ -273,6 +273,7 @@ SIGNATURES = {
     "mh_commit_queue_stats": (i32, [vp, C.POINTER(u64), C.POINTER(u64)]),
     "mh_dual_proof_v2_pb_decode_batch": (i32, [vp, u64, u8p, vp, vp, vp, u8p, vp, u8p, u64, vp,
                                                u8p, u64, vp]),
+    "mh_htree_inclusion_proof_pb_decode_batch": (i32, [vp, u64, u8p, vp, vp, vp, vp, u8p, u64, vp]),
     "mh_multi_create": (i32, [i32, vp, C.POINTER(vp)]),
     "mh_multi_destroy": (i32, [vp]),
     "mh_multi_size": (i32, [vp, C.POINTER(i32)]),

@@ -236,6 +236,7 @@ int dual_proof_v2_core(mh_ctx *c, uint64_t n, const mh_tx_header *sh, const mh_t
                        const uint8_t *cons_terms, const uint64_t *src, const uint64_t *tgt,
                        const uint8_t *src_alh, const uint8_t *tgt_alh, int32_t *status,
                        bool alh_checked) {
+    MH_HIP(hipSetDevice(c->device));
     const uint64_t ni = incl_off[n] - incl_off[0], nc = cons_off[n] - cons_off[0];
     const uint64_t nh = alh_checked ? 0 : 2 * n;  // headers hashed here
     // host-built inputs first (one contiguous upload), then device-only data

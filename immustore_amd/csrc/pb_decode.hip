@@ -7,6 +7,7 @@
 //   TxHeaderFromProto     :235-247                        schema.proto:349-378
 //   TxMetadataFromProto   :249-262 (-> TxMetadata.Bytes(), tx_metadata.go:145-157)
 //   DigestFromProto / DigestsFromProto  :293-305 (copy of up to 32 bytes)
+//   InclusionProofFromProto  :123-129                    schema.proto:534-545
 //
 // proto3 wire format as protobuf-go's Unmarshal reads it: fields in any
 // order; a scalar or bytes field seen twice keeps the last value; an embedded
@@ -304,6 +305,56 @@ __global__ __launch_bounds__(256) void k_pbd_dual(uint64_t n, const uint8_t *__r
     if (lt) md_write(mt, md_blob + m0 + ls);
 }
 
+// One InclusionProof message per lane (InclusionProofFromProto,
+// database_protoconv.go:123-129): Leaf / Width are int32 on the wire and Go
+// ints after the conversion (sign-extended; stored as their 64-bit pattern).
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_pbd_incl(uint64_t n, const uint8_t *__restrict__ msgs,
+                                                  const uint64_t *__restrict__ msg_off,
+                                                  uint64_t *__restrict__ cnt,
+                                                  const uint64_t *__restrict__ term_off,
+                                                  uint8_t *__restrict__ terms,
+                                                  uint64_t *__restrict__ leaf,
+                                                  uint64_t *__restrict__ width,
+                                                  int32_t *__restrict__ status) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t o0 = msg_off[p], o1 = msg_off[p + 1] >= o0 ? msg_off[p + 1] : o0;
+    const bool corrupt = WRITE && status[p] == MH_ERR_CORRUPTED_DATA;
+    PbIn in{msgs + o0, corrupt ? msgs + o0 : msgs + o1};
+    uint64_t lf = 0, wd = 0, k = 0;
+    uint8_t *t = WRITE ? terms + 32 * term_off[p] : nullptr;
+    bool ok = true;
+    while (ok && in.p < in.end) {
+        uint32_t f, wt;
+        if (!in.key(f, wt)) {
+            ok = false;
+            break;
+        }
+        uint64_t v;
+        const uint8_t *b;
+        if (wt == 0 && (f == 1 || f == 2)) {
+            ok = in.varint(v);
+            const uint64_t x = (uint64_t)(int64_t)(int32_t)(uint32_t)v;  // int(int32)
+            if (f == 1) lf = x;
+            else wd = x;
+        } else if (wt == 2 && f == 3) {
+            ok = in.bytes(b, v);
+            if (WRITE) digest_from(b, v, t + 32 * k);
+            k++;
+        } else {
+            ok = in.skip_value(f, wt);
+        }
+    }
+    if (!WRITE) {
+        status[p] = ok ? MH_OK : MH_ERR_CORRUPTED_DATA;
+        cnt[p] = ok ? k : 0;
+        return;
+    }
+    leaf[p] = corrupt ? 0 : lf;
+    width[p] = corrupt ? 0 : wd;
+}
+
 }  // namespace
 
 extern "C" int mh_dual_proof_v2_pb_decode_batch(
@@ -382,6 +433,66 @@ extern "C" int mh_dual_proof_v2_pb_decode_batch(
         if (md_total) MH_HIP(hipMemcpyAsync(md_blob, base + b_md, md_total, hipMemcpyDeviceToHost, st));
         if (ti) MH_HIP(hipMemcpyAsync(incl_terms, dti, ti * 32, hipMemcpyDeviceToHost, st));
         if (tc) MH_HIP(hipMemcpyAsync(cons_terms, dtc, tc * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_htree_inclusion_proof_pb_decode_batch(mh_ctx *c, uint64_t n, const uint8_t *msgs,
+                                                        const uint64_t *msg_off, uint64_t *leaf,
+                                                        uint64_t *width, uint64_t *term_off,
+                                                        uint8_t *terms, uint64_t term_cap,
+                                                        int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!msg_off || !leaf || !width || !term_off || !status)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) {
+            if (term_off) term_off[0] = 0;
+            return MH_OK;
+        }
+        if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
+        if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        size_t scan_bytes = 0;
+        MH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (int)n, st));
+        Layout L;
+        const uint64_t b_msg = L.add(mb + 16), b_off = L.add((n + 1) * 8), b_cnt = L.add(n * 8),
+                       b_to = L.add((n + 1) * 8), b_st = L.add(n * 4), b_scan = L.add(scan_bytes),
+                       b_lw = L.add(2 * n * 8);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        if (mb) MH_HIP(hipMemcpyAsync(base + b_msg, msgs + m0, mb, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_off, msg_off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const unsigned grid = (unsigned)((n + 255) / 256);
+        const uint8_t *dmsg = base + b_msg - m0;
+        uint64_t *to = (uint64_t *)(base + b_to), *lw = (uint64_t *)(base + b_lw);
+        hipLaunchKernelGGL(k_pbd_incl<false>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), (uint64_t *)(base + b_cnt), nullptr,
+                           nullptr, nullptr, nullptr, (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        MH_HIP(hipMemsetAsync(to, 0, 8, st));
+        size_t sb = scan_bytes;
+        MH_HIP(hipcub::DeviceScan::InclusiveSum(base + b_scan, sb, (const uint64_t *)(base + b_cnt),
+                                                to + 1, (int)n, st));
+        MH_HIP(hipMemcpyAsync(term_off, to, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(status, base + b_st, n * 4, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        const uint64_t tt = term_off[n];
+        if (tt > term_cap) return MH_ERR_BUFFER_TOO_SMALL;
+        if (tt && !terms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        DevBuf &tb = c->s_tree;
+        MH_HIP(tb.ensure(std::max<uint64_t>(tt, 1) * 32));
+        hipLaunchKernelGGL(k_pbd_incl<true>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), nullptr, to, tb.as<uint8_t>(), lw,
+                           lw + n, (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        MH_HIP(hipMemcpyAsync(leaf, lw, n * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(width, lw + n, n * 8, hipMemcpyDeviceToHost, st));
+        if (tt) MH_HIP(hipMemcpyAsync(terms, tb.as<uint8_t>(), tt * 32, hipMemcpyDeviceToHost, st));
         MH_HIP(hipStreamSynchronize(st));
         return MH_OK;
     });

@@ -36,7 +36,10 @@ __global__ __launch_bounds__(512) void k_htree_verify(uint64_t np, const uint64_
     uint32_t d[8], calc[8], root[8];
     load_digest(digests + p * 32, d);
     leaf_hash(d, calc);
-    uint64_t i = leaf[p], r = width[p] - 1;
+    // Go's int arithmetic (htree.go:175-190): leaf / width are the bits of
+    // a Go int; a negative one (a proof decoded from the wire) takes the
+    // signed % and / (truncating), as Go does
+    int64_t i = (int64_t)leaf[p], r = (int64_t)(width[p] - 1);
     // offsets running backwards (device CSR, unchecked by the host): no terms
     const uint64_t t0 = term_off[p], t1 = max(term_off[p + 1], t0);
     for (uint64_t t = t0; t < t1; t++) {
@@ -49,8 +52,8 @@ __global__ __launch_bounds__(512) void k_htree_verify(uint64_t np, const uint64_
             rr[j] = calc_left ? term[j] : calc[j];
         }
         node_hash_tab(l, rr, calc, tab);
-        i >>= 1;
-        r >>= 1;
+        i /= 2;
+        r /= 2;
     }
     load_digest(roots + p * 32, root);
     ok[p] = (i == r) && eq8(calc, root);

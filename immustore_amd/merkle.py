@@ -259,8 +259,9 @@ def verify_inclusion_batch(proofs: Sequence[InclusionProof], digests, roots,
     n = len(proofs)
     if n == 0:
         return np.zeros(0, bool)
-    leaf = np.array([p.leaf for p in proofs], np.uint64)
-    width = np.array([p.width for p in proofs], np.uint64)
+    # Go ints: negative values travel as their 64-bit pattern
+    leaf = np.array([p.leaf & 0xFFFFFFFFFFFFFFFF for p in proofs], np.uint64)
+    width = np.array([p.width & 0xFFFFFFFFFFFFFFFF for p in proofs], np.uint64)
     off = np.zeros(n + 1, np.uint64)
     off[1:] = np.cumsum([len(p.terms) for p in proofs])
     terms = _digests([t for p in proofs for t in p.terms] or [b"\0" * 32])
@@ -282,6 +283,37 @@ def verify_inclusion(proof: Optional[InclusionProof], digest: bytes, root: bytes
 
 
 VerifyInclusion = verify_inclusion
+
+
+def decode_inclusion_proof_pb(msgs, ctx: Optional[Context] = None):
+    """InclusionProofFromProto (database_protoconv.go:123-129) over many
+    encoded InclusionProof messages, on the device -> (status[n], proofs[n]);
+    proofs[p] is an InclusionProof (Go int leaf / width, possibly negative)
+    or None where status[p] is MH_ERR_CORRUPTED_DATA."""
+    ctx = ctx or default_context()
+    n = len(msgs)
+    off = np.zeros(n + 1, np.uint64)
+    if n:
+        off[1:] = np.cumsum([len(x) for x in msgs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+    leaf, width = np.zeros(max(n, 1), np.uint64), np.zeros(max(n, 1), np.uint64)
+    to = np.zeros(n + 1, np.uint64)
+    st = np.zeros(max(n, 1), np.int32)
+    L = N.load()
+    rc = L.mh_htree_inclusion_proof_pb_decode_batch(ctx.handle, n, _addr(buf), _addr(off),
+                                                    _addr(leaf), _addr(width), _addr(to), None, 0,
+                                                    _addr(st))
+    if rc != N.MH_ERR_BUFFER_TOO_SMALL:
+        N.check(rc)
+    t = np.zeros((max(int(to[n]), 1), 32), np.uint8)
+    N.check(L.mh_htree_inclusion_proof_pb_decode_batch(ctx.handle, n, _addr(buf), _addr(off),
+                                                       _addr(leaf), _addr(width), _addr(to),
+                                                       _addr(t), int(to[n]), _addr(st)))
+    li, wi = leaf.view(np.int64), width.view(np.int64)
+    proofs = [None if st[p] else InclusionProof(int(li[p]), int(wi[p]),
+                                                [t[k].tobytes() for k in range(int(to[p]), int(to[p + 1]))])
+              for p in range(n)]
+    return st[:n], proofs
 
 
 # -------------------------------------------------------------------- ahtree

@@ -168,7 +168,8 @@ int mh_htree_levels_device(mh_htree *t, const uint8_t **dptr);
 
 /* htree.VerifyInclusion batch (htree.go:166-195; store.VerifyInclusion
  * verification.go:28-30).  Proof p has terms [term_off[p], term_off[p+1]).
- * ok[p] = 1 if it verifies.  Host pointers. */
+ * leaf / width are the bits of Go ints (values >= 2^63 are negative and take
+ * Go's signed % and /).  ok[p] = 1 if it verifies.  Host pointers. */
 int mh_htree_verify_inclusion_batch(mh_ctx *ctx, uint64_t nproofs, const uint64_t *leaf,
                                     const uint64_t *width, const uint64_t *term_off,
                                     const uint8_t *terms, const uint8_t *digests,
@@ -674,6 +675,18 @@ int mh_dual_proof_v2_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msg
                                      mh_tx_header *tgt_hdr, uint8_t *md_blob, uint64_t *incl_off,
                                      uint8_t *incl_terms, uint64_t incl_cap, uint64_t *cons_off,
                                      uint8_t *cons_terms, uint64_t cons_cap, int32_t *status);
+/* InclusionProofFromProto (database_protoconv.go:123-129) over n InclusionProof
+ * messages (msgs / msg_off as above), on the device -> the arguments of
+ * mh_htree_verify_inclusion_batch: leaf[p] / width[p] (the wire's int32 as a
+ * Go int: sign-extended, stored as its 64-bit pattern; htree verification
+ * takes them with Go's signed arithmetic), term_off (n + 1) and the terms (32
+ * bytes each, DigestFromProto).  status[p]: MH_OK or MH_ERR_CORRUPTED_DATA
+ * (no terms, leaf = width = 0).  term_cap < term_off[n]: offsets and statuses
+ * only, MH_ERR_BUFFER_TOO_SMALL. */
+int mh_htree_inclusion_proof_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msgs,
+                                             const uint64_t *msg_off, uint64_t *leaf,
+                                             uint64_t *width, uint64_t *term_off, uint8_t *terms,
+                                             uint64_t term_cap, int32_t *status);
 
 /* InclusionProof messages (schema.proto:534-540, InclusionProofToProto
  * database_protoconv.go:115-121) of (*HTree).InclusionProof(leaf[p])

@@ -299,10 +299,12 @@ int orc_htree_inclusion_proof(const uint8_t *levels, uint64_t width, uint64_t i,
 
 int orc_htree_verify_inclusion(uint64_t leaf, uint64_t width, const uint8_t *terms,
                                uint32_t nterms, const uint8_t digest[32], const uint8_t root[32]) {
-    /* htree.go:166-195 (a nil proof is modelled by the caller) */
+    /* htree.go:166-195 (a nil proof is modelled by the caller).  Leaf and
+     * Width are Go ints: signed, truncating % and / (a negative value comes
+     * from a decoded wire proof, InclusionProofFromProto) */
     uint8_t calc[32];
     leaf_hash(digest, calc);
-    uint64_t i = leaf, r = width - 1;
+    int64_t i = (int64_t)leaf, r = (int64_t)(width - 1);
     for (uint32_t t = 0; t < nterms; t++) {
         if (i % 2 == 0 && i != r)
             node_hash(calc, terms + t * 32, calc);

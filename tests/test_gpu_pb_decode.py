@@ -73,6 +73,8 @@ def _go_varints_ok(b, kind="top"):
             elif wt == 2:
                 ln, i = varint(i)
                 sub, i = b[i:i + ln], i + ln
+                # DualProofV2 ("top") -> TxHeader -> TxMetadata; "incl" (an
+                # InclusionProof) has no sub-messages
                 nested = {"top": {1: "hdr", 2: "hdr"}, "hdr": {9: "md"}}.get(kind, {})
                 if not groups and f in nested and not _go_varints_ok(sub, nested[f]):
                     return False
@@ -371,3 +373,144 @@ def test_decode_capacity_and_arguments(m, ctx, wire):
         assert call(it, ti, ct, tc, bad) == 2
     assert L.mh_dual_proof_v2_pb_decode_batch(h, 0, None, _addr(off), None, None, None, _addr(io),
                                               None, 0, _addr(co), None, 0, None) == 0
+
+
+# ------------------------------------------------------------ InclusionProof
+def go_verify_inclusion(leaf, width, terms, digest, root):
+    """htree.VerifyInclusion (htree.go:166-195) with Go's int arithmetic
+    (truncating / and %), in Python: the checker for negative leaf / width."""
+    import hashlib
+    calc = hashlib.sha256(b"\0" + digest).digest()
+    i, r = leaf, width - 1
+    tdiv = lambda x: -((-x) // 2) if x < 0 else x // 2  # noqa: E731
+    for t in terms:
+        if i % 2 == 0 and i != r:
+            calc = hashlib.sha256(b"\1" + calc + t).digest()
+        else:
+            calc = hashlib.sha256(b"\1" + t + calc).digest()
+        i, r = tdiv(i), tdiv(r)
+    return i == r and calc == root
+
+
+def random_incl_msg(wire, rng):
+    M = wire.MSG["InclusionProof"]()
+    if rng.random() < 0.9:
+        M.leaf = int(rng.choice([0, 1, 5, (1 << 31) - 1, -1, -2, -(1 << 31)]) if rng.random() < 0.3
+                     else rng.integers(0, 1 << 24))
+    if rng.random() < 0.9:
+        M.width = int(rng.choice([0, 1, 2, -1, -(1 << 31)]) if rng.random() < 0.3
+                      else rng.integers(1, 1 << 24))
+    for _ in range(int(rng.integers(0, 26))):
+        M.terms.append(bytes(rng.integers(0, 256, int(rng.choice([32, 32, 32, 0, 7, 33])),
+                                          dtype=np.uint8)))
+    raw = M.SerializeToString()
+    r = rng.random()
+    if r < 0.1:
+        raw += tag(9, 0) + bytes([1]) + tag(10, 3) + tag(1, 2) + bytes([0]) + tag(10, 4)
+    elif r < 0.2:
+        raw += tag(1, 0) + bytes([0xff] * 9 + [1])  # leaf again (last wins), 10-byte varint
+    elif r < 0.25:
+        raw = tag(3, 0) + bytes([3]) + raw  # terms with the wrong wire type: skipped
+    return raw
+
+
+def expect_incl(wire, raw):
+    from google.protobuf.message import DecodeError
+    if not _go_varints_ok(raw, "incl"):
+        return 14, None
+    try:
+        mm = wire.MSG["InclusionProof"].FromString(raw)
+    except DecodeError:
+        return 14, None
+    return 0, (mm.leaf, mm.width, [d32(x) for x in mm.terms])
+
+
+def test_inclusion_decode_random_vs_protobuf(m, ctx, wire):
+    rng = np.random.default_rng(404)
+    raws = [random_incl_msg(wire, rng) for _ in range(3000)]
+    for raw in list(raws[:600]):
+        b = bytearray(raw or b"\x08")
+        if rng.random() < 0.5:
+            raws.append(bytes(b[:int(rng.integers(0, len(b)))]))
+        else:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            raws.append(bytes(b))
+    raws += [b"", tag(1, 0) + bytes([0x80] * 9 + [2]), tag(2, 0) + bytes([0xff] * 5 + [0x0f])]
+    st, proofs = m.decode_inclusion_proof_pb(raws, ctx=ctx)
+    seen = set()
+    for k, raw in enumerate(raws):
+        est, e = expect_incl(wire, raw)
+        assert int(st[k]) == est, (k, raw.hex())
+        seen.add(est)
+        if est == 0:
+            p = proofs[k]
+            assert (p.leaf, p.width, p.terms) == e, k
+        else:
+            assert proofs[k] is None
+    assert seen == {0, 14}
+
+
+def test_inclusion_decode_then_verify(m, ctx, orc):
+    """InclusionProof messages written on the device (HTree.inclusion_proof_pb_batch)
+    decode back to the proofs the tree gives, and every one verifies on the
+    device; a flipped term or a wrong leaf does not."""
+    rng = np.random.default_rng(8)
+    for w in [1, 2, 3, 1000, (1 << 17) + 5]:
+        d = rng.integers(0, 256, (w, 32), dtype=np.uint8)
+        h = m.HTree(w, ctx)
+        h.build_with(d)
+        root = h.root()
+        leaves = np.concatenate([rng.integers(0, w, 300), [0, w - 1]]).astype(np.uint64)
+        msgs, st = h.inclusion_proof_pb_batch(leaves)
+        assert (st == 0).all()
+        dst, proofs = m.decode_inclusion_proof_pb(msgs, ctx=ctx)
+        assert (dst == 0).all()
+        for k in (0, 1, len(leaves) - 1):
+            want = h.inclusion_proof(int(leaves[k]))
+            assert (proofs[k].leaf, proofs[k].width, proofs[k].terms) == (want.leaf, want.width, want.terms)
+        dig = d[leaves.astype(int)]
+        ok = m.verify_inclusion_batch(proofs, dig, [root] * len(proofs), ctx=ctx)
+        assert ok.all(), w
+        if w > 2:
+            bad = [m.InclusionProof(p.leaf, p.width, [bytes([p.terms[0][0] ^ 1]) + p.terms[0][1:]] + p.terms[1:])
+                   for p in proofs[:20]]
+            bad += [m.InclusionProof(p.leaf ^ 1, p.width, p.terms) for p in proofs[20:40]]
+            # a changed leaf can still verify where Go's walk takes the same
+            # branches (e.g. leaf 3 of width 3): the restatement decides
+            exp = [go_verify_inclusion(p.leaf, p.width, p.terms, dig[k].tobytes(), root)
+                   for k, p in enumerate(bad)]
+            assert not any(exp[:20])
+            assert list(m.verify_inclusion_batch(bad, dig[:40], [root] * 40, ctx=ctx)) == exp
+
+
+def test_inclusion_verify_negative_leaf_width(m, ctx, orc, wire):
+    """Wire proofs may carry negative int32 leaf / width (Go ints after
+    InclusionProofFromProto); VerifyInclusion then runs Go's signed arithmetic.
+    Roots are computed with the Python restatement, so some of these verify only
+    under signed semantics (leaf -2, width 1, two terms)."""
+    import hashlib
+    rng = np.random.default_rng(12)
+    cases = []
+    for leaf, width, nt in [(-2, 1, 2), (-1, 0, 1), (-5, -3, 3), (-(1 << 31), 4, 31), (3, -7, 4),
+                            (-2, 1, 1), (6, 7, 3), (-3, -3, 2)]:
+        digest = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        terms = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(nt)]
+        # the root the proof's own hash walk yields
+        calc = hashlib.sha256(b"\0" + digest).digest()
+        i, r = leaf, width - 1
+        for t in terms:
+            calc = hashlib.sha256(b"\1" + (calc + t if i % 2 == 0 and i != r else t + calc)).digest()
+            i, r = (-((-i) // 2) if i < 0 else i // 2), (-((-r) // 2) if r < 0 else r // 2)
+        for root in (calc, bytes(32)):
+            cases.append((leaf, width, terms, digest, root))
+    msgs = [wire.MSG["InclusionProof"](leaf=c[0], width=c[1], terms=c[2]).SerializeToString()
+            for c in cases]
+    st, proofs = m.decode_inclusion_proof_pb(msgs, ctx=ctx)
+    assert (st == 0).all()
+    assert [(p.leaf, p.width) for p in proofs] == [(c[0], c[1]) for c in cases]
+    ok = m.verify_inclusion_batch(proofs, [c[3] for c in cases], [c[4] for c in cases], ctx=ctx)
+    exp = [go_verify_inclusion(*c) for c in cases]
+    orc_ok = [orc.htree_verify_inclusion(c[0] & 0xFFFFFFFFFFFFFFFF, c[1] & 0xFFFFFFFFFFFFFFFF,
+                                         c[2], c[3], c[4]) for c in cases]
+    assert list(ok) == exp == orc_ok
+    assert exp[0] and sum(exp) >= 4  # (-2, 1) verifies: signed arithmetic
