@@ -8,6 +8,8 @@
 //   TxMetadataFromProto   :249-262 (-> TxMetadata.Bytes(), tx_metadata.go:145-157)
 //   DigestFromProto / DigestsFromProto  :293-305 (copy of up to 32 bytes)
 //   InclusionProofFromProto  :123-129                    schema.proto:534-545
+//   DualProofFromProto (v1)  :213-224, LinearProofFromProto :264-270,
+//   LinearAdvanceProofFromProto :272-287                 schema.proto:388-434
 //
 // proto3 wire format as protobuf-go's Unmarshal reads it: fields in any
 // order; a scalar or bytes field seen twice keeps the last value; an embedded
@@ -34,7 +36,7 @@ constexpr uint32_t kMaxExtra = 256;                    // maxExtraLen, tx_metada
 
 struct PbIn {
     const uint8_t *p, *end;
-    __device__ bool varint(uint64_t &v) {
+    __device__ __forceinline__ bool varint(uint64_t &v) {
         v = 0;
         for (int i = 0; i < 10; i++) {
             if (p >= end) return false;
@@ -45,18 +47,18 @@ struct PbIn {
         }
         return false;
     }
-    __device__ bool bytes(const uint8_t *&q, uint64_t &len) {
+    __device__ __forceinline__ bool bytes(const uint8_t *&q, uint64_t &len) {
         if (!varint(len) || len > (uint64_t)(end - p)) return false;
         q = p;
         p += len;
         return true;
     }
-    __device__ bool skip(uint64_t n) {
+    __device__ __forceinline__ bool skip(uint64_t n) {
         if (n > (uint64_t)(end - p)) return false;
         p += n;
         return true;
     }
-    __device__ bool key(uint32_t &field, uint32_t &wt) {
+    __device__ __forceinline__ bool key(uint32_t &field, uint32_t &wt) {
         uint64_t k;
         if (!varint(k)) return false;
         field = (uint32_t)(k >> 3);
@@ -207,7 +209,7 @@ __device__ __forceinline__ uint32_t md_len(const MdState &md) {
            (md.extra_len > 0 && md.extra_len <= kMaxExtra ? 3u + (uint32_t)md.extra_len : 0u);
 }
 
-__device__ void md_write(const MdState &md, uint8_t *out) {
+__device__ void md_write(const MdState md, uint8_t *out) {  // by value: keeps the caller's state out of scratch
     uint32_t k = 0;
     if (!md.present) return;
     if (md.trunc > 0) {
@@ -355,6 +357,155 @@ __global__ __launch_bounds__(256) void k_pbd_incl(uint64_t n, const uint8_t *__r
     width[p] = corrupt ? 0 : wd;
 }
 
+// ---------------------------------------------------------------- DualProof (v1)
+// DualProofFromProto (database_protoconv.go:213-224) with LinearProofFromProto
+// (:264-270; not nil-checked: a message without linearProof panics in Go ->
+// MH_ERR_ILLEGAL_ARGUMENTS) and LinearAdvanceProofFromProto (:272-287; nil ->
+// has_advance 0; only the nested InclusionProofs' terms are kept).
+enum : int { kI = 0, kC, kL, kLin, kAdv, kQ, kQT, kMd, kCounts };  // per-message counts
+
+struct Dual1Out {  // device-side outputs of the write pass
+    const uint64_t *off[kCounts];  // scanned offsets (n + 1 each)
+    uint8_t *terms[5];             // incl, cons, last, linear, advance
+    uint8_t *qterms;               // nested inclusion proofs' terms
+    uint64_t *qoff;                // nested proofs' term offsets
+    mh_tx_header *src_hdr, *tgt_hdr;
+    uint8_t *md_blob, *tbl_alh, *has_lin, *has_adv;
+    uint64_t *lin_src, *lin_tgt;
+};
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_pbd_dual1(uint64_t n, const uint8_t *__restrict__ msgs,
+                                                   const uint64_t *__restrict__ msg_off,
+                                                   uint64_t *__restrict__ cnt,  // kCounts x n
+                                                   Dual1Out o, int32_t *__restrict__ status) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t o0 = msg_off[p], o1 = msg_off[p + 1] >= o0 ? msg_off[p + 1] : o0;
+    const bool corrupt = WRITE && status[p] == MH_ERR_CORRUPTED_DATA;
+    mh_tx_header *hs = WRITE ? o.src_hdr + p : nullptr, *ht = WRITE ? o.tgt_hdr + p : nullptr;
+    if (WRITE) {
+        *hs = mh_tx_header{};
+        *ht = mh_tx_header{};
+        uint2 *z = (uint2 *)(o.tbl_alh + 32 * p);
+        for (int i = 0; i < 4; i++) z[i] = make_uint2(0, 0);
+    }
+    PbIn in{msgs + o0, corrupt ? msgs + o0 : msgs + o1};
+    MdState ms, mt;
+    bool have_s = false, have_t = false, have_lin = false, have_adv = false;
+    // running counts (plain scalars: an array or a capturing lambda here sends
+    // the readers to scratch)
+    uint64_t ki = 0, kc = 0, kl = 0, kln = 0, ka = 0, kq = 0, kqt = 0;
+    uint64_t lsrc = 0, ltgt = 0;
+    bool ok = true;
+#define PBD_TERM(J, CNT, B, BL)                                                          \
+    do {                                                                                 \
+        if (WRITE) digest_from(B, BL, o.terms[J] + 32 * (o.off[J][p] + CNT));            \
+        CNT++;                                                                           \
+    } while (0)
+    while (ok && in.p < in.end) {
+        uint32_t f, wt;
+        if (!in.key(f, wt)) {
+            ok = false;
+            break;
+        }
+        const uint8_t *b;
+        uint64_t bl;
+        if (wt == 2 && f == 1) {
+            ok = in.bytes(b, bl) && parse_header<WRITE>(b, bl, hs, ms);
+            have_s = true;
+        } else if (wt == 2 && f == 2) {
+            ok = in.bytes(b, bl) && parse_header<WRITE>(b, bl, ht, mt);
+            have_t = true;
+        } else if (wt == 2 && f == 3) {
+            if ((ok = in.bytes(b, bl))) PBD_TERM(kI, ki, b, bl);
+        } else if (wt == 2 && f == 4) {
+            if ((ok = in.bytes(b, bl))) PBD_TERM(kC, kc, b, bl);
+        } else if (wt == 2 && f == 5) {
+            if ((ok = in.bytes(b, bl)) && WRITE) digest_from(b, bl, o.tbl_alh + 32 * p);
+        } else if (wt == 2 && f == 6) {
+            if ((ok = in.bytes(b, bl))) PBD_TERM(kL, kl, b, bl);
+        } else if (wt == 2 && f == 7) {  // LinearProof (merged)
+            have_lin = true;
+            if (!(ok = in.bytes(b, bl))) break;
+            PbIn li{b, b + bl};
+            while (ok && li.p < li.end) {
+                uint32_t g, gt;
+                if (!li.key(g, gt)) {
+                    ok = false;
+                    break;
+                }
+                const uint8_t *c;
+                uint64_t cl;
+                if (gt == 0 && g == 1) ok = li.varint(lsrc);
+                else if (gt == 0 && g == 2) ok = li.varint(ltgt);
+                else if (gt == 2 && g == 3) {
+                    if ((ok = li.bytes(c, cl))) PBD_TERM(kLin, kln, c, cl);
+                } else ok = li.skip_value(g, gt);
+            }
+        } else if (wt == 2 && f == 8) {  // LinearAdvanceProof (merged)
+            have_adv = true;
+            if (!(ok = in.bytes(b, bl))) break;
+            PbIn ai{b, b + bl};
+            while (ok && ai.p < ai.end) {
+                uint32_t g, gt;
+                if (!ai.key(g, gt)) {
+                    ok = false;
+                    break;
+                }
+                const uint8_t *c;
+                uint64_t cl;
+                if (gt == 2 && g == 1) {
+                    if ((ok = ai.bytes(c, cl))) PBD_TERM(kAdv, ka, c, cl);
+                } else if (gt == 2 && g == 2) {  // one more InclusionProof: its terms
+                    if (!(ok = ai.bytes(c, cl))) break;
+                    if (WRITE) o.qoff[o.off[kQ][p] + kq] = o.off[kQT][p] + kqt;
+                    kq++;
+                    PbIn qi{c, c + cl};
+                    while (ok && qi.p < qi.end) {
+                        uint32_t h, htp;
+                        if (!qi.key(h, htp)) {
+                            ok = false;
+                            break;
+                        }
+                        const uint8_t *d;
+                        uint64_t dl;
+                        if (htp == 2 && h == 3) {
+                            if ((ok = qi.bytes(d, dl))) {
+                                if (WRITE) digest_from(d, dl, o.qterms + 32 * (o.off[kQT][p] + kqt));
+                                kqt++;
+                            }
+                        } else ok = qi.skip_value(h, htp);  // leaf / width: not kept
+                    }
+                } else ok = ai.skip_value(g, gt);
+            }
+        } else {
+            ok = in.skip_value(f, wt);
+        }
+    }
+#undef PBD_TERM
+    if (!WRITE) {
+        status[p] = !ok ? MH_ERR_CORRUPTED_DATA
+                        : (!have_s || !have_t || !have_lin) ? MH_ERR_ILLEGAL_ARGUMENTS : MH_OK;
+        const uint64_t v[kCounts] = {ki, kc, kl, kln, ka, kq, kqt, md_len(ms) + md_len(mt)};
+#pragma unroll
+        for (int j = 0; j < kCounts; j++) cnt[(uint64_t)j * n + p] = ok ? v[j] : 0;
+        return;
+    }
+    o.has_lin[p] = !corrupt && have_lin;
+    o.has_adv[p] = !corrupt && have_adv;
+    o.lin_src[p] = corrupt ? 0 : lsrc;
+    o.lin_tgt[p] = corrupt ? 0 : ltgt;
+    const uint64_t m0 = o.off[kMd][p];
+    const uint32_t ls = corrupt ? 0u : md_len(ms), lt = corrupt ? 0u : md_len(mt);
+    hs->md_off = (uint32_t)m0;
+    hs->md_len = ls;
+    ht->md_off = (uint32_t)(m0 + ls);
+    ht->md_len = lt;
+    if (ls) md_write(ms, o.md_blob + m0);
+    if (lt) md_write(mt, o.md_blob + m0 + ls);
+}
+
 }  // namespace
 
 extern "C" int mh_dual_proof_v2_pb_decode_batch(
@@ -494,6 +645,135 @@ extern "C" int mh_htree_inclusion_proof_pb_decode_batch(mh_ctx *c, uint64_t n, c
         MH_HIP(hipMemcpyAsync(width, lw + n, n * 8, hipMemcpyDeviceToHost, st));
         if (tt) MH_HIP(hipMemcpyAsync(terms, tb.as<uint8_t>(), tt * 32, hipMemcpyDeviceToHost, st));
         MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_dual_proof_pb_decode_batch(mh_ctx *c, uint64_t n, const uint8_t *msgs,
+                                             const uint64_t *msg_off, mh_dual_proof_decoded *out,
+                                             int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!c || !out) return MH_ERR_ILLEGAL_ARGUMENTS;
+        uint64_t *offs[kCounts - 1] = {out->incl_off,   out->cons_off,           out->last_off,
+                                       out->linear_off, out->advance_off,        out->advance_incl_first,
+                                       nullptr};  // nested term offsets: advance_incl_off below
+        if (n && (!msg_off || !status || !out->src_hdr || !out->tgt_hdr || !out->md_blob ||
+                  !out->target_bl_tx_alh || !out->has_linear || !out->linear_src ||
+                  !out->linear_tgt || !out->has_advance || !out->advance_incl_off))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        for (int j = 0; j < kQT; j++)
+            if (!offs[j]) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) {
+            for (int j = 0; j < kQT; j++) offs[j][0] = 0;
+            if (out->advance_incl_off) out->advance_incl_off[0] = 0;
+            out->nested_proofs = out->nested_terms = 0;
+            return MH_OK;
+        }
+        if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
+        if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        size_t scan_bytes = 0;
+        MH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (int)n, st));
+        Layout L;
+        const uint64_t b_msg = L.add(mb + 16), b_off = L.add((n + 1) * 8),
+                       b_cnt = L.add(kCounts * n * 8), b_so = L.add(kCounts * (n + 1) * 8),
+                       b_st = L.add(n * 4), b_scan = L.add(scan_bytes),
+                       b_h = L.add(2 * n * sizeof(mh_tx_header)), b_md = L.add(2 * n * (uint64_t)kMdSlot),
+                       b_tba = L.add(n * 32), b_flags = L.add(2 * n), b_ls = L.add(2 * n * 8);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        if (mb) MH_HIP(hipMemcpyAsync(base + b_msg, msgs + m0, mb, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_off, msg_off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+        const unsigned grid = (unsigned)((n + 255) / 256);
+        const uint8_t *dmsg = base + b_msg - m0;
+        uint64_t *cnt = (uint64_t *)(base + b_cnt), *so = (uint64_t *)(base + b_so);
+        hipLaunchKernelGGL(k_pbd_dual1<false>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), cnt, Dual1Out{},
+                           (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        for (int j = 0; j < kCounts; j++) {
+            uint64_t *sj = so + (uint64_t)j * (n + 1);
+            MH_HIP(hipMemsetAsync(sj, 0, 8, st));
+            size_t sb = scan_bytes;
+            MH_HIP(hipcub::DeviceScan::InclusiveSum(base + b_scan, sb, (const uint64_t *)(cnt + j * n),
+                                                    sj + 1, (int)n, st));
+        }
+        for (int j = 0; j < kQT; j++)
+            MH_HIP(hipMemcpyAsync(offs[j], so + (uint64_t)j * (n + 1), (n + 1) * 8,
+                                  hipMemcpyDeviceToHost, st));
+        uint64_t tot[2] = {0, 0};  // nested terms, metadata bytes
+        MH_HIP(hipMemcpyAsync(&tot[0], so + (uint64_t)kQT * (n + 1) + n, 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(&tot[1], so + (uint64_t)kMd * (n + 1) + n, 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(status, base + b_st, n * 4, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        const uint64_t caps[kCounts - 1] = {out->incl_cap,   out->cons_cap,        out->last_cap,
+                                            out->linear_cap, out->advance_cap,     out->advance_incl_cap,
+                                            out->advance_incl_terms_cap};
+        uint8_t *hterms[5] = {out->incl_terms, out->cons_terms, out->last_terms, out->linear_terms,
+                              out->advance_terms};
+        uint64_t totals[kCounts - 1];
+        for (int j = 0; j < kQT; j++) totals[j] = offs[j][n];
+        totals[kQT] = tot[0];
+        out->nested_proofs = totals[kQ];
+        out->nested_terms = totals[kQT];
+        for (int j = 0; j < kCounts - 1; j++)
+            if (totals[j] > caps[j]) return MH_ERR_BUFFER_TOO_SMALL;
+        for (int j = 0; j < 5; j++)
+            if (totals[j] && !hterms[j]) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (totals[kQT] && !out->advance_incl_terms) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // device term area: the five lists, the nested terms, the nested offsets
+        uint64_t tpos[6], tall = 0;
+        for (int j = 0; j < 5; j++) {
+            tpos[j] = tall;
+            tall += totals[j];
+        }
+        tpos[5] = tall;
+        tall += totals[kQT];
+        const uint64_t nq = totals[kQ];
+        DevBuf &tb = c->s_tree;
+        MH_HIP(tb.ensure(tall * 32 + (nq + 1) * 8 + 8));
+        uint8_t *dt = tb.as<uint8_t>();
+        uint64_t *dq = (uint64_t *)(dt + tall * 32);
+        Dual1Out o;
+        for (int j = 0; j < kCounts; j++) o.off[j] = so + (uint64_t)j * (n + 1);
+        for (int j = 0; j < 5; j++) o.terms[j] = dt + tpos[j] * 32;
+        o.qterms = dt + tpos[5] * 32;
+        o.qoff = dq;
+        o.src_hdr = (mh_tx_header *)(base + b_h);
+        o.tgt_hdr = o.src_hdr + n;
+        o.md_blob = base + b_md;
+        o.tbl_alh = base + b_tba;
+        o.has_lin = base + b_flags;
+        o.has_adv = base + b_flags + n;
+        o.lin_src = (uint64_t *)(base + b_ls);
+        o.lin_tgt = o.lin_src + n;
+        hipLaunchKernelGGL(k_pbd_dual1<true>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), nullptr, o, (int32_t *)(base + b_st));
+        MH_HIP(hipGetLastError());
+        const size_t hb = n * sizeof(mh_tx_header);
+        MH_HIP(hipMemcpyAsync(out->src_hdr, base + b_h, hb, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->tgt_hdr, base + b_h + hb, hb, hipMemcpyDeviceToHost, st));
+        if (tot[1]) MH_HIP(hipMemcpyAsync(out->md_blob, base + b_md, tot[1], hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->target_bl_tx_alh, base + b_tba, n * 32, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->has_linear, base + b_flags, n, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->has_advance, base + b_flags + n, n, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->linear_src, base + b_ls, n * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out->linear_tgt, base + b_ls + n * 8, n * 8, hipMemcpyDeviceToHost, st));
+        for (int j = 0; j < 5; j++)
+            if (totals[j])
+                MH_HIP(hipMemcpyAsync(hterms[j], dt + tpos[j] * 32, totals[j] * 32,
+                                      hipMemcpyDeviceToHost, st));
+        if (totals[kQT])
+            MH_HIP(hipMemcpyAsync(out->advance_incl_terms, dt + tpos[5] * 32, totals[kQT] * 32,
+                                  hipMemcpyDeviceToHost, st));
+        if (nq) MH_HIP(hipMemcpyAsync(out->advance_incl_off, dq, nq * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        out->advance_incl_off[nq] = totals[kQT];
         return MH_OK;
     });
 }

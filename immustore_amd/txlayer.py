@@ -388,3 +388,96 @@ def decode_dual_proof_v2_pb(msgs, ctx: Optional[Context] = None):
                                                _addr(md), _addr(io), _addr(it), int(io[n]),
                                                _addr(co), _addr(ct), int(co[n]), _addr(st)))
     return st[:n], sh[:n], th[:n], md.tobytes(), io, it[:int(io[n])], co, ct[:int(co[n])]
+
+
+class _DualProofDecoded(C.Structure):
+    """mirror of mh_dual_proof_decoded (include/immustore_merkle.h)"""
+    _fields_ = [(f, C.c_void_p) for f in (
+        "src_hdr", "tgt_hdr", "md_blob", "target_bl_tx_alh", "has_linear", "linear_src",
+        "linear_tgt", "has_advance", "incl_off", "cons_off", "last_off", "linear_off",
+        "advance_off", "advance_incl_first", "advance_incl_off", "incl_terms", "cons_terms",
+        "last_terms", "linear_terms", "advance_terms", "advance_incl_terms")] + \
+        [(f, C.c_uint64) for f in ("incl_cap", "cons_cap", "last_cap", "linear_cap", "advance_cap",
+                                   "advance_incl_cap", "advance_incl_terms_cap", "nested_proofs",
+                                   "nested_terms")]
+
+
+_TERM_LISTS = ("incl", "cons", "last", "linear", "advance")
+
+
+def decode_dual_proof_pb(msgs, ctx: Optional[Context] = None):
+    """DualProofFromProto (v1, database_protoconv.go:213-287) over many encoded
+    DualProof messages, on the device -> (status[n], dict of the
+    mh_dual_proof_batch arrays: src_hdr, tgt_hdr, md_blob, target_bl_tx_alh,
+    has_linear, linear_src, linear_tgt, has_advance, <list>_off / <list>_terms
+    for incl, cons, last, linear, advance, advance_incl_first,
+    advance_incl_off, advance_incl_terms)."""
+    n = len(msgs)
+    off = np.zeros(n + 1, np.uint64)
+    if n:
+        off[1:] = np.cumsum([len(x) for x in msgs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+    m = max(n, 1)
+    a = {"src_hdr": np.zeros(m, TX_HEADER), "tgt_hdr": np.zeros(m, TX_HEADER),
+         "md_blob": np.zeros(max(2 * n * 268, 1), np.uint8),
+         "target_bl_tx_alh": np.zeros((m, 32), np.uint8), "has_linear": np.zeros(m, np.uint8),
+         "linear_src": np.zeros(m, np.uint64), "linear_tgt": np.zeros(m, np.uint64),
+         "has_advance": np.zeros(m, np.uint8), "advance_incl_first": np.zeros(n + 1, np.uint64),
+         "advance_incl_off": np.zeros(1, np.uint64)}
+    for t in _TERM_LISTS:
+        a[t + "_off"] = np.zeros(n + 1, np.uint64)
+    st = np.zeros(m, np.int32)
+    L, h = N.load(), _ctx(ctx).handle
+
+    def call(caps):
+        for t in _TERM_LISTS + ("advance_incl",):
+            a[t + "_terms"] = np.zeros((max(caps.get(t, 0), 1), 32), np.uint8)
+        a["advance_incl_off"] = np.zeros(caps.get("nested", 0) + 1, np.uint64)
+        d = _DualProofDecoded(*[_addr(a[f]) for f, _ in _DualProofDecoded._fields_[:21]],
+                              *[caps.get(t, 0) for t in _TERM_LISTS],
+                              caps.get("nested", 0), caps.get("advance_incl", 0), 0, 0)
+        rc = L.mh_dual_proof_pb_decode_batch(h, n, _addr(buf), _addr(off), C.byref(d), _addr(st))
+        return rc, d
+
+    rc, d = call({})
+    if rc == N.MH_ERR_BUFFER_TOO_SMALL:
+        caps = {t: int(a[t + "_off"][n]) for t in _TERM_LISTS}
+        caps["nested"], caps["advance_incl"] = int(d.nested_proofs), int(d.nested_terms)
+        rc, d = call(caps)
+    N.check(rc)
+    for t in _TERM_LISTS:
+        a[t + "_terms"] = a[t + "_terms"][:int(a[t + "_off"][n])]
+    a["advance_incl_terms"] = a["advance_incl_terms"][:int(d.nested_terms)]
+    for f in ("src_hdr", "tgt_hdr", "target_bl_tx_alh", "has_linear", "linear_src", "linear_tgt",
+              "has_advance"):
+        a[f] = a[f][:n]
+    return st[:n], a
+
+
+def verify_decoded_dual_proof_batch(dec, src, tgt, src_alh, tgt_alh,
+                                    ctx: Optional[Context] = None) -> np.ndarray:
+    """VerifyDualProof (v1) straight over decode_dual_proof_pb's arrays -> ok[n]."""
+    n = dec["src_hdr"].size
+    if n == 0:
+        return np.zeros(0, bool)
+    keep = []
+
+    def k(x):
+        x = np.ascontiguousarray(x) if len(x) else np.zeros(32, np.uint8)
+        keep.append(x)
+        return _addr(x)
+
+    s_, t_ = np.asarray(src, np.uint64), np.asarray(tgt, np.uint64)
+    sa, ta = _d32(src_alh, n), _d32(tgt_alh, n)
+    b = _DualProofBatch(n, k(dec["src_hdr"]), k(dec["tgt_hdr"]), k(dec["md_blob"]),
+                        dec["md_blob"].size, k(dec["incl_off"]), k(dec["incl_terms"]),
+                        k(dec["cons_off"]), k(dec["cons_terms"]), k(dec["target_bl_tx_alh"]),
+                        k(dec["last_off"]), k(dec["last_terms"]), k(dec["has_linear"]),
+                        k(dec["linear_src"]), k(dec["linear_tgt"]), k(dec["linear_off"]),
+                        k(dec["linear_terms"]), k(dec["has_advance"]), k(dec["advance_off"]),
+                        k(dec["advance_terms"]), k(dec["advance_incl_first"]),
+                        k(dec["advance_incl_off"]), k(dec["advance_incl_terms"]), k(s_), k(t_),
+                        k(sa), k(ta))
+    ok = np.zeros(n, np.uint8)
+    N.check(N.load().mh_verify_dual_proof_batch(_ctx(ctx).handle, C.byref(b), _addr(ok)))
+    return ok.astype(bool)

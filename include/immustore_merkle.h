@@ -478,6 +478,39 @@ typedef struct mh_dual_proof_batch {
 } mh_dual_proof_batch;
 int mh_verify_dual_proof_batch(mh_ctx *ctx, const mh_dual_proof_batch *b, uint8_t *ok);
 
+/* The wire side of v1: DualProofFromProto (database_protoconv.go:213-224,
+ * LinearProofFromProto :264-270, LinearAdvanceProofFromProto :272-287) over n
+ * DualProof messages msgs[msg_off[p] .. msg_off[p+1]), on the device, into the
+ * arrays of mh_dual_proof_batch (same names and layout; tx metadata packed into
+ * md_blob as for mh_dual_proof_v2_pb_decode_batch).  status[p]: MH_OK;
+ * MH_ERR_CORRUPTED_DATA (not a valid encoding: zero headers, no terms);
+ * MH_ERR_ILLEGAL_ARGUMENTS (a header or the linear proof missing: Go's
+ * conversion dereferences them).  Capacities are in terms, advance_incl_cap in
+ * nested InclusionProofs; when one is short the n + 1 offset arrays and the
+ * statuses are written and MH_ERR_BUFFER_TOO_SMALL is returned (the size query;
+ * nested_proofs / nested_terms report the nested totals on every return). */
+typedef struct mh_dual_proof_decoded {
+    mh_tx_header *src_hdr;        /* n */
+    mh_tx_header *tgt_hdr;        /* n */
+    uint8_t *md_blob;             /* room for 2n x MH_MAX_TX_METADATA_LEN */
+    uint8_t *target_bl_tx_alh;    /* n x 32 */
+    uint8_t *has_linear;          /* n */
+    uint64_t *linear_src;         /* n */
+    uint64_t *linear_tgt;         /* n */
+    uint8_t *has_advance;         /* n */
+    uint64_t *incl_off, *cons_off, *last_off, *linear_off, *advance_off; /* n + 1 each */
+    uint64_t *advance_incl_first; /* n + 1 */
+    uint64_t *advance_incl_off;   /* advance_incl_cap + 1 */
+    uint8_t *incl_terms, *cons_terms, *last_terms, *linear_terms, *advance_terms;
+    uint8_t *advance_incl_terms;
+    uint64_t incl_cap, cons_cap, last_cap, linear_cap, advance_cap;
+    uint64_t advance_incl_cap, advance_incl_terms_cap;
+    uint64_t nested_proofs, nested_terms; /* out */
+} mh_dual_proof_decoded;
+int mh_dual_proof_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msgs,
+                                  const uint64_t *msg_off, mh_dual_proof_decoded *out,
+                                  int32_t *status);
+
 /* Tx-log read path (Tx.readFrom tx.go:388-630: readHeader, readEntry,
  * buildAndValidateHtree) over buf = back-to-back tx records as written by
  * immustore.go:1812-1924.  Parses up to max_txs records, stopping at id 0 (a

@@ -14,6 +14,8 @@ with the C oracle (oracle.py) the way the Go server does, and serialises it:
   DualProofV2     schema.proto:437-445, DualProofV2ToProto    database_protoconv.go:152-159
   TxHeader        schema.proto:349-367, TxHeaderToProto       database_protoconv.go:161-177
   TxMetadata      schema.proto:380-383, TxMetadataToProto     database_protoconv.go:179-193
+  DualProof (v1), LinearProof, LinearAdvanceProof  schema.proto:388-434
+                  (the decode direction: DualProofFromProto database_protoconv.go:211-224)
   ImmuStore.DualProofV2                                        immustore.go:2356-2387
   TxMetadata.ReadFrom                                          tx_metadata.go:159-195
 
@@ -73,10 +75,24 @@ def _build():
     msg("InclusionProof", [("leaf", 1, _F.TYPE_INT32, O_, None),
                            ("width", 2, _F.TYPE_INT32, O_, None),
                            ("terms", 3, _F.TYPE_BYTES, R_, None)])
+    msg("LinearProof", [("sourceTxId", 1, _F.TYPE_UINT64, O_, None),
+                        ("TargetTxId", 2, _F.TYPE_UINT64, O_, None),
+                        ("terms", 3, _F.TYPE_BYTES, R_, None)])
+    msg("LinearAdvanceProof", [("linearProofTerms", 1, _F.TYPE_BYTES, R_, None),
+                               ("inclusionProofs", 2, _F.TYPE_MESSAGE, R_, "InclusionProof")])
+    msg("DualProof", [("sourceTxHeader", 1, _F.TYPE_MESSAGE, O_, "TxHeader"),
+                      ("targetTxHeader", 2, _F.TYPE_MESSAGE, O_, "TxHeader"),
+                      ("inclusionProof", 3, _F.TYPE_BYTES, R_, None),
+                      ("consistencyProof", 4, _F.TYPE_BYTES, R_, None),
+                      ("targetBlTxAlh", 5, _F.TYPE_BYTES, O_, None),
+                      ("lastInclusionProof", 6, _F.TYPE_BYTES, R_, None),
+                      ("linearProof", 7, _F.TYPE_MESSAGE, O_, "LinearProof"),
+                      ("LinearAdvanceProof", 8, _F.TYPE_MESSAGE, O_, "LinearAdvanceProof")])
     pool = descriptor_pool.DescriptorPool()
     pool.Add(fdp)
     get = lambda n: message_factory.GetMessageClass(pool.FindMessageTypeByName("immudb.schema." + n))
-    return {n: get(n) for n in ("TxMetadata", "TxHeader", "DualProofV2", "InclusionProof")}
+    return {n: get(n) for n in ("TxMetadata", "TxHeader", "DualProofV2", "InclusionProof",
+                                "DualProof", "LinearProof", "LinearAdvanceProof")}
 
 
 MSG = _build()

@@ -507,7 +507,8 @@ def synthetic():
     return res
 
 
-SCHEMA_MESSAGES = ("TxMetadata", "TxHeader", "DualProofV2", "InclusionProof")
+SCHEMA_MESSAGES = ("TxMetadata", "TxHeader", "DualProofV2", "InclusionProof", "DualProof",
+                   "LinearProof", "LinearAdvanceProof")
 
 
 def schema_fields():
@@ -538,6 +539,11 @@ def schema_fields():
 def main():
     if not os.path.isdir(REF):
         sys.exit("needs /root/reference (build container only)")
+    if "--schema-only" in sys.argv:  # refresh schema_fields.json alone
+        with open(os.path.join(OUT, "schema_fields.json"), "w") as f:
+            json.dump(schema_fields(), f, indent=1, sort_keys=True)
+        print("ok")
+        return
     fx = {}
     for name, rel in [("long_linear_proof", "test/data_long_linear_proof"),
                       ("v110_defaultdb", "test/data_v1.1.0/defaultdb"),

@@ -75,7 +75,10 @@ def _go_varints_ok(b, kind="top"):
                 sub, i = b[i:i + ln], i + ln
                 # DualProofV2 ("top") -> TxHeader -> TxMetadata; "incl" (an
                 # InclusionProof) has no sub-messages
-                nested = {"top": {1: "hdr", 2: "hdr"}, "hdr": {9: "md"}}.get(kind, {})
+                # DualProof v1 ("top1") adds LinearProof / LinearAdvanceProof
+                nested = {"top": {1: "hdr", 2: "hdr"}, "hdr": {9: "md"},
+                          "top1": {1: "hdr", 2: "hdr", 7: "lin", 8: "adv"},
+                          "adv": {2: "incl"}}.get(kind, {})
                 if not groups and f in nested and not _go_varints_ok(sub, nested[f]):
                     return False
             elif wt == 3:
@@ -514,3 +517,174 @@ def test_inclusion_verify_negative_leaf_width(m, ctx, orc, wire):
                                          c[2], c[3], c[4]) for c in cases]
     assert list(ok) == exp == orc_ok
     assert exp[0] and sum(exp) >= 4  # (-2, 1) verifies: signed arithmetic
+
+
+# ------------------------------------------------------------ DualProof (v1)
+def dual_v1_msg(wire, a):
+    """DualProofToProto (database_protoconv.go:131-142, LinearProofToProto,
+    LinearAdvanceProofToProto) of orc.verify_dual_proof arguments -> bytes"""
+    from test_gpu_formats import _rec_hdr
+    sh, th, blob, incl, cons, tbl, last, lin, lap = a[:9]
+    M = wire.MSG["DualProof"]()
+    M.sourceTxHeader.CopyFrom(wire.tx_header_msg(_rec_hdr(sh, blob))[1])
+    M.targetTxHeader.CopyFrom(wire.tx_header_msg(_rec_hdr(th, blob))[1])
+    M.inclusionProof.extend(incl)
+    M.consistencyProof.extend(cons)
+    M.targetBlTxAlh = tbl
+    M.lastInclusionProof.extend(last)
+    if lin is not None:
+        M.linearProof.SetInParent()
+        M.linearProof.sourceTxId, M.linearProof.TargetTxId = lin[0], lin[1]
+        M.linearProof.terms.extend(lin[2])
+    if lap is not None:
+        M.LinearAdvanceProof.SetInParent()
+        M.LinearAdvanceProof.linearProofTerms.extend(lap[0])
+        for ip in lap[1]:
+            M.LinearAdvanceProof.inclusionProofs.add(terms=ip)
+    return M.SerializeToString()
+
+
+def test_dual_v1_decode_then_verify_fixture_cases(m, ctx, orc, wire, fixtures):
+    """The Go stores' v1 DualProofs (with tampered linear, linear-advance, last
+    inclusion and TargetBlTxAlh parts) marshalled as DualProof messages, decoded
+    on the device, verified straight from the decoded arrays: the verdicts are
+    the oracle's on the original proofs."""
+    from immustore_amd import txlayer
+    from test_tx_oracle import dual_v1_args
+    from tx_util import headers_from_fixture
+    args = []
+    for name, fx in fixtures.items():
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        for c in fx["dual_v1"]:
+            for tamper in (None, "lap", "lin", "last", "tbl"):
+                args.append(dual_v1_args(c, recs, blob, alhs, tamper))
+    msgs = [dual_v1_msg(wire, a) for a in args]
+    st, dec = txlayer.decode_dual_proof_pb(msgs, ctx=ctx)
+    assert (st == 0).all()
+    for k in range(0, len(args), 37):  # decoded arrays == the proof's parts
+        a = args[k]
+        assert dec["src_hdr"][k].tobytes()[:128] == np.asarray(a[0]).tobytes()[:128]
+        assert dec["target_bl_tx_alh"][k].tobytes() == a[5]
+        lo = dec["linear_off"]
+        assert [x.tobytes() for x in dec["linear_terms"][int(lo[k]):int(lo[k + 1])]] == a[7][2]
+        assert (int(dec["linear_src"][k]), int(dec["linear_tgt"][k])) == a[7][:2]
+        assert bool(dec["has_advance"][k]) == (a[8] is not None)
+    ok = txlayer.verify_decoded_dual_proof_batch(dec, [a[9] for a in args], [a[10] for a in args],
+                                                 [a[11] for a in args], [a[12] for a in args],
+                                                 ctx=ctx)
+    exp = [orc.verify_dual_proof(*a) for a in args]
+    assert list(ok) == exp
+    assert sum(exp) > 400 and not all(exp)
+
+
+def random_dual_v1_msg(wire, rng):
+    M = wire.MSG["DualProof"]()
+    rb = lambda: bytes(rng.integers(0, 256, int(rng.choice([32, 32, 32, 0, 9, 40])),  # noqa: E731
+                                    dtype=np.uint8))
+
+    def hdr(h):
+        h.id = int(rng.integers(0, 1 << 40))
+        h.blTxId = int(rng.integers(0, 1 << 40))
+        h.version = int(rng.choice([0, 1, 2]))
+        h.nentries = int(rng.integers(-5, 1 << 20))
+        h.prevAlh, h.eH, h.blRoot = rb(), rb(), rb()
+        if rng.random() < 0.4:
+            h.metadata.truncatedTxID = int(rng.integers(0, 1 << 30))
+            if rng.random() < 0.5:
+                h.metadata.extra = rb()
+    if rng.random() < 0.95:
+        hdr(M.sourceTxHeader)
+    if rng.random() < 0.95:
+        hdr(M.targetTxHeader)
+    for fld in (M.inclusionProof, M.consistencyProof, M.lastInclusionProof):
+        fld.extend(rb() for _ in range(int(rng.integers(0, 12))))
+    if rng.random() < 0.8:
+        M.targetBlTxAlh = rb()
+    if rng.random() < 0.9:
+        M.linearProof.SetInParent()
+        M.linearProof.sourceTxId = int(rng.integers(0, 1 << 40))
+        M.linearProof.TargetTxId = int(rng.integers(0, 1 << 40))
+        M.linearProof.terms.extend(rb() for _ in range(int(rng.integers(0, 10))))
+    if rng.random() < 0.6:
+        M.LinearAdvanceProof.SetInParent()
+        M.LinearAdvanceProof.linearProofTerms.extend(rb() for _ in range(int(rng.integers(0, 6))))
+        for _ in range(int(rng.integers(0, 5))):
+            ip = M.LinearAdvanceProof.inclusionProofs.add(leaf=int(rng.integers(-3, 100)),
+                                                           width=int(rng.integers(0, 100)))
+            ip.terms.extend(rb() for _ in range(int(rng.integers(0, 6))))
+    raw = M.SerializeToString()
+    r = rng.random()
+    if r < 0.1:  # unknown fields at the top, a group inside
+        raw += tag(20, 2) + bytes([2, 8, 1]) + tag(21, 3) + tag(3, 5) + bytes(4) + tag(21, 4)
+    elif r < 0.2:  # a second LinearAdvanceProof occurrence: merged (lists appended)
+        la = wire.MSG["LinearAdvanceProof"](linearProofTerms=[bytes(range(32))])
+        la.inclusionProofs.add(terms=[bytes(32), b"x"])
+        b = la.SerializeToString()
+        raw += tag(8, 2) + bytes([len(b)]) + b
+    elif r < 0.3:  # a second LinearProof occurrence: ids replaced, terms appended
+        lp = wire.MSG["LinearProof"](sourceTxId=7, terms=[bytes(range(1, 33))])
+        b = lp.SerializeToString()
+        raw += tag(7, 2) + bytes([len(b)]) + b
+    return raw
+
+
+def expect_v1(wire, raw):
+    from google.protobuf.message import DecodeError
+    if not _go_varints_ok(raw, "top1"):
+        return 14, None
+    try:
+        M = wire.MSG["DualProof"].FromString(raw)
+    except DecodeError:
+        return 14, None
+    ok = M.HasField("sourceTxHeader") and M.HasField("targetTxHeader") and M.HasField("linearProof")
+    e = {"incl": [d32(x) for x in M.inclusionProof], "cons": [d32(x) for x in M.consistencyProof],
+         "last": [d32(x) for x in M.lastInclusionProof], "tbl": d32(M.targetBlTxAlh),
+         "has_linear": M.HasField("linearProof"), "has_advance": M.HasField("LinearAdvanceProof"),
+         "linear": (M.linearProof.sourceTxId, M.linearProof.TargetTxId,
+                    [d32(x) for x in M.linearProof.terms]),
+         "advance": [d32(x) for x in M.LinearAdvanceProof.linearProofTerms],
+         "nested": [[d32(x) for x in ip.terms] for ip in M.LinearAdvanceProof.inclusionProofs],
+         "src_id": M.sourceTxHeader.id, "tgt_bl": M.targetTxHeader.blTxId}
+    return (0 if ok else 2), e
+
+
+def test_dual_v1_decode_random_vs_protobuf(m, ctx, wire):
+    from immustore_amd import txlayer
+    rng = np.random.default_rng(1001)
+    raws = [random_dual_v1_msg(wire, rng) for _ in range(1500)]
+    for raw in list(raws[:400]):
+        b = bytearray(raw)
+        if rng.random() < 0.5:
+            raws.append(bytes(b[:int(rng.integers(0, len(b)))]))
+        else:
+            for _ in range(int(rng.integers(1, 3))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            raws.append(bytes(b))
+    raws += [b"", tag(7, 2) + bytes([0]) + tag(1, 2) + bytes([0]) + tag(2, 2) + bytes([0])]
+    st, d = txlayer.decode_dual_proof_pb(raws, ctx=ctx)
+    seen = set()
+
+    def terms(name, k):
+        o = d[name + "_off"]
+        return [x.tobytes() for x in d[name + "_terms"][int(o[k]):int(o[k + 1])]]
+
+    for k, raw in enumerate(raws):
+        est, e = expect_v1(wire, raw)
+        assert int(st[k]) == est, (k, raw.hex())
+        seen.add(est)
+        if est == 14:
+            assert all(int(d[t + "_off"][k]) == int(d[t + "_off"][k + 1])
+                       for t in ("incl", "cons", "last", "linear", "advance"))
+            continue
+        assert terms("incl", k) == e["incl"] and terms("cons", k) == e["cons"], k
+        assert terms("last", k) == e["last"] and terms("advance", k) == e["advance"], k
+        assert d["target_bl_tx_alh"][k].tobytes() == e["tbl"], k
+        assert bool(d["has_linear"][k]) == e["has_linear"], k
+        assert bool(d["has_advance"][k]) == e["has_advance"], k
+        assert (int(d["linear_src"][k]), int(d["linear_tgt"][k]), terms("linear", k)) == e["linear"], k
+        q0, q1 = int(d["advance_incl_first"][k]), int(d["advance_incl_first"][k + 1])
+        qo, qt = d["advance_incl_off"], d["advance_incl_terms"]
+        got = [[x.tobytes() for x in qt[int(qo[q]):int(qo[q + 1])]] for q in range(q0, q1)]
+        assert got == e["nested"], k
+        assert int(d["src_hdr"][k]["id"]) == e["src_id"] and int(d["tgt_hdr"][k]["bl_tx_id"]) == e["tgt_bl"]
+    assert seen == {0, 2, 14}
