@@ -956,6 +956,28 @@ def run_single(a):
 
         tdec = timed(step_decode, max(1, a.steps // 2), 1, sync)
         ok &= bool((dst == 0).all())
+        # ... then VerifyDualProofV2 over the decoded arrays (host in, statuses
+        # out), against the fused call (messages in, statuses out)
+        from immustore_amd import txlayer as TL
+        _, s_alh = TL.tx_alh_batch(hs_h, b"", ctx)
+        _, t_alh = TL.tx_alh_batch(ht_h, b"", ctx)
+        vsrc, vtgt = hs_h["id"].copy(), ht_h["id"].copy()
+        vst = np.zeros(n_dec, np.int32)
+
+        def step_verify():
+            N.check(L.mh_verify_dual_proof_v2_batch(
+                ctx.handle, n_dec, A(dsh), A(dth), A(dmd), dmd.size, A(dio), A(dit), A(dco), A(dct),
+                A(vsrc), A(vtgt), A(s_alh), A(t_alh), A(vst)))
+
+        fst = np.zeros(n_dec, np.int32)
+
+        def step_fused():
+            N.check(L.mh_verify_dual_proof_v2_pb_batch(ctx.handle, n_dec, A(msgs_h), A(moff),
+                                                       A(vsrc), A(vtgt), A(s_alh), A(t_alh), A(fst)))
+
+        tver = timed(step_verify, max(1, a.steps // 2), 1, sync)
+        tfus = timed(step_fused, max(1, a.steps // 2), 1, sync)
+        ok &= bool((vst == fst).all())
         for k in [int(x) for x in rng.integers(0, P, 300)]:
             ok &= dsh[k].tobytes()[:128] == hs_h[k].tobytes()[:128]
             ok &= dth[k].tobytes()[:128] == ht_h[k].tobytes()[:128]
@@ -973,6 +995,16 @@ def run_single(a):
                    "bytes_in": int(moff[-1]), "in_GBps": round(int(moff[-1]) / tdec / 1e9, 2),
                    "note": "host buffers (pageable): H2D of the messages, D2H of the headers, "
                            "the packed metadata and the terms"},
+               "verify_decoded_dual_proof_v2": {"M_proofs_per_s": round(n_dec / tver / 1e6, 3),
+                                                "ms_per_step": round(tver * 1e3, 3)},
+               "verify_dual_proof_v2_from_wire_fused": {
+                   "M_messages_per_s": round(n_dec / tfus / 1e6, 3),
+                   "ms_per_step": round(tfus * 1e3, 3),
+                   "vs_decode_then_verify": round((tdec + tver) / tfus, 2),
+                   "statuses_equal": bool((vst == fst).all()),
+                   "note": "mh_verify_dual_proof_v2_pb_batch: messages + ids + Alh values up, "
+                           "statuses down; the bench tree's payloads are not these headers' Alh, "
+                           "so the verdicts are 'inclusion not valid' (every kernel still runs)"},
                "sample_vs_oracle": bool(ok)}
 
     out["workload"] = a.workload

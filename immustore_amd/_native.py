@@ -266,6 +266,7 @@ SIGNATURES = {
                                             u8p, u8p, vp]),
     "mh_verify_dual_proof_batch": (i32, [vp, vp, u8p]),
     "mh_dual_proof_pb_decode_batch": (i32, [vp, u64, u8p, vp, vp, vp]),
+    "mh_verify_dual_proof_v2_pb_batch": (i32, [vp, u64, u8p, vp, vp, vp, u8p, u8p, vp]),
     "mh_verify_document_batch": (i32, [vp, vp, vp, u8p]),
     "mh_commit_queue_new": (i32, [vp, i32, u64, u32, u32, C.POINTER(vp)]),
     "mh_commit_queue_free": (i32, [vp]),

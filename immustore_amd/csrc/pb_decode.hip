@@ -506,6 +506,73 @@ __global__ __launch_bounds__(256) void k_pbd_dual1(uint64_t n, const uint8_t *__
     if (lt) md_write(mt, o.md_blob + m0 + ls);
 }
 
+// ------------------------------------------- DualProofV2 from the wire, verified
+// VerifyDualProofV2's argument checks (verification.go:303-316) and the arrays
+// of its two ahtree proofs (:342-370) from the decoded headers, on the device
+// (the host loops of mh_verify_dual_proof_v2_batch); headers that cannot be
+// hashed are flagged and hashed as empty v1 headers.  Decoded metadata is
+// canonical and at most 268 bytes, so only the version can make a header
+// unhashable here.
+__global__ __launch_bounds__(256) void k_dpv2_prep(uint64_t n, const mh_tx_header *__restrict__ hd,
+                                                   const uint64_t *__restrict__ src,
+                                                   const uint64_t *__restrict__ tgt,
+                                                   int32_t *__restrict__ status,
+                                                   mh_tx_header *__restrict__ hh,
+                                                   uint64_t *__restrict__ ii, uint64_t *__restrict__ ij,
+                                                   uint64_t *__restrict__ ci, uint8_t *__restrict__ sel,
+                                                   uint8_t *__restrict__ sbl, uint8_t *__restrict__ tbl) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    mh_tx_header sh = hd[p], th = hd[n + p];
+    int32_t s = status[p];
+    // a v0 innerHash never reads the metadata (tx.go:258-263), which a wire
+    // header may carry; a version other than 0 / 1 panics in Go's innerHash
+    if (sh.version == 0) sh.md_len = 0;
+    if (th.version == 0) th.md_len = 0;
+    if (s == MH_OK) {
+        if (sh.id == 0 || sh.id != src[p] || th.id != tgt[p]) s = MH_ERR_ILLEGAL_ARGUMENTS;
+        else if (src[p] > tgt[p]) s = MH_ERR_SOURCE_TX_NEWER;
+        else if (sh.version > 1 || th.version > 1) s = MH_ERR_ILLEGAL_ARGUMENTS;
+    }
+    status[p] = s;
+    ii[p] = src[p];
+    ij[p] = th.bl_tx_id;
+    sel[p] = src[p] == 1;
+    ci[p] = src[p] == 1 ? src[p] : sh.bl_tx_id;
+    for (int k = 0; k < 32; k++) {
+        sbl[32 * p + k] = sh.bl_root[k];
+        tbl[32 * p + k] = th.bl_root[k];
+    }
+    if (s != MH_OK) {  // keep the Alh kernel's reads inside md_blob; result unused
+        sh.version = th.version = 1;
+        sh.md_len = th.md_len = 0;
+    }
+    hh[p] = sh;
+    hh[n + p] = th;
+}
+
+// verification.go:318-370 after the Alh values and the two ahtree proofs
+__global__ __launch_bounds__(256) void k_dpv2_final(uint64_t n, const mh_tx_header *__restrict__ hd,
+                                                    const uint64_t *__restrict__ src,
+                                                    const uint64_t *__restrict__ tgt,
+                                                    const int32_t *__restrict__ alh_st,
+                                                    const uint8_t *__restrict__ oki,
+                                                    const uint8_t *__restrict__ okc,
+                                                    int32_t *__restrict__ status) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    int32_t s = status[p];
+    if (s == MH_OK) {
+        const mh_tx_header &sh = hd[p], &th = hd[n + p];
+        if (alh_st[p] != MH_OK || alh_st[n + p] != MH_OK) s = MH_ERR_ILLEGAL_ARGUMENTS;
+        else if (sh.id - 1 != sh.bl_tx_id || th.id - 1 != th.bl_tx_id) s = MH_ERR_UNEXPECTED_LINKING;
+        else if (src[p] == tgt[p]) s = MH_OK;
+        else if (!oki[p]) s = MH_ERR_INCLUSION_NOT_VALID;
+        else if (!okc[p]) s = MH_ERR_CONSISTENCY_NOT_VALID;
+    }
+    status[p] = s;
+}
+
 }  // namespace
 
 extern "C" int mh_dual_proof_v2_pb_decode_batch(
@@ -774,6 +841,98 @@ extern "C" int mh_dual_proof_pb_decode_batch(mh_ctx *c, uint64_t n, const uint8_
         if (nq) MH_HIP(hipMemcpyAsync(out->advance_incl_off, dq, nq * 8, hipMemcpyDeviceToHost, st));
         MH_HIP(hipStreamSynchronize(st));
         out->advance_incl_off[nq] = totals[kQT];
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uint8_t *msgs,
+                                                const uint64_t *msg_off, const uint64_t *src,
+                                                const uint64_t *tgt, const uint8_t *src_alh,
+                                                const uint8_t *tgt_alh, int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!msg_off || !src || !tgt || !src_alh || !tgt_alh || !status)))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (n == 0) return MH_OK;
+        if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
+        if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(hipSetDevice(c->device));
+        hipStream_t st = c->stream;
+        size_t scan_bytes = 0;
+        MH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (int)n, st));
+        Layout L;
+        // caller arrays (x = source Alh values then target Alh values, as the
+        // Alh kernel expects them), then device-only data
+        const uint64_t b_msg = L.add(mb + 16), b_off = L.add((n + 1) * 8), b_src = L.add(n * 8),
+                       b_tgt = L.add(n * 8), b_x = L.add(2 * n * 32), b_cnt = L.add(3 * n * 8),
+                       b_io = L.add((n + 1) * 8), b_co = L.add((n + 1) * 8), b_mo = L.add((n + 1) * 8),
+                       b_st = L.add(n * 4), b_scan = L.add(scan_bytes),
+                       b_hd = L.add(2 * n * sizeof(mh_tx_header)), b_hh = L.add(2 * n * sizeof(mh_tx_header)),
+                       b_md = L.add(2 * n * (uint64_t)kMdSlot), b_s = L.add(2 * n * kTxInnerStride),
+                       b_ast = L.add(2 * n * 4), b_ii = L.add(n * 8), b_ij = L.add(n * 8),
+                       b_ci = L.add(n * 8), b_sel = L.add(n), b_sbl = L.add(n * 32), b_tbl = L.add(n * 32),
+                       b_leaf = L.add(n * 32), b_ca = L.add(n * 32), b_oki = L.add(n), b_okc = L.add(n);
+        MH_HIP(c->s_tx.ensure(L.total));
+        uint8_t *base = c->s_tx.as<uint8_t>();
+        if (mb) MH_HIP(hipMemcpyAsync(base + b_msg, msgs + m0, mb, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_off, msg_off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_src, src, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_tgt, tgt, n * 8, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_x, src_alh, n * 32, hipMemcpyHostToDevice, st));
+        MH_HIP(hipMemcpyAsync(base + b_x + n * 32, tgt_alh, n * 32, hipMemcpyHostToDevice, st));
+        const unsigned grid = (unsigned)((n + 255) / 256);
+        const uint8_t *dmsg = base + b_msg - m0;
+        uint64_t *cnt = (uint64_t *)(base + b_cnt), *io = (uint64_t *)(base + b_io),
+                 *co = (uint64_t *)(base + b_co), *mo = (uint64_t *)(base + b_mo);
+        int32_t *dst = (int32_t *)(base + b_st);
+        // decode: validate + count, scans
+        hipLaunchKernelGGL(k_pbd_dual<false>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), cnt, cnt + n, cnt + 2 * n, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dst);
+        MH_HIP(hipGetLastError());
+        uint64_t *outs[3] = {io, co, mo};
+        for (int k = 0; k < 3; k++) {
+            MH_HIP(hipMemsetAsync(outs[k], 0, 8, st));
+            size_t sb = scan_bytes;
+            MH_HIP(hipcub::DeviceScan::InclusiveSum(base + b_scan, sb, (const uint64_t *)(cnt + k * n),
+                                                    outs[k] + 1, (int)n, st));
+        }
+        // the term totals size the term area: one small read-back
+        uint64_t tot[2] = {0, 0};
+        MH_HIP(hipMemcpyAsync(&tot[0], io + n, 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(&tot[1], co + n, 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        DevBuf &tb = c->s_tree;
+        MH_HIP(tb.ensure(std::max<uint64_t>(tot[0] + tot[1], 1) * 32));
+        uint8_t *dti = tb.as<uint8_t>(), *dtc = dti + tot[0] * 32;
+        mh_tx_header *hd = (mh_tx_header *)(base + b_hd), *hh = (mh_tx_header *)(base + b_hh);
+        hipLaunchKernelGGL(k_pbd_dual<true>, dim3(grid), dim3(256), 0, st, n, dmsg,
+                           (const uint64_t *)(base + b_off), nullptr, nullptr, nullptr, io, co, mo,
+                           dti, dtc, hd, hd + n, base + b_md, dst);
+        MH_HIP(hipGetLastError());
+        // VerifyDualProofV2 (verification.go:303-370)
+        uint64_t *ii = (uint64_t *)(base + b_ii), *ij = (uint64_t *)(base + b_ij),
+                 *ci = (uint64_t *)(base + b_ci);
+        const uint64_t *dsrc = (const uint64_t *)(base + b_src), *dtgt = (const uint64_t *)(base + b_tgt);
+        hipLaunchKernelGGL(k_dpv2_prep, dim3(grid), dim3(256), 0, st, n, hd, dsrc, dtgt, dst, hh, ii,
+                           ij, ci, base + b_sel, base + b_sbl, base + b_tbl);
+        MH_HIP(hipGetLastError());
+        MH_HIP(launch_tx_alh(st, c->tm(), 2 * n, hh, base + b_md, nullptr, base + b_s, base + b_x,
+                             nullptr, nullptr, nullptr, (int32_t *)(base + b_ast)));
+        MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_x, base + b_leaf));
+        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, ii, ij, io, dti, base + b_leaf,
+                                    base + b_tbl, base + b_oki, nullptr));
+        MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
+        MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n, ci, ij, co, dtc, base + b_ca,
+                                    base + b_tbl, base + b_okc, nullptr));
+        hipLaunchKernelGGL(k_dpv2_final, dim3(grid), dim3(256), 0, st, n, hd, dsrc, dtgt,
+                           (const int32_t *)(base + b_ast), base + b_oki, base + b_okc, dst);
+        MH_HIP(hipGetLastError());
+        MH_HIP(hipMemcpyAsync(status, dst, n * 4, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
         return MH_OK;
     });
 }

@@ -481,3 +481,22 @@ def verify_decoded_dual_proof_batch(dec, src, tgt, src_alh, tgt_alh,
     ok = np.zeros(n, np.uint8)
     N.check(N.load().mh_verify_dual_proof_batch(_ctx(ctx).handle, C.byref(b), _addr(ok)))
     return ok.astype(bool)
+
+
+def verify_dual_proof_v2_pb_batch(msgs, src, tgt, src_alh, tgt_alh,
+                                  ctx: Optional[Context] = None) -> np.ndarray:
+    """DualProofV2FromProto + VerifyDualProofV2 over many encoded DualProofV2
+    messages in one device pass (mh_verify_dual_proof_v2_pb_batch) -> status[n]."""
+    n = len(msgs)
+    if n == 0:
+        return np.zeros(0, np.int32)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in msgs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+    s_, t_ = np.asarray(src, np.uint64), np.asarray(tgt, np.uint64)
+    sa, ta = _d32(src_alh, n), _d32(tgt_alh, n)
+    st = np.zeros(n, np.int32)
+    N.check(N.load().mh_verify_dual_proof_v2_pb_batch(_ctx(ctx).handle, n, _addr(buf), _addr(off),
+                                                      _addr(s_), _addr(t_), _addr(sa), _addr(ta),
+                                                      _addr(st)))
+    return st

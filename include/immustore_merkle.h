@@ -716,6 +716,21 @@ int mh_dual_proof_v2_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msg
  * bytes each, DigestFromProto).  status[p]: MH_OK or MH_ERR_CORRUPTED_DATA
  * (no terms, leaf = width = 0).  term_cap < term_off[n]: offsets and statuses
  * only, MH_ERR_BUFFER_TOO_SMALL. */
+/* What a client auditing many VerifiableTxV2 answers does per answer --
+ * DualProofV2FromProto then store.VerifyDualProofV2 (verification.go:303-372)
+ * -- for n DualProofV2 messages in one call, entirely on the device: the
+ * messages go up once, only the statuses come back.  status[p] is
+ * mh_dual_proof_v2_pb_decode_batch's failure for message p (CORRUPTED_DATA,
+ * ILLEGAL_ARGUMENTS) or else mh_verify_dual_proof_v2_batch's verdict on the
+ * decoded proof with (src[p], tgt[p], src_alh[32 p], tgt_alh[32 p]), except
+ * that a version-0 header's metadata is ignored, as Go's innerHash ignores it
+ * (tx.go:258-263; mh_verify_dual_proof_v2_batch rejects a v0 header with
+ * md_len > 0, a combination the tx log cannot hold but a message can). */
+int mh_verify_dual_proof_v2_pb_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msgs,
+                                     const uint64_t *msg_off, const uint64_t *src,
+                                     const uint64_t *tgt, const uint8_t *src_alh,
+                                     const uint8_t *tgt_alh, int32_t *status);
+
 int mh_htree_inclusion_proof_pb_decode_batch(mh_ctx *ctx, uint64_t n, const uint8_t *msgs,
                                              const uint64_t *msg_off, uint64_t *leaf,
                                              uint64_t *width, uint64_t *term_off, uint8_t *terms,

@@ -688,3 +688,105 @@ def test_dual_v1_decode_random_vs_protobuf(m, ctx, wire):
         assert got == e["nested"], k
         assert int(d["src_hdr"][k]["id"]) == e["src_id"] and int(d["tgt_hdr"][k]["bl_tx_id"]) == e["tgt_bl"]
     assert seen == {0, 2, 14}
+
+
+# ------------------------------------------- DualProofV2 from the wire, verified
+def _compose(txlayer, msgs, S, T, SA, TA, ctx):
+    """decode, then mh_verify_dual_proof_v2_batch, with Go's v0 rule (a v0
+    header's metadata is not hashed): the fused call must agree"""
+    dst, sh, th, md, io, it, co, ct = txlayer.decode_dual_proof_v2_pb(msgs, ctx=ctx)
+    for h in (sh, th):
+        h["md_len"][h["version"] == 0] = 0
+    incl = [it[int(io[k]):int(io[k + 1])] for k in range(len(msgs))]
+    cons = [ct[int(co[k]):int(co[k + 1])] for k in range(len(msgs))]
+    vs = txlayer.verify_dual_proof_v2_batch(sh, th, md, incl, cons, S, T, SA, TA, ctx=ctx)
+    return np.where(dst != 0, dst, vs)
+
+
+def test_verify_from_wire_fixture_stores(m, ctx, fixtures):
+    """mh_verify_dual_proof_v2_pb_batch over the device-written DualProofV2
+    messages of the Go stores: every proof verifies; flipped message bytes,
+    wrong ids / Alh and swapped source / target give the decode-then-verify
+    composition's verdicts."""
+    from immustore_amd import txlayer
+    from tx_util import headers_from_fixture
+    rng = np.random.default_rng(3)
+    seen = set()
+    for name, fx in fixtures.items():
+        pay = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
+        t = m.AHtree(ctx)
+        t.append_batch(pay)
+        recs, blob, alhs = headers_from_fixture(fx["txs"])
+        cases = [(c["src"], c["tgt"]) for c in fx["dual_v2"] if c["src"] <= c["tgt"]]
+        S = np.array([a for a, _ in cases], np.uint64)
+        T = np.array([b for _, b in cases], np.uint64)
+        msgs, st = t.dual_proof_v2_pb_batch(recs[S.astype(int) - 1], recs[T.astype(int) - 1], blob)
+        SA = [alhs[int(x) - 1] for x in S]
+        TA = [alhs[int(x) - 1] for x in T]
+        fused = txlayer.verify_dual_proof_v2_pb_batch(msgs, S, T, SA, TA, ctx=ctx)
+        assert (fused == 0).all(), name
+        # variants: flipped bytes, wrong target id, zero source Alh, swapped pair
+        M2, S2, T2, SA2, TA2 = [], [], [], [], []
+        for k, msg in enumerate(msgs):
+            for v in range(4):
+                b = bytearray(msg)
+                s_, t_, sa, ta = int(S[k]), int(T[k]), SA[k], TA[k]
+                if v == 0:
+                    for _ in range(2):
+                        b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+                elif v == 1:
+                    t_ += 1
+                elif v == 2:
+                    sa = bytes(32)
+                else:
+                    s_, t_, sa, ta = t_, s_, ta, sa
+                M2.append(bytes(b))
+                S2.append(s_)
+                T2.append(t_)
+                SA2.append(sa)
+                TA2.append(ta)
+        fused = txlayer.verify_dual_proof_v2_pb_batch(M2, S2, T2, SA2, TA2, ctx=ctx)
+        comp = _compose(txlayer, M2, S2, T2, SA2, TA2, ctx)
+        assert list(fused) == list(comp), name
+        seen |= set(comp.tolist())
+    assert len(seen) >= 3
+
+
+def test_verify_from_wire_random_vs_composition(m, ctx, orc, wire):
+    """Messages over a 70 000-append tree with random headers (every metadata
+    shape) plus random protobuf-built and mutated ones: the fused call equals
+    decode + mh_verify_dual_proof_v2_batch on every message."""
+    from immustore_amd import txlayer
+    from test_gpu_formats import _random_headers
+    rng = np.random.default_rng(44)
+    N_TX = 70000
+    t = m.AHtree(ctx)
+    t.append_batch(rng.integers(0, 256, (N_TX, 32), dtype=np.uint8))
+    recs, blob = _random_headers(rng, N_TX + 10)
+    tgt = rng.integers(1, N_TX + 1, 1500)
+    src = np.array([int(rng.integers(1, x + 1)) for x in tgt])
+    msgs, st = t.dual_proof_v2_pb_batch(recs[src - 1], recs[tgt - 1], blob)
+    msgs = list(msgs)
+    S, T = list(src), list(tgt)
+    SA = [orc.tx_header_alh(recs[int(x) - 1], blob)[2] for x in src]
+    TA = [orc.tx_header_alh(recs[int(x) - 1], blob)[2] for x in tgt]
+    for k in range(500):  # mutated copies
+        b = bytearray(msgs[k])
+        b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        msgs.append(bytes(b))
+        S.append(S[k])
+        T.append(T[k])
+        SA.append(SA[k])
+        TA.append(TA[k])
+    for _ in range(500):  # random protobuf messages (ids mostly mismatched)
+        msgs.append(random_msg(wire, rng))
+        S.append(int(rng.integers(1, 5)))
+        T.append(int(rng.integers(1, 5)))
+        SA.append(bytes(32))
+        TA.append(bytes(32))
+    fused = txlayer.verify_dual_proof_v2_pb_batch(msgs, S, T, SA, TA, ctx=ctx)
+    comp = _compose(txlayer, msgs, S, T, SA, TA, ctx)
+    assert list(fused) == list(comp)
+    # the tree's payloads are not these headers' Alh: inclusion fails (12) where
+    # the arguments pass; plus ILLEGAL_ARGUMENTS and CORRUPTED_DATA
+    assert {2, 12, 14} <= set(comp.tolist())
