@@ -978,6 +978,16 @@ def run_single(a):
         tver = timed(step_verify, max(1, a.steps // 2), 1, sync)
         tfus = timed(step_fused, max(1, a.steps // 2), 1, sync)
         ok &= bool((vst == fst).all())
+        # the same with the messages in a pinned arena (a cgo shim's receive buffer)
+        msgs_pin = torch.empty(msgs_h.size, dtype=torch.uint8).pin_memory().numpy()
+        msgs_pin[:] = msgs_h
+
+        def step_fused_pinned():
+            N.check(L.mh_verify_dual_proof_v2_pb_batch(ctx.handle, n_dec, A(msgs_pin), A(moff),
+                                                       A(vsrc), A(vtgt), A(s_alh), A(t_alh), A(fst)))
+
+        tfp = timed(step_fused_pinned, max(1, a.steps // 2), 1, sync)
+        ok &= bool((vst == fst).all())
         for k in [int(x) for x in rng.integers(0, P, 300)]:
             ok &= dsh[k].tobytes()[:128] == hs_h[k].tobytes()[:128]
             ok &= dth[k].tobytes()[:128] == ht_h[k].tobytes()[:128]
@@ -1001,6 +1011,8 @@ def run_single(a):
                    "M_messages_per_s": round(n_dec / tfus / 1e6, 3),
                    "ms_per_step": round(tfus * 1e3, 3),
                    "vs_decode_then_verify": round((tdec + tver) / tfus, 2),
+                   "pinned_messages": {"M_messages_per_s": round(n_dec / tfp / 1e6, 3),
+                                       "ms_per_step": round(tfp * 1e3, 3)},
                    "statuses_equal": bool((vst == fst).all()),
                    "note": "mh_verify_dual_proof_v2_pb_batch: messages + ids + Alh values up, "
                            "statuses down; the bench tree's payloads are not these headers' Alh, "
