@@ -191,6 +191,63 @@ int main(int argc, char **argv) {
         CHECK(mh_htree_free(et));
         free(ko); free(mo); free(vo); free(kb); free(mb); free(vb); free(ov); free(use); free(hv);
     }
+    {
+        /* A self-consistent store, built the way ImmuStore does it: tx k's header
+         * links the tree of the first k-1 Alh values (BlTxID k-1, BlRoot), its
+         * Alh is appended next.  Then DualProofV2 messages over it
+         * (mh_ahtree_dual_proof_v2_pb_batch, the server side) checked by the
+         * client side in one call (mh_verify_dual_proof_v2_pb_batch). */
+        const uint64_t ntx = 64, np = 40;
+        mh_tx_header *h = calloc(ntx, sizeof(mh_tx_header));
+        uint8_t *alh = malloc(ntx * 32), inner[32];
+        mh_ahtree *st;
+        CHECK(mh_ahtree_new(ctx, &st));
+        for (uint64_t k = 0; k < ntx; k++) {
+            h[k].id = k + 1;
+            h[k].ts = (int64_t)(1700000000 + k);
+            h[k].bl_tx_id = k;
+            h[k].version = 1;
+            h[k].nentries = (uint32_t)(1 + k % 7);
+            for (int j = 0; j < 32; j++) {
+                h[k].eh[j] = (uint8_t)(k * 7 + j);
+                h[k].prev_alh[j] = k ? alh[(k - 1) * 32 + j] : 0;
+            }
+            if (k) CHECK(mh_ahtree_root_at(st, k, h[k].bl_root));
+            CHECK(mh_tx_alh_batch(ctx, 1, &h[k], NULL, 0, inner, alh + k * 32));
+            CHECK(mh_ahtree_append_batch(st, alh + k * 32, 1, 32, NULL));
+        }
+        mh_tx_header *sh = malloc(np * sizeof(mh_tx_header)), *th = malloc(np * sizeof(mh_tx_header));
+        uint64_t *si = malloc(np * 8), *ti = malloc(np * 8), *off = malloc((np + 1) * 8);
+        uint8_t *sa = malloc(np * 32), *ta = malloc(np * 32);
+        int32_t *pst = malloc(np * 4), *vst = malloc(np * 4);
+        for (uint64_t q = 0; q < np; q++) {
+            ti[q] = 2 + (q * 37) % (ntx - 1);
+            si[q] = 1 + (q * 11) % ti[q];
+            sh[q] = h[si[q] - 1];
+            th[q] = h[ti[q] - 1];
+            memcpy(sa + q * 32, alh + (si[q] - 1) * 32, 32);
+            memcpy(ta + q * 32, alh + (ti[q] - 1) * 32, 32);
+        }
+        uint64_t cap = 0;
+        int r = mh_ahtree_dual_proof_v2_pb_batch(st, np, sh, th, NULL, 0, NULL, 0, off, pst);
+        if (r != MH_ERR_BUFFER_TOO_SMALL && r != MH_OK) CHECK(r);
+        cap = off[np];
+        uint8_t *msgs = malloc(cap ? cap : 1);
+        CHECK(mh_ahtree_dual_proof_v2_pb_batch(st, np, sh, th, NULL, 0, msgs, cap, off, pst));
+        CHECK(mh_verify_dual_proof_v2_pb_batch(ctx, np, msgs, off, si, ti, sa, ta, vst));
+        uint64_t good = 0;
+        for (uint64_t q = 0; q < np; q++) good += pst[q] == MH_OK && vst[q] == MH_OK;
+        printf("wire_verify_ok %llu/%llu\n", (unsigned long long)good, (unsigned long long)np);
+        /* a term byte of the last message flipped: that proof alone fails */
+        msgs[off[np] - 1] ^= 1;
+        CHECK(mh_verify_dual_proof_v2_pb_batch(ctx, np, msgs, off, si, ti, sa, ta, vst));
+        good = 0;
+        for (uint64_t q = 0; q + 1 < np; q++) good += vst[q] == MH_OK;
+        printf("wire_verify_tampered %d %llu\n", vst[np - 1], (unsigned long long)good);
+        CHECK(mh_ahtree_free(st));
+        free(h); free(alh); free(sh); free(th); free(si); free(ti); free(off); free(sa); free(ta);
+        free(pst); free(vst); free(msgs);
+    }
     CHECK(mh_ctx_destroy(ctx));
     free(d);
     free(p);

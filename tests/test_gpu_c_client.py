@@ -96,6 +96,11 @@ def test_c_client_matches_oracle(w, m):
     assert out["htree_proof"] == terms.tobytes().hex()
     assert out["htree_verify"] == "1"
     assert out["htree_verify_tampered"] == ("0" if len(terms) else "1")
+    # server-side DualProofV2 messages over a self-linked store, verified from the
+    # wire by the client call: all pass; a flipped last byte fails that proof only
+    assert out["wire_verify_ok"] == "40/40"
+    code, rest = out["wire_verify_tampered"].split()
+    assert int(code) != 0 and rest == "39"
 
     t = O.AHtree(cap=m)
     t.append_batch(p)
