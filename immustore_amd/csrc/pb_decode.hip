@@ -590,6 +590,7 @@ extern "C" int mh_dual_proof_v2_pb_decode_batch(
             return MH_OK;
         }
         if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (n > 0x7fffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // hipcub's int item count
         if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
         if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
@@ -668,6 +669,7 @@ extern "C" int mh_htree_inclusion_proof_pb_decode_batch(mh_ctx *c, uint64_t n, c
             if (term_off) term_off[0] = 0;
             return MH_OK;
         }
+        if (n > 0x7fffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // hipcub's int item count
         if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
         if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
@@ -737,6 +739,7 @@ extern "C" int mh_dual_proof_pb_decode_batch(mh_ctx *c, uint64_t n, const uint8_
             return MH_OK;
         }
         if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (n > 0x7fffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // hipcub's int item count
         if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
         if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
@@ -854,6 +857,7 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
             return MH_ERR_ILLEGAL_ARGUMENTS;
         if (n == 0) return MH_OK;
         if (2 * n * (uint64_t)kMdSlot > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // md_off
+        if (n > 0x7fffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;  // hipcub's int item count
         if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t m0 = msg_off[0], mb = msg_off[n] - m0;
         if (mb && !msgs) return MH_ERR_ILLEGAL_ARGUMENTS;
