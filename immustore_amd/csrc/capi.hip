@@ -241,8 +241,9 @@ extern "C" uint64_t mh_htree_level_offset(uint64_t n, int level) {
     return g.off[level];
 }
 
-static int write_root(hipStream_t st, const LevelGeom &g, uint8_t *levels, uint8_t *root) {
-    if (!root) return MH_OK;
+static int write_root(hipStream_t st, const LevelGeom &g, uint8_t *levels, uint8_t *root,
+                      bool in_kernel = false) {
+    if (!root || in_kernel) return MH_OK;
     if (g.n == 0) {
         MH_HIP(hipMemcpyAsync(root, kEmptyRoot, 32, hipMemcpyHostToDevice, st));
         return MH_OK;
@@ -254,19 +255,24 @@ static int write_root(hipStream_t st, const LevelGeom &g, uint8_t *levels, uint8
 // Fused fixed-stride path (device pointers, stream st).
 static int build_fixed(hipStream_t st, Timer *tm, int version, uint64_t n, const uint8_t *keys,
                        uint32_t key_len, const uint8_t *vals, uint32_t val_len, uint8_t *hvals_out,
-                       uint8_t *levels, const LevelGeom &g) {
+                       uint8_t *levels, const LevelGeom &g, uint8_t *root = nullptr,
+                       bool *root_done = nullptr) {
     int done = 0;
     MH_HIP(launch_entries_fixed(st, tm, version, n, keys, key_len, vals, val_len, hvals_out, levels,
                                 g, &done));
-    MH_HIP(launch_reduce(st, tm, levels, g, done));
+    // the last k_reduce launch stores the root itself when there is one
+    MH_HIP(launch_reduce(st, tm, levels, g, done, root));
+    if (root_done) *root_done = root && done < g.nlevels - 1;
     return MH_OK;
 }
 
 static int build_digests(hipStream_t st, Timer *tm, const uint8_t *digests, uint64_t n,
-                         uint8_t *levels, const LevelGeom &g) {
+                         uint8_t *levels, const LevelGeom &g, uint8_t *root = nullptr,
+                         bool *root_done = nullptr) {
     int done = 0;
     MH_HIP(launch_leaves_from_digests(st, tm, digests, n, levels, g, &done));
-    MH_HIP(launch_reduce(st, tm, levels, g, done));
+    MH_HIP(launch_reduce(st, tm, levels, g, done, root));
+    if (root_done) *root_done = root && done < g.nlevels - 1;
     return MH_OK;
 }
 
@@ -293,11 +299,12 @@ extern "C" int mh_dev_htree_build_digests(mh_ctx *c, const uint8_t *digests, uin
         if (((uintptr_t)digests & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
         g.init(n);
+        bool rk = false;
         if (n) {
-            int st = build_digests(c->stream, c->tm(), digests, n, levels, g);
+            int st = build_digests(c->stream, c->tm(), digests, n, levels, g, root, &rk);
             if (st) return st;
         }
-        return write_root(c->stream, g, levels, root);
+        return write_root(c->stream, g, levels, root, rk);
     });
 }
 
@@ -312,10 +319,11 @@ extern "C" int mh_dev_htree_build_entries_fixed(mh_ctx *c, int version, uint64_t
         if (((uintptr_t)levels & 15) || ((uintptr_t)hvals_out & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
         LevelGeom g;
         g.init(n);
+        bool rk = false;
         if (n) {
             if (entries_fixed_supported(version, keys, key_len, vals, val_len)) {
                 int st = build_fixed(c->stream, c->tm(), version, n, keys, key_len, vals, val_len,
-                                     hvals_out, levels, g);
+                                     hvals_out, levels, g, root, &rk);
                 if (st) return st;
             } else {
                 // odd shapes: general CSR path over generated offsets
@@ -329,7 +337,7 @@ extern "C" int mh_dev_htree_build_entries_fixed(mh_ctx *c, int version, uint64_t
                 if (st) return st;
             }
         }
-        return write_root(c->stream, g, levels, root);
+        return write_root(c->stream, g, levels, root, rk);
     });
 }
 

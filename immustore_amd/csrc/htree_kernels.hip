@@ -564,7 +564,7 @@ __global__ void k_copy_nodes(const uint8_t *__restrict__ src, uint64_t n, uint8_
 // ============================================================================
 template <int T>
 __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, LevelArgs la, int l0,
-                                              int nsteps) {
+                                              int nsteps, int top, uint8_t *__restrict__ root) {
     __shared__ uint32_t buf[2][T][9];  // +1 word pad: conflict-free 2t / 2t+1 reads
     const int t = threadIdx.x;
     const uint64_t blk = blockIdx.x;
@@ -580,6 +580,7 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
                 copy8(out, lft);
             }
             store_digest(levels + (la.off[l0 + 1] + q) * 32, out);
+            if (l0 + 1 == top) store_digest(root, out);
 #pragma unroll
             for (int j = 0; j < 8; j++) buf[0][t][j] = out[j];
         }
@@ -603,6 +604,7 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
                     copy8(out, lft);
                 }
                 store_digest(levels + (la.off[l] + q) * 32, out);
+                if (l == top) store_digest(root, out);
 #pragma unroll
                 for (int j = 0; j < 8; j++) buf[cur ^ 1][t][j] = out[j];
             }
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(T) void k_reduce(uint8_t *__restrict__ levels, Leve
 // Every level is written (htree.go:158 needs them for InclusionProof).
 template <int T>
 __global__ __launch_bounds__(T) void k_reduce4(uint8_t *__restrict__ levels, LevelArgs la, int l0,
-                                               int nsteps) {
+                                               int nsteps, int top, uint8_t *__restrict__ root) {
     __shared__ uint32_t buf[2][T][9];
     const int t = threadIdx.x;
     const uint64_t q = (uint64_t)blockIdx.x * T + t;  // node of level l0 + 2
@@ -642,12 +644,16 @@ __global__ __launch_bounds__(T) void k_reduce4(uint8_t *__restrict__ levels, Lev
                 copy8(out, lft);
             }
             store_digest(levels + (la.off[l] + p) * 32, out);
+            if (l == top) store_digest(root, out);
             if (k == 0) copy8(A, out);
             else if (k == 1) copy8(B, out);
             else copy8(A, out);
         }
         // width[l0+1] odd and 2q+1 past it: node q of level l0+2 is the promoted 2q
-        if (2 * q + 1 >= la.width[l0 + 1]) store_digest(levels + (la.off[l0 + 2] + q) * 32, A);
+        if (2 * q + 1 >= la.width[l0 + 1]) {
+            store_digest(levels + (la.off[l0 + 2] + q) * 32, A);
+            if (l0 + 2 == top) store_digest(root, A);
+        }
 #pragma unroll
         for (int j = 0; j < 8; j++) buf[0][t][j] = A[j];
     }
@@ -670,6 +676,7 @@ __global__ __launch_bounds__(T) void k_reduce4(uint8_t *__restrict__ levels, Lev
                     copy8(out, lft);
                 }
                 store_digest(levels + (la.off[l] + qq) * 32, out);
+                if (l == top) store_digest(root, out);
 #pragma unroll
                 for (int j = 0; j < 8; j++) buf[cur ^ 1][t][j] = out[j];
             }
@@ -800,17 +807,20 @@ hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *
 }
 
 hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const LevelGeom &g,
-                         int from_level) {
+                         int from_level, uint8_t *root) {
     // Each launch: a workgroup of T threads turns 2T nodes into log2(2T)
     // levels.  The last (top) launch uses 512 threads = 10 levels, so a
     // 2^20-leaf tree whose leaf kernel stopped at level 10 needs one launch.
     LevelArgs la = level_args(g);
+    // the launch that produces the top level also stores the root (saves the
+    // 32-byte copy launch after it); -1 = no root pointer
+    const int top = root ? g.nlevels - 1 : -1;
     int cur = from_level;
     while (cur < g.nlevels - 1) {
         const int left = g.nlevels - 1 - cur;
         TimerScope ts(tm, "reduce", st);
         if (left <= 10 && g.width[cur] <= 1024) {
-            hipLaunchKernelGGL(k_reduce<512>, dim3(1), dim3(512), 0, st, levels, la, cur, left);
+            hipLaunchKernelGGL(k_reduce<512>, dim3(1), dim3(512), 0, st, levels, la, cur, left, top, root);
             cur += left;
         } else if (left >= 3 && g.width[cur] >= (uint64_t)4 * 256 * 256) {
             // throughput regime (>= 256 workgroups): two in-lane levels + up
@@ -819,12 +829,12 @@ hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const Level
             // instead of three for the in-lane pair.
             const int steps = std::min(10, left);
             const unsigned grid = grid_for(g.width[cur + 2], 256);
-            hipLaunchKernelGGL(k_reduce4<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);
+            hipLaunchKernelGGL(k_reduce4<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps, top, root);
             cur += steps;
         } else {
             const int steps = std::min(9, left);
             const unsigned grid = grid_for(g.width[cur + 1], 256);
-            hipLaunchKernelGGL(k_reduce<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps);
+            hipLaunchKernelGGL(k_reduce<256>, dim3(grid), dim3(256), 0, st, levels, la, cur, steps, top, root);
             cur += steps;
         }
     }

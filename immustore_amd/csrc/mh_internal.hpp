@@ -112,7 +112,7 @@ hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *
 // Copy nodes into level 0 (no leaf hashing): used for reducing subtree roots.
 // Reduce levels [from, top] in place (htree.go:85-110).
 hipError_t launch_reduce(hipStream_t st, Timer *tm, uint8_t *levels, const LevelGeom &g,
-                         int from_level);
+                         int from_level, uint8_t *root = nullptr);
 
 // Generic helpers
 hipError_t launch_fill_random(hipStream_t st, uint8_t *dst, uint64_t nbytes, uint64_t seed);
