@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Split a rocprofv3 kernel trace of `bench.py` into its phases and summarise
-the dominant kernel: warmup, timed region (W builds in flight) and the
-isolated launches bench.py makes after the timed region.
+the dominant kernel: clock pre-warm + warmup, timed region (builds in flight)
+and the isolated launches bench.py makes after the timed region.  The trace is
+split from its end (ISO isolated launches last, the K timed ones before them),
+so the pre-warm's variable build count does not shift the phases.
 
 usage: prof_summary.py run_kernel_trace.csv --steps K --warmup W [--isolated 5]
 """
@@ -21,9 +23,11 @@ def main():
     rows = [r for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
-    w, k = a.warmup, a.steps
-    timed, iso = dur[w:w + k], dur[w + k:w + k + a.isolated]
+    k, m = a.steps, a.isolated
+    iso = dur[len(dur) - m:] if m else []
+    timed = dur[len(dur) - m - k:len(dur) - m]
     out = {"kernel": a.kernel, "launches": len(dur),
+           "before_timed_region": len(dur) - m - k,
            "timed_region_mean_ms": round(sum(timed) / max(len(timed), 1), 4),
            "isolated_mean_ms": round(sum(iso) / max(len(iso), 1), 4) if iso else None,
            "all_mean_ms": round(sum(dur) / max(len(dur), 1), 4)}
