@@ -435,10 +435,11 @@ def main():
     k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
     contended_ms = k_ms / max(k_cnt, 1)
     kern_ms = iso_ms
-    lpl = int(os.environ.get("MH_LPL", "4" if n >= 4 * 262144 else ("2" if n >= 2 * 262144 else "1")))
+    # mirrors choose_lpl / launch_entries_fixed in htree_kernels.hip
+    lpl = int(os.environ.get("MH_LPL", "2" if n >= 2 * 262144 else "1"))
     # levels written by one launch of the dominant kernel: the lanes' groups
     # up to level log2(lpl), then each workgroup's subtree 8 levels higher
-    wgl = int(os.environ.get("MH_WG_LEVELS", "2"))  # default of launch_entries_fixed
+    wgl = int(os.environ.get("MH_WG_LEVELS", "1"))  # default of launch_entries_fixed
     top = min({1: 0, 2: 1, 4: 2}[lpl] + wgl, max(m.levels_len(n) and (n - 1).bit_length(), 0))
     widths = [-(-n // (1 << l)) for l in range(top + 1)]
     nodes_written = sum(widths)

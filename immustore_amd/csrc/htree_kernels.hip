@@ -735,8 +735,13 @@ static int choose_lpl(uint64_t n) {
         int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) return v;
     }
-    // keep >= 256 CUs x 16 waves x 64 lanes busy
-    if (n >= (uint64_t)4 * 262144) return 4;
+    // keep >= 256 CUs x 16 waves x 64 lanes busy.  Two entries per lane (one
+    // in-lane node level) from 2^19 entries up: at 2^20 that is 2048
+    // workgroups, 8 per CU in one round, against 4 per CU with four entries
+    // per lane -- twice the waves per SIMD to hide the DMA and LDS latency of
+    // an isolated launch (round-2 sweep, profiles/ab_lpl_wgl_r02.txt: leaf
+    // launch 0.835 -> 0.79 ms, single build 0.96-0.97 -> 0.93-0.94 ms, three
+    // builds in flight within 0.2 %).  MH_LPL=4 restores the round-1 shape.
     if (n >= (uint64_t)2 * 262144) return 2;
     return 1;
 }
@@ -766,7 +771,7 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
     // with builds in flight at 1000-2000 steps (round-2 sweep in
     // profiles/ab_wg_levels_r02.txt; 4 in round 1's 20-step A/B): deeper
     // in-kernel subtrees idle most lanes at the end of the leaf kernel.
-    int wgl = 2;
+    int wgl = 1;  // with two entries per lane (profiles/ab_lpl_wgl_r02.txt)
     if (const char *e = getenv("MH_WG_LEVELS")) wgl = std::max(0, std::min(8, atoi(e)));
     {
         TimerScope ts(tm, "entries_fixed", st);
