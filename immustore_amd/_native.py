@@ -288,8 +288,11 @@ SIGNATURES = {
                                                      vp]),
     "mh_multi_htree_build_entries": (i32, [vp, i32, u64, u8p, vp, u8p, vp, u8p, vp, u8p,
                                            u8p, u8p, u8p, u8p]),
-    "mh_multi_dev_ahtree_append_batch": (i32, [vp, u64, vp, u32, vp, vp]),
-    "mh_multi_ahtree_append_batch": (i32, [vp, u8p, u64, u32, u8p, u8p]),
+    "mh_multi_dev_ahtree_append_batch": (i32, [vp, u64, u8p, u64, vp, u32, vp, vp]),
+    "mh_multi_ahtree_append_batch": (i32, [vp, u64, u8p, u8p, u64, u32, u8p, u8p]),
+    "mh_ahtree_range_plan": (i32, [u64, u64, i32, C.POINTER(i32), vp, C.POINTER(i32)]),
+    "mh_dev_ahtree_append_range": (i32, [vp, u8p, u64, u8p, u8p, u64, u32, u8p]),
+    "mh_dev_ahtree_peaks": (i32, [vp, u8p, u64, u8p]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
                                 u8p, vp]),
     "mh_commit_pipe_new": (i32, [vp, u64, C.POINTER(vp)]),

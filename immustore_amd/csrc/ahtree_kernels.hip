@@ -31,6 +31,15 @@ __device__ __forceinline__ uint64_t dev_nodes_until(uint64_t n) {
     return until_from_s(n, popsum_below(n));
 }
 
+// node(k, l) of an append range that starts after edge.lo: a node ending at
+// or before edge.lo is a peak of edge.lo (the perfect subtree of its set bit
+// l), kept in the frontier edge.fr[l] instead of the dLog.  With no edge
+// (lo = 0) every node comes from the dLog.
+__device__ __forceinline__ const uint8_t *edge_node(const uint8_t *dlog, const AhtEdge &edge,
+                                                    uint64_t k, int l) {
+    return k <= edge.lo ? edge.fr + l * 32 : dlog + (dev_nodes_until(k) + (uint64_t)l) * 32;
+}
+
 // phase 1: d_0 = leaf of payload (plen == 32: one block, the store's Alh),
 // plus, when asked, the appendable records of the same appends (SURVEY.md
 // 8(f) row 4): pLog BE32 len || payload (ahtree.go:266-282) and cLog
@@ -106,13 +115,13 @@ __global__ __launch_bounds__(256) void k_aht_leaves(uint8_t *__restrict__ dlog, 
 
 // phase 2: perfect nodes of level l ending at e = (j+1)*2^l, j in [j0, j0+cnt)
 __global__ __launch_bounds__(256) void k_aht_perfect(uint8_t *__restrict__ dlog, int l,
-                                                     uint64_t j0, uint64_t cnt) {
+                                                     uint64_t j0, uint64_t cnt, AhtEdge edge) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const uint64_t e = (j0 + t + 1) << l;
     const uint64_t half = 1ull << (l - 1);
     uint32_t a[8], b[8], o[8];
-    load_digest(dlog + (dev_nodes_until(e - half) + (uint64_t)(l - 1)) * 32, a);
+    load_digest(edge_node(dlog, edge, e - half, l - 1), a);
     const uint64_t ue = dev_nodes_until(e);
     load_digest(dlog + (ue + (uint64_t)(l - 1)) * 32, b);
     node_hash(a, b, o);
@@ -121,7 +130,8 @@ __global__ __launch_bounds__(256) void k_aht_perfect(uint8_t *__restrict__ dlog,
 
 // phase 3: spine chains (ahtree.go:296-322 above the trailing-ones run)
 __global__ __launch_bounds__(256) void k_aht_spine(uint8_t *__restrict__ dlog, uint64_t n0,
-                                                   uint64_t m, uint8_t *__restrict__ roots_out) {
+                                                   uint64_t m, uint8_t *__restrict__ roots_out,
+                                                   AhtEdge edge) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint64_t n = n0 + 1 + i;
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(256) void k_aht_spine(uint8_t *__restrict__ dlog, u
         const int l = __builtin_ctzll(rest);
         const uint64_t uk = until_from_s(rest, sk);  // nodesUntil(k), k = rest
         uint32_t left[8];
-        load_digest(dlog + (uk + (uint64_t)l) * 32, left);
+        load_digest(rest <= edge.lo ? edge.fr + l * 32 : dlog + (uk + (uint64_t)l) * 32, left);
         node_hash(left, h, h);
         t++;
         store_digest(dlog + (un + (uint64_t)t) * 32, h);
@@ -155,7 +165,7 @@ __global__ __launch_bounds__(256) void k_aht_spine(uint8_t *__restrict__ dlog, u
 // loop, so the table cost is amortised over many node hashes.
 
 __global__ __launch_bounds__(512) void k_aht_perfect_t(uint8_t *__restrict__ dlog, int l,
-                                                       uint64_t j0, uint64_t cnt) {
+                                                       uint64_t j0, uint64_t cnt, AhtEdge edge) {
     extern __shared__ uint32_t tab[];
     node_tab_init(tab);
     const uint64_t half = 1ull << (l - 1);
@@ -163,7 +173,7 @@ __global__ __launch_bounds__(512) void k_aht_perfect_t(uint8_t *__restrict__ dlo
          t += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t e = (j0 + t + 1) << l;
         uint32_t a[8], b[8], o[8];
-        load_digest(dlog + (dev_nodes_until(e - half) + (uint64_t)(l - 1)) * 32, a);
+        load_digest(edge_node(dlog, edge, e - half, l - 1), a);
         const uint64_t ue = dev_nodes_until(e);
         load_digest(dlog + (ue + (uint64_t)(l - 1)) * 32, b);
         node_hash_tab(a, b, o, tab);
@@ -195,7 +205,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k
                                                             uint8_t *__restrict__ roots_out,
                                                             SpinePairs pr, uint64_t blk0,
                                                             uint64_t nblk,
-                                                            uint32_t *__restrict__ work_ctr) {
+                                                            uint32_t *__restrict__ work_ctr,
+                                                            AhtEdge edge) {
     extern __shared__ uint32_t tab[];
     node_tab_init(tab);
     const int lane = threadIdx.x & 63;
@@ -251,7 +262,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6))) void k
             // drop the lowest set bit l of rest (rank popcount(rest) from the
             // top) and prefetch the next step's left node before hashing
             const int l = __builtin_ctzll(rest);
-            load_digest(dlog + (until_from_s(rest, sk) + (uint64_t)l) * 32, left);
+            load_digest(rest <= edge.lo ? edge.fr + l * 32
+                                        : dlog + (until_from_s(rest, sk) + (uint64_t)l) * 32,
+                        left);
             sk -= (l ? ((uint64_t)l << (l - 1)) : 0) +
                   ((uint64_t)(__builtin_popcountll(rest) - 1) << l);
             rest &= rest - 1;
@@ -319,7 +332,7 @@ hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64
 
 // Phase 2: perfect nodes of levels [lmin, lmax] whose end lies in (n0, n_end].
 hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
-                                 uint64_t n_end, int lmin, int lmax) {
+                                 uint64_t n_end, int lmin, int lmax, const AhtEdge &edge) {
     const bool tab = use_node_table();
     TimerScope ts(tm, "aht_perfect", st);
     for (int l = std::max(lmin, 1); l <= std::min(lmax, 63) && (n_end >> l) != 0; l++) {
@@ -330,18 +343,18 @@ hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint6
         if (tab && j1 - j0 >= (1ull << 18))
             hipLaunchKernelGGL(k_aht_perfect_t,
                                dim3(resident_grid((const void *)k_aht_perfect_t, 512, j1 - j0)),
-                               dim3(512), kNodeTabBytes, st, dlog, l, j0, j1 - j0);
+                               dim3(512), kNodeTabBytes, st, dlog, l, j0, j1 - j0, edge);
         else
             hipLaunchKernelGGL(k_aht_perfect, dim3(grid_for(j1 - j0, 256)), dim3(256), 0, st, dlog,
-                               l, j0, j1 - j0);
+                               l, j0, j1 - j0, edge);
     }
     return hipGetLastError();
 }
 
 // Phase 3: spine chains of (n0, n0 + m] (every perfect node they read must be
-// in the dLog already).
+// in the dLog already, or a peak of edge.lo in the frontier).
 hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0, uint64_t m,
-                               uint8_t *roots_out, uint32_t *work_ctr) {
+                               uint8_t *roots_out, uint32_t *work_ctr, const AhtEdge &edge) {
     if (!m) return hipSuccess;
     TimerScope ts(tm, "aht_spine", st);
     const uint64_t n_end = n0 + m;
@@ -352,21 +365,22 @@ hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_
         hipLaunchKernelGGL(k_aht_spine_pairs,
                            dim3(resident_grid((const void *)k_aht_spine_pairs, 512, nblk * 64)),
                            dim3(512), kNodeTabBytes, st, dlog, n0, m, roots_out, pairs, blk0, nblk,
-                           work_ctr);
+                           work_ctr, edge);
     } else {
         hipLaunchKernelGGL(k_aht_spine, dim3(grid_for(m, 256)), dim3(256), 0, st, dlog, n0, m,
-                           roots_out);
+                           roots_out, edge);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
-                                uint8_t *roots_out, uint32_t *work_ctr, const AhtLogs &lg) {
+                                uint8_t *roots_out, uint32_t *work_ctr, const AhtLogs &lg,
+                                const AhtEdge &edge) {
     if (!m) return hipSuccess;
     if (hipError_t e = launch_ahtree_leaves(st, tm, dlog, n0, payloads, m, plen, lg)) return e;
-    if (hipError_t e = launch_ahtree_perfect(st, tm, dlog, n0, n0 + m, 1, 63)) return e;
-    return launch_ahtree_spine(st, tm, dlog, n0, m, roots_out, work_ctr);
+    if (hipError_t e = launch_ahtree_perfect(st, tm, dlog, n0, n0 + m, 1, 63, edge)) return e;
+    return launch_ahtree_spine(st, tm, dlog, n0, m, roots_out, work_ctr, edge);
 }
 
 // Sharded appends: write the all-gathered shard roots
@@ -390,6 +404,109 @@ hipError_t launch_ahtree_put_shard_roots(hipStream_t st, Timer *tm, uint8_t *dlo
     if (hipError_t e = hipGetLastError()) return e;
     // the cross-shard perfect nodes above them, for every end <= count * 2^level
     return launch_ahtree_perfect(st, tm, dlog, 0, count << level, level + 1, 63);
+}
+
+// ---------------------------------------------------------------------------
+// Ranged multi-device append (capi_multi.hip): pieces, the piece tree, frontiers.
+
+__device__ __forceinline__ void copy32(uint8_t *dst, const uint8_t *src) {
+    reinterpret_cast<uint4 *>(dst)[0] = reinterpret_cast<const uint4 *>(src)[0];
+    reinterpret_cast<uint4 *>(dst)[1] = reinterpret_cast<const uint4 *>(src)[1];
+}
+
+__global__ void k_aht_gather_pieces(const uint8_t *__restrict__ dlog, int k, uint64_t e0,
+                                    uint64_t count, uint8_t *__restrict__ send) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint64_t e = (e0 + i) << k;
+    copy32(send + i * 32, dlog + (dev_nodes_until(e) + (uint64_t)k) * 32);
+}
+
+// One workgroup.  Piece level l' (global level k + l') holds slots
+// j in [N0 >> l', Pend >> l'] (node ending at (j << l') * S); slot N0 >> l' is
+// the old peak of n0 at level k + l' when that bit of n0 is set (a left child
+// ending at or before n0 is always one), every other slot is new:
+// level 0 = the all-gathered piece roots, level l' = H(slot 2j-1, slot 2j) of
+// level l'-1 (ahtree.go:296-322 restricted to perfect nodes).  The tree is
+// tiny (tens of pieces per device); it runs replicated on every device.
+__global__ __launch_bounds__(256) void k_aht_top(AhtTopArgs a, const uint8_t *__restrict__ recv,
+                                                 const uint8_t *__restrict__ peaks_n0,
+                                                 uint8_t *__restrict__ top,
+                                                 uint8_t *__restrict__ dlog,
+                                                 uint8_t *__restrict__ fr) {
+    const int t = threadIdx.x;
+    for (uint64_t j = a.N0 + t; j <= a.Pend; j += 256) {
+        uint8_t *dst = top + (a.lev_off[0] + j - a.N0) * 32;
+        if (j == a.N0) {
+            if ((a.n0 >> a.k) & 1) copy32(dst, peaks_n0 + a.k * 32);
+            continue;
+        }
+        int d = 0;
+        while (d + 1 < a.G && j > a.pe0[d + 1]) d++;
+        copy32(dst, recv + ((uint64_t)d * a.Pmax + (j - a.pe0[d] - 1)) * 32);
+    }
+    __syncthreads();
+    for (int l = 1; l < a.nlev; l++) {
+        const uint64_t b = a.N0 >> l, bp = a.N0 >> (l - 1), jend = a.Pend >> l;
+        const int gl = a.k + l;
+        for (uint64_t j = b + t; j <= jend; j += 256) {
+            uint8_t *dst = top + (a.lev_off[l] + j - b) * 32;
+            if (j == b) {
+                if ((a.n0 >> gl) & 1) copy32(dst, peaks_n0 + gl * 32);
+                continue;
+            }
+            uint32_t x[8], y[8], o[8];
+            load_digest(top + (a.lev_off[l - 1] + 2 * j - 1 - bp) * 32, x);
+            load_digest(top + (a.lev_off[l - 1] + 2 * j - bp) * 32, y);
+            node_hash(x, y, o);
+            store_digest(dst, o);
+            const uint64_t e = j << gl;
+            if (e > a.lo && e <= a.hi) store_digest(dlog + (dev_nodes_until(e) + (uint64_t)gl) * 32, o);
+        }
+        __syncthreads();
+    }
+    // the peaks of lo (a multiple of S, so every set bit is >= k)
+    if (a.lo > a.n0 && t < 64 && t >= a.k && ((a.lo >> t) & 1)) {
+        const int lp = t - a.k;
+        const uint64_t j = (a.lo >> a.k) >> lp;
+        copy32(fr + t * 32, top + (a.lev_off[lp] + j - (a.N0 >> lp)) * 32);
+    }
+}
+
+__global__ void k_aht_peaks(const uint8_t *__restrict__ dlog, uint64_t n, uint8_t *__restrict__ fr) {
+    const int l = threadIdx.x;
+    if (l >= 64 || !((n >> l) & 1)) return;
+    const uint64_t kk = l ? (n >> l) << l : n;
+    copy32(fr + l * 32, dlog + (dev_nodes_until(kk) + (uint64_t)l) * 32);
+}
+
+hipError_t launch_ahtree_gather_pieces(hipStream_t st, const uint8_t *dlog, int k, uint64_t e0,
+                                       uint64_t count, uint8_t *send) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_aht_gather_pieces, dim3(grid_for(count, 256)), dim3(256), 0, st, dlog, k,
+                       e0, count, send);
+    return hipGetLastError();
+}
+
+hipError_t launch_ahtree_top(hipStream_t st, const AhtTopArgs &a, const uint8_t *recv,
+                             const uint8_t *peaks_n0, uint8_t *top, uint8_t *dlog, uint8_t *fr) {
+    hipLaunchKernelGGL(k_aht_top, dim3(1), dim3(256), 0, st, a, recv, peaks_n0, top, dlog, fr);
+    return hipGetLastError();
+}
+
+__global__ void k_aht_put_slots(AhtSlots s, uint8_t *__restrict__ dst) {
+    const int t = threadIdx.x;  // 128 threads x 16 B
+    reinterpret_cast<uint4 *>(dst)[t] = reinterpret_cast<const uint4 *>(s.b)[t];
+}
+
+hipError_t launch_ahtree_put_slots(hipStream_t st, const AhtSlots &s, uint8_t *dst) {
+    hipLaunchKernelGGL(k_aht_put_slots, dim3(1), dim3(128), 0, st, s, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_ahtree_peaks(hipStream_t st, const uint8_t *dlog, uint64_t n, uint8_t *fr) {
+    hipLaunchKernelGGL(k_aht_peaks, dim3(1), dim3(64), 0, st, dlog, n, fr);
+    return hipGetLastError();
 }
 
 }  // namespace mh

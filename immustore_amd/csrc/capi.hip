@@ -897,6 +897,53 @@ extern "C" uint64_t mh_ahtree_node_index(uint64_t n, int level) {
     return ahtree_nodes_until(n) + (uint64_t)level;
 }
 
+extern "C" int mh_dev_ahtree_append_range(mh_ctx *c, uint8_t *dlog_range, uint64_t n0,
+                                          const uint8_t *peaks, const uint8_t *payloads,
+                                          uint64_t m, uint32_t plen, uint8_t *roots_out) {
+    return mh_guard([&]() -> int {
+        if (!c || (m && (!dlog_range || (!payloads && plen))) || (n0 && !peaks))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (((uintptr_t)dlog_range & 15) || m > ~0ull - n0) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!m) return MH_OK;
+        hipSetDevice(c->device);
+        AhtSlots slots;
+        memset(slots.b, 0, sizeof slots.b);
+        for (int l = 0, q = 0; l < 64; l++)
+            if ((n0 >> l) & 1) memcpy(slots.b + l * 32, peaks + 32 * (q++), 32);
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(c->s_ctr.ensure(256));
+        MH_HIP(c->s_edge.ensure(64 * 32));
+        MH_HIP(launch_ahtree_put_slots(c->stream, slots, c->s_edge.as<uint8_t>()));
+        AhtEdge edge;
+        edge.fr = c->s_edge.as<uint8_t>();
+        edge.lo = n0;
+        // dLog index x lives at dlog_range + (x - nodesUpto(n0)) * 32
+        uint8_t *vb = reinterpret_cast<uint8_t *>((uintptr_t)dlog_range -
+                                                  (uintptr_t)(ahtree_nodes_upto(n0) * 32));
+        MH_HIP(launch_ahtree_append(c->stream, c->tm(), vb, n0, payloads, m, plen, roots_out,
+                                    c->s_ctr.as<uint32_t>(), AhtLogs(), edge));
+        return MH_OK;
+    });
+}
+
+extern "C" int mh_dev_ahtree_peaks(mh_ctx *c, const uint8_t *dlog, uint64_t n, uint8_t *peaks_out) {
+    return mh_guard([&]() -> int {
+        if (!c || (n && (!dlog || !peaks_out))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if ((uintptr_t)dlog & 15) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!n) return MH_OK;
+        hipSetDevice(c->device);
+        std::lock_guard<std::mutex> lk(c->mu);
+        MH_HIP(c->s_edge.ensure(64 * 32));
+        MH_HIP(launch_ahtree_peaks(c->stream, dlog, n, c->s_edge.as<uint8_t>()));
+        uint8_t slots[64 * 32];
+        MH_HIP(hipMemcpyAsync(slots, c->s_edge.p, sizeof slots, hipMemcpyDeviceToHost, c->stream));
+        MH_HIP(hipStreamSynchronize(c->stream));
+        for (int l = 0, q = 0; l < 64; l++)
+            if ((n >> l) & 1) memcpy(peaks_out + 32 * (q++), slots + l * 32, 32);
+        return MH_OK;
+    });
+}
+
 extern "C" int mh_dev_ahtree_append_local(mh_ctx *c, uint8_t *dlog, uint64_t n0,
                                           const uint8_t *payloads, uint64_t m, uint32_t plen,
                                           int shard_bits) {

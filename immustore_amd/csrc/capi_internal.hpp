@@ -177,6 +177,7 @@ struct mh_ctx {
     EventTimer timer;
     std::mutex mu;  // guards scratch for mh_dev_* calls
     DevBuf s_hvals, s_msgoff, s_msgs, s_digests, s_idx, s_offs, s_ctr;
+    DevBuf s_edge;        // ahtree frontier of a ranged append (64 x 32 B)
     DevBuf s_sort;        // length-class sort of ragged messages (varlen_kernels.hip)
     DevBuf s_tx, s_tree;  // tx layer (capi_tx.hip)
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate

@@ -75,8 +75,10 @@ struct mh_multi {
     bool use_rccl = true;
     struct Dev {
         DevBuf keys, vals, hv, levels, send, recv, top, dlog, ovr;
+        DevBuf fr, pk, ctr;  // ranged ahtree append: frontier, old peaks, work queue
     };
     std::vector<std::unique_ptr<Dev>> buf;
+    std::vector<hipEvent_t> ev;  // duplicate-device gathers (one per context)
     std::mutex mu;  // one build at a time per mh_multi
 };
 
@@ -145,6 +147,7 @@ extern "C" int mh_multi_destroy(mh_multi *m) {
         for (int d = 0; d < (int)m->buf.size(); d++) {
             hipSetDevice(m->dev[d]);
             m->buf[d].reset();  // frees on the owning device
+            if (d < (int)m->ev.size()) hipEventDestroy(m->ev[d]);
         }
         for (mh_ctx *c : m->ctx)
             if (c) mh_ctx_destroy(c);
@@ -204,19 +207,36 @@ int per_device(int n, F &&fn) {
     return MH_OK;
 }
 
-// All-gather of one 32-byte root per device (send[d] -> recv[d] = K x 32 B),
-// on each device's context stream.
-int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
-                 const std::vector<uint8_t *> &recv) {
+// All-gather of `bytes` per device (send[d] -> recv[d] = K x bytes), on each
+// device's context stream.
+int gather_bytes(mh_multi *m, const std::vector<const uint8_t *> &send,
+                 const std::vector<uint8_t *> &recv, uint64_t bytes) {
     if (!m->use_rccl) {
-        // shards sharing devices: wait for every subtree, then copy the roots
+        // shards sharing devices: wait for every subtree, then copy the
+        // slices; every stream then waits for every stream's copies, so no
+        // later work on stream s (which may overwrite send[s]) can overtake a
+        // copy that reads it
         for (int d = 0; d < m->K; d++)
             if (int st = mh_ctx_synchronize(m->ctx[d])) return st;
+        if ((int)m->ev.size() < m->K) {
+            for (int d = (int)m->ev.size(); d < m->K; d++) {
+                MH_HIP(hipSetDevice(m->dev[d]));
+                hipEvent_t e;
+                MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                m->ev.push_back(e);
+            }
+        }
         for (int d = 0; d < m->K; d++) {
             MH_HIP(hipSetDevice(m->dev[d]));
             for (int s = 0; s < m->K; s++)
-                MH_HIP(hipMemcpyAsync(recv[d] + 32 * s, send[s], 32, hipMemcpyDefault,
+                MH_HIP(hipMemcpyAsync(recv[d] + bytes * s, send[s], bytes, hipMemcpyDefault,
                                       m->ctx[d]->stream));
+            MH_HIP(hipEventRecord(m->ev[d], m->ctx[d]->stream));
+        }
+        for (int s = 0; s < m->K; s++) {
+            MH_HIP(hipSetDevice(m->dev[s]));
+            for (int d = 0; d < m->K; d++)
+                if (d != s) MH_HIP(hipStreamWaitEvent(m->ctx[s]->stream, m->ev[d], 0));
         }
         return MH_OK;
     }
@@ -224,7 +244,7 @@ int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
     MH_NCCL(R.group_start());
     for (int d = 0; d < m->K; d++) {
         MH_HIP(hipSetDevice(m->dev[d]));
-        if (R.all_gather(send[d], recv[d], 32, ncclUint8, m->comm[d], m->ctx[d]->stream) !=
+        if (R.all_gather(send[d], recv[d], bytes, ncclUint8, m->comm[d], m->ctx[d]->stream) !=
             ncclSuccess) {
             R.group_end();
             return MH_ERR_COLLECTIVE;
@@ -232,6 +252,11 @@ int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
     }
     MH_NCCL(R.group_end());
     return MH_OK;
+}
+
+int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,
+                 const std::vector<uint8_t *> &recv) {
+    return gather_bytes(m, send, recv, 32);
 }
 
 }  // namespace
@@ -482,135 +507,244 @@ extern "C" int mh_multi_htree_build_entries(mh_multi *m, int version, uint64_t n
 }
 
 // ============================================================================
-// Sharded ahtree batch append (C3 at scale; ahtree.go:246-373 over K devices).
-// A batch of `total` appends to an EMPTY tree is cut into K ranges of S = 2^k
-// appends (the smallest S with K*S >= total); device d appends (dS, dS + m_d]
-// into its own globally indexed dLog: the leaves, the perfect nodes of levels
-// <= k and every spine node below level k lie inside its range; only the
-// nodes above level k need the other ranges, and they are built from the
-// complete shards' roots, all-gathered once (32 B per device, RCCL).  The
-// phases are the ones mh_dev_ahtree_append_local / put_shard_roots /
-// append_spine expose to torch.distributed ranks.
+// Sharded ahtree batch append onto a tree of any size n0 (C3 at scale, and
+// the replay of syncBinaryLinking, immustore.go:1198-1232, which resumes at
+// aht.Size()+1 on every open, :686-693): ahtree.go:246-373 over K devices.
+//
+// The batch (n0, n0 + total] is cut at multiples of S = 2^k into G <= K
+// ranges (b[d], b[d+1]] of nearly equal size (S <= total / 8K, so each range
+// holds >= 8 aligned pieces of S appends and the split is within 1/8 of even).
+// Every node an append reads is either inside its own range or a PEAK of the
+// range's left end b[d] (the perfect subtree of a set bit of b[d]; for the
+// first range these are the old tree's peaks, which the caller passes), so a
+// device keeps only its own dLog range plus a 64-slot frontier:
+//   1. leaves + perfect nodes of levels 1..k ending in (b[d], b[d+1]]
+//      (range 0 reads the old peaks below level k; the others read nothing
+//      outside their range);
+//   2. all-gather of the level-k roots of the complete pieces (<= Pmax per
+//      device; RCCL, 32 B each);
+//   3. the piece tree above level k (replicated, tens of nodes), its nodes
+//      that end in the device's range into its dLog range, the peaks of
+//      b[d] into its frontier;
+//   4. the spine chains of the range (left nodes at or before b[d] from the
+//      frontier).
 // ============================================================================
 namespace {
 
-int ahtree_shard_bits(uint64_t total, int K) {
-    int k = 0;
-    while ((uint64_t)K * (1ull << k) < total) k++;
-    return k;
+struct AhtPlan {
+    int k = 0, G = 0;
+    uint64_t b[kAhtMaxRanges + 1] = {};
+};
+
+int aht_plan(uint64_t n0, uint64_t total, int ndev, AhtPlan &p) {
+    if (ndev < 1 || ndev > kAhtMaxRanges || total > ~0ull - n0) return MH_ERR_ILLEGAL_ARGUMENTS;
+    p = AhtPlan();
+    p.b[0] = n0;
+    if (!total) return MH_OK;
+    const uint64_t target = total / (uint64_t)ndev + (total % (uint64_t)ndev != 0);
+    while (p.k < 62 && (16ull << p.k) <= target) p.k++;  // largest S with 8 S <= target
+    const uint64_t S = 1ull << p.k, end = n0 + total;
+    for (int d = 1; d < ndev; d++) {
+        const unsigned __int128 x = (unsigned __int128)total * (unsigned)d + (unsigned)ndev / 2;
+        const uint64_t want = n0 + (uint64_t)(x / (unsigned)ndev);
+        uint64_t r = (want >> p.k) << p.k;  // nearest multiple of S
+        if (S > 1 && want - r >= S / 2) r += S;
+        if (r > p.b[p.G] && r < end) p.b[++p.G] = r;
+    }
+    p.b[++p.G] = end;
+    return MH_OK;
 }
 
-// phases 2-3 once every device has run phase 1 into dlog[d]: shard roots
-// all-gathered, the nodes above shard level, then each device's spine
-int ahtree_multi_finish(mh_multi *m, uint64_t total, int k, uint8_t *const *dlog,
-                        uint8_t *const *roots_out) {
-    const int K = m->K;
-    const uint64_t S = 1ull << k;
-    std::vector<const uint8_t *> send(K);
-    std::vector<uint8_t *> recv(K);
-    for (int d = 0; d < K; d++) {
+// packed peaks of n (lowest level first, popcount(n) x 32 B) -> 64 slots
+void expand_peaks(uint64_t n, const uint8_t *packed, AhtSlots &slots) {
+    memset(slots.b, 0, sizeof slots.b);
+    int q = 0;
+    for (int l = 0; l < 64; l++)
+        if ((n >> l) & 1) memcpy(slots.b + l * 32, packed + 32 * (q++), 32);
+}
+
+inline uint8_t *range_base(uint8_t *buf, uint64_t lo) {
+    // dLog index x of the range lives at buf + (x - nodesUpto(lo)) * 32
+    return reinterpret_cast<uint8_t *>((uintptr_t)buf - (uintptr_t)(ahtree_nodes_upto(lo) * 32));
+}
+
+// Phases 1-4 for ranges already planned; payload[d] / dlog[d] are device
+// pointers of range d (dlog[d] holds nodesUpto(b[d+1]) - nodesUpto(b[d])
+// digests), slots = the old peaks of n0 in the 64-slot layout (host).
+int aht_multi_run(mh_multi *m, const AhtPlan &p, const AhtSlots &slots,
+                  const std::vector<const uint8_t *> &payload, uint32_t plen,
+                  const std::vector<uint8_t *> &dlog, const std::vector<uint8_t *> &roots_out) {
+    const int K = m->K, G = p.G, k = p.k;
+    const uint64_t n0 = p.b[0];
+    uint64_t Pmax = 1;
+    AhtTopArgs ta;
+    ta.k = k;
+    ta.G = G;
+    ta.n0 = n0;
+    ta.N0 = n0 >> k;
+    ta.Pend = p.b[G] >> k;
+    for (int d = 0; d <= G; d++) ta.pe0[d] = p.b[d] >> k;
+    for (int d = 0; d < G; d++) Pmax = std::max<uint64_t>(Pmax, ta.pe0[d + 1] - ta.pe0[d]);
+    ta.Pmax = Pmax;
+    uint64_t top_slots = 0;
+    ta.nlev = 0;
+    while (ta.nlev < 64 - k && (ta.Pend >> ta.nlev) != 0) {
+        ta.lev_off[ta.nlev] = top_slots;
+        top_slots += (ta.Pend >> ta.nlev) - (ta.N0 >> ta.nlev) + 1;
+        ta.nlev++;
+    }
+    // 1. leaves + perfect levels (all of them when one range holds the batch)
+    for (int d = 0; d < G; d++) {
         mh_multi::Dev &B = *m->buf[d];
         MH_HIP(hipSetDevice(m->dev[d]));
-        const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
-        if (md == S) {
-            send[d] = dlog[d] + 32 * mh_ahtree_node_index(n0 + S, k);
-        } else {  // a short or empty last range has no shard root: zeros, unused
-            MH_HIP(B.send.ensure(32));
-            MH_HIP(hipMemsetAsync(B.send.p, 0, 32, m->ctx[d]->stream));
-            send[d] = B.send.as<uint8_t>();
-        }
-        MH_HIP(B.recv.ensure(32 * (uint64_t)K));
-        recv[d] = B.recv.as<uint8_t>();
+        hipStream_t st = m->ctx[d]->stream;
+        MH_HIP(B.pk.ensure(64 * 32));
+        MH_HIP(B.fr.ensure(64 * 32));
+        MH_HIP(B.ctr.ensure(256));
+        // by value through the kernel arguments: nothing host-side to outlive
+        MH_HIP(launch_ahtree_put_slots(st, slots, B.pk.as<uint8_t>()));
+        const uint64_t lo = p.b[d], hi = p.b[d + 1];
+        uint8_t *vb = range_base(dlog[d], lo);
+        AhtEdge edge;
+        edge.fr = d ? B.fr.as<uint8_t>() : B.pk.as<uint8_t>();
+        edge.lo = lo;
+        MH_HIP(launch_ahtree_leaves(st, m->ctx[d]->tm(), vb, lo, payload[d], hi - lo, plen));
+        MH_HIP(launch_ahtree_perfect(st, m->ctx[d]->tm(), vb, lo, hi, 1, G == 1 ? 63 : k, edge));
     }
-    if (int st = gather_roots(m, send, recv)) return st;
-    const uint64_t complete = std::min<uint64_t>(total / S, (uint64_t)K);
-    for (int d = 0; d < K; d++) {
-        const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
-        if (!md) continue;
-        if (int st = mh_dev_ahtree_put_shard_roots(m->ctx[d], dlog[d], k, complete, recv[d]))
-            return st;
-        if (int st = mh_dev_ahtree_append_spine(m->ctx[d], dlog[d], n0, md,
-                                                roots_out ? roots_out[d] : nullptr))
-            return st;
+    if (G > 1) {
+        // 2. the complete pieces' level-k roots, Pmax slots per device
+        std::vector<const uint8_t *> send(K);
+        std::vector<uint8_t *> recv(K);
+        for (int d = 0; d < K; d++) {
+            mh_multi::Dev &B = *m->buf[d];
+            MH_HIP(hipSetDevice(m->dev[d]));
+            MH_HIP(B.send.ensure(Pmax * 32));
+            MH_HIP(B.recv.ensure((uint64_t)K * Pmax * 32));
+            if (d < G)
+                MH_HIP(launch_ahtree_gather_pieces(m->ctx[d]->stream, range_base(dlog[d], p.b[d]),
+                                                   k, ta.pe0[d] + 1, ta.pe0[d + 1] - ta.pe0[d],
+                                                   B.send.as<uint8_t>()));
+            send[d] = B.send.as<uint8_t>();
+            recv[d] = B.recv.as<uint8_t>();
+        }
+        if (int st = gather_bytes(m, send, recv, Pmax * 32)) return st;
+        // 3. piece tree, the device's nodes above level k, its frontier
+        for (int d = 0; d < G; d++) {
+            mh_multi::Dev &B = *m->buf[d];
+            MH_HIP(hipSetDevice(m->dev[d]));
+            MH_HIP(B.top.ensure(top_slots * 32));
+            AhtTopArgs a = ta;
+            a.lo = p.b[d];
+            a.hi = p.b[d + 1];
+            MH_HIP(launch_ahtree_top(m->ctx[d]->stream, a, recv[d], B.pk.as<uint8_t>(),
+                                     B.top.as<uint8_t>(), range_base(dlog[d], p.b[d]),
+                                     B.fr.as<uint8_t>()));
+        }
+    }
+    // 4. spines
+    for (int d = 0; d < G; d++) {
+        mh_multi::Dev &B = *m->buf[d];
+        MH_HIP(hipSetDevice(m->dev[d]));
+        AhtEdge edge;
+        edge.fr = d ? B.fr.as<uint8_t>() : B.pk.as<uint8_t>();
+        edge.lo = p.b[d];
+        MH_HIP(launch_ahtree_spine(m->ctx[d]->stream, m->ctx[d]->tm(), range_base(dlog[d], p.b[d]),
+                                   p.b[d], p.b[d + 1] - p.b[d], roots_out[d],
+                                   B.ctr.as<uint32_t>(), edge));
     }
     return MH_OK;
 }
 
+int peaks_ok(uint64_t n0, const uint8_t *peaks) { return n0 == 0 || peaks != nullptr; }
+
 }  // namespace
 
-extern "C" int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t total,
-                                                const uint8_t *const *payloads, uint32_t plen,
-                                                uint8_t *const *dlog, uint8_t *const *roots_out) {
+extern "C" int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *shard_bits,
+                                    uint64_t *bounds, int *nranges) {
     return mh_guard([&]() -> int {
-        if (!m || !dlog || (total && !payloads)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        if (total == 0) return MH_OK;
-        std::lock_guard<std::mutex> lk(m->mu);
-        const int K = m->K;
-        const int k = ahtree_shard_bits(total, K);
-        const uint64_t S = 1ull << k;
-        for (int d = 0; d < K; d++) {
-            const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
-            if (!md) continue;
-            if (!dlog[d] || (plen && !payloads[d])) return MH_ERR_ILLEGAL_ARGUMENTS;
-            if (int st = mh_dev_ahtree_append_local(m->ctx[d], dlog[d], n0, payloads[d], md, plen,
-                                                    k))
-                return st;
-        }
-        return ahtree_multi_finish(m, total, k, dlog, roots_out);
+        if (!shard_bits || !bounds || !nranges) return MH_ERR_ILLEGAL_ARGUMENTS;
+        AhtPlan p;
+        if (int st = aht_plan(n0, total, ndev, p)) return st;
+        *shard_bits = p.k;
+        *nranges = p.G;
+        for (int d = 0; d <= p.G; d++) bounds[d] = p.b[d];
+        return MH_OK;
     });
 }
 
-extern "C" int mh_multi_ahtree_append_batch(mh_multi *m, const uint8_t *payloads, uint64_t total,
-                                            uint32_t plen, uint8_t *dlog_out, uint8_t root[32]) {
+extern "C" int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint8_t *peaks,
+                                                uint64_t total, const uint8_t *const *payloads,
+                                                uint32_t plen, uint8_t *const *dlog,
+                                                uint8_t *const *roots_out) {
     return mh_guard([&]() -> int {
-        if (!m || !root || (total && plen && !payloads)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        if (total == 0) return MH_ERR_UNEXISTENT_DATA;  // RootAt(0) of an empty tree
+        if (!m || !dlog || (total && !payloads) || !peaks_ok(n0, peaks))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (total == 0) return MH_OK;
+        AhtPlan p;
+        if (int st = aht_plan(n0, total, m->K, p)) return st;
+        std::vector<const uint8_t *> pay(m->K, nullptr);
+        std::vector<uint8_t *> dl(m->K, nullptr), ro(m->K, nullptr);
+        for (int d = 0; d < p.G; d++) {
+            if (!dlog[d] || ((uintptr_t)dlog[d] & 15) || (plen && !payloads[d]))
+                return MH_ERR_ILLEGAL_ARGUMENTS;
+            pay[d] = payloads[d];
+            dl[d] = dlog[d];
+            ro[d] = roots_out ? roots_out[d] : nullptr;
+        }
+        AhtSlots slots;
+        expand_peaks(n0, peaks, slots);
         std::lock_guard<std::mutex> lk(m->mu);
-        const int K = m->K;
-        const int k = ahtree_shard_bits(total, K);
-        const uint64_t S = 1ull << k;
-        const uint64_t nd = mh_ahtree_nodes_upto(total);
-        int last = 0;  // device of the last append: its final root is RootAt(total)
-        for (int d = 0; d < K; d++)
-            if ((uint64_t)d * S < total) last = d;
-        std::vector<uint8_t *> dl(K, nullptr), ro(K, nullptr);
-        // 1. payload ranges in, leaves + perfect nodes up to shard level (every
-        //    device from its own thread: each range crosses its own PCIe link)
-        if (int e = per_device(K, [&](int d) -> int {
-                const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
-                if (!md) return MH_OK;
+        return aht_multi_run(m, p, slots, pay, plen, dl, ro);
+    });
+}
+
+extern "C" int mh_multi_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint8_t *peaks,
+                                            const uint8_t *payloads, uint64_t total, uint32_t plen,
+                                            uint8_t *dlog_out, uint8_t root[32]) {
+    return mh_guard([&]() -> int {
+        if (!m || !root || (total && plen && !payloads) || !peaks_ok(n0, peaks))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        // nothing appended: RootAt(0) of an empty tree, or nothing to compute
+        if (total == 0) return n0 ? MH_ERR_ILLEGAL_ARGUMENTS : MH_ERR_UNEXISTENT_DATA;
+        AhtPlan p;
+        if (int st = aht_plan(n0, total, m->K, p)) return st;
+        AhtSlots slots;
+        expand_peaks(n0, peaks, slots);
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int G = p.G;
+        const uint64_t base = ahtree_nodes_upto(n0);
+        std::vector<const uint8_t *> pay(m->K, nullptr);
+        std::vector<uint8_t *> dl(m->K, nullptr), ro(m->K, nullptr);
+        // 0. each range's payloads in (every device from its own thread: each
+        //    range crosses its own PCIe link)
+        if (int e = per_device(G, [&](int d) -> int {
                 mh_multi::Dev &B = *m->buf[d];
+                const uint64_t lo = p.b[d], md = p.b[d + 1] - lo;
                 MH_HIP(hipSetDevice(m->dev[d]));
-                MH_HIP(B.dlog.ensure(nd * 32));
+                MH_HIP(B.dlog.ensure((ahtree_nodes_upto(p.b[d + 1]) - ahtree_nodes_upto(lo)) * 32));
                 MH_HIP(B.vals.ensure(md * plen + 16));
-                if (d == last) MH_HIP(B.hv.ensure(md * 32));
+                if (d == G - 1) MH_HIP(B.hv.ensure(md * 32));
                 dl[d] = B.dlog.as<uint8_t>();
-                if (d == last) ro[d] = B.hv.as<uint8_t>();
-                hipStream_t st = m->ctx[d]->stream;
+                pay[d] = B.vals.as<uint8_t>();
+                if (d == G - 1) ro[d] = B.hv.as<uint8_t>();
                 if (plen)
-                    MH_HIP(hipMemcpyAsync(B.vals.p, payloads + n0 * plen, md * plen,
-                                          hipMemcpyHostToDevice, st));
-                return mh_dev_ahtree_append_local(m->ctx[d], dl[d], n0, B.vals.as<uint8_t>(), md,
-                                                  plen, k);
+                    MH_HIP(hipMemcpyAsync(B.vals.p, payloads + (lo - n0) * plen, md * plen,
+                                          hipMemcpyHostToDevice, m->ctx[d]->stream));
+                return MH_OK;
             }))
             return e;
-        // 2-3. shard roots exchanged, nodes above shard level, spines
-        if (int st = ahtree_multi_finish(m, total, k, dl.data(), ro.data())) return st;
-        // 4. every device's own dLog range back (ranges tile [0, nodesUpto(total)))
-        if (int e = per_device(K, [&](int d) -> int {
-                const uint64_t n0 = std::min((uint64_t)d * S, total), md = std::min(S, total - n0);
-                if (!md) return MH_OK;
+        if (int st = aht_multi_run(m, p, slots, pay, plen, dl, ro)) return st;
+        // 5. every range's digests back (the ranges tile the new dLog stream)
+        if (int e = per_device(G, [&](int d) -> int {
                 MH_HIP(hipSetDevice(m->dev[d]));
                 hipStream_t st = m->ctx[d]->stream;
-                if (dlog_out) {
-                    const uint64_t lo = mh_ahtree_node_index(n0 + 1, 0);
-                    const uint64_t hi = mh_ahtree_nodes_upto(n0 + md);
-                    MH_HIP(hipMemcpyAsync(dlog_out + lo * 32, dl[d] + lo * 32, (hi - lo) * 32,
+                const uint64_t lo = ahtree_nodes_upto(p.b[d]), hi = ahtree_nodes_upto(p.b[d + 1]);
+                if (dlog_out)
+                    MH_HIP(hipMemcpyAsync(dlog_out + (lo - base) * 32, dl[d], (hi - lo) * 32,
                                           hipMemcpyDeviceToHost, st));
-                }
-                if (d == last)
-                    MH_HIP(hipMemcpyAsync(root, ro[d] + (md - 1) * 32, 32, hipMemcpyDeviceToHost,
-                                          st));
+                if (d == G - 1)
+                    MH_HIP(hipMemcpyAsync(root, ro[d] + (p.b[d + 1] - p.b[d] - 1) * 32, 32,
+                                          hipMemcpyDeviceToHost, st));
                 return mh_ctx_synchronize(m->ctx[d]);
             }))
             return e;

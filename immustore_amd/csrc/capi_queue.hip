@@ -43,6 +43,7 @@ struct mh_commit_queue {
     std::condition_variable cv_work, cv_done;
     std::deque<Req *> pending;
     bool stop = false;
+    uint32_t submitters = 0;  // inside mh_commit_queue_submit (free waits for 0)
     bool gathering = false;  // one worker at a time collects the next batch
     struct Worker {
         mh_commit_pipe *pipe = nullptr;
@@ -228,6 +229,12 @@ extern "C" int mh_commit_queue_free(mh_commit_queue *q) {
         q->cv_work.notify_all();
         for (auto &w : q->workers)
             if (w->th.joinable()) w->th.join();  // the workers drain what is pending first
+        {
+            // a submitter woken by the last batch still re-takes q->mu on its
+            // way out: the queue must outlive every one of them
+            std::unique_lock<std::mutex> lk(q->mu);
+            q->cv_done.wait(lk, [&] { return q->submitters == 0; });
+        }
         for (auto &w : q->workers) mh_commit_pipe_free(w->pipe);
         delete q;
         return MH_OK;
@@ -267,10 +274,15 @@ extern "C" int mh_commit_queue_submit(mh_commit_queue *q, uint64_t n, const uint
         std::unique_lock<std::mutex> lk(q->mu);
         if (q->stop) return MH_ERR_ILLEGAL_STATE;
         q->pending.push_back(&r);
+        q->submitters++;
         // all: the worker gathering a batch must see it, not only an idle one
         q->cv_work.notify_all();
         q->cv_done.wait(lk, [&] { return r.done; });
-        return r.status;
+        const int st = r.status;
+        // the last one out wakes a waiting mh_commit_queue_free (notified
+        // under the lock: free cannot delete q between this and unlock)
+        if (--q->submitters == 0 && q->stop) q->cv_done.notify_all();
+        return st;
     });
 }
 

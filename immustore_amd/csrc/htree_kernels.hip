@@ -196,6 +196,7 @@ struct Log2 {
 // ============================================================================
 constexpr int kFixedThreads = 256;
 constexpr int kWaveLds = 8192;
+constexpr uint32_t kFixedMaxValLen = 1u << 24;  // see entries_fixed_supported
 
 // Workgroup timeline probe points of k_entries_fixed (0: start, 3: first value
 // block hashed, 1: leaf phase done, 2: end); empty in the library, defined by
@@ -735,13 +736,29 @@ static int choose_lpl(uint64_t n) {
         int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) return v;
     }
-    // keep >= 256 CUs x 16 waves x 64 lanes busy.  Two entries per lane (one
-    // in-lane node level) from 2^19 entries up: at 2^20 that is 2048
-    // workgroups, 8 per CU in one round, against 4 per CU with four entries
-    // per lane -- twice the waves per SIMD to hide the DMA and LDS latency of
-    // an isolated launch (round-2 sweep, profiles/ab_lpl_wgl_r02.txt: leaf
-    // launch 0.835 -> 0.79 ms, single build 0.96-0.97 -> 0.93-0.94 ms, three
-    // builds in flight within 0.2 %).  MH_LPL=4 restores the round-1 shape.
+    // Two entries per lane (one in-lane node level) from 2^19 entries up.  At
+    // 2^20 that is 2048 workgroups of 256 lanes; each takes 33 KB of LDS and
+    // the kernel 104 VGPRs, so 4 workgroups (4 waves per SIMD) are resident
+    // per CU and the grid runs as two rounds of 1024, against one round of
+    // 1024 with four entries per lane.  The halved work per workgroup halves
+    // the straggler tail of the last round and the in-LDS subtree phase
+    // (profiles/ab_lpl_wgl_r02.txt: leaf launch 0.835 -> 0.79 ms, single
+    // build 0.96-0.97 -> 0.93-0.94 ms, three builds in flight within 0.2 %;
+    // residency in profiles/wg_residency_r03.txt).  MH_LPL=4 restores the
+    // round-1 shape.
+    if (n >= (uint64_t)2 * 262144) return 2;
+    return 1;
+}
+
+// Leaves from caller digests (one compression per leaf, no value blocks) keep
+// the round-1 rule: four leaves per lane from 2^20 up.  The two-per-lane
+// change above was measured on k_entries_fixed only; MH_DIGEST_LPL overrides.
+static int choose_digest_lpl(uint64_t n) {
+    if (const char *e = getenv("MH_DIGEST_LPL")) {
+        int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) return v;
+    }
+    if (n >= (uint64_t)4 * 262144) return 4;
     if (n >= (uint64_t)2 * 262144) return 2;
     return 1;
 }
@@ -753,6 +770,11 @@ bool entries_fixed_supported(int version, const uint8_t *keys, uint32_t key_len,
     if (((uintptr_t)keys & 3) || (key_len & 3)) return false;
     if (version == 1 && key_len > 16) return false;
     if (version == 0 && key_len > 20) return false;
+    // dma_issue forms each lane's offset from the wave's first entry in 32
+    // bits: rel * val_len + 112 with rel <= 64 * LPL - 1 <= 255, so values up
+    // to 16 MiB (255 * 2^24 + 112 < 2^32).  Go accepts any MaxValueLen
+    // (options.go:364-365): longer values take the CSR path (64-bit offsets).
+    if (val_len > kFixedMaxValLen) return false;
     return true;
 }
 
@@ -767,11 +789,11 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
     const size_t lds = (kFixedThreads / 64) * kWaveLds + 256;
     // levels each leaf workgroup reduces in LDS after its lanes (0..8); 0
     // leaves the whole upper tree to k_reduce, which a concurrent build on
-    // another stream can overlap (MH_WG_LEVELS overrides).  2 measured best
-    // with builds in flight at 1000-2000 steps (round-2 sweep in
-    // profiles/ab_wg_levels_r02.txt; 4 in round 1's 20-step A/B): deeper
-    // in-kernel subtrees idle most lanes at the end of the leaf kernel.
-    int wgl = 1;  // with two entries per lane (profiles/ab_lpl_wgl_r02.txt)
+    // another stream can overlap (MH_WG_LEVELS overrides).  With two entries
+    // per lane the default is 1 (profiles/ab_lpl_wgl_r02.txt: LPL 2 / 1 level
+    // against LPL 4 / 2 levels); deeper in-kernel subtrees idle most lanes at
+    // the end of the leaf kernel.
+    int wgl = 1;
     if (const char *e = getenv("MH_WG_LEVELS")) wgl = std::max(0, std::min(8, atoi(e)));
     {
         TimerScope ts(tm, "entries_fixed", st);
@@ -793,7 +815,7 @@ hipError_t launch_leaves_from_digests(hipStream_t st, Timer *tm, const uint8_t *
                                       uint64_t n, uint8_t *levels, const LevelGeom &g,
                                       int *levels_done) {
     LaneLevels la = lane_levels(g);
-    const int lpl = choose_lpl(n);
+    const int lpl = choose_digest_lpl(n);
     const uint64_t lanes = (n + lpl - 1) / lpl;
     {
         TimerScope ts(tm, "leaves", st);

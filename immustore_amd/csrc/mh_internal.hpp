@@ -142,21 +142,64 @@ struct AhtLogs {
     uint8_t *clog = nullptr;
     uint64_t p_off0 = 0;
 };
+// The left edge of an append range (n0, ...] whose dLog buffer does not hold
+// the nodes before it: every node such a range reads that ends at or before
+// lo is a peak of lo (node(lo with the bits below l cleared, l) for a set bit
+// l of lo, ahtree.go:296-322), so the 64-slot frontier fr[l] (device, 32 B
+// per level, only set bits of lo meaningful) replaces the old dLog.  lo = 0:
+// no edge, every node from the dLog.
+struct AhtEdge {
+    const uint8_t *fr = nullptr;
+    uint64_t lo = 0;
+};
 hipError_t launch_ahtree_append(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
                                 uint8_t *roots_out, uint32_t *work_ctr,
-                                const AhtLogs &lg = AhtLogs());
+                                const AhtLogs &lg = AhtLogs(), const AhtEdge &edge = AhtEdge());
 // The three phases of launch_ahtree_append, for sharded appends.
 // dlog == nullptr: records only.
 hipError_t launch_ahtree_leaves(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
                                 const uint8_t *payloads, uint64_t m, uint32_t plen,
                                 const AhtLogs &lg = AhtLogs());
 hipError_t launch_ahtree_perfect(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0,
-                                 uint64_t n_end, int lmin, int lmax);
+                                 uint64_t n_end, int lmin, int lmax,
+                                 const AhtEdge &edge = AhtEdge());
 hipError_t launch_ahtree_spine(hipStream_t st, Timer *tm, uint8_t *dlog, uint64_t n0, uint64_t m,
-                               uint8_t *roots_out, uint32_t *work_ctr);
+                               uint8_t *roots_out, uint32_t *work_ctr,
+                               const AhtEdge &edge = AhtEdge());
 hipError_t launch_ahtree_put_shard_roots(hipStream_t st, Timer *tm, uint8_t *dlog, int level,
                                          uint64_t count, const uint8_t *roots);
+
+// Ranged multi-device append (capi_multi.hip): the batch (n0, n0 + total] is
+// cut at multiples of S = 2^k into G <= 64 device ranges (b[d], b[d+1]]; a
+// device keeps only its own dLog range.  Pieces are the aligned blocks of S
+// appends; piece E ends at E*S and its level-k root is node(E*S, k).
+constexpr int kAhtMaxRanges = 64;
+struct AhtTopArgs {
+    int k = 0;                           // shard bits: S = 2^k
+    int nlev = 0;                        // levels of the piece tree (l' = 0 .. nlev-1)
+    int G = 0;                           // device ranges
+    uint64_t n0 = 0;                     // old size
+    uint64_t lo = 0, hi = 0;             // this device's range (lo, hi]
+    uint64_t N0 = 0, Pend = 0, Pmax = 0; // floor(n0/S), floor((n0+total)/S), pieces per send slot
+    uint64_t lev_off[64] = {};           // slot offset of piece level l' in the top buffer
+    uint64_t pe0[kAhtMaxRanges + 1] = {};  // floor(b[d]/S), d = 0..G
+};
+// the level-k roots of this device's pieces E in (pe0[d], pe0[d+1]] into send
+hipError_t launch_ahtree_gather_pieces(hipStream_t st, const uint8_t *dlog, int k, uint64_t e0,
+                                       uint64_t count, uint8_t *send);
+// piece tree over the all-gathered piece roots and the old peaks of n0 (levels
+// >= k), the nodes above level k that end in (lo, hi] into dlog, and this
+// device's frontier (peaks of lo) into fr (lo > n0 only)
+hipError_t launch_ahtree_top(hipStream_t st, const AhtTopArgs &a, const uint8_t *recv,
+                             const uint8_t *peaks_n0, uint8_t *top, uint8_t *dlog, uint8_t *fr);
+// the 64-slot frontier (32 B per level) by value, written to dst on st
+struct AhtSlots {
+    uint8_t b[64 * 32];
+};
+hipError_t launch_ahtree_put_slots(hipStream_t st, const AhtSlots &s, uint8_t *dst);
+// the peaks of n from a device dLog into the 64-slot frontier layout
+hipError_t launch_ahtree_peaks(hipStream_t st, const uint8_t *dlog, uint64_t n, uint8_t *fr);
 
 // host-side index math shared with the C API
 uint64_t ahtree_nodes_upto(uint64_t n);

@@ -23,6 +23,27 @@ def shard_plan(n: int, ndev: int) -> Tuple[int, int]:
     return s.value, g.value
 
 
+def ahtree_range_plan(n0: int, total: int, ndev: int) -> Tuple[int, list]:
+    """(k, bounds): the ranges (bounds[d], bounds[d+1]] of a multi-device
+    ahtree append of `total` appends onto a tree of n0 (interior bounds are
+    multiples of 2^k), as mh_multi_(dev_)ahtree_append_batch cut them."""
+    k, g = C.c_int(), C.c_int()
+    b = (C.c_uint64 * (ndev + 1))()
+    N.check(N.load().mh_ahtree_range_plan(n0, total, ndev, C.byref(k), b, C.byref(g)))
+    return k.value, [b[i] for i in range(g.value + 1)]
+
+
+def peaks_of(dlog: np.ndarray, n: int) -> bytes:
+    """The popcount(n) peaks of a tree of size n (lowest level first) from a
+    host dLog indexed from 0: node(n with the bits below l cleared, l)."""
+    L = N.load()
+    out = []
+    for l in range(64):
+        if (n >> l) & 1:
+            out.append(bytes(dlog[L.mh_ahtree_node_index((n >> l) << l, l)]))
+    return b"".join(out)
+
+
 class MultiDevice:
     """mh_multi over the given device ordinals (a device may repeat: more
     shards than devices, roots gathered by device copies instead of RCCL)."""
@@ -74,25 +95,32 @@ class MultiDevice:
             self.handle, version, n_per_dev, P(*keys), key_len, P(*vals), val_len,
             P(*hvals) if hvals is not None else None, P(*levels), P(*top_levels), P(*roots)))
 
-    def ahtree_append_batch(self, payloads, want_dlog: bool = True):
-        """AppendBatch of the rows of `payloads` (m, plen) to an empty ahtree
-        across the devices -> (dlog (nodesUpto(m), 32) or None, RootAt(m))."""
+    def ahtree_append_batch(self, payloads, want_dlog: bool = True, n0: int = 0,
+                            peaks: bytes = None):
+        """AppendBatch of the rows of `payloads` (m, plen) onto an ahtree of
+        size n0 with the given peaks (see peaks_of) across the devices ->
+        (the NEW dLog digests (nodesUpto(n0+m) - nodesUpto(n0), 32) or None,
+        RootAt(n0 + m))."""
         p = np.ascontiguousarray(payloads, np.uint8)
         m, plen = p.shape
         L = N.load()
-        dl = np.zeros((max(L.mh_ahtree_nodes_upto(m), 1), 32), np.uint8) if want_dlog else None
+        nd = L.mh_ahtree_nodes_upto(n0 + m) - L.mh_ahtree_nodes_upto(n0)
+        dl = np.zeros((max(nd, 1), 32), np.uint8) if want_dlog else None
         root = np.zeros(32, np.uint8)
-        N.check(L.mh_multi_ahtree_append_batch(self.handle, _addr(p), m, plen, _addr(dl),
-                                                _addr(root)))
-        return (dl[:L.mh_ahtree_nodes_upto(m)] if want_dlog else None), root.tobytes()
+        pk = np.frombuffer(peaks, np.uint8) if peaks else None
+        N.check(L.mh_multi_ahtree_append_batch(self.handle, n0, _addr(pk), _addr(p), m, plen,
+                                                _addr(dl), _addr(root)))
+        return (dl[:nd] if want_dlog else None), root.tobytes()
 
-    def dev_ahtree_append_batch(self, total, payloads, plen, dlogs, roots_out=None):
-        """Device pointers per device (sequences of ints; None entries for devices
-        with no appends) -- asynchronous."""
+    def dev_ahtree_append_batch(self, total, payloads, plen, dlogs, roots_out=None, n0: int = 0,
+                                peaks: bytes = None):
+        """Device pointers per range (sequences of ints; None entries for
+        unused ranges; range d as ahtree_range_plan cuts it) -- asynchronous."""
         K = len(self.devices)
         P = C.c_void_p * K
+        pk = np.frombuffer(peaks, np.uint8) if peaks else None
         N.check(N.load().mh_multi_dev_ahtree_append_batch(
-            self.handle, total, P(*payloads), plen, P(*dlogs),
+            self.handle, n0, _addr(pk), total, P(*payloads), plen, P(*dlogs),
             P(*roots_out) if roots_out is not None else None))
 
     def build_entries(self, version, kb, ko, mb, mo, vb, vo, ov=None, use=None,

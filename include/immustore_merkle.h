@@ -324,6 +324,20 @@ int mh_dev_ahtree_put_shard_roots(mh_ctx *ctx, uint8_t *dlog, int shard_bits, ui
 int mh_dev_ahtree_append_spine(mh_ctx *ctx, uint8_t *dlog, uint64_t n0, uint64_t m,
                                uint8_t *roots_out);
 
+/* One device, the dLog kept as a RANGE (the replay of syncBinaryLinking,
+ * immustore.go:1198-1232, with no copy of the old dLog on the device):
+ * append m payloads onto a tree of size n0 whose peaks (as for
+ * mh_multi_ahtree_append_batch, host memory, NULL when n0 == 0) are given;
+ * dlog_range (device, 16-byte aligned) receives the new digests
+ * [nodesUpto(n0), nodesUpto(n0 + m)) from its start, roots_out (may be NULL)
+ * RootAt after each append.  Asynchronous on the context stream. */
+int mh_dev_ahtree_append_range(mh_ctx *ctx, uint8_t *dlog_range, uint64_t n0,
+                               const uint8_t *peaks, const uint8_t *payloads, uint64_t m,
+                               uint32_t plen, uint8_t *roots_out);
+/* The popcount(n) peaks of a tree of size n, lowest level first, from a
+ * device dLog indexed from 0 (synchronous; peaks_out in host memory). */
+int mh_dev_ahtree_peaks(mh_ctx *ctx, const uint8_t *dlog, uint64_t n, uint8_t *peaks_out);
+
 /* ahtree proof re-hash, batch (verification.go).  kind = MH_AHT_*.
  * INCLUSION:      a = leaf (leafFor(alh)), b = root of j
  * CONSISTENCY:    a = root of i, b = root of j
@@ -652,28 +666,43 @@ int mh_multi_dev_htree_build_entries_fixed(mh_multi *m, int version, uint64_t n_
                                            const uint8_t *const *vals, uint32_t val_len,
                                            uint8_t *const *hvals_out, uint8_t *const *levels,
                                            uint8_t *const *top_levels, uint8_t *const *root);
-/* ahtree AppendBatch of `total` payloads (plen bytes each) to an EMPTY tree
- * across the K devices (ahtree.go:246-373; BASELINE configs[2] at scale): S =
- * 2^k is the smallest power of two with K*S >= total and device d appends
- * (dS, min((d+1)S, total)] -- its leaves, perfect nodes of levels <= k and the
- * spine nodes below level k all lie inside its own range -- then the complete
- * shards' roots are all-gathered over RCCL (32 B per device) and every device
- * builds the nodes above level k from them and finishes its spine (the three
- * phases of mh_dev_ahtree_append_local / _put_shard_roots / _append_spine).
- * Device variant: payloads[d] holds device d's appends, dlog[d] is device
- * memory for mh_ahtree_nodes_upto(total) digests indexed like the global dLog
- * (device d fills its range [mh_ahtree_node_index(dS + 1, 0),
- * mh_ahtree_nodes_upto(dS + m_d)) and the nodes above level k), roots_out
- * (may be NULL, or hold NULL entries) receives device d's m_d roots (RootAt
- * after each of its appends).  Asynchronous on the devices' context streams.
- * Host variant: payloads and dlog_out (nodesUpto(total) x 32 bytes, the
- * tree/NNNNNNNN.sha stream, may be NULL) in host memory, root = RootAt(total);
- * total == 0 -> MH_ERR_UNEXISTENT_DATA (ahtree.go:727-745). */
-int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t total, const uint8_t *const *payloads,
-                                     uint32_t plen, uint8_t *const *dlog,
-                                     uint8_t *const *roots_out);
-int mh_multi_ahtree_append_batch(mh_multi *m, const uint8_t *payloads, uint64_t total,
-                                 uint32_t plen, uint8_t *dlog_out, uint8_t root[32]);
+/* ahtree AppendBatch of `total` payloads (plen bytes each) onto a tree of
+ * size n0 across the K devices (ahtree.go:246-373; BASELINE configs[2] at
+ * scale, and the replay of syncBinaryLinking, immustore.go:1198-1232, which
+ * resumes at aht.Size()+1 on every open, :686-693).  The batch
+ * (n0, n0 + total] is cut at multiples of S = 2^k (S <= total / 8K) into
+ * G <= K nearly equal ranges (mh_ahtree_range_plan); device d appends range
+ * d and keeps ONLY that range's digests: dLog indices
+ * [mh_ahtree_nodes_upto(b[d]), mh_ahtree_nodes_upto(b[d+1])).  Every node a
+ * range reads outside itself is a peak of its left end (the perfect subtree
+ * of a set bit of b[d]); the old tree's peaks come from the caller and the
+ * others are built on the devices from the ranges' level-k piece roots,
+ * all-gathered over RCCL (32 B per piece, tens of pieces per device).
+ * peaks: the popcount(n0) peaks of the old tree, lowest level first, in host
+ * memory -- peak l is node(n0 with the bits below l cleared, l) =
+ * dLog[mh_ahtree_node_index(n0 & ~(2^l - 1), l)] for every set bit l of n0
+ * (NULL when n0 == 0; mh_dev_ahtree_peaks reads them from a resident dLog).
+ * Device variant: payloads[d] holds range d's b[d+1] - b[d] payloads and
+ * dlog[d] the room for its digests (16-byte aligned); roots_out (may be NULL,
+ * or hold NULL entries) receives RootAt after each append of range d.
+ * Ranges d >= G are unused.  Asynchronous on the devices' context streams.
+ * Host variant: payloads and dlog_out (the NEW digests only,
+ * (nodesUpto(n0 + total) - nodesUpto(n0)) x 32 bytes = what Append writes to
+ * tree/NNNNNNNN.sha, may be NULL) in host memory, root = RootAt(n0 + total);
+ * total == 0 -> MH_ERR_UNEXISTENT_DATA for an empty tree (ahtree.go:727-745),
+ * MH_ERR_ILLEGAL_ARGUMENTS otherwise. */
+int mh_multi_dev_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint8_t *peaks,
+                                     uint64_t total, const uint8_t *const *payloads, uint32_t plen,
+                                     uint8_t *const *dlog, uint8_t *const *roots_out);
+int mh_multi_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint8_t *peaks,
+                                 const uint8_t *payloads, uint64_t total, uint32_t plen,
+                                 uint8_t *dlog_out, uint8_t root[32]);
+/* The range plan of those calls (host only): bounds[0..*nranges] (room for
+ * ndev + 1 values; bounds[0] = n0, bounds[*nranges] = n0 + total, the others
+ * multiples of 2^*shard_bits), range d = (bounds[d], bounds[d+1]] on device d.
+ * ndev <= 64. */
+int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *shard_bits, uint64_t *bounds,
+                         int *nranges);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

@@ -102,7 +102,7 @@ int main(int argc, char **argv) {
             CHECK(mh_multi_create(ndv[v], devs[v], &mm));
             uint8_t mr[32];
             memset(dl2, 0, nd * 32);
-            CHECK(mh_multi_ahtree_append_batch(mm, p, m, 32, dl2, mr));
+            CHECK(mh_multi_ahtree_append_batch(mm, 0, NULL, p, m, 32, dl2, mr));
             printf("%s %d\n", v ? "multi3_ahtree_root_equal" : "multi1_ahtree_root_equal",
                    memcmp(mr, r, 32) == 0);
             printf("%s %d\n", v ? "multi3_ahtree_dlog_equal" : "multi1_ahtree_dlog_equal",

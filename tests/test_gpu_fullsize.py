@@ -86,6 +86,52 @@ def test_c4_per_gpu_full_vs_oracle(m, ctx, orc):
     assert np.array_equal(lv.cpu().numpy().reshape(-1, 32), olv)
 
 
+# ------------------------------------------------- values past the 32-bit lane offsets
+# Go accepts any positive MaxValueLen (embedded/store/options.go:364-365); the
+# fixed-stride kernel forms each lane's DMA offset from the wave's first entry
+# in 32 bits (rel * val_len, rel <= 64 * LPL - 1), so values above 16 MiB must
+# take the CSR path.  Each case hashes ~4.3 GB of values (immustore.go:1620-1630).
+@pytest.mark.parametrize("n,vlen,lpl", [
+    (64, (64 << 20) + 16, None),      # 63 * vlen alone is past 2^32
+    (128, 33818640, "2"),             # LPL 2: 127 * vlen = 2^32 - 16, chunks wrap
+    (256, 1 << 24, "4"),              # the largest fast-path value, rel up to 255
+])
+def test_big_values_vs_oracle(m, ctx, orc, n, vlen, lpl):
+    import torch
+    from immustore_amd import _native as N
+    L = N.load()
+    old = os.environ.get("MH_LPL")
+    if lpl:
+        os.environ["MH_LPL"] = lpl
+    try:
+        dev = torch.device("cuda", 0)
+        vals = torch.empty(n * vlen, dtype=torch.uint8, device=dev)
+        keys = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+        N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 21))
+        N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, 0))
+        lv = torch.empty(m.levels_len(n) * 32, dtype=torch.uint8, device=dev)
+        hv = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        root = torch.empty(32, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        N.check(L.mh_dev_htree_build_entries_fixed(ctx.handle, 1, n, keys.data_ptr(), 8,
+                                                   vals.data_ptr(), vlen, hv.data_ptr(),
+                                                   lv.data_ptr(), root.data_ptr()))
+        ctx.synchronize()
+        del vals
+    finally:
+        if old is None:
+            os.environ.pop("MH_LPL", None)
+        else:
+            os.environ["MH_LPL"] = old
+    hk = np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8).reshape(n, 8)
+    hvals = orc.fill_random(n * vlen, 21).reshape(n, vlen)
+    ohv, olv, oroot = orc.build_entries_fixed(1, hk, hvals, nthreads=min(16, os.cpu_count() or 1))
+    del hvals
+    assert np.array_equal(hv.cpu().numpy().reshape(n, 32), ohv)
+    assert np.array_equal(lv.cpu().numpy().reshape(-1, 32), olv)
+    assert root.cpu().numpy().tobytes() == oroot
+
+
 # ---------------------------------------------------------------- configs[4]
 P_C5, D_C5 = 10 ** 6, 24
 

@@ -99,88 +99,151 @@ def test_multi_device_resident_vs_oracle(m, orc, devices, n_per_dev):
                 o = m.level_offset(n, k + j)
                 assert np.array_equal(tg[m.level_offset(K, j):m.level_offset(K, j) + w],
                                       olv[o:o + w]), (d, j)
+        # back-to-back builds with no host sync between them: on repeated
+        # devices every stream's top reduce (which overwrites root[s]) must
+        # wait for the other streams' copies of root[s]
+        for rep in range(8):
+            md.dev_build_entries_fixed(1, n_per_dev, ptr(dk), 8, ptr(dv), 1024, ptr(lv), ptr(top),
+                                       ptr(rt), None)
+        md.synchronize()
+        for d in range(K):
+            assert rt[d].cpu().numpy().tobytes() == oroot, ("repeat", d)
         N.check(0)
     finally:
         md.close()
 
 
+# one oracle tree long enough for every (n0, total) below: the dLog of the
+# first n appends is the same prefix whatever comes after
+_AHT_N0S = (0, 1, (1 << 13) - 1, 10 ** 6 + 3)
+_AHT_TOTALS = (1, 2, 3, 5, 8, 9, 1000, 4096, 70001, (1 << 17) + 5)
+
+
+@pytest.fixture(scope="module")
+def aht_ref(orc):
+    N_all = max(_AHT_N0S) + max(_AHT_TOTALS)
+    pay = orc.fill_random(32 * N_all, 123).reshape(N_all, 32)
+    o = orc.AHtree(N_all)
+    o.append_batch(pay)
+    return pay, o, np.frombuffer(o.dlog_bytes(), np.uint8).reshape(-1, 32)
+
+
 @pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
-def test_multi_ahtree_append_vs_oracle(m, orc, devices):
-    """mh_multi_ahtree_append_batch: the whole dLog (tree/*.sha stream) and
-    RootAt(m) equal the oracle's single AppendBatch (ahtree.go:246-373,
-    :727-771) -- ranges of 2^k appends per device, the shard roots exchanged
-    (RCCL for [0], device copies when the device repeats)."""
+def test_multi_ahtree_append_vs_oracle(m, orc, aht_ref, devices):
+    """mh_multi_ahtree_append_batch onto trees of n0 in {0, 1, 2^13-1,
+    10^6+3} (the replay of syncBinaryLinking resumes at aht.Size()+1,
+    immustore.go:1198-1232): the new dLog digests (tree/*.sha stream) and
+    RootAt(n0 + total) equal the oracle's single AppendBatch (ahtree.go:246-373,
+    :727-771) -- nearly equal ranges per device, each device holding only its
+    own range; the piece roots exchanged over RCCL for [0], by device copies
+    when the device repeats."""
     from immustore_amd import _native as N
-    from immustore_amd.multi import MultiDevice
+    from immustore_amd.multi import MultiDevice, peaks_of
+    L = N.load()
+    pay, o, ref = aht_ref
     md = MultiDevice(devices)
     try:
-        for total in (1, 2, 3, 5, 8, 9, 1000, 4096, 70001, (1 << 17) + 5):
-            pay = orc.fill_random(32 * total, total).reshape(total, 32)
-            dl, root = md.ahtree_append_batch(pay)
-            o = orc.AHtree(total)
-            o.append_batch(pay)
-            assert dl.tobytes() == o.dlog_bytes(), (devices, total)
-            assert root == bytes(o.root_at(total)[1]), (devices, total)
+        for n0 in _AHT_N0S:
+            pk = peaks_of(ref, n0)
+            for total in _AHT_TOTALS:
+                dl, root = md.ahtree_append_batch(pay[n0:n0 + total], n0=n0, peaks=pk)
+                lo, hi = L.mh_ahtree_nodes_upto(n0), L.mh_ahtree_nodes_upto(n0 + total)
+                assert np.array_equal(dl, ref[lo:hi]), (devices, n0, total)
+                assert root == bytes(o.root_at(n0 + total)[1]), (devices, n0, total)
         # other payload sizes (the leaf kernel's per-lane byte path)
         for plen in (0, 1, 100):
-            pay = orc.fill_random(plen * 777 + 1, plen)[:plen * 777].reshape(777, plen)
-            dl, root = md.ahtree_append_batch(pay)
-            o = orc.AHtree(777)
-            o.append_batch(pay)
-            assert dl.tobytes() == o.dlog_bytes() and root == bytes(o.root_at(777)[1]), plen
+            p2 = orc.fill_random(plen * 777 + 1, plen)[:plen * 777].reshape(777, plen)
+            dl, root = md.ahtree_append_batch(p2)
+            o2 = orc.AHtree(777)
+            o2.append_batch(p2)
+            assert dl.tobytes() == o2.dlog_bytes() and root == bytes(o2.root_at(777)[1]), plen
+            # the same batch in two calls: the second onto the first's peaks
+            full = np.frombuffer(o2.dlog_bytes(), np.uint8).reshape(-1, 32)
+            dl2, root2 = md.ahtree_append_batch(p2[300:], n0=300, peaks=peaks_of(full, 300))
+            assert dl2.tobytes() == o2.dlog_bytes()[L.mh_ahtree_nodes_upto(300) * 32:], plen
+            assert root2 == root
         with pytest.raises(N.MerkleError):
             md.ahtree_append_batch(np.zeros((0, 32), np.uint8))
+        with pytest.raises(N.MerkleError):  # n0 > 0 needs the old peaks
+            md.ahtree_append_batch(pay[:5], n0=5)
     finally:
         md.close()
 
 
 @pytest.mark.parametrize("devices,total", [([0], 1 << 14), ([0, 0, 0, 0], 1 << 16),
-                                           ([0, 0, 0, 0], 3 * (1 << 14) + 5)])
-def test_multi_dev_ahtree_append_vs_oracle(m, orc, devices, total):
-    """Device-resident ranges (the configs[2]-at-scale shape): device d fills
-    its range of a globally indexed dLog byte-identically to one device's
-    append; its roots_out are RootAt after each of its appends."""
+                                           ([0, 0, 0, 0], 3 * (1 << 14) + 5),
+                                           ([0] * 8, 100003)])
+@pytest.mark.parametrize("n0", _AHT_N0S)
+def test_multi_dev_ahtree_append_vs_oracle(m, orc, aht_ref, devices, total, n0):
+    """Device-resident ranges (the configs[2]-at-scale shape, and replay):
+    device d holds only its range's digests [nodesUpto(b[d]), nodesUpto(b[d+1]))
+    -- memory O(total / K) -- byte-identical to one device's append of the
+    whole batch; its roots_out are RootAt after each of its appends."""
     import torch
     from immustore_amd import _native as N
-    from immustore_amd.multi import MultiDevice
+    from immustore_amd.multi import MultiDevice, ahtree_range_plan, peaks_of
     L = N.load()
     K = len(devices)
-    k = 0
-    while K * (1 << k) < total:
-        k += 1
-    S = 1 << k
-    pay = orc.fill_random(32 * total, 5).reshape(total, 32)
-    nd = L.mh_ahtree_nodes_upto(total)
-    o = orc.AHtree(total)
-    o.append_batch(pay)
-    ref = np.frombuffer(o.dlog_bytes(), np.uint8).reshape(-1, 32)
+    pay, o, ref = aht_ref
+    _, b = ahtree_range_plan(n0, total, K)
+    G = len(b) - 1
     md = MultiDevice(devices)
     try:
-        spans = [(min(d * S, total), min(S, max(total - d * S, 0))) for d in range(K)]
-        dp = [torch.from_numpy(pay[n0:n0 + c].reshape(-1).copy()).cuda() if c else None
-              for n0, c in spans]
-        dl = [torch.empty(nd * 32, dtype=torch.uint8, device="cuda") if c else None
-              for _, c in spans]
-        ro = [torch.empty(c * 32, dtype=torch.uint8, device="cuda") if c else None
-              for _, c in spans]
+        up = L.mh_ahtree_nodes_upto
+        dp = [torch.from_numpy(pay[b[d]:b[d + 1]].reshape(-1).copy()).cuda() if d < G else None
+              for d in range(K)]
+        dl = [torch.empty((up(b[d + 1]) - up(b[d])) * 32, dtype=torch.uint8, device="cuda")
+              if d < G else None for d in range(K)]
+        ro = [torch.empty((b[d + 1] - b[d]) * 32, dtype=torch.uint8, device="cuda")
+              if d < G else None for d in range(K)]
         torch.cuda.synchronize()
         ptr = lambda ts: [t.data_ptr() if t is not None else None for t in ts]  # noqa: E731
-        md.dev_ahtree_append_batch(total, ptr(dp), 32, ptr(dl), ptr(ro))
+        md.dev_ahtree_append_batch(total, ptr(dp), 32, ptr(dl), ptr(ro), n0=n0,
+                                   peaks=peaks_of(ref, n0))
         md.synchronize()
-        covered = 0
-        for d, (n0, c) in enumerate(spans):
-            if not c:
-                continue
-            lo, hi = L.mh_ahtree_node_index(n0 + 1, 0), L.mh_ahtree_nodes_upto(n0 + c)
+        for d in range(G):
             got = dl[d].cpu().numpy().reshape(-1, 32)
-            assert np.array_equal(got[lo:hi], ref[lo:hi]), d
-            covered += hi - lo
+            assert np.array_equal(got, ref[up(b[d]):up(b[d + 1])]), (d, b)
             r = ro[d].cpu().numpy().reshape(-1, 32)
+            c = b[d + 1] - b[d]
             for j in (0, c // 2, c - 1):
-                assert r[j].tobytes() == bytes(o.root_at(n0 + j + 1)[1]), (d, j)
-        assert covered == nd
+                assert r[j].tobytes() == bytes(o.root_at(b[d] + j + 1)[1]), (d, j)
     finally:
         md.close()
+
+
+@pytest.mark.parametrize("n0", _AHT_N0S + (2 ** 20, 2 ** 20 - 1))
+def test_dev_ahtree_append_range_vs_oracle(m, orc, aht_ref, n0):
+    """One device, the dLog kept as a range (mh_dev_ahtree_append_range):
+    only the old tree's peaks on the device (read back from a resident dLog
+    with mh_dev_ahtree_peaks), the new digests and roots equal the oracle's."""
+    import torch
+    from immustore_amd import _native as N
+    from immustore_amd.multi import peaks_of
+    L = N.load()
+    pay, o, ref = aht_ref
+    ctx = m.Context(0)
+    up = L.mh_ahtree_nodes_upto
+    pk = peaks_of(ref, n0)
+    if n0:
+        dref = torch.from_numpy(ref[:up(n0)].reshape(-1).copy()).cuda()
+        got = np.zeros(len(pk), np.uint8)
+        N.check(L.mh_dev_ahtree_peaks(ctx.handle, dref.data_ptr(), n0, got.ctypes.data))
+        assert got.tobytes() == pk
+        del dref
+    for total in (1, 2, 777, 70001):
+        dp = torch.from_numpy(pay[n0:n0 + total].reshape(-1).copy()).cuda()
+        dl = torch.empty((up(n0 + total) - up(n0)) * 32, dtype=torch.uint8, device="cuda")
+        ro = torch.empty(total * 32, dtype=torch.uint8, device="cuda")
+        pkb = np.frombuffer(pk, np.uint8) if n0 else None
+        N.check(L.mh_dev_ahtree_append_range(ctx.handle, dl.data_ptr(), n0,
+                                             pkb.ctypes.data if n0 else None, dp.data_ptr(),
+                                             total, 32, ro.data_ptr()))
+        ctx.synchronize()
+        assert np.array_equal(dl.cpu().numpy().reshape(-1, 32), ref[up(n0):up(n0 + total)])
+        r = ro.cpu().numpy().reshape(-1, 32)
+        for j in (0, total // 2, total - 1):
+            assert r[j].tobytes() == bytes(o.root_at(n0 + j + 1)[1]), (n0, total, j)
 
 
 def _ragged(orc, n, seed, md=True):
