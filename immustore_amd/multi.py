@@ -66,6 +66,10 @@ class MultiDevice:
         except Exception:
             pass
 
+    def uses_rccl(self) -> bool:
+        """RCCL clique (distinct devices) vs device copies (a device repeats)."""
+        return len(set(self.devices)) == len(self.devices)
+
     def ctx_handle(self, d: int):
         return N.load().mh_multi_ctx(self.handle, d)
 

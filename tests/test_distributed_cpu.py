@@ -199,3 +199,23 @@ def test_bench_rejects_mismatched_world():
     r = subprocess.run([sys.executable, os.path.join(root_dir, "bench.py"), "--gpus", "2",
                         "--launch-check"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0
+
+
+def test_bench_cabi_mode_routing():
+    """--api cabi is one process over N devices (mh_multi_*): it must refuse to
+    run when fewer than N devices are visible -- before any clique is made --
+    and under torch.distributed.run (VERDICT r02 next #1)."""
+    import subprocess
+    import sys
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bench = os.path.join(root_dir, "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, bench, "--api", "cabi", "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0
+    assert "device(s) visible" in r.stderr, r.stderr[-2000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    env2 = dict(env, WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, bench, "--api", "cabi", "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=240, env=env2)
+    assert r.returncode != 0 and "one process" in r.stderr, r.stderr[-2000:]

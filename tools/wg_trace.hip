@@ -78,9 +78,13 @@ int main(int argc, char **argv) {
     hipEventElapsedTime(&ms, a, b);
     std::vector<unsigned long long> p(8 * 4096);
     hipMemcpyFromSymbol(p.data(), HIP_SYMBOL(g_probe), p.size() * 8);
-    const unsigned nwg = (unsigned)((n / 4 + 255) / 256);
+    // entries per lane as choose_lpl picks them (MH_LPL, else 2 from 2^19 up)
+    const char *le = getenv("MH_LPL");
+    const uint64_t lpl = le ? (uint64_t)atoi(le) : (n >= (1ull << 19) ? 2 : 1);
+    const unsigned nwg = (unsigned)((n / lpl + 255) / 256);
     printf("{\"warm\": %d, \"contended\": %d, \"kernel_ms\": %.4f, \"workgroups\": %u, "
-           "\"clock_mhz\": 100, \"wg\": [", warm, contended, ms, nwg);
+           "\"lpl\": %llu, \"clock_mhz\": 100, \"wg\": [", warm, contended, ms, nwg,
+           (unsigned long long)lpl);
     for (unsigned w = 0; w < nwg; w++)
         printf("%s[%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu]", w ? "," : "", p[8 * w + 3] >> 32,
                p[8 * w + 3] & 0xffffffffull, p[8 * w], p[8 * w + 1], p[8 * w + 2], p[8 * w + 4],

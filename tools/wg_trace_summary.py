@@ -17,10 +17,28 @@ def summary(path):
     byc = collections.defaultdict(list)
     for i in range(len(w)):
         byc[(xcc[i], cu[i])].append(l[i])
-    ranks = np.array([sorted(v) for v in byc.values() if len(v) == 4])
+    per_cu = collections.Counter(len(v) for v in byc.values())
+    ranks = np.array([sorted(v) for v in byc.values() if len(v) == max(per_cu)])
+    # residency: the most workgroups of one CU alive at the same instant
+    # (start <= t < end), over every CU
+    alive = collections.defaultdict(list)
+    for i in range(len(w)):
+        alive[(xcc[i], cu[i])].append((s[i], e[i]))
+    conc = []
+    for iv in alive.values():
+        ev = sorted([(a, 1) for a, _ in iv] + [(b, -1) for _, b in iv], key=lambda x: (x[0], x[1]))
+        cur = best = 0
+        for _, dlt in ev:
+            cur += dlt
+            best = max(best, cur)
+        conc.append(best)
     return {
         "file": path, "warm": d.get("warm"), "contended": d.get("contended"),
-        "kernel_ms": d["kernel_ms"],
+        "kernel_ms": d["kernel_ms"], "workgroups": int(len(w)), "lpl": d.get("lpl"),
+        "workgroups_per_cu": dict(sorted((int(k), v) for k, v in per_cu.items())),
+        "max_concurrent_per_cu": int(max(conc)) if conc else None,
+        "cus_reaching_max": int(sum(1 for c in conc if c == max(conc))) if conc else None,
+        "start_us_quantiles": [round(float(np.percentile(s, q)), 1) for q in (0, 25, 50, 75, 100)],
         "start_us_max": round(float(s.max()), 1),
         "end_us_max": round(float(e.max()), 1),
         "per_cu_leaf_end_us_by_rank": ranks.mean(0).round(1).tolist() if len(ranks) else None,
