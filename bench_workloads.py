@@ -205,7 +205,8 @@ def distributed_main(a):
 
 def make_parser():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged", "document"],
+    p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged", "document",
+                                          "values"],
                    required=True)
     p.add_argument("--logs", action="store_true",
                    help="c3: also write the pLog / cLog appendable records (8(f) row 4)")
@@ -484,6 +485,101 @@ def document(a, ctx):
                                        "the docs' txs with the HValues as overrides (EntrySpec "
                                        "digests + htree, 16 threads) beside SHA256 of every "
                                        "document (1 thread)"}}
+
+
+def values(a, m, N, L, ctx, dev, sync):
+    """readValueAt's integrity check (immustore.go:3235) over a batch of
+    a.entries ragged values (0..a.max_vlen B, seeded), 1 % corrupted: device
+    resident (mh_dev_verify_values_batch), and from pinned host memory through
+    the chunked copy / check pipeline (mh_verify_values_batch)."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    n = a.entries
+    rng = np.random.default_rng(8)
+    lens = rng.integers(0, a.max_vlen + 1, n).astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    total = int(off[-1])
+    vb = torch.empty(total + 16, dtype=torch.uint8).pin_memory()
+    vb.numpy()[:] = orc.fill_random(total + 16, 18)
+    dv = vb.to(dev)
+    do = torch.from_numpy(off.view(np.int64)).to(dev)
+    dh = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    sync()
+    N.check(L.mh_dev_sha256_batch(ctx.handle, dv.data_ptr(), do.data_ptr(), n, dh.data_ptr()))
+    sync()
+    hv = dh.cpu().numpy().reshape(n, 32).copy()
+    bad = rng.choice(n, n // 100, replace=False)
+    hv[bad, 0] ^= 1
+    dh.copy_(torch.from_numpy(hv.reshape(-1)))
+    dl = torch.from_numpy(lens.view(np.int64)).to(dev)
+    ds = torch.empty(n, dtype=torch.int32, device=dev)
+    sync()
+
+    def step():
+        N.check(L.mh_dev_verify_values_batch(ctx.handle, n, dv.data_ptr(), do.data_ptr(),
+                                             dl.data_ptr(), dh.data_ptr(), ds.data_ptr()))
+
+    prewarm(step, sync, a.prewarm)
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    t = timed(step, a.steps, a.warmup, sync)
+    ctx.set_timing(False)
+    runs = a.steps + a.warmup
+    kms = ctx.timing("verify_values")[0] / runs
+    sort_ms = ctx.timing("varlen_sort")[0] / runs
+    st = ds.cpu().numpy()
+    comp = int(((lens.astype(np.int64) + 72) // 64).sum())
+    # host memory in and out (pinned values), the pipelined call
+    hp = torch.from_numpy(hv.reshape(-1)).pin_memory()
+    stp = torch.empty(n, dtype=torch.int32).pin_memory()
+    import ctypes as C
+    badc = C.c_uint64()
+    offc = np.ascontiguousarray(off)
+    lenc = np.ascontiguousarray(lens)
+
+    def host_step():
+        N.check(L.mh_verify_values_batch(ctx.handle, n, vb.data_ptr(), offc.ctypes.data,
+                                         lenc.ctypes.data, hp.data_ptr(), stp.data_ptr(),
+                                         C.byref(badc)))
+
+    th = timed(host_step, max(1, a.steps // 2), 1, sync)
+    # plain pinned H2D of the same value bytes: the PCIe bound of the host call
+    tmp = torch.empty(total, dtype=torch.uint8, device=dev)
+    th2d = timed(lambda: tmp.copy_(vb[:total], non_blocking=True), 3, 1, sync)
+    del tmp
+    ok_dev = bool(np.array_equal(np.sort(np.nonzero(st)[0]), np.sort(bad)))
+    ok_host = bool(np.array_equal(stp.numpy(), st)) and badc.value == len(bad)
+    # CPU baseline: the oracle on 16 threads over the first 2^18 values
+    ns = min(n, 1 << 18)
+    t0 = time.perf_counter()
+    oc, ost = orc.verify_values(vb.numpy(), off[:ns + 1], hv[:ns], lens[:ns], nthreads=16)
+    tc = time.perf_counter() - t0
+    ok_orc = bool(np.array_equal(ost, st[:ns]))
+    SHA_PEAK = 30.9
+    return {"metric": "readValueAt integrity check (immustore.go:3235) over a batch of ragged "
+                      "values, device resident", "entries": n, "value_bytes": total,
+            "value": round(total / t / 2 ** 30, 2), "unit": "GiB/s of values",
+            "M_values_per_s": round(n / t / 1e6, 2), "ms_per_step": round(t * 1e3, 3),
+            "kernel_ms": {"verify_values": round(kms, 4), "varlen_sort": round(sort_ms, 4)},
+            "sha": {"kernel": "k_sha_varlen (compare fused)",
+                    "gcomp_per_s": round(comp / (kms * 1e-3) / 1e9, 2),
+                    "frac": round(comp / (kms * 1e-3) / 1e9 / SHA_PEAK, 4)},
+            "roofline": {"bound": "hbm", "achieved": round((total + 52 * n) / (kms * 1e-3) / 1e9, 1),
+                         "peak": 8000.0, "unit": "GB/s",
+                         "frac": round((total + 52 * n) / (kms * 1e-3) / 1e9 / 8000.0, 4)},
+            "host_pinned": {"ms": round(th * 1e3, 3), "gib_per_s": round(total / th / 2 ** 30, 2),
+                            "h2d_only_ms": round(th2d * 1e3, 3),
+                            "note": "mh_verify_values_batch from pinned host memory (64 MiB "
+                                    "chunks, copy stream + compute stream) vs a plain pinned "
+                                    "H2D of the same bytes"},
+            "corrupted": len(bad), "statuses_match": ok_dev and ok_host and ok_orc,
+            "cpu_baseline": {"kind": "port", "cores": 16, "unit": "GiB/s of values",
+                             "value": round(int(off[ns]) / tc / 2 ** 30, 2),
+                             "sample": "oracle orc_verify_values over the first %d values, 16 "
+                                       "threads, SHA-NI=%s" % (ns, orc.has_shani())}}
 
 
 def run_single(a):
@@ -813,6 +909,8 @@ def run_single(a):
         out = ragged(a, m, N, L, ctx, dev, sync)
     elif a.workload == "document":
         out = document(a, ctx)
+    elif a.workload == "values":
+        out = values(a, m, N, L, ctx, dev, sync)
     elif a.workload == "c2e2e":
         n, vlen, klen = 1 << 20, 1024, 8
         hv = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()

@@ -15,7 +15,8 @@ from .merkle import (Context, default_context, device_count, HTree, InclusionPro
                      verify_inclusion, verify_inclusion_batch, VerifyInclusion, AHtree,
                      nodes_upto, levels_len, level_offset, ahtree_verify_inclusion,
                      ahtree_eval_inclusion, ahtree_verify_consistency, ahtree_eval_consistency,
-                     ahtree_verify_last_inclusion, ahtree_verify_batch, build_hash_tree)
+                     ahtree_verify_last_inclusion, ahtree_verify_batch, build_hash_tree,
+                     verify_values)
 from . import txlayer
 from .txlayer import (TX_HEADER, tx_alh_batch, htree_build_many, verify_linear_proof_batch,
                       verify_dual_proof_v2_batch, VerifyDualProofV2, verify_dual_proof_batch,

@@ -221,6 +221,8 @@ SIGNATURES = {
                                          u8p, u8p]),
     "mh_dev_htree_reduce_nodes": (i32, [vp, u8p, u64, u8p, u8p]),
     "mh_dev_sha256_batch": (i32, [vp, u8p, vp, u64, u8p]),
+    "mh_verify_values_batch": (i32, [vp, u64, u8p, vp, vp, u8p, vp, C.POINTER(u64)]),
+    "mh_dev_verify_values_batch": (i32, [vp, u64, u8p, vp, vp, u8p, vp]),
     "mh_dev_htree_verify_inclusion_batch": (i32, [vp, u64, vp, vp, vp, u8p, u8p, u8p, u8p]),
     "mh_ahtree_new": (i32, [vp, C.POINTER(vp)]),
     "mh_ahtree_free": (i32, [vp]),

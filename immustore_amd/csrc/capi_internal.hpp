@@ -184,7 +184,29 @@ struct mh_ctx {
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
     PinBuf p_stage;       // host-built arrays of one call, staged for a single upload
+    // second stream for host->device copies that overlap the compute stream
+    // (chunked pipelines), its events, and the double-buffered chunk slots
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+    DevBuf s_chunk[2];
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
+    // creates copy_stream and the events on first use (c->mu held)
+    hipError_t copy_lane() {
+        if (copy_stream) return hipSuccess;
+        hipError_t e = hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking);
+        for (int k = 0; k < 2 && e == hipSuccess; k++) {
+            e = hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming);
+        }
+        return e;
+    }
+    ~mh_ctx() {
+        for (int k = 0; k < 2; k++) {
+            if (ev_copied[k]) hipEventDestroy(ev_copied[k]);
+            if (ev_done[k]) hipEventDestroy(ev_done[k]);
+        }
+        if (copy_stream) hipStreamDestroy(copy_stream);
+    }
 };
 
 struct mh_htree {

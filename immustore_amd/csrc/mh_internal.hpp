@@ -93,6 +93,12 @@ size_t sha_varlen_scratch_bytes(uint64_t n);
 hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
                              uint64_t n, const uint8_t *override32, const uint8_t *use_override,
                              uint8_t *out32, uint8_t *scratch);
+// readValueAt's integrity check (immustore.go:3235) over a batch: status[i] =
+// MH_OK iff off[i+1] - off[i] == exp_len[i] (exp_len may be null) and
+// SHA256(buf[off[i] .. off[i+1])) == expect[i], else MH_ERR_CORRUPTED_DATA.
+hipError_t launch_verify_values(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
+                                uint64_t n, const uint64_t *exp_len, const uint8_t *expect,
+                                int32_t *status, uint8_t *scratch);
 // Fused ragged entries (varlen_kernels.hip): hVal (or override) -> hvals_out
 // (may be null), entry digest (tx.go:690-731) -> out32, or its htree leaf when
 // leaf is set (level 0 of the tree).  scratch as for launch_sha256_csr.

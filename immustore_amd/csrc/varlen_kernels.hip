@@ -198,13 +198,22 @@ struct MsgWalk {
 
 // One lane per message; lanes take messages in perm order (or input order
 // when perm is null).  out32[i] = SHA256(buf[off[i] .. off[i+1])), or
-// override32[i] where use_override[i] != 0.
+// override32[i] where use_override[i] != 0.  With cmp.expect (the read-side
+// check of readValueAt, immustore.go:3235): status[i] = MH_OK when the
+// message's length equals exp_len[i] (when given) and its digest equals
+// expect[i], else MH_ERR_CORRUPTED_DATA; out32 may then be null.
+struct ShaCompare {
+    const uint8_t *expect = nullptr;
+    const uint64_t *exp_len = nullptr;
+    int32_t *status = nullptr;
+};
+
 __global__ __launch_bounds__(256) void k_sha_varlen(const uint8_t *__restrict__ buf,
                                                     const uint64_t *__restrict__ off, uint64_t n,
                                                     const uint32_t *__restrict__ perm,
                                                     const uint8_t *__restrict__ override32,
                                                     const uint8_t *__restrict__ use_override,
-                                                    uint8_t *__restrict__ out32) {
+                                                    uint8_t *__restrict__ out32, ShaCompare cmp) {
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const bool valid = g < n;
     const uint64_t gc = valid ? g : n - 1;
@@ -228,6 +237,16 @@ __global__ __launch_bounds__(256) void k_sha_varlen(const uint8_t *__restrict__ 
         if (on) compress(s, w);
     }
     if (!valid) return;
+    if (cmp.expect) {
+        uint32_t e[8];
+        load_digest(cmp.expect + i * 32, e);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) diff |= e[j] ^ s.h[j];
+        const bool len_ok = !cmp.exp_len || cmp.exp_len[i] == L;
+        cmp.status[i] = (diff == 0 && len_ok) ? MH_OK : MH_ERR_CORRUPTED_DATA;
+        if (!out32) return;
+    }
     if (ovr) {
         reinterpret_cast<uint4 *>(out32 + i * 32)[0] =
             reinterpret_cast<const uint4 *>(override32 + i * 32)[0];
@@ -494,7 +513,24 @@ hipError_t launch_sha256_csr(hipStream_t st, Timer *tm, const uint8_t *buf, cons
     if (e != hipSuccess) return e;
     TimerScope ts(tm, "sha256_csr", st);
     hipLaunchKernelGGL(k_sha_varlen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, buf, off, n,
-                       perm, override32, use_override, out32);
+                       perm, override32, use_override, out32, ShaCompare());
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_values(hipStream_t st, Timer *tm, const uint8_t *buf, const uint64_t *off,
+                                uint64_t n, const uint64_t *exp_len, const uint8_t *expect,
+                                int32_t *status, uint8_t *scratch) {
+    if (!n) return hipSuccess;
+    hipError_t e;
+    const uint32_t *perm = nb_sort(st, tm, off, nullptr, n, scratch, &e);
+    if (e != hipSuccess) return e;
+    TimerScope ts(tm, "verify_values", st);
+    ShaCompare cmp;
+    cmp.expect = expect;
+    cmp.exp_len = exp_len;
+    cmp.status = status;
+    hipLaunchKernelGGL(k_sha_varlen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, buf, off, n,
+                       perm, nullptr, nullptr, nullptr, cmp);
     return hipGetLastError();
 }
 

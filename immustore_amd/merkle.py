@@ -522,3 +522,22 @@ def build_hash_tree(version: int, keys, values, mds=None, hval_overrides=None,
         return t.root(), hv, t.levels()
     finally:
         t.close()
+
+
+def verify_values(vals, off, hvals, vlen=None, ctx: Optional[Context] = None):
+    """ImmuStore.readValueAt's integrity check (immustore.go:3235) over a
+    batch (mh_verify_values_batch): value i = vals[off[i]:off[i+1]] (the bytes
+    read), hvals (n, 32) the stored hVals, vlen (n,) the stored lengths (or
+    None) -> (corrupted count, status int32[n]: 0 or MH_ERR_CORRUPTED_DATA)."""
+    ctx = ctx or default_context()
+    off = np.ascontiguousarray(off, np.uint64)
+    n = len(off) - 1
+    v = np.ascontiguousarray(vals, np.uint8)
+    hv = np.ascontiguousarray(hvals, np.uint8)
+    vl = None if vlen is None else np.ascontiguousarray(vlen, np.uint64)
+    st = np.zeros(max(n, 1), np.int32)
+    bad = C.c_uint64()
+    N.check(N.load().mh_verify_values_batch(ctx.handle, n, _addr(v) if v.size else None,
+                                            _addr(off), _addr(vl), _addr(hv), _addr(st),
+                                            C.byref(bad)))
+    return bad.value, st[:n]

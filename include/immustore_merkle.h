@@ -199,6 +199,22 @@ int mh_dev_htree_reduce_nodes(mh_ctx *ctx, const uint8_t *nodes, uint64_t w, uin
 /* SHA-256 of n byte ranges buf[off[i], off[i+1]) -> out (n*32). */
 int mh_dev_sha256_batch(mh_ctx *ctx, const uint8_t *buf, const uint64_t *off, uint64_t n,
                         uint8_t *out);
+/* The read-side value integrity check of ImmuStore.readValueAt
+ * (embedded/store/immustore.go:3183-3240, the check at :3235) over a batch:
+ * value i is vals[off[i], off[i+1]) -- the n_i bytes the vLog or the value
+ * cache returned for a buffer of the entry's stored length vlen[i] -- and
+ * status[i] = MH_OK, or MH_ERR_CORRUPTED_DATA when n_i != vlen[i] or
+ * SHA256(value) != hvals[i] (32 bytes per entry), exactly as Go rejects it
+ * ("value length or digest mismatch").  vlen may be NULL (lengths not
+ * checked).  Host variant: host memory in and out, synchronous; the value
+ * bytes go up in ~64 MiB chunks on a copy stream while the previous chunk is
+ * checked; *ncorrupted (may be NULL) = entries not MH_OK.  Device variant:
+ * every pointer device memory, asynchronous on the context stream. */
+int mh_verify_values_batch(mh_ctx *ctx, uint64_t n, const uint8_t *vals, const uint64_t *off,
+                           const uint64_t *vlen, const uint8_t *hvals, int32_t *status,
+                           uint64_t *ncorrupted);
+int mh_dev_verify_values_batch(mh_ctx *ctx, uint64_t n, const uint8_t *vals, const uint64_t *off,
+                               const uint64_t *vlen, const uint8_t *hvals, int32_t *status);
 /* Device variants of the batch proof generators: every pointer is device
  * memory (levels of a tree of `width` leaves / a dLog of `size` appends). */
 int mh_dev_htree_inclusion_proof_batch(mh_ctx *ctx, const uint8_t *levels, uint64_t width,

@@ -400,6 +400,57 @@ int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32
     return OK;
 }
 
+/* ------------------------------------------------------- value integrity */
+/* embedded/store/immustore.go:3183-3240: readValueAt reads vLen bytes of the
+ * value (vLog or cache) into b and returns ErrCorruptedData when
+ * len(b) != n || hvalue != sha256.Sum256(b[:n]) (:3235). */
+typedef struct {
+    uint64_t lo, hi;
+    const uint8_t *vals;
+    const uint64_t *off, *vlen;
+    const uint8_t *hv;
+    int32_t *st;
+    uint64_t bad;
+} values_job;
+
+static void *values_worker(void *arg) {
+    values_job *j = (values_job *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const uint64_t len = j->off[i + 1] - j->off[i];
+        uint8_t h[32];
+        orc_sha256(len ? j->vals + j->off[i] : NULL, len, h);
+        const int ok = (!j->vlen || j->vlen[i] == len) && memcmp(h, j->hv + 32 * i, 32) == 0;
+        j->st[i] = ok ? 0 : 14;
+        j->bad += !ok;
+    }
+    return NULL;
+}
+
+uint64_t orc_verify_values(uint64_t n, const uint8_t *vals, const uint64_t *off,
+                           const uint64_t *vlen, const uint8_t *hvals, int32_t *status,
+                           int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    values_job jobs[64];
+    pthread_t th[64];
+    const uint64_t per = (n + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        const uint64_t lo = (uint64_t)t * per < n ? (uint64_t)t * per : n;
+        const uint64_t hi = lo + per < n ? lo + per : n;
+        jobs[t] = (values_job){lo, hi, vals, off, vlen, hvals, status, 0};
+    }
+    if (nthreads == 1) {
+        values_worker(&jobs[0]);
+    } else {
+        for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, values_worker, &jobs[t]);
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    }
+    uint64_t bad = 0;
+    for (int t = 0; t < nthreads; t++) bad += jobs[t].bad;
+    return bad;
+}
+
 /* ------------------------------------------------------- precommit batch */
 /* ImmuStore.precommit over many transactions (immustore.go:1620-1632, the
  * Eh check of :1649-1654): orc_build_entries per tx, txs spread over

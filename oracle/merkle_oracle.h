@@ -82,6 +82,13 @@ int orc_build_entries_fixed(int version, uint64_t n, const uint8_t *keys, uint32
 /* ImmuStore.precommit over ntx transactions (immustore.go:1620-1632, 2301-2313;
  * Eh check :1649-1654): same contract as mh_precommit_batch
  * (include/immustore_merkle.h); nthreads splits the txs. */
+/* ImmuStore.readValueAt's integrity check (immustore.go:3235) over a batch:
+ * status[i] = 0 when off[i+1]-off[i] == vlen[i] (vlen may be NULL) and
+ * SHA256(vals[off[i]..off[i+1])) == hvals[i], else ERR_CORRUPTED_DATA (14);
+ * entries split over nthreads threads.  Returns the number not OK. */
+uint64_t orc_verify_values(uint64_t n, const uint8_t *vals, const uint64_t *off,
+                           const uint64_t *vlen, const uint8_t *hvals, int32_t *status,
+                           int nthreads);
 int orc_precommit_batch(int version, uint64_t max_width, uint64_t ntx, const uint64_t *tx_off,
                         const uint8_t *keys, const uint64_t *key_off, const uint8_t *md,
                         const uint64_t *md_off, const uint8_t *vals, const uint64_t *val_off,

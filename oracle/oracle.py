@@ -351,6 +351,24 @@ def ahtree_verify_last_inclusion(proof, i, leaf, root):
     return bool(lib().orc_ahtree_verify_last_inclusion(tp, nt, i, _p(_u8(leaf)), _p(_u8(root))))
 
 
+def verify_values(vals, off, hvals, vlen=None, nthreads=1):
+    """readValueAt's check (immustore.go:3235) per value -> (bad count,
+    status int32[n]: 0 or 14 = ErrCorruptedData)."""
+    off = np.ascontiguousarray(off, np.uint64)
+    n = len(off) - 1
+    v = np.ascontiguousarray(vals, np.uint8)
+    if v.size == 0:
+        v = np.zeros(1, np.uint8)
+    hv = np.ascontiguousarray(hvals, np.uint8)
+    vl = None if vlen is None else np.ascontiguousarray(vlen, np.uint64)
+    st = np.zeros(max(n, 1), np.int32)
+    L = lib()
+    L.orc_verify_values.restype = C.c_uint64
+    bad = L.orc_verify_values(C.c_uint64(n), _p(v), _p(off), _p(vl) if vl is not None else None,
+                              _p(hv), st.ctypes.data_as(C.c_void_p), nthreads)
+    return int(bad), st[:n]
+
+
 def fill_random(nbytes, seed):
     out = np.zeros(nbytes, np.uint8)
     lib().orc_fill_random(_p(out), nbytes, seed)

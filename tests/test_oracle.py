@@ -219,3 +219,46 @@ def test_fill_random_matches_generator(orc):
     for seed in (1, 2, 3, 12345):
         for n in (1, 7, 8, 100, 4096):
             assert orc.fill_random(n, seed).tobytes() == mg.rand_bytes(seed, n)
+
+
+def _values_case(seed, n=500):
+    """Values, their stored hVals and expected lengths with the corruptions
+    readValueAt rejects (immustore.go:3235): a flipped byte, a short read
+    (vLen above the bytes returned), a long read, a wrong hVal; empty values."""
+    import hashlib
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, n)
+    lens[:20] = 0
+    vals = [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in lens]
+    hv = np.frombuffer(b"".join(hashlib.sha256(v).digest() for v in vals), np.uint8).reshape(n, 32).copy()
+    vlen = lens.astype(np.uint64).copy()
+    bad = np.zeros(n, bool)
+    for i in rng.choice(n, min(60, n // 2), replace=False):
+        kind = int(rng.integers(0, 4))
+        if kind == 0 and len(vals[i]):
+            b = bytearray(vals[i])
+            b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            vals[i] = bytes(b)
+        elif kind == 1 and len(vals[i]):
+            vals[i] = vals[i][:-1]           # short read: n < len(b)
+        elif kind == 2:
+            vlen[i] += 1                       # stored length above the bytes read
+        else:
+            hv[i, int(rng.integers(0, 32))] ^= 0x80
+        bad[i] = True
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum([len(v) for v in vals], out=off[1:])
+    return np.frombuffer(b"".join(vals) + b"\0", np.uint8)[:int(off[-1])].copy(), off, hv, vlen, bad
+
+
+def test_verify_values_oracle_vs_hashlib(orc):
+    for seed in (1, 2):
+        vb, off, hv, vlen, bad = _values_case(seed)
+        for nt in (1, 4):
+            c, st = orc.verify_values(vb, off, hv, vlen, nthreads=nt)
+            assert c == int(bad.sum())
+            assert np.array_equal(st != 0, bad)
+            assert set(np.unique(st)) <= {0, 14}
+        # no lengths: only the digest decides (a long vLen alone passes)
+        c2, st2 = orc.verify_values(vb, off, hv, None)
+        assert np.all(st2[~bad] == 0) and c2 <= c
