@@ -2,6 +2,7 @@
 // units (capi.hip: htree / ahtree handles; capi_tx.hip: tx layer).
 #pragma once
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -189,6 +190,7 @@ struct mh_ctx {
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf s_chunk[2];
+    std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
     // creates copy_stream and the events on first use (c->mu held)
     hipError_t copy_lane() {
@@ -205,6 +207,7 @@ struct mh_ctx {
             if (ev_copied[k]) hipEventDestroy(ev_copied[k]);
             if (ev_done[k]) hipEventDestroy(ev_done[k]);
         }
+        for (hipEvent_t e : ev_chunks) hipEventDestroy(e);
         if (copy_stream) hipStreamDestroy(copy_stream);
     }
 };

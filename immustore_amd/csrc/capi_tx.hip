@@ -951,23 +951,43 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                                  int32_t *status_out) {
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        // The raw records go to the device first: the copy (DMA when buf is
-        // pinned) runs under the host hop below.
+        // The raw records go to the device first, on the context's copy
+        // stream in chunks of 8 MiB with an event after each: the copy (DMA
+        // when buf is pinned) runs under the host hop below, and the device
+        // work on the records whose bytes have already arrived can start
+        // before the last chunks land.
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         hipStream_t st = c->stream;
+        MH_HIP(c->copy_lane());
+        hipStream_t cs = c->copy_stream;
         if (len) MH_HIP(c->s_txlog.ensure(len));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
-        // The copy call itself can hold its caller for the whole transfer
-        // (measured: a 75 MB pinned H2D kept the host busy ~1.3 ms), so it is
-        // issued from a helper thread while this one hops; joined before
-        // anything else goes on the stream.
+        const uint64_t chunk = 8ull << 20;
+        const uint64_t nck = (len + chunk - 1) / chunk;
+        while (c->ev_chunks.size() < nck) {
+            hipEvent_t e;
+            MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->ev_chunks.push_back(e);
+        }
+        // the copy may overwrite s_txlog only once earlier work on st is done
+        MH_HIP(hipEventRecord(c->ev_done[0], st));
+        MH_HIP(hipStreamWaitEvent(cs, c->ev_done[0], 0));
+        // The copy calls themselves can hold their caller for the whole
+        // transfer (measured: a 75 MB pinned H2D kept the host busy ~1.3 ms),
+        // so they are issued from a helper thread while this one hops; joined
+        // before anything else goes on the streams.
         hipError_t cp_err = hipSuccess;
         std::thread cp;
         if (len) {
             auto issue = [&]() {
-                hipSetDevice(c->device);
-                cp_err = hipMemcpyAsync(dbuf, buf, len, hipMemcpyHostToDevice, st);
+                hipError_t e = hipSetDevice(c->device);
+                for (uint64_t k = 0; k < nck && !e; k++) {
+                    const uint64_t o = k * chunk, b = std::min(chunk, len - o);
+                    e = hipMemcpyAsync(dbuf + o, buf + o, b, hipMemcpyHostToDevice, cs);
+                    if (!e) e = hipEventRecord(c->ev_chunks[k], cs);
+                }
+                cp_err = e;
             };
             if (len >= (8ull << 20)) {
                 try {
@@ -993,13 +1013,16 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         }
         if (cp.joinable()) cp.join();
         MH_HIP(cp_err);
+        // copy chunks already on the device now (the rest still in flight)
+        uint64_t arrived = 0;
+        while (arrived < nck && hipEventQuery(c->ev_chunks[arrived]) == hipSuccess) arrived++;
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
         // on an error hop.end is the failing record's offset = the end of the last good one
         if (ntx_out) *ntx_out = ntx;
         if (consumed_out) *consumed_out = hop.end;
         if (!ntx) {
-            MH_HIP(hipStreamSynchronize(st));  // buf stays the caller's once we return
+            MH_HIP(hipStreamSynchronize(cs));  // buf stays the caller's once we return
             return rc;
         }
         uint64_t E = 0, wmax = 0;
@@ -1014,6 +1037,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         std::vector<uint64_t> patch;  // [ne idx][ne off][nh idx][nh off | len << 32]
         uint64_t npe = 0, nph = 0;
         if (!hop.P.empty()) {
+            if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));  // whole log in
             std::vector<uint64_t> first_leaf(ntx);
             for (uint64_t k = 0, acc = 0; k < ntx; k++) {
                 first_leaf[k] = acc;
@@ -1091,40 +1115,70 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             lo[ntx] = acc;
         }
         MH_HIP(hipMemcpyAsync(base + b_ro, pin, idx_bytes, hipMemcpyHostToDevice, st));
-        MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), ntx, dbuf, (const uint64_t *)(base + b_ro),
-                                      (MhTxHeader *)(base + b_h), (uint64_t *)(base + b_es)));
-        // per-entry index, then entry digests hashed in place from the raw
-        // entry records (tx.go:578-585 -> 690-731); small trees take the
-        // leaves straight away (htree.go:79-83)
-        MH_HIP(launch_txe_index(st, c->tm(), ntx, dbuf, (const MhTxHeader *)(base + b_h),
-                                (const uint64_t *)(base + b_es), (const uint64_t *)(base + b_lo),
-                                (uint64_t *)(base + b_rec), base + b_ver));
-        if (npe + nph) {
-            const uint64_t *pl = reinterpret_cast<const uint64_t *>(dbuf + patch[0]);
-            MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
-                                      pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
+        // Two groups of txs when every tree is small and nothing is patched:
+        // the records whose bytes had arrived when the hop ended (their
+        // kernels and outputs go first, under the rest of the copy), then the
+        // others after the last chunk.  Otherwise one group after the copy.
+        uint64_t split = ntx;
+        if (small && !(npe + nph) && arrived < nck && nck > 1) {
+            const uint64_t ready = arrived * chunk;  // bytes [0, ready) on the device
+            split = 0;
+            while (split < ntx && hop.R[split].alh + 32 <= ready) split++;
         }
-        MH_HIP(launch_txe_leaf(st, c->tm(), E, dbuf, (const uint64_t *)(base + b_rec), base + b_ver,
-                               small, base + b_lv));
-        // one htree per tx (tx.go:617-621)
-        if (small) {
-            MH_HIP(launch_small_roots(st, c->tm(), ntx, (const uint64_t *)(base + b_lo), base + b_lv,
-                                      base + b_eh));
-        } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_lv,
-                                            base + b_eh, pin + idx_bytes)) {
-            return e;
-        }
-        // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
-        MH_HIP(launch_tx_alh(st, c->tm(), ntx, (const MhTxHeader *)(base + b_h), dbuf,
-                             base + b_eh, base + b_s, dbuf, (const uint64_t *)(base + b_ap),
-                             nullptr, base + b_a, (int32_t *)(base + b_st)));
-        if (status_out)
-            MH_HIP(hipMemcpyAsync(status_out, base + b_st, ntx * 4, hipMemcpyDeviceToHost, st));
-        if (alh_out) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
-        if (hdrs_out) {  // the device headers with the rebuilt Eh
-            MH_HIP(launch_put_eh(st, ntx, base + b_eh, (MhTxHeader *)(base + b_h)));
-            MH_HIP(hipMemcpyAsync(hdrs_out, base + b_h, ntx * sizeof(mh_tx_header),
-                                  hipMemcpyDeviceToHost, st));
+        const uint64_t groups[3] = {0, split, ntx};
+        for (int g = 0; g < 2; g++) {
+            const uint64_t t0 = groups[g], t1 = groups[g + 1], nt = t1 - t0;
+            if (!nt) continue;
+            // the first group of a split reads only chunks that have arrived
+            if (nck && t1 == ntx) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
+            const uint64_t *ro = (const uint64_t *)(base + b_ro) + t0;
+            const uint64_t *lo = (const uint64_t *)(base + b_lo) + t0;
+            MhTxHeader *hd = (MhTxHeader *)(base + b_h) + t0;
+            const uint64_t *es = (const uint64_t *)(base + b_es) + t0;
+            const uint64_t e0 = (g == 0) ? 0 : [&] {
+                uint64_t a = 0;
+                for (uint64_t k = 0; k < t0; k++) a += hop.R[k].nent;
+                return a;
+            }();
+            uint64_t eg = 0;
+            for (uint64_t k = t0; k < t1; k++) eg += hop.R[k].nent;
+            MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, dbuf, ro, hd, (uint64_t *)es));
+            // per-entry index, then entry digests hashed in place from the raw
+            // entry records (tx.go:578-585 -> 690-731); small trees take the
+            // leaves straight away (htree.go:79-83)
+            MH_HIP(launch_txe_index(st, c->tm(), nt, dbuf, hd, es, lo, (uint64_t *)(base + b_rec),
+                                    base + b_ver));
+            if (npe + nph) {
+                const uint64_t *pl = reinterpret_cast<const uint64_t *>(dbuf + patch[0]);
+                MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
+                                          pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
+            }
+            MH_HIP(launch_txe_leaf(st, c->tm(), eg, dbuf, (const uint64_t *)(base + b_rec) + e0,
+                                   base + b_ver + e0, small, base + b_lv + e0 * 32));
+            // one htree per tx (tx.go:617-621)
+            if (small) {
+                MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + b_lv + e0 * 32,
+                                          base + b_eh + t0 * 32));
+            } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_lv,
+                                                base + b_eh, pin + idx_bytes)) {
+                return e;
+            }
+            // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
+            MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, dbuf, base + b_eh + t0 * 32,
+                                 base + b_s + t0 * kTxInnerStride, dbuf,
+                                 (const uint64_t *)(base + b_ap) + t0, nullptr, base + b_a + t0 * 32,
+                                 (int32_t *)(base + b_st) + t0));
+            if (status_out)
+                MH_HIP(hipMemcpyAsync(status_out + t0, base + b_st + t0 * 4, nt * 4,
+                                      hipMemcpyDeviceToHost, st));
+            if (alh_out)
+                MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, base + b_a + t0 * 32, nt * 32,
+                                      hipMemcpyDeviceToHost, st));
+            if (hdrs_out) {  // the device headers with the rebuilt Eh
+                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
+                MH_HIP(hipMemcpyAsync(hdrs_out + t0, hd, nt * sizeof(mh_tx_header),
+                                      hipMemcpyDeviceToHost, st));
+            }
         }
         MH_HIP(hipStreamSynchronize(st));
         return rc;
