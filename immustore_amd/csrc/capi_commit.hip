@@ -181,7 +181,7 @@ int enqueue(mh_commit_pipe *p, mh_commit_pipe::Slot &s, const Req &R, uint64_t t
         MH_HIP(hipMemcpyAsync(base + b_lo, s.pin.p, (nt + 1) * 8, hipMemcpyHostToDevice, st));
         MH_HIP(launch_leaf_for(st, tm, n, base + b_dig, base + b_lv));  // htree.go:79-83
         MH_HIP(launch_small_roots(st, tm, nt, (const uint64_t *)(base + b_lo), base + b_lv,
-                                  base + b_eh));
+                                  base + b_eh, wmax));
     } else if (int e = run_tree_plan_on(s.tree, st, tm, P, nt, n, base + b_dig, base + b_eh,
                                         reinterpret_cast<uint8_t *>(s.pin.p))) {
         return e;

@@ -185,9 +185,12 @@ struct mh_ctx {
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
     PinBuf p_stage;       // host-built arrays of one call, staged for a single upload
+    PinBuf p_small;       // a few words a kernel stores straight into host memory
     // second stream for host->device copies that overlap the compute stream
     // (chunked pipelines), its events, and the double-buffered chunk slots
     hipStream_t copy_stream = nullptr;
+    hipStream_t copy_stream2 = nullptr;  // a second copy lane (ChunkCopier)
+    hipStream_t d2h_stream = nullptr;  // device->host results of an early part of a call
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf s_chunk[2];
     std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call
@@ -196,6 +199,8 @@ struct mh_ctx {
     hipError_t copy_lane() {
         if (copy_stream) return hipSuccess;
         hipError_t e = hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&copy_stream2, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking);
         for (int k = 0; k < 2 && e == hipSuccess; k++) {
             e = hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming);
@@ -209,8 +214,108 @@ struct mh_ctx {
         }
         for (hipEvent_t e : ev_chunks) hipEventDestroy(e);
         if (copy_stream) hipStreamDestroy(copy_stream);
+        if (copy_stream2) hipStreamDestroy(copy_stream2);
+        if (d2h_stream) hipStreamDestroy(d2h_stream);
     }
 };
+
+// Host-to-device copies of a call cut into chunks, issued from one helper
+// thread (or two, chunk k on lane k % 2) onto the context's copy stream(s)
+// with an event after each chunk.  A copy call from pinned memory holds its
+// caller until the transfer is done, so every chunk boundary leaves the DMA
+// engine idle for the next call's setup (60-100 us measured,
+// profiles/txlog_copy_trace_r03.txt): few, large chunks.  The consumer
+// waits for chunk k (wait(k): the copy and its event are enqueued) and then
+// orders its stream after event ev(k).  c->mu must be held; both lanes start
+// after everything queued on c->stream before start().
+struct ChunkCopier {
+    struct Piece {
+        void *dst;
+        const void *src;
+        uint64_t bytes;
+    };
+    mh_ctx *c = nullptr;
+    std::vector<std::vector<Piece>> chunks;
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<uint8_t> done;  // chunk k enqueued (guarded by m)
+    hipError_t err = hipSuccess;
+    std::thread th[2];
+    int lanes = 1;  // 1: one helper thread / copy stream; 2: two
+
+    explicit ChunkCopier(mh_ctx *ctx) : c(ctx) {}
+    ~ChunkCopier() { join(); }
+    // chunks must be filled; events for every chunk must exist in c->ev_chunks
+    hipError_t start() {
+        done.assign(chunks.size(), 0);
+        if (hipError_t e = hipEventRecord(c->ev_done[0], c->stream)) return e;
+        if (hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_done[0], 0)) return e;
+        if (hipError_t e = hipStreamWaitEvent(c->copy_stream2, c->ev_done[0], 0)) return e;
+        for (int j = 0; j < lanes; j++) {
+            auto lane = [this, j]() {
+                hipError_t e = hipSetDevice(c->device);
+                hipStream_t s = j ? c->copy_stream2 : c->copy_stream;
+                for (size_t k = (size_t)j; k < chunks.size(); k += (size_t)lanes) {
+                    for (const Piece &p : chunks[k])
+                        if (!e && p.bytes) e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, s);
+                    if (!e) e = hipEventRecord(c->ev_chunks[k], s);
+                    std::lock_guard<std::mutex> g(m);
+                    if (e) {
+                        err = e;
+                        cv.notify_all();
+                        return;
+                    }
+                    done[k] = 1;
+                    cv.notify_all();
+                }
+            };
+            if (chunks.size() <= 1) {  // one chunk: no thread worth starting
+                lane();
+                continue;
+            }
+            try {
+                th[j] = std::thread(lane);
+            } catch (...) {
+                lane();  // no thread: issue this lane's copies here
+            }
+        }
+        return hipSuccess;
+    }
+    // chunk k's copies and event are enqueued (or an error happened)
+    hipError_t wait(size_t k) {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return done[k] || err != hipSuccess; });
+        return err;
+    }
+    // chunks [0, result) are enqueued AND complete on the device now
+    size_t arrived() {
+        size_t a = 0;
+        while (a < chunks.size()) {
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (!done[a]) break;
+            }
+            if (hipEventQuery(c->ev_chunks[a]) != hipSuccess) break;
+            a++;
+        }
+        return a;
+    }
+    hipError_t join() {
+        for (auto &t : th)
+            if (t.joinable()) t.join();
+        return err;
+    }
+};
+
+// events for n chunks in c->ev_chunks
+inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
+    while (c->ev_chunks.size() < n) {
+        hipEvent_t e;
+        if (hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming)) return r;
+        c->ev_chunks.push_back(e);
+    }
+    return hipSuccess;
+}
 
 struct mh_htree {
     mh_ctx *ctx = nullptr;

@@ -10,6 +10,10 @@
 #include <thread>
 #include <vector>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+
 #include "capi_internal.hpp"
 
 namespace {
@@ -137,7 +141,7 @@ int build_many_dev(mh_ctx *c, hipStream_t st, uint64_t ntrees, const uint64_t *l
         MH_HIP(hipMemcpyAsync(s_lo.p, leaf_off, (ntrees + 1) * 8, hipMemcpyHostToDevice, st));
         MH_HIP(launch_leaf_for(st, c->tm(), E, d_dig, s_lv.as<uint8_t>()));  // htree.go:79-83
         MH_HIP(launch_small_roots(st, c->tm(), ntrees, s_lo.as<uint64_t>(), s_lv.as<uint8_t>(),
-                                  d_roots));
+                                  d_roots, wmax));
         // leaf_off is the caller's host memory: done with it before returning
         MH_HIP(hipStreamSynchronize(st));
     } else {
@@ -945,84 +949,80 @@ extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entr
     });
 }
 
+// MH_TXLOG_TRACE=1: host timestamps of the call's phases on stderr (A/B
+// measurements of the copy / hop / device overlap)
+namespace {
+struct PhaseTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    char buf[512];
+    int n = 0;
+    PhaseTrace() : on(getenv("MH_TXLOG_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char *what) {
+        if (!on || n > 400) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        n += snprintf(buf + n, sizeof buf - n, " %s=%.0f", what, us);
+    }
+    ~PhaseTrace() {
+        if (on) fprintf(stderr, "txlog_trace%s\n", buf);
+    }
+};
+}  // namespace
+
 extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                                  uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
                                  uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
                                  int32_t *status_out) {
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        // The raw records go to the device first, on the context's copy
-        // stream in chunks of 8 MiB with an event after each: the copy (DMA
-        // when buf is pinned) runs under the host hop below, and the device
-        // work on the records whose bytes have already arrived can start
-        // before the last chunks land.
+        PhaseTrace tr;
+        // The raw records go to the device first, in chunks of 8 MiB with an
+        // event after each: the copy (DMA when buf is pinned) runs under the
+        // host hop below, and the device work on the records whose bytes have
+        // already arrived starts before the last chunks land.
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         hipStream_t st = c->stream;
         MH_HIP(c->copy_lane());
-        hipStream_t cs = c->copy_stream;
         if (len) MH_HIP(c->s_txlog.ensure(len));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
-        const uint64_t chunk = 8ull << 20;
-        const uint64_t nck = (len + chunk - 1) / chunk;
-        while (c->ev_chunks.size() < nck) {
-            hipEvent_t e;
-            MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->ev_chunks.push_back(e);
+        // two chunks from 16 MiB up: the first three quarters, then the rest
+        // (every extra copy call costs ~0.1 ms of DMA setup, so no more);
+        // the copies run under the host hop on a helper thread (ChunkCopier),
+        // which joins on every way out (they read the caller's buf)
+        const uint64_t chunk = len >= (16ull << 20) ? ((len / 4 * 3) & ~4095ull) : len;
+        const uint64_t nck = len ? (chunk < len ? 2 : 1) : 0;
+        MH_HIP(ensure_chunk_events(c, nck));
+        ChunkCopier cc(c);
+        cc.chunks.resize(nck);
+        for (uint64_t k = 0; k < nck; k++) {
+            const uint64_t o = k * chunk;
+            cc.chunks[k] = {{dbuf + o, buf + o, k + 1 < nck ? chunk : len - o}};
         }
-        // the copy may overwrite s_txlog only once earlier work on st is done
-        MH_HIP(hipEventRecord(c->ev_done[0], st));
-        MH_HIP(hipStreamWaitEvent(cs, c->ev_done[0], 0));
-        // The copy calls themselves can hold their caller for the whole
-        // transfer (measured: a 75 MB pinned H2D kept the host busy ~1.3 ms),
-        // so they are issued from a helper thread while this one hops; joined
-        // before anything else goes on the streams.
-        hipError_t cp_err = hipSuccess;
-        std::thread cp;
-        if (len) {
-            auto issue = [&]() {
-                hipError_t e = hipSetDevice(c->device);
-                for (uint64_t k = 0; k < nck && !e; k++) {
-                    const uint64_t o = k * chunk, b = std::min(chunk, len - o);
-                    e = hipMemcpyAsync(dbuf + o, buf + o, b, hipMemcpyHostToDevice, cs);
-                    if (!e) e = hipEventRecord(c->ev_chunks[k], cs);
-                }
-                cp_err = e;
-            };
-            if (len >= (8ull << 20)) {
-                try {
-                    cp = std::thread(issue);
-                } catch (...) {  // no thread: issue it here
-                    issue();
-                }
-            } else {
-                issue();
-            }
-        }
+        MH_HIP(cc.start());
+        auto join_copies = [&]() -> int {
+            hipError_t e = cc.join();
+            return e == hipSuccess ? MH_OK : -(int)e;
+        };
         // ---- host hop (tx.go:419-603): record structure and limits only.  Per
         // entry the host reads the two lengths it needs to find the next entry
         // (several threads over a long log, hop_all); the per-entry index (record
         // offsets, versions, message lengths) is rebuilt on the device from each
         // tx's first entry (k_txe_index).
         HopOut hop;
-        try {
-            hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
-        } catch (...) {
-            if (cp.joinable()) cp.join();
-            throw;
-        }
-        if (cp.joinable()) cp.join();
-        MH_HIP(cp_err);
-        // copy chunks already on the device now (the rest still in flight)
-        uint64_t arrived = 0;
-        while (arrived < nck && hipEventQuery(c->ev_chunks[arrived]) == hipSuccess) arrived++;
+        tr.mark("copies_started");
+        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
+        tr.mark("hop");
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
         // on an error hop.end is the failing record's offset = the end of the last good one
         if (ntx_out) *ntx_out = ntx;
         if (consumed_out) *consumed_out = hop.end;
         if (!ntx) {
-            MH_HIP(hipStreamSynchronize(cs));  // buf stays the caller's once we return
+            if (int e = join_copies()) return e;
+            // buf stays the caller's once we return
+            MH_HIP(hipStreamSynchronize(c->copy_stream));
+            MH_HIP(hipStreamSynchronize(c->copy_stream2));
             return rc;
         }
         uint64_t E = 0, wmax = 0;
@@ -1037,6 +1037,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         std::vector<uint64_t> patch;  // [ne idx][ne off][nh idx][nh off | len << 32]
         uint64_t npe = 0, nph = 0;
         if (!hop.P.empty()) {
+            if (int e = join_copies()) return e;
             if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));  // whole log in
             std::vector<uint64_t> first_leaf(ntx);
             for (uint64_t k = 0, acc = 0; k < ntx; k++) {
@@ -1116,21 +1117,28 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         }
         MH_HIP(hipMemcpyAsync(base + b_ro, pin, idx_bytes, hipMemcpyHostToDevice, st));
         // Two groups of txs when every tree is small and nothing is patched:
-        // the records whose bytes had arrived when the hop ended (their
-        // kernels and outputs go first, under the rest of the copy), then the
-        // others after the last chunk.  Otherwise one group after the copy.
+        // the records inside the first copy chunk (their kernels and outputs
+        // go as soon as that chunk lands, under the copy of the rest), then
+        // the others after the last chunk.  Otherwise one group after the copy.
         uint64_t split = ntx;
-        if (small && !(npe + nph) && arrived < nck && nck > 1) {
-            const uint64_t ready = arrived * chunk;  // bytes [0, ready) on the device
+        if (small && !(npe + nph) && nck == 2) {
             split = 0;
-            while (split < ntx && hop.R[split].alh + 32 <= ready) split++;
+            while (split < ntx && hop.R[split].alh + 32 <= chunk) split++;
         }
         const uint64_t groups[3] = {0, split, ntx};
         for (int g = 0; g < 2; g++) {
             const uint64_t t0 = groups[g], t1 = groups[g + 1], nt = t1 - t0;
             if (!nt) continue;
-            // the first group of a split reads only chunks that have arrived
-            if (nck && t1 == ntx) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
+            // the first group of a split reads only the first chunk
+            if (t1 == ntx) {
+                if (int e = join_copies()) return e;
+                tr.mark("joined");
+                if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
+            } else {
+                if (hipError_t e = cc.wait(0)) return -(int)e;
+                tr.mark("chunk0_issued");
+                MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[0], 0));
+            }
             const uint64_t *ro = (const uint64_t *)(base + b_ro) + t0;
             const uint64_t *lo = (const uint64_t *)(base + b_lo) + t0;
             MhTxHeader *hd = (MhTxHeader *)(base + b_h) + t0;
@@ -1158,7 +1166,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             // one htree per tx (tx.go:617-621)
             if (small) {
                 MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + b_lv + e0 * 32,
-                                          base + b_eh + t0 * 32));
+                                          base + b_eh + t0 * 32, wmax));
             } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_lv,
                                                 base + b_eh, pin + idx_bytes)) {
                 return e;
@@ -1168,19 +1176,31 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                                  base + b_s + t0 * kTxInnerStride, dbuf,
                                  (const uint64_t *)(base + b_ap) + t0, nullptr, base + b_a + t0 * 32,
                                  (int32_t *)(base + b_st) + t0));
+            if (hdrs_out)  // the device headers with the rebuilt Eh
+                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
+            // the first group's results go down on their own stream while
+            // the second group's kernels run
+            hipStream_t ds = st;
+            if (t1 < ntx) {
+                ds = c->d2h_stream;
+                MH_HIP(hipEventRecord(c->ev_done[1], st));
+                MH_HIP(hipStreamWaitEvent(ds, c->ev_done[1], 0));
+            }
             if (status_out)
                 MH_HIP(hipMemcpyAsync(status_out + t0, base + b_st + t0 * 4, nt * 4,
-                                      hipMemcpyDeviceToHost, st));
+                                      hipMemcpyDeviceToHost, ds));
             if (alh_out)
                 MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, base + b_a + t0 * 32, nt * 32,
-                                      hipMemcpyDeviceToHost, st));
-            if (hdrs_out) {  // the device headers with the rebuilt Eh
-                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
+                                      hipMemcpyDeviceToHost, ds));
+            if (hdrs_out)
                 MH_HIP(hipMemcpyAsync(hdrs_out + t0, hd, nt * sizeof(mh_tx_header),
-                                      hipMemcpyDeviceToHost, st));
-            }
+                                      hipMemcpyDeviceToHost, ds));
         }
+        tr.mark("enqueued");
+        if (split < ntx) MH_HIP(hipStreamSynchronize(c->d2h_stream));
+        tr.mark("d2h_a_done");
         MH_HIP(hipStreamSynchronize(st));
+        tr.mark("done");
         return rc;
     });
 }

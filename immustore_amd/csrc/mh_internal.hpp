@@ -234,16 +234,19 @@ hipError_t launch_advance_chain(hipStream_t st, Timer *tm, uint64_t n, const uin
 // roots of many htrees (widths leaf_off[t+1]-leaf_off[t], small), one lane
 // each, in place over nodes = their leaf hashes back to back
 constexpr uint64_t kSmallTreeMax = 64;
-// launch_small_roots is the right tool when a tree's serial chain is short
-// (one lane walks <= 15 node hashes) or there are few trees (a wave per tree,
-// level by level); many trees of 17..64 leaves go level-parallel through the
-// host tree plan instead (k_seg_level: every node of a level at once) --
-// e.g. 8192 trees of 64 leaves: 0.29 ms one lane per tree vs ~0.07 ms.
+// launch_small_roots covers every batch whose widest tree has <= 64 leaves
+// without a host tree plan: a wave per tree for <= 2048 trees (latency), the
+// level-parallel packed kernel for more (every node of a level at once,
+// 512 / P trees per workgroup); wider trees go through the host tree plan
+// (k_seg_level).
 inline bool small_roots_fit(uint64_t ntrees, uint64_t wmax) {
-    return wmax <= kSmallTreeMax && (wmax <= 16 || ntrees <= 2048);
+    (void)ntrees;
+    return wmax <= kSmallTreeMax;
 }
+// wmax: the widest tree (<= kSmallTreeMax picks the level-parallel kernel
+// for many trees)
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
-                              uint8_t *nodes, uint8_t *roots);
+                              uint8_t *nodes, uint8_t *roots, uint64_t wmax);
 // headers + first-entry offsets of tx records from the raw log (md_off relative to buf)
 hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                                   const uint64_t *rec_off, MhTxHeader *hdrs, uint64_t *ent_start);

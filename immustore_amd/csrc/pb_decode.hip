@@ -573,6 +573,18 @@ __global__ __launch_bounds__(256) void k_dpv2_final(uint64_t n, const mh_tx_head
     status[p] = s;
 }
 
+// Two device words into pinned host memory by a kernel store: a small
+// read-back without a DMA copy, which would queue behind the large
+// host-to-device chunks in flight on the copy engine.
+__global__ void k_put2_host(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b,
+                            volatile uint64_t *out) {
+    if (threadIdx.x == 0) {
+        out[0] = *a;
+        out[1] = *b;
+        __threadfence_system();
+    }
+}
+
 }  // namespace
 
 extern "C" int mh_dual_proof_v2_pb_decode_batch(
@@ -871,9 +883,10 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
         std::lock_guard<std::mutex> lk(c->mu);
         MH_HIP(hipSetDevice(c->device));
         MH_HIP(c->copy_lane());
-        hipStream_t st = c->stream, cs = c->copy_stream;
+        MH_HIP(c->p_small.ensure(64));
+        hipStream_t st = c->stream;
         // chunks: consecutive messages up to chunk_bytes (one at least)
-        uint64_t chunk_bytes = 64ull << 20;
+        uint64_t chunk_bytes = 128ull << 20;
         if (const char *e = getenv("MH_PB_CHUNK_MIB")) chunk_bytes = std::max(1, atoi(e)) * (1ull << 20);
         std::vector<uint64_t> cut{0};
         for (uint64_t i = 0; i < n;) {
@@ -885,11 +898,7 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
         const int nch = (int)cut.size() - 1;
         uint64_t max_nk = 0;
         for (int k = 0; k < nch; k++) max_nk = std::max(max_nk, cut[k + 1] - cut[k]);
-        while ((int)c->ev_chunks.size() < nch) {
-            hipEvent_t e;
-            MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->ev_chunks.push_back(e);
-        }
+        MH_HIP(ensure_chunk_events(c, nch));
         size_t scan_bytes = 0;
         MH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const uint64_t *)nullptr,
                                                 (uint64_t *)nullptr, (int)max_nk, st));
@@ -899,8 +908,8 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
         // per-chunk offset arrays hold n_k + 1 entries at [lo + k, hi + k]
         const uint64_t nc = n + (uint64_t)nch;
         const uint64_t b_msg = L.add(mb + 16), b_off = L.add((n + 1) * 8), b_src = L.add(n * 8),
-                       b_tgt = L.add(n * 8), b_x = L.add(2 * n * 32), b_cnt = L.add(3 * n * 8),
-                       b_io = L.add(nc * 8), b_co = L.add(nc * 8), b_mo = L.add(nc * 8),
+                       b_tgt = L.add(n * 8), b_xa = L.add(2 * n * 32), b_x = L.add(2 * n * 32),
+                       b_cnt = L.add(3 * n * 8), b_io = L.add(nc * 8), b_co = L.add(nc * 8), b_mo = L.add(nc * 8),
                        b_st = L.add(n * 4), b_scan = L.add(scan_bytes),
                        b_hd = L.add(2 * n * sizeof(mh_tx_header)), b_hh = L.add(2 * n * sizeof(mh_tx_header)),
                        b_md = L.add(2 * n * (uint64_t)kMdSlot), b_s = L.add(2 * n * kTxInnerStride),
@@ -913,51 +922,27 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
         DevBuf &tb = c->s_tree;
         MH_HIP(tb.ensure(std::max<uint64_t>(chunk_bytes / 34 + 64, 1) * 32));
         uint8_t *base = c->s_tx.as<uint8_t>();
-        // everything queued before this call on the compute stream (an
-        // earlier call's kernels reading these buffers) ends before the copies
-        MH_HIP(hipEventRecord(c->ev_done[0], st));
-        MH_HIP(hipStreamWaitEvent(cs, c->ev_done[0], 0));
-        std::mutex qm;
-        std::condition_variable qcv;
-        int issued = 0;
-        hipError_t copy_err = hipSuccess;
-        auto copier = [&]() {
-            hipError_t e = hipSetDevice(c->device);
-            for (int k = 0; k < nch && e == hipSuccess; k++) {
-                const uint64_t lo = cut[k], hi = cut[k + 1], nk = hi - lo;
-                const uint64_t b0 = msg_off[lo] - m0, bb = msg_off[hi] - msg_off[lo];
-                if (bb) e = hipMemcpyAsync(base + b_msg + b0, msgs + msg_off[lo], bb, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipMemcpyAsync(base + b_off + lo * 8, msg_off + lo, (nk + 1) * 8, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipMemcpyAsync(base + b_src + lo * 8, src + lo, nk * 8, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipMemcpyAsync(base + b_tgt + lo * 8, tgt + lo, nk * 8, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipMemcpyAsync(base + b_x + 2 * lo * 32, src_alh + lo * 32, nk * 32, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipMemcpyAsync(base + b_x + (2 * lo + nk) * 32, tgt_alh + lo * 32, nk * 32, hipMemcpyHostToDevice, cs);
-                if (!e) e = hipEventRecord(c->ev_chunks[k], cs);
-                std::lock_guard<std::mutex> g(qm);
-                if (e) copy_err = e;
-                else issued = k + 1;
-                qcv.notify_all();
-            }
-            std::lock_guard<std::mutex> g(qm);
-            if (e) copy_err = e;
-            issued = nch + (e ? 1 : 0);  // wake the consumer either way
-            qcv.notify_all();
-        };
-        std::thread th(copier);
-        struct Join {
-            std::thread &t;
-            ~Join() {
-                if (t.joinable()) t.join();
-            }
-        } join{th};
+        // the copies, one helper thread: chunk 0 = the per-message arrays
+        // whole (offsets, ids, Alh values: few large copies -- each copy call
+        // costs the DMA engine ~0.1 ms of setup) and the first messages, chunk
+        // k = its messages
+        ChunkCopier cc(c);
+        cc.chunks.resize(nch);
+        cc.chunks[0] = {{base + b_off, msg_off, (n + 1) * 8},
+                        {base + b_src, src, n * 8},
+                        {base + b_tgt, tgt, n * 8},
+                        {base + b_xa, src_alh, n * 32},
+                        {base + b_xa + n * 32, tgt_alh, n * 32}};
+        for (int k = 0; k < nch; k++) {
+            const uint64_t lo = cut[k], hi = cut[k + 1];
+            const uint64_t b0 = msg_off[lo] - m0, bb = msg_off[hi] - msg_off[lo];
+            cc.chunks[k].push_back({base + b_msg + b0, msgs + msg_off[lo], bb});
+        }
+        MH_HIP(cc.start());
         const uint8_t *dmsg = base + b_msg - m0;
         int32_t *dst_all = (int32_t *)(base + b_st);
         for (int k = 0; k < nch; k++) {
-            {
-                std::unique_lock<std::mutex> g(qm);
-                qcv.wait(g, [&] { return issued > k || copy_err != hipSuccess; });
-                if (copy_err) return -(int)copy_err;
-            }
+            MH_HIP(cc.wait(k));
             MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[k], 0));
             const uint64_t lo = cut[k], nk = cut[k + 1] - lo;
             const unsigned grid = (unsigned)((nk + 255) / 256);
@@ -981,10 +966,13 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
                                                         outs[q] + 1, (int)nk, st));
             }
             // the chunk's term totals size its term area: one small read-back
-            // (waits for this chunk only; later chunks keep copying)
-            uint64_t tot[2] = {0, 0};
-            MH_HIP(hipMemcpyAsync(&tot[0], io + nk, 8, hipMemcpyDeviceToHost, st));
-            MH_HIP(hipMemcpyAsync(&tot[1], co + nk, 8, hipMemcpyDeviceToHost, st));
+            // (waits for this chunk only; later chunks keep copying), stored
+            // by a kernel into pinned memory rather than copied by the DMA
+            // engine that is busy with the next chunks
+            volatile uint64_t *tot = c->p_small.as<volatile uint64_t>();
+            hipLaunchKernelGGL(k_put2_host, dim3(1), dim3(64), 0, st, io + nk, co + nk,
+                               (uint64_t *)c->p_small.p);
+            MH_HIP(hipGetLastError());
             MH_HIP(hipStreamSynchronize(st));
             MH_HIP(tb.ensure(std::max<uint64_t>(tot[0] + tot[1], 1) * 32));
             uint8_t *dti = tb.as<uint8_t>(), *dtc = dti + tot[0] * 32;
@@ -1003,6 +991,10 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
                     *ca = base + b_ca + lo * 32, *sel = base + b_sel + lo, *oki = base + b_oki + lo,
                     *okc = base + b_okc + lo;
             int32_t *ast = (int32_t *)(base + b_ast) + 2 * lo;
+            // the chunk's Alh values source-then-target, as the Alh kernel reads them
+            MH_HIP(hipMemcpyAsync(x, base + b_xa + lo * 32, nk * 32, hipMemcpyDeviceToDevice, st));
+            MH_HIP(hipMemcpyAsync(x + nk * 32, base + b_xa + (n + lo) * 32, nk * 32,
+                                  hipMemcpyDeviceToDevice, st));
             hipLaunchKernelGGL(k_dpv2_prep, dim3(grid), dim3(256), 0, st, nk, hd, dsrc, dtgt, dst, hh,
                                ii, ij, ci, sel, sbl, tbl);
             MH_HIP(hipGetLastError());
@@ -1019,6 +1011,7 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
                                oki, okc, dst);
             MH_HIP(hipGetLastError());
         }
+        MH_HIP(cc.join());
         MH_HIP(hipMemcpyAsync(status, dst_all, n * 4, hipMemcpyDeviceToHost, st));
         MH_HIP(hipStreamSynchronize(st));
         return MH_OK;

@@ -453,14 +453,97 @@ __global__ __launch_bounds__(256) void k_small_roots_wave(uint64_t ntrees,
     }
 }
 
+// The same roots for MANY small trees, level-parallel: a 256-thread
+// workgroup takes TPW = 512 / P consecutive trees (P = the widest tree rounded
+// up to a power of two, <= 64), their leaves in LDS at stride P, and hashes
+// every node of a level at once -- node j of tree k at level l on thread
+// k * (P >> l) + j, so level 1 keeps all 256 threads busy (for trees of the
+// widest width), each further level half as many -- double-buffered in LDS
+// (htree.go:85-110: pairs hashed, an odd last node promoted).  Against one
+// lane per tree (k_small_roots: w - 1 dependent node hashes on a lone wave
+// per SIMD) the work is the same but spread over 8x the waves.
+__global__ __launch_bounds__(256) void k_small_roots_pack(uint64_t ntrees,
+                                                          const uint64_t *__restrict__ leaf_off,
+                                                          const uint8_t *__restrict__ nodes,
+                                                          uint8_t *__restrict__ roots, int lgp) {
+    __shared__ uint32_t buf[2][512][9];  // +1 word pad: 2j / 2j+1 reads spread over the banks
+    const int P = 1 << lgp, TPW = 512 >> lgp;
+    const int tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TPW;
+    const uint64_t o0 = leaf_off[0];
+    for (int i = tid; i < TPW * P; i += 256) {
+        const int k = i >> lgp, j = i & (P - 1);
+        const uint64_t t = t0 + k;
+        if (t >= ntrees) continue;
+        const uint64_t lo = leaf_off[t], w = leaf_off[t + 1] - lo;
+        if ((uint64_t)j < w) {
+            uint32_t d[8];
+            load_digest(nodes + (lo - o0 + j) * 32, d);
+#pragma unroll
+            for (int q = 0; q < 8; q++) buf[0][i][q] = d[q];
+        }
+    }
+    int cur = 0;
+    for (int l = 1; l <= lgp; l++) {
+        __syncthreads();
+        const int S = P >> l;  // node slots per tree at level l
+        if (tid < TPW * S) {
+            const int k = tid / S, j = tid - k * S;
+            const uint64_t t = t0 + k;
+            if (t < ntrees) {
+                const uint64_t w = leaf_off[t + 1] - leaf_off[t];
+                const uint64_t wp = (w + (1ull << (l - 1)) - 1) >> (l - 1);  // width at level l-1
+                const int a = k * P + 2 * j;
+                if ((uint64_t)(2 * j + 1) < wp) {
+                    uint32_t x[8], y[8], h[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        x[q] = buf[cur][a][q];
+                        y[q] = buf[cur][a + 1][q];
+                    }
+                    node_hash_g(x, y, h);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) buf[cur ^ 1][k * P + j][q] = h[q];
+                } else if ((uint64_t)(2 * j) < wp) {  // odd last node: promoted
+#pragma unroll
+                    for (int q = 0; q < 8; q++) buf[cur ^ 1][k * P + j][q] = buf[cur][a][q];
+                }
+            }
+        }
+        cur ^= 1;
+    }
+    __syncthreads();
+    if (tid < TPW) {
+        const uint64_t t = t0 + tid;
+        if (t < ntrees) {
+            if (leaf_off[t + 1] == leaf_off[t]) {  // width 0: SHA256(nil), htree.go:73-77
+                reinterpret_cast<uint4 *>(roots + t * 32)[0] = reinterpret_cast<const uint4 *>(kEmptyRootDev)[0];
+                reinterpret_cast<uint4 *>(roots + t * 32)[1] = reinterpret_cast<const uint4 *>(kEmptyRootDev)[1];
+            } else {
+                uint32_t r[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) r[q] = buf[cur][tid * P][q];
+                store_digest(roots + t * 32, r);
+            }
+        }
+    }
+}
+
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
-                              uint8_t *nodes, uint8_t *roots) {
+                              uint8_t *nodes, uint8_t *roots, uint64_t wmax) {
     if (!ntrees) return hipSuccess;
     TimerScope ts(tm, "small_roots", st);
     if (ntrees <= 2048) {
         // few trees: latency-bound, a wave per tree
         hipLaunchKernelGGL(k_small_roots_wave, dim3(grid_for(ntrees, 4)), dim3(256), 0, st, ntrees,
                            leaf_off, nodes, roots);
+    } else if (wmax <= 64 && !getenv("MH_SMALL_ROOTS_LANE")) {
+        int lgp = 0;
+        while ((1ull << lgp) < wmax) lgp++;
+        lgp = std::max(lgp, 1);
+        const uint64_t tpw = 512 >> lgp;
+        hipLaunchKernelGGL(k_small_roots_pack, dim3(grid_for(ntrees, (unsigned)tpw)), dim3(256), 0,
+                           st, ntrees, leaf_off, nodes, roots, lgp);
     } else {
         hipLaunchKernelGGL(k_small_roots, dim3(grid_for(ntrees, 256)), dim3(256), kNodeTabBytes, st,
                            ntrees, leaf_off, nodes, roots);
