@@ -15,4 +15,4 @@ for ctrs in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs --output-format csv -d "$OUT/b$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench_workloads.py" --workload wire --steps 3 --warmup 1 > "$OUT/b$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/b$i.log"; exit 1; }
 done
-python3 "$GRAFT_REPO_ROOT/tools/pmc_table.py" pb_ $(find "$OUT" -name "*counter_collection.csv") > "$OUT/table.txt"
+python3 "$GRAFT_REPO_ROOT/tools/pmc_table.py" "${PMC_MATCH:-pb_}" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/table.txt"
