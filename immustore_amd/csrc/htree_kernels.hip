@@ -764,17 +764,18 @@ static int choose_lpl(uint64_t n) {
     return 1;
 }
 
-// Leaves from caller digests (one compression per leaf, no value blocks) keep
-// the round-1 rule: four leaves per lane from 2^20 up.  The two-per-lane
-// change above was measured on k_entries_fixed only; MH_DIGEST_LPL overrides.
+// Leaves from caller digests (one compression per leaf, no value blocks):
+// two per lane from 2^19 up, as for entries -- an A/B of the whole
+// mh_dev_htree_build_digests (profiles/ab_digest_lpl_r03.txt) gives 1.96 ms
+// (LPL 2) / 1.97 (4) / 2.04 (1) at 2^24 digests and 0.250-0.255 ms for all
+// three at 2^20 (the in-lane levels only move node hashes between the leaf
+// launch and the reduce).  MH_DIGEST_LPL overrides.
 static int choose_digest_lpl(uint64_t n) {
     if (const char *e = getenv("MH_DIGEST_LPL")) {
         int v = atoi(e);
         if (v == 1 || v == 2 || v == 4) return v;
     }
-    if (n >= (uint64_t)4 * 262144) return 4;
-    if (n >= (uint64_t)2 * 262144) return 2;
-    return 1;
+    return n >= (uint64_t)2 * 262144 ? 2 : 1;
 }
 
 bool entries_fixed_supported(int version, const uint8_t *keys, uint32_t key_len,
