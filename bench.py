@@ -84,7 +84,7 @@ def parse():
                    help="torch: one process per GPU over torch.distributed (driver default); "
                         "cabi: one process, mh_multi_* over N devices with the in-library "
                         "RCCL clique (the cgo caller's path)")
-    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r02.json"),
+    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r03.json"),
                    help="PMC-derived HBM bytes per launch of the dominant kernel (or missing)")
     return p.parse_args()
 
