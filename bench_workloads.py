@@ -206,7 +206,7 @@ def distributed_main(a):
 def make_parser():
     p = argparse.ArgumentParser()
     p.add_argument("--workload", choices=["c3", "c5", "c2e2e", "txlog", "commit", "wire", "ragged", "document",
-                                          "values"],
+                                          "values", "c3range"],
                    required=True)
     p.add_argument("--logs", action="store_true",
                    help="c3: also write the pLog / cLog appendable records (8(f) row 4)")
@@ -582,6 +582,54 @@ def values(a, m, N, L, ctx, dev, sync):
                                        "threads, SHA-NI=%s" % (ns, orc.has_shani())}}
 
 
+def c3range(a, m, N, L, ctx, dev, sync):
+    """syncBinaryLinking's replay (immustore.go:1198-1232) on one device:
+    a.m appends onto a tree of n0 = 10^6 + 3, (1) with the whole old dLog
+    resident (mh_dev_ahtree_append_batch) and (2) with only the old tree's
+    peaks on the device and the new digests in a buffer of their own
+    (mh_dev_ahtree_append_range, the form each device of the multi-GPU append
+    runs).  Both new dLog slices and last roots are compared."""
+    import numpy as np
+    import torch
+    from immustore_amd.multi import peaks_of
+    M, n0 = a.m, 10 ** 6 + 3
+    up = L.mh_ahtree_nodes_upto
+    pay = torch.empty((n0 + M) * 32, dtype=torch.uint8, device=dev)
+    N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 3))
+    full = torch.empty(up(n0 + M) * 32, dtype=torch.uint8, device=dev)
+    # the old tree (n0 appends), its peaks read back from the device dLog
+    N.check(L.mh_dev_ahtree_append_batch(ctx.handle, full.data_ptr(), 0, pay.data_ptr(), n0, 32, None))
+    sync()
+    pk = np.zeros(32 * bin(n0).count("1"), np.uint8)
+    N.check(L.mh_dev_ahtree_peaks(ctx.handle, full.data_ptr(), n0, pk.ctypes.data))
+    rng_buf = torch.empty((up(n0 + M) - up(n0)) * 32, dtype=torch.uint8, device=dev)
+    ro_a = torch.empty(M * 32, dtype=torch.uint8, device=dev)
+    ro_b = torch.empty(M * 32, dtype=torch.uint8, device=dev)
+    newp = pay[n0 * 32:]
+
+    def step_full():
+        N.check(L.mh_dev_ahtree_append_batch(ctx.handle, full.data_ptr(), n0, newp.data_ptr(), M,
+                                             32, ro_a.data_ptr()))
+
+    def step_range():
+        N.check(L.mh_dev_ahtree_append_range(ctx.handle, rng_buf.data_ptr(), n0, pk.ctypes.data,
+                                             newp.data_ptr(), M, 32, ro_b.data_ptr()))
+
+    prewarm(step_full, sync, a.prewarm)
+    res = {}
+    for name, st in (("full_dlog", step_full), ("range", step_range), ("full_dlog_2", step_full),
+                     ("range_2", step_range)):
+        t = timed(st, a.steps, a.warmup, sync)
+        res[name] = round(t * 1e3, 3)
+    same = bool(torch.equal(full[up(n0) * 32:], rng_buf) and torch.equal(ro_a, ro_b))
+    t = min(res["range"], res["range_2"]) * 1e-3
+    return {"metric": "ahtree replay append onto a tree of 10^6+3: 10^7 x 32 B payloads, one "
+                      "device, only the old peaks resident (mh_dev_ahtree_append_range)",
+            "value": round(M / t / 1e6, 1), "unit": "M appends/s", "ms": res,
+            "device_bytes": {"range": int(rng_buf.numel()), "full_dlog": int(full.numel())},
+            "identical_to_full_dlog_append": same}
+
+
 def run_single(a):
     """One GPU: run workload a.workload, return its result dict."""
     import numpy as np
@@ -911,6 +959,8 @@ def run_single(a):
         out = document(a, ctx)
     elif a.workload == "values":
         out = values(a, m, N, L, ctx, dev, sync)
+    elif a.workload == "c3range":
+        out = c3range(a, m, N, L, ctx, dev, sync)
     elif a.workload == "c2e2e":
         n, vlen, klen = 1 << 20, 1024, 8
         hv = torch.empty(n * vlen, dtype=torch.uint8).pin_memory()
