@@ -243,11 +243,21 @@ struct ChunkCopier {
     std::thread th[2];
     int lanes = 1;  // 1: one helper thread / copy stream; 2: two
 
+    bool started = false;
     explicit ChunkCopier(mh_ctx *ctx) : c(ctx) {}
-    ~ChunkCopier() { join(); }
+    // on every way out of the call: no copy may still read the caller's
+    // host memory once it returns (an error path skips the final sync)
+    ~ChunkCopier() {
+        join();
+        if (started) {
+            hipStreamSynchronize(c->copy_stream);
+            hipStreamSynchronize(c->copy_stream2);
+        }
+    }
     // chunks must be filled; events for every chunk must exist in c->ev_chunks
     hipError_t start() {
         done.assign(chunks.size(), 0);
+        started = true;
         if (hipError_t e = hipEventRecord(c->ev_done[0], c->stream)) return e;
         if (hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_done[0], 0)) return e;
         if (hipError_t e = hipStreamWaitEvent(c->copy_stream2, c->ev_done[0], 0)) return e;

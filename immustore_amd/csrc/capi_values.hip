@@ -69,6 +69,12 @@ extern "C" int mh_verify_values_batch(mh_ctx *c, uint64_t n, const uint8_t *vals
         uint8_t *d_hv = base + b_hv;
         int32_t *d_st = reinterpret_cast<int32_t *>(base + b_st);
         hipStream_t cs = c->copy_stream, st = c->stream;
+        // an error below may leave copies of the caller's values in flight:
+        // wait for them on every way out
+        struct CopyGuard {
+            hipStream_t s;
+            ~CopyGuard() { hipStreamSynchronize(s); }
+        } copy_guard{cs};
         MH_HIP(hipMemcpyAsync(d_off, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
         if (vlen) MH_HIP(hipMemcpyAsync(d_len, vlen, n * 8, hipMemcpyHostToDevice, st));
         MH_HIP(hipMemcpyAsync(d_hv, hvals, n * 32, hipMemcpyHostToDevice, st));
