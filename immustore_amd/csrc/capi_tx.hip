@@ -912,8 +912,11 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
             }
         out.R.insert(out.R.end(), o->R.begin(), o->R.begin() + take);
         if (want_headers) out.H.insert(out.H.end(), o->H.begin(), o->H.begin() + take);
-        if (take < o->R.size()) {         // max_txs reached inside this chunk
-            pos = out.R.back().alh + 32;
+        // max_txs reached inside or at the end of this chunk: the sequential
+        // parse stops before reading the next record, so whatever stopped this
+        // chunk's parse after it is not an error of the result
+        if (take < o->R.size() || out.R.size() == max_txs) {
+            if (take) pos = out.R.back().alh + 32;
             break;
         }
         pos = o->end;
@@ -922,7 +925,6 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
             out.stopped = true;
             break;
         }
-        if (out.R.size() == max_txs) break;
     }
     out.end = pos;
 }
@@ -1004,41 +1006,217 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             hipError_t e = cc.join();
             return e == hipSuccess ? MH_OK : -(int)e;
         };
+        const HopLimits lim{max_entries, max_key_len};
+        tr.mark("copies_started");
         // ---- host hop (tx.go:419-603): record structure and limits only.  Per
         // entry the host reads the two lengths it needs to find the next entry
         // (several threads over a long log, hop_all); the per-entry index (record
         // offsets, versions, message lengths) is rebuilt on the device from each
         // tx's first entry (k_txe_index).
+        //
+        // With two copy chunks the hop runs in two phases to match them: the
+        // records wholly inside the first chunk first (a record crossing its
+        // end reads as truncated there and is parsed again by the second
+        // phase), and their device work is queued at once -- it starts as
+        // soon as that chunk lands, under the copy of the rest and the second
+        // phase of the hop.  The result is the sequential parse's either way.
+        //
+        // With two copy chunks the hop runs in two phases to match them: first
+        // the records wholly inside the first chunk (a record crossing its end
+        // reads as truncated there and is parsed again by the second phase),
+        // whose device work is queued at once -- it starts as soon as that
+        // chunk lands, under the copy of the rest and the second phase.  The
+        // records and the return code are the one-pass parse's either way
+        // (every check of hop_record reads only bytes it has bounds-checked).
         HopOut hop;
-        tr.mark("copies_started");
-        hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, hop, false);
-        tr.mark("hop");
+        uint64_t nA = 0, eA = 0;  // records / entries of the early group
+        const bool phases = nck == 2 && len <= 0xffffffffull;
+        // device layout: per entry record offset, version, leaf digest; per tx
+        // header, entry-count word, record offset, Alh offset, leaf offset,
+        // Eh, inner-hash scratch, Alh, status.  Record / Alh / leaf offsets are
+        // staged in pinned memory (pro | pap | plo, ntx_cap + 1 each).
+        Layout L;
+        uint64_t b_rec = 0, b_ver = 0, b_lv = 0, b_h = 0, b_es = 0, b_ro = 0, b_ap = 0, b_lo = 0,
+                 b_eh = 0, b_s = 0, b_a = 0, b_st = 0, ntx_cap = 0, E_cap = 0, idx_bytes = 0;
+        uint8_t *base = nullptr;
+        uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
+        auto alloc = [&](uint64_t nt, uint64_t ne) -> int {
+            ntx_cap = nt;
+            E_cap = ne;
+            L = Layout();
+            b_rec = L.add(ne * 8);
+            b_ver = L.add(ne);
+            b_lv = L.add(std::max<uint64_t>(ne, 1) * 32);
+            b_h = L.add(nt * sizeof(mh_tx_header));
+            b_es = L.add(nt * 8);
+            b_ro = L.add(nt * 8);
+            b_ap = L.add(nt * 8);
+            b_lo = L.add((nt + 1) * 8);
+            b_eh = L.add(nt * 32);
+            b_s = L.add(nt * kTxInnerStride);
+            b_a = L.add(nt * 32);
+            b_st = L.add(nt * 4);
+            MH_HIP(c->s_tx.ensure(L.total));
+            base = c->s_tx.as<uint8_t>();
+            idx_bytes = 3 * (nt + 1) * 8;
+            MH_HIP(c->p_tx.ensure(idx_bytes));
+            pro = c->p_tx.as<uint64_t>();
+            pap = pro + (nt + 1);
+            plo = pap + (nt + 1);
+            return MH_OK;
+        };
+        // ---- the device work of records R[t0, t1) (entries from e0), reading
+        // the log at db: index arrays up, headers, per-entry index (tx.go:578-585),
+        // entry digests hashed in place from the raw entry records (tx.go:690-731),
+        // one htree per tx (tx.go:617-621; small trees one lane / wave per tree,
+        // a batch with a wide tx through the host tree plan), Alh with the
+        // rebuilt Eh vs the stored one (tx.go:623-627); outputs down on ds
+        auto group = [&](uint64_t t0, uint64_t t1, uint64_t e0, const uint8_t *db, hipStream_t ds,
+                         const uint64_t *pl, uint64_t npe, uint64_t nph) -> int {
+            const uint64_t nt = t1 - t0;
+            uint64_t acc = e0, wmax = 0;
+            for (uint64_t k = t0; k < t1; k++) {
+                pro[k] = hop.R[k].rec;
+                pap[k] = hop.R[k].alh;
+                plo[k] = acc;
+                acc += hop.R[k].nent;
+                wmax = std::max<uint64_t>(wmax, hop.R[k].nent);
+            }
+            plo[t1] = acc;
+            const uint64_t eg = acc - e0;
+            const bool small = small_roots_fit(nt, wmax);
+            TreePlan P;
+            if (!small) {
+                std::vector<uint64_t> lof(nt + 1);
+                for (uint64_t k = 0; k <= nt; k++) lof[k] = plo[t0 + k] - e0;
+                P.build(nt, lof.data());
+                const uint64_t need = idx_bytes + plan_index_bytes(P, nt);
+                if (c->p_tx.cap < need) {
+                    // p_tx moves: an earlier group's staging must be consumed first
+                    MH_HIP(hipStreamSynchronize(st));
+                    std::vector<uint64_t> keep(pro, pro + 3 * (ntx_cap + 1));
+                    MH_HIP(c->p_tx.ensure(need));
+                    pro = c->p_tx.as<uint64_t>();
+                    pap = pro + (ntx_cap + 1);
+                    plo = pap + (ntx_cap + 1);
+                    memcpy(pro, keep.data(), keep.size() * 8);
+                }
+            }
+            MH_HIP(hipMemcpyAsync(base + b_ro + t0 * 8, pro + t0, nt * 8, hipMemcpyHostToDevice, st));
+            MH_HIP(hipMemcpyAsync(base + b_ap + t0 * 8, pap + t0, nt * 8, hipMemcpyHostToDevice, st));
+            MH_HIP(hipMemcpyAsync(base + b_lo + t0 * 8, plo + t0, (nt + 1) * 8,
+                                  hipMemcpyHostToDevice, st));
+            const uint64_t *ro = (const uint64_t *)(base + b_ro) + t0;
+            const uint64_t *lo = (const uint64_t *)(base + b_lo) + t0;
+            MhTxHeader *hd = (MhTxHeader *)(base + b_h) + t0;
+            uint64_t *es = (uint64_t *)(base + b_es) + t0;
+            MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, db, ro, hd, es));
+            MH_HIP(launch_txe_index(st, c->tm(), nt, db, hd, es, lo, (uint64_t *)(base + b_rec),
+                                    base + b_ver));
+            if (npe + nph)
+                MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
+                                          pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
+            MH_HIP(launch_txe_leaf(st, c->tm(), eg, db, (const uint64_t *)(base + b_rec) + e0,
+                                   base + b_ver + e0, small, base + b_lv + e0 * 32));
+            if (small) {
+                MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + b_lv + e0 * 32,
+                                          base + b_eh + t0 * 32, wmax));
+            } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, nt, eg, base + b_lv + e0 * 32,
+                                                base + b_eh + t0 * 32,
+                                                reinterpret_cast<uint8_t *>(pro) + idx_bytes)) {
+                return e;
+            }
+            MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, db, base + b_eh + t0 * 32,
+                                 base + b_s + t0 * kTxInnerStride, db,
+                                 (const uint64_t *)(base + b_ap) + t0, nullptr, base + b_a + t0 * 32,
+                                 (int32_t *)(base + b_st) + t0));
+            if (hdrs_out)  // the device headers with the rebuilt Eh
+                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
+            if (ds != st) {
+                MH_HIP(hipEventRecord(c->ev_done[1], st));
+                MH_HIP(hipStreamWaitEvent(ds, c->ev_done[1], 0));
+            }
+            if (status_out)
+                MH_HIP(hipMemcpyAsync(status_out + t0, base + b_st + t0 * 4, nt * 4,
+                                      hipMemcpyDeviceToHost, ds));
+            if (alh_out)
+                MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, base + b_a + t0 * 32, nt * 32,
+                                      hipMemcpyDeviceToHost, ds));
+            if (hdrs_out)
+                MH_HIP(hipMemcpyAsync(hdrs_out + t0, hd, nt * sizeof(mh_tx_header),
+                                      hipMemcpyDeviceToHost, ds));
+            return MH_OK;
+        };
+        if (phases) {
+            hop_all(buf, chunk, max_txs, lim, hop, false);
+            tr.mark("hop1");
+            nA = hop.R.size();
+            uint64_t w1 = 0;
+            for (const HopRec &r : hop.R) {
+                eA += r.nent;
+                w1 = std::max<uint64_t>(w1, r.nent);
+            }
+            const bool more = nA < max_txs && (hop.rc == MH_ERR_TRUNCATED ||
+                                               (hop.rc == MH_OK && hop.end + 8 > chunk));
+            // the early group: small trees, nothing to patch, and more to come
+            if (more && nA && hop.P.empty() && small_roots_fit(nA, w1)) {
+                // sized for the most records / entries the log can hold (a
+                // record is >= 124 bytes, an entry >= 48)
+                if (int e = alloc(std::min<uint64_t>(max_txs, len / 124 + 1), len / 48 + 1)) return e;
+                if (hipError_t e = cc.wait(0)) return -(int)e;
+                MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[0], 0));
+                if (int e = group(0, nA, 0, dbuf, c->d2h_stream, nullptr, 0, 0)) return e;
+                tr.mark("group_a");
+            } else {
+                nA = eA = 0;
+            }
+            if (more) {
+                const uint64_t p2 = hop.end, r0 = hop.R.size();
+                HopOut h2;
+                hop_all(buf + p2, len - p2, max_txs - r0, lim, h2, false);
+                for (const HopRec &r : h2.R) hop.R.push_back(HopRec{r.rec + p2, r.alh + p2, r.nent, 0});
+                for (HopPatch &pt : h2.P) {
+                    pt.rec += r0;
+                    hop.P.push_back(std::move(pt));
+                }
+                hop.rc = h2.rc;
+                hop.end = p2 + h2.end;
+                tr.mark("hop2");
+            }
+        } else {
+            hop_all(buf, len, max_txs, lim, hop, false);
+            tr.mark("hop");
+        }
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
         // on an error hop.end is the failing record's offset = the end of the last good one
         if (ntx_out) *ntx_out = ntx;
         if (consumed_out) *consumed_out = hop.end;
+        if (int e = join_copies()) return e;
+        tr.mark("joined");
         if (!ntx) {
-            if (int e = join_copies()) return e;
             // buf stays the caller's once we return
             MH_HIP(hipStreamSynchronize(c->copy_stream));
             MH_HIP(hipStreamSynchronize(c->copy_stream2));
             return rc;
         }
-        uint64_t E = 0, wmax = 0;
-        for (const HopRec &r : hop.R) {
-            E += r.nent;
-            wmax = std::max<uint64_t>(wmax, r.nent);
+        if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));  // the whole log in
+        uint64_t E = 0;
+        for (const HopRec &r : hop.R) E += r.nent;
+        if (nA) {
+            if (ntx > ntx_cap || E > E_cap) return MH_ERR_ILLEGAL_STATE;  // cannot happen: bounds
+        } else if (int e = alloc(ntx, E)) {
+            return e;
         }
         // ---- metadata that parses but is not in canonical form (a log not
         // written by immudb): Go hashes KVMetadata.Bytes() / TxMetadata.Bytes(),
         // so the canonical entry records / tx metadata go after the log bytes
-        // on the device and the entry index / headers point at them.
-        std::vector<uint64_t> patch;  // [ne idx][ne off][nh idx][nh off | len << 32]
+        // in a copy of the log on the device, and the entry index / headers
+        // point at them.  (The early group never has any.)
+        const uint8_t *db = dbuf;
+        const uint64_t *pl = nullptr;
         uint64_t npe = 0, nph = 0;
         if (!hop.P.empty()) {
-            if (int e = join_copies()) return e;
-            if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));  // whole log in
             std::vector<uint64_t> first_leaf(ntx);
             for (uint64_t k = 0, acc = 0; k < ntx; k++) {
                 first_leaf[k] = acc;
@@ -1052,7 +1230,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             if (len + side > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
             std::vector<uint8_t> sbuf;
             sbuf.reserve(side);
-            patch.resize(2 * (npe + nph));
+            std::vector<uint64_t> patch(2 * (npe + nph));  // [ne idx][ne off][nh idx][nh off | len << 32]
             uint64_t ie = 0, ih = 0;
             for (const HopPatch &pt : hop.P) {
                 const uint64_t off = len + sbuf.size();
@@ -1065,142 +1243,22 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 }
                 sbuf.insert(sbuf.end(), pt.bytes.begin(), pt.bytes.end());
             }
-            MH_HIP(c->s_txpatch.ensure(len + side + patch.size() * 8));
+            const uint64_t po = (len + side + 7) & ~7ull;
+            MH_HIP(c->s_txpatch.ensure(po + patch.size() * 8));
             uint8_t *nb = c->s_txpatch.as<uint8_t>();
             MH_HIP(hipMemcpyAsync(nb, dbuf, len, hipMemcpyDeviceToDevice, st));
             MH_HIP(hipMemcpyAsync(nb + len, sbuf.data(), side, hipMemcpyHostToDevice, st));
-            MH_HIP(hipMemcpyAsync(nb + ((len + side + 7) & ~7ull), patch.data(), patch.size() * 8,
-                                  hipMemcpyHostToDevice, st));
+            MH_HIP(hipMemcpyAsync(nb + po, patch.data(), patch.size() * 8, hipMemcpyHostToDevice, st));
             MH_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
-            dbuf = nb;
-            patch.assign(1, (len + side + 7) & ~7ull);  // device offset of the patch lists
+            db = nb;
+            pl = reinterpret_cast<const uint64_t *>(nb + po);
         }
-        // ---- device: headers, entry index, digests, trees, Alh
-        // small trees (every tx here: a handful of entries) get their roots one
-        // lane per tree; a batch with a wide tx goes through the host tree plan
-        const bool small = small_roots_fit(ntx, wmax);
-        Layout L;
-        const uint64_t b_rec = L.add(E * 8), b_ver = L.add(E),
-                       b_lv = L.add(std::max<uint64_t>(E, 1) * 32),
-                       b_h = L.add(ntx * sizeof(mh_tx_header)), b_es = L.add(ntx * 8),
-                       b_ro = L.add(ntx * 8), b_ap = L.add(ntx * 8), b_lo = L.add((ntx + 1) * 8),
-                       b_eh = L.add(ntx * 32), b_s = L.add(ntx * kTxInnerStride), b_a = L.add(ntx * 32),
-                       b_st = L.add(ntx * 4);
-        MH_HIP(c->s_tx.ensure(L.total));
-        uint8_t *base = c->s_tx.as<uint8_t>();
-        // record offsets, Alh positions and leaf offsets are contiguous in the
-        // device layout: written once into pinned staging, one DMA
-        const uint64_t idx_bytes = b_lo + (ntx + 1) * 8 - b_ro;
-        std::vector<uint64_t> leaf_off;
-        TreePlan P;
-        if (!small) {
-            leaf_off.resize(ntx + 1);
-            leaf_off[0] = 0;
-            for (uint64_t k = 0; k < ntx; k++) leaf_off[k + 1] = leaf_off[k] + hop.R[k].nent;
-            P.build(ntx, leaf_off.data());
-        }
-        const uint64_t pin_bytes = idx_bytes + (small ? 0 : plan_index_bytes(P, ntx));
-        MH_HIP(c->p_tx.ensure(pin_bytes));
-        uint8_t *pin = c->p_tx.as<uint8_t>();
-        {
-            uint64_t *ro = reinterpret_cast<uint64_t *>(pin);
-            uint64_t *ap = reinterpret_cast<uint64_t *>(pin + (b_ap - b_ro));
-            uint64_t *lo = reinterpret_cast<uint64_t *>(pin + (b_lo - b_ro));
-            uint64_t acc = 0;
-            for (uint64_t k = 0; k < ntx; k++) {
-                ro[k] = hop.R[k].rec;
-                ap[k] = hop.R[k].alh;
-                lo[k] = acc;
-                acc += hop.R[k].nent;
-            }
-            lo[ntx] = acc;
-        }
-        MH_HIP(hipMemcpyAsync(base + b_ro, pin, idx_bytes, hipMemcpyHostToDevice, st));
-        // Two groups of txs when every tree is small and nothing is patched:
-        // the records inside the first copy chunk (their kernels and outputs
-        // go as soon as that chunk lands, under the copy of the rest), then
-        // the others after the last chunk.  Otherwise one group after the copy.
-        uint64_t split = ntx;
-        if (small && !(npe + nph) && nck == 2) {
-            split = 0;
-            while (split < ntx && hop.R[split].alh + 32 <= chunk) split++;
-        }
-        const uint64_t groups[3] = {0, split, ntx};
-        for (int g = 0; g < 2; g++) {
-            const uint64_t t0 = groups[g], t1 = groups[g + 1], nt = t1 - t0;
-            if (!nt) continue;
-            // the first group of a split reads only the first chunk
-            if (t1 == ntx) {
-                if (int e = join_copies()) return e;
-                tr.mark("joined");
-                if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
-            } else {
-                if (hipError_t e = cc.wait(0)) return -(int)e;
-                tr.mark("chunk0_issued");
-                MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[0], 0));
-            }
-            const uint64_t *ro = (const uint64_t *)(base + b_ro) + t0;
-            const uint64_t *lo = (const uint64_t *)(base + b_lo) + t0;
-            MhTxHeader *hd = (MhTxHeader *)(base + b_h) + t0;
-            const uint64_t *es = (const uint64_t *)(base + b_es) + t0;
-            const uint64_t e0 = (g == 0) ? 0 : [&] {
-                uint64_t a = 0;
-                for (uint64_t k = 0; k < t0; k++) a += hop.R[k].nent;
-                return a;
-            }();
-            uint64_t eg = 0;
-            for (uint64_t k = t0; k < t1; k++) eg += hop.R[k].nent;
-            MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, dbuf, ro, hd, (uint64_t *)es));
-            // per-entry index, then entry digests hashed in place from the raw
-            // entry records (tx.go:578-585 -> 690-731); small trees take the
-            // leaves straight away (htree.go:79-83)
-            MH_HIP(launch_txe_index(st, c->tm(), nt, dbuf, hd, es, lo, (uint64_t *)(base + b_rec),
-                                    base + b_ver));
-            if (npe + nph) {
-                const uint64_t *pl = reinterpret_cast<const uint64_t *>(dbuf + patch[0]);
-                MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
-                                          pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
-            }
-            MH_HIP(launch_txe_leaf(st, c->tm(), eg, dbuf, (const uint64_t *)(base + b_rec) + e0,
-                                   base + b_ver + e0, small, base + b_lv + e0 * 32));
-            // one htree per tx (tx.go:617-621)
-            if (small) {
-                MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + b_lv + e0 * 32,
-                                          base + b_eh + t0 * 32, wmax));
-            } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, ntx, E, base + b_lv,
-                                                base + b_eh, pin + idx_bytes)) {
-                return e;
-            }
-            // Alh with the rebuilt Eh vs the stored one (tx.go:623-627)
-            MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, dbuf, base + b_eh + t0 * 32,
-                                 base + b_s + t0 * kTxInnerStride, dbuf,
-                                 (const uint64_t *)(base + b_ap) + t0, nullptr, base + b_a + t0 * 32,
-                                 (int32_t *)(base + b_st) + t0));
-            if (hdrs_out)  // the device headers with the rebuilt Eh
-                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
-            // the first group's results go down on their own stream while
-            // the second group's kernels run
-            hipStream_t ds = st;
-            if (t1 < ntx) {
-                ds = c->d2h_stream;
-                MH_HIP(hipEventRecord(c->ev_done[1], st));
-                MH_HIP(hipStreamWaitEvent(ds, c->ev_done[1], 0));
-            }
-            if (status_out)
-                MH_HIP(hipMemcpyAsync(status_out + t0, base + b_st + t0 * 4, nt * 4,
-                                      hipMemcpyDeviceToHost, ds));
-            if (alh_out)
-                MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, base + b_a + t0 * 32, nt * 32,
-                                      hipMemcpyDeviceToHost, ds));
-            if (hdrs_out)
-                MH_HIP(hipMemcpyAsync(hdrs_out + t0, hd, nt * sizeof(mh_tx_header),
-                                      hipMemcpyDeviceToHost, ds));
-        }
+        if (int e = group(nA, ntx, eA, db, st, pl, npe, nph)) return e;
         tr.mark("enqueued");
-        if (split < ntx) MH_HIP(hipStreamSynchronize(c->d2h_stream));
-        tr.mark("d2h_a_done");
+        if (nA) MH_HIP(hipStreamSynchronize(c->d2h_stream));
         MH_HIP(hipStreamSynchronize(st));
         tr.mark("done");
         return rc;
     });
 }
+

@@ -204,6 +204,50 @@ def test_txlog_validate_parallel_hop(m, ctx, orc):
     same(raw, max_txs=4321)
 
 
+def test_txlog_validate_two_phase_split(m, ctx, orc):
+    """From 16 MiB the log goes up in two copy chunks and the hop runs in two
+    phases (the records inside the first chunk are validated while the rest
+    is parsed): errors on either side of the split and in the record that
+    straddles it, max_txs at the split, non-canonical metadata (patched
+    records) and wide txs (tree plan) before or after it -- all equal the
+    one-pass oracle."""
+    from tx_util import metadata_logs
+    rng = np.random.default_rng(5)
+    raw, starts = _bulk_txlog(rng, 9000)
+    assert len(raw) >= (16 << 20)
+
+    def same(buf, **kw):
+        a = m.txlog_validate(buf, ctx=ctx, **kw)
+        b = orc.txlog_validate(buf, **kw)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]), kw
+        assert list(a[5]) == list(b[4]) and np.array_equal(a[4], b[3]), kw
+        return a
+
+    chunk = (len(raw) // 4 * 3) & ~4095
+    j = max(k for k in range(len(starts)) if starts[k] < chunk)  # straddles the split
+    for k in (j - 1, j, j + 1):
+        bad = bytearray(raw)
+        bad[starts[k] + 89] = 7  # unknown header version
+        a = same(bytes(bad))
+        assert (a[0], a[1], a[2]) == (17, k, starts[k])
+    bad = bytearray(raw)  # hVal of the straddling record's last entry
+    bad[starts[j + 1] - 33] ^= 1
+    same(bytes(bad))
+    for mt in (j - 1, j, j + 1):
+        a = same(raw, max_txs=mt)
+        assert a[1] == mt
+    same(raw[:chunk + 5])
+    same(raw[:starts[j + 1]] + bytes(len(raw) - starts[j + 1]))
+    # patched records after the split only / before it only
+    md = b"".join(r for name, r in metadata_logs(orc) if name == "noncanonical_sealed_canonical")
+    same(raw + md * 50)
+    same(md * 50 + raw)
+    # wide txs after the split only / before it only
+    wide = _synthetic_txlog(rng, 20, orc, max_entries=300)
+    same(raw + wide)
+    same(wide + raw)
+
+
 def test_dual_proof_v2_fixture_cases(m, ctx, orc, fixtures):
     seen = set()
     for name, fx in fixtures.items():

@@ -67,6 +67,16 @@ def test_scan_parallel_hop_matches_sequential(txl, orc):
     same(txl, orc, raw[:starts[5000]] + bytes(3 << 20))
     for mt in (1, 4321, 8999, 9000, 10 ** 6):
         same(txl, orc, raw, max_txs=mt)
+    # max_txs reached right before a structural error / a cut: the sequential
+    # parse never reads the bad record (the merge once reported the error of
+    # the hop chunk that holds it)
+    bad = bytearray(raw)
+    bad[starts[4444] + 89] = 9
+    for mt in (4443, 4444, 4445):
+        a = same(txl, orc, bytes(bad), max_txs=mt)
+        assert a[0] == (0 if mt <= 4444 else 17)
+    for cut in range(starts[6000] + 1, starts[6000] + 100, 33):
+        same(txl, orc, raw[:cut], max_txs=6000)
     # records that span whole hop chunks: 3 txs of 90 000 entries (~4.6 MB each)
     import struct
     recs = bytearray()
