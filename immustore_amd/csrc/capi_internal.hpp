@@ -3,6 +3,7 @@
 #pragma once
 #include <algorithm>
 #include <condition_variable>
+#include <deque>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -184,6 +185,10 @@ struct mh_ctx {
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
+    // mh_txlog_validate's groups (one per copy chunk): device arrays and
+    // pinned index staging of each, kept across calls
+    std::deque<DevBuf> s_txg;
+    std::deque<PinBuf> p_txg;
     PinBuf p_stage;       // host-built arrays of one call, staged for a single upload
     PinBuf p_small;       // a few words a kernel stores straight into host memory
     // second stream for host->device copies that overlap the compute stream
@@ -242,6 +247,7 @@ struct ChunkCopier {
     hipError_t err = hipSuccess;
     std::thread th[2];
     int lanes = 1;  // 1: one helper thread / copy stream; 2: two
+    bool inline_issue = false;  // issue every copy from the caller (pinned sources: no blocking)
 
     bool started = false;
     explicit ChunkCopier(mh_ctx *ctx) : c(ctx) {}
@@ -279,7 +285,7 @@ struct ChunkCopier {
                     cv.notify_all();
                 }
             };
-            if (chunks.size() <= 1) {  // one chunk: no thread worth starting
+            if (chunks.size() <= 1 || inline_issue) {  // no thread worth starting
                 lane();
                 continue;
             }
@@ -296,6 +302,11 @@ struct ChunkCopier {
         std::unique_lock<std::mutex> g(m);
         cv.wait(g, [&] { return done[k] || err != hipSuccess; });
         return err;
+    }
+    // chunk k's copies and event are enqueued already (no waiting)
+    bool issued(size_t k) {
+        std::lock_guard<std::mutex> g(m);
+        return done[k] || err != hipSuccess;
     }
     // chunks [0, result) are enqueued AND complete on the device now
     size_t arrived() {

@@ -7,6 +7,7 @@
 // / htree_kernels.hip.
 #include <cstring>
 #include <cstdlib>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -851,7 +852,83 @@ uint64_t find_record_start(const uint8_t *buf, uint64_t len, uint64_t from, uint
     return ~0ull;
 }
 
-// The whole hop: one thread below 8 MiB, else up to 8 threads parse chunks
+// Parked helper threads for the hop (started on first use, kept for the life
+// of the process: a validation call runs the hop twice, and starting 15
+// threads each time cost about as much as the hop over a quarter of the log).
+// run(T, fn) calls fn(k) for k in [0, T): the caller takes tasks too, so a
+// pool that could not start threads still finishes.  One run at a time; a
+// concurrent caller (another context's hop) gets busy() and starts its own
+// threads instead.
+class HopPool {
+  public:
+    static HopPool &get() {
+        static HopPool *p = new HopPool();  // never destroyed: its threads stay parked
+        return *p;
+    }
+    bool try_run(unsigned T, const std::function<void(unsigned)> &fn) {
+        std::unique_lock<std::mutex> call(call_mu, std::try_to_lock);
+        if (!call.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            try {
+                while (th.size() + 1 < T) {
+                    th.emplace_back([this] { loop(); });
+                    th.back().detach();
+                }
+            } catch (...) {  // fewer threads: the caller takes more tasks
+            }
+            job = &fn;
+            next = 0;
+            total = T;
+            finished = 0;
+            failed = false;
+        }
+        cv_go.notify_all();
+        take();
+        std::unique_lock<std::mutex> lk(mu);
+        cv_done.wait(lk, [&] { return finished == total; });
+        job = nullptr;
+        if (failed) throw std::bad_alloc();
+        return true;
+    }
+
+  private:
+    std::mutex call_mu, mu;
+    std::condition_variable cv_go, cv_done;
+    std::vector<std::thread> th;
+    const std::function<void(unsigned)> *job = nullptr;
+    unsigned next = 0, total = 0, finished = 0;
+    bool failed = false;
+    // take tasks until none are left (caller and helpers alike)
+    void take() {
+        std::unique_lock<std::mutex> lk(mu);
+        while (job && next < total) {
+            const unsigned k = next++;
+            const std::function<void(unsigned)> *f = job;
+            lk.unlock();
+            bool ok = true;
+            try {
+                (*f)(k);
+            } catch (...) {
+                ok = false;
+            }
+            lk.lock();
+            failed |= !ok;
+            if (++finished == total) cv_done.notify_all();
+        }
+    }
+    void loop() {
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_go.wait(lk, [&] { return job && next < total; });
+            }
+            take();
+        }
+    }
+};
+
+// The whole hop: one thread below 1 MiB, else up to 16 threads parse chunks
 // from speculated record starts; chunks whose start does not match the
 // previous chunk's end are re-parsed sequentially, so the result is always
 // the sequential parse's.
@@ -866,7 +943,10 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
         return (unsigned)std::min(64l, std::max(1l, v));
     }();
     unsigned T = std::min(kHopThreads, std::max(1u, std::thread::hardware_concurrency()));
-    if (len < (8ull << 20)) T = 1;
+    // at least 512 KiB per thread (the threads are parked, not started per
+    // call: a validation call hops each copy chunk separately, the smallest a
+    // few MiB)
+    T = (unsigned)std::min<uint64_t>(T, std::max<uint64_t>(1, len >> 19));
     if (T == 1) {
         hop_range(buf, len, 0, ~0ull, max_txs, lim, out);
         return;
@@ -876,7 +956,7 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
     cut[T] = ~0ull;
     std::vector<HopOut> part(T);
     for (auto &pt : part) pt.want_headers = want_headers;
-    auto work = [&](unsigned k) {
+    const std::function<void(unsigned)> work = [&](unsigned k) {
         const uint64_t s = k ? find_record_start(buf, len, cut[k], std::min(cut[k + 1], len), lim) : 0;
         if (s == ~0ull) {
             part[k].start = ~0ull;
@@ -884,15 +964,17 @@ void hop_all(const uint8_t *buf, uint64_t len, uint64_t max_txs, const HopLimits
         }
         hop_range(buf, len, s, cut[k + 1], max_txs, lim, part[k]);
     };
-    std::vector<std::thread> th;
-    unsigned started = 0;
-    try {  // no thread (resource limits): the remaining chunks run on this one
-        for (; started + 1 < T; started++) th.emplace_back(work, started + 1);
-    } catch (...) {
+    if (!HopPool::get().try_run(T, work)) {
+        std::vector<std::thread> th;
+        unsigned started = 0;
+        try {  // no thread (resource limits): the remaining chunks run on this one
+            for (; started + 1 < T; started++) th.emplace_back(work, started + 1);
+        } catch (...) {
+        }
+        work(0);
+        for (unsigned k = started + 1; k < T; k++) work(k);
+        for (auto &t : th) t.join();
     }
-    work(0);
-    for (unsigned k = started + 1; k < T; k++) work(k);
-    for (auto &t : th) t.join();
     uint64_t pos = 0;
     out.start = 0;
     for (unsigned k = 0; k < T; k++) {
@@ -951,6 +1033,37 @@ extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entr
     });
 }
 
+// The device address of [p, p + bytes) when the whole range is pinned host
+// memory the kernels can store to (one registration or allocation, word
+// aligned), else null.  MH_TXLOG_KERNEL_STORES=0 turns the path off.
+static uint32_t *host_words(void *p, uint64_t bytes) {
+    static const bool on = [] {
+        const char *e = getenv("MH_TXLOG_KERNEL_STORES");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || !p || !bytes || ((uintptr_t)p & 3) || (bytes & 3)) return nullptr;
+    hipPointerAttribute_t a, b;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess ||
+        hipPointerGetAttributes(&b, (uint8_t *)p + bytes - 1) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || b.type != hipMemoryTypeHost || !a.devicePointer ||
+        (uint8_t *)b.devicePointer - (uint8_t *)a.devicePointer != (ptrdiff_t)(bytes - 1))
+        return nullptr;
+    return (uint32_t *)a.devicePointer;
+}
+
+// copy chunks of a long tx log: MH_TXLOG_CHUNKS (1..16, read once), default 4
+static uint64_t txlog_chunks() {
+    static const uint64_t k = [] {
+        const char *e = getenv("MH_TXLOG_CHUNKS");
+        const long v = e ? strtol(e, nullptr, 10) : 4;
+        return (uint64_t)std::min(16l, std::max(1l, v));
+    }();
+    return k;
+}
+
 // MH_TXLOG_TRACE=1: host timestamps of the call's phases on stderr (A/B
 // measurements of the copy / hop / device overlap)
 namespace {
@@ -978,214 +1091,278 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
         PhaseTrace tr;
-        // The raw records go to the device first, in chunks of 8 MiB with an
-        // event after each: the copy (DMA when buf is pinned) runs under the
-        // host hop below, and the device work on the records whose bytes have
-        // already arrived starts before the last chunks land.
+        // The raw records go to the device first, in chunks with an event
+        // after each: the copy (DMA when buf is pinned) runs under the host
+        // hop, and the device work on the records of a chunk starts as soon as
+        // it has landed, under the copy of the rest.
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
         hipStream_t st = c->stream;
         MH_HIP(c->copy_lane());
         if (len) MH_HIP(c->s_txlog.ensure(len));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
-        // two chunks from 16 MiB up: the first three quarters, then the rest
-        // (every extra copy call costs ~0.1 ms of DMA setup, so no more);
-        // the copies run under the host hop on a helper thread (ChunkCopier),
-        // which joins on every way out (they read the caller's buf)
-        const uint64_t chunk = len >= (16ull << 20) ? ((len / 4 * 3) & ~4095ull) : len;
-        const uint64_t nck = len ? (chunk < len ? 2 : 1) : 0;
-        MH_HIP(ensure_chunk_events(c, nck));
+        // A pinned log: K chunks from 16 MiB up (MH_TXLOG_CHUNKS, default 4)
+        // of decreasing size, K : K-1 : ... : 1 (the last chunk's device work
+        // is the tail after the copy), all queued from this thread at once.  A
+        // pageable one is staged by the runtime inside each copy call, so a
+        // helper thread (ChunkCopier) issues those under the hop, in two
+        // chunks (3/4 + 1/4: every staged call has its own setup).  Events
+        // ev_chunks[0, K) mark the chunks' arrival, ev_chunks[K, 2K) the end
+        // of each group's kernels.
+        bool pinned = false;
+        {
+            static const int inl = [] {
+                const char *e = getenv("MH_TXLOG_INLINE_COPY");
+                return e ? atoi(e) : 1;
+            }();
+            hipPointerAttribute_t a;
+            if (len && hipPointerGetAttributes(&a, buf) == hipSuccess)
+                pinned = a.type == hipMemoryTypeHost;
+            else
+                (void)hipGetLastError();
+            pinned = pinned && inl;
+        }
+        const uint64_t K = len < (16ull << 20) ? 1 : pinned ? txlog_chunks() : 2;
+        std::vector<uint64_t> cut(K + 1, 0);
+        for (uint64_t k = 1; k < K; k++) {
+            if (!pinned) {
+                cut[k] = (len / 4 * 3) & ~4095ull;
+                continue;
+            }
+            const uint64_t w = K * (K + 1) / 2, pre = k * K - k * (k - 1) / 2;  // sum of the first k weights
+            cut[k] = (uint64_t)((double)len * pre / w) & ~4095ull;
+        }
+        cut[K] = len;
+        const uint64_t nck = len ? K : 0;
+        MH_HIP(ensure_chunk_events(c, 2 * nck));
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
-        for (uint64_t k = 0; k < nck; k++) {
-            const uint64_t o = k * chunk;
-            cc.chunks[k] = {{dbuf + o, buf + o, k + 1 < nck ? chunk : len - o}};
-        }
+        for (uint64_t k = 0; k < nck; k++)
+            cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], cut[k + 1] - cut[k]}};
+        cc.inline_issue = pinned;
         MH_HIP(cc.start());
         auto join_copies = [&]() -> int {
             hipError_t e = cc.join();
             return e == hipSuccess ? MH_OK : -(int)e;
         };
-        const HopLimits lim{max_entries, max_key_len};
         tr.mark("copies_started");
-        // ---- host hop (tx.go:419-603): record structure and limits only.  Per
-        // entry the host reads the two lengths it needs to find the next entry
-        // (several threads over a long log, hop_all); the per-entry index (record
-        // offsets, versions, message lengths) is rebuilt on the device from each
-        // tx's first entry (k_txe_index).
-        //
-        // With two copy chunks the hop runs in two phases to match them: the
-        // records wholly inside the first chunk first (a record crossing its
-        // end reads as truncated there and is parsed again by the second
-        // phase), and their device work is queued at once -- it starts as
-        // soon as that chunk lands, under the copy of the rest and the second
-        // phase of the hop.  The result is the sequential parse's either way.
-        //
-        // With two copy chunks the hop runs in two phases to match them: first
-        // the records wholly inside the first chunk (a record crossing its end
-        // reads as truncated there and is parsed again by the second phase),
-        // whose device work is queued at once -- it starts as soon as that
-        // chunk lands, under the copy of the rest and the second phase.  The
-        // records and the return code are the one-pass parse's either way
-        // (every check of hop_record reads only bytes it has bounds-checked).
+        const HopLimits lim{max_entries, max_key_len};
+
+        // ---- one group of records: its own device arrays (per entry record
+        // offset, version, leaf digest; per tx header, entry-count word, record
+        // offset, Alh offset, leaf offset, Eh, inner-hash scratch, Alh, status)
+        // and pinned index staging, all indexed from the group's first record
+        struct Grp {
+            uint64_t t0 = 0, t1 = 0, e0 = 0, E = 0, wmax = 0, k = 0;
+            bool small = true, fetched = false;
+            uint8_t *base = nullptr;
+            uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
+            uint64_t b_rec, b_ver, b_lv, b_h, b_es, b_ro, b_ap, b_lo, b_eh, b_s, b_a, b_st, idx_bytes;
+            TreePlan P;
+        };
         HopOut hop;
-        uint64_t nA = 0, eA = 0;  // records / entries of the early group
-        const bool phases = nck == 2 && len <= 0xffffffffull;
-        // device layout: per entry record offset, version, leaf digest; per tx
-        // header, entry-count word, record offset, Alh offset, leaf offset,
-        // Eh, inner-hash scratch, Alh, status.  Record / Alh / leaf offsets are
-        // staged in pinned memory (pro | pap | plo, ntx_cap + 1 each).
-        Layout L;
-        uint64_t b_rec = 0, b_ver = 0, b_lv = 0, b_h = 0, b_es = 0, b_ro = 0, b_ap = 0, b_lo = 0,
-                 b_eh = 0, b_s = 0, b_a = 0, b_st = 0, ntx_cap = 0, E_cap = 0, idx_bytes = 0;
-        uint8_t *base = nullptr;
-        uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
-        auto alloc = [&](uint64_t nt, uint64_t ne) -> int {
-            ntx_cap = nt;
-            E_cap = ne;
-            L = Layout();
-            b_rec = L.add(ne * 8);
-            b_ver = L.add(ne);
-            b_lv = L.add(std::max<uint64_t>(ne, 1) * 32);
-            b_h = L.add(nt * sizeof(mh_tx_header));
-            b_es = L.add(nt * 8);
-            b_ro = L.add(nt * 8);
-            b_ap = L.add(nt * 8);
-            b_lo = L.add((nt + 1) * 8);
-            b_eh = L.add(nt * 32);
-            b_s = L.add(nt * kTxInnerStride);
-            b_a = L.add(nt * 32);
-            b_st = L.add(nt * 4);
-            MH_HIP(c->s_tx.ensure(L.total));
-            base = c->s_tx.as<uint8_t>();
-            idx_bytes = 3 * (nt + 1) * 8;
-            MH_HIP(c->p_tx.ensure(idx_bytes));
-            pro = c->p_tx.as<uint64_t>();
-            pap = pro + (nt + 1);
-            plo = pap + (nt + 1);
+        std::vector<Grp> gs;
+        gs.reserve(nck + 1);
+        // records [t0, t1) of hop.R (entries from e0) as group number gi
+        auto prepare = [&](Grp &g, size_t gi, uint64_t t0, uint64_t t1, uint64_t e0) -> int {
+            g.t0 = t0;
+            g.t1 = t1;
+            g.e0 = e0;
+            const uint64_t nt = t1 - t0;
+            for (uint64_t t = t0; t < t1; t++) {
+                g.E += hop.R[t].nent;
+                g.wmax = std::max<uint64_t>(g.wmax, hop.R[t].nent);
+            }
+            g.small = small_roots_fit(nt, g.wmax);
+            while (c->s_txg.size() <= gi) c->s_txg.emplace_back();
+            while (c->p_txg.size() <= gi) c->p_txg.emplace_back();
+            Layout L;
+            g.b_rec = L.add(g.E * 8);
+            g.b_ver = L.add(g.E);
+            g.b_lv = L.add(std::max<uint64_t>(g.E, 1) * 32);
+            g.b_h = L.add(nt * sizeof(mh_tx_header));
+            g.b_es = L.add(nt * 8);
+            g.b_ro = L.add(nt * 8);
+            g.b_ap = L.add(nt * 8);
+            g.b_lo = L.add((nt + 1) * 8);
+            g.b_eh = L.add(nt * 32);
+            g.b_s = L.add(nt * kTxInnerStride);
+            g.b_a = L.add(nt * 32);
+            g.b_st = L.add(nt * 4);
+            MH_HIP(c->s_txg[gi].ensure(L.total));
+            g.base = c->s_txg[gi].as<uint8_t>();
+            g.idx_bytes = 3 * (nt + 1) * 8;
+            uint64_t pin = g.idx_bytes;
+            if (!g.small) {
+                std::vector<uint64_t> lof(nt + 1);
+                lof[0] = 0;
+                for (uint64_t t = 0; t < nt; t++) lof[t + 1] = lof[t] + hop.R[t0 + t].nent;
+                g.P.build(nt, lof.data());
+                pin += plan_index_bytes(g.P, nt);
+            }
+            // the previous call's kernels read this staging: done (synced)
+            MH_HIP(c->p_txg[gi].ensure(pin));
+            g.pro = c->p_txg[gi].as<uint64_t>();
+            g.pap = g.pro + (nt + 1);
+            g.plo = g.pap + (nt + 1);
+            uint64_t acc = 0;
+            for (uint64_t t = 0; t < nt; t++) {
+                g.pro[t] = hop.R[t0 + t].rec;
+                g.pap[t] = hop.R[t0 + t].alh;
+                g.plo[t] = acc;
+                acc += hop.R[t0 + t].nent;
+            }
+            g.plo[nt] = acc;
             return MH_OK;
         };
-        // ---- the device work of records R[t0, t1) (entries from e0), reading
-        // the log at db: index arrays up, headers, per-entry index (tx.go:578-585),
-        // entry digests hashed in place from the raw entry records (tx.go:690-731),
-        // one htree per tx (tx.go:617-621; small trees one lane / wave per tree,
-        // a batch with a wide tx through the host tree plan), Alh with the
-        // rebuilt Eh vs the stored one (tx.go:623-627); outputs down on ds
-        auto group = [&](uint64_t t0, uint64_t t1, uint64_t e0, const uint8_t *db, hipStream_t ds,
-                         const uint64_t *pl, uint64_t npe, uint64_t nph) -> int {
-            const uint64_t nt = t1 - t0;
-            uint64_t acc = e0, wmax = 0;
-            for (uint64_t k = t0; k < t1; k++) {
-                pro[k] = hop.R[k].rec;
-                pap[k] = hop.R[k].alh;
-                plo[k] = acc;
-                acc += hop.R[k].nent;
-                wmax = std::max<uint64_t>(wmax, hop.R[k].nent);
-            }
-            plo[t1] = acc;
-            const uint64_t eg = acc - e0;
-            const bool small = small_roots_fit(nt, wmax);
-            TreePlan P;
-            if (!small) {
-                std::vector<uint64_t> lof(nt + 1);
-                for (uint64_t k = 0; k <= nt; k++) lof[k] = plo[t0 + k] - e0;
-                P.build(nt, lof.data());
-                const uint64_t need = idx_bytes + plan_index_bytes(P, nt);
-                if (c->p_tx.cap < need) {
-                    // p_tx moves: an earlier group's staging must be consumed first
-                    MH_HIP(hipStreamSynchronize(st));
-                    std::vector<uint64_t> keep(pro, pro + 3 * (ntx_cap + 1));
-                    MH_HIP(c->p_tx.ensure(need));
-                    pro = c->p_tx.as<uint64_t>();
-                    pap = pro + (ntx_cap + 1);
-                    plo = pap + (ntx_cap + 1);
-                    memcpy(pro, keep.data(), keep.size() * 8);
-                }
-            }
-            MH_HIP(hipMemcpyAsync(base + b_ro + t0 * 8, pro + t0, nt * 8, hipMemcpyHostToDevice, st));
-            MH_HIP(hipMemcpyAsync(base + b_ap + t0 * 8, pap + t0, nt * 8, hipMemcpyHostToDevice, st));
-            MH_HIP(hipMemcpyAsync(base + b_lo + t0 * 8, plo + t0, (nt + 1) * 8,
-                                  hipMemcpyHostToDevice, st));
-            const uint64_t *ro = (const uint64_t *)(base + b_ro) + t0;
-            const uint64_t *lo = (const uint64_t *)(base + b_lo) + t0;
-            MhTxHeader *hd = (MhTxHeader *)(base + b_h) + t0;
-            uint64_t *es = (uint64_t *)(base + b_es) + t0;
+        // ---- its device work, reading the log at db: index arrays up (a
+        // kernel reads them from the pinned staging: a DMA copy would wait
+        // behind the log chunks still in flight), headers, per-entry index
+        // (tx.go:578-585), entry digests hashed in place from the raw entry
+        // records (tx.go:690-731), one htree per tx (tx.go:617-621; small
+        // trees one lane / wave per tree, a group with a wide tx through the
+        // host tree plan), Alh with the rebuilt Eh vs the stored one
+        // (tx.go:623-627).  pl: the group's metadata patch lists (below).
+        auto run = [&](Grp &g, const uint8_t *db, const uint64_t *pl, uint64_t npe,
+                       uint64_t nph) -> int {
+            const uint64_t nt = g.t1 - g.t0;
+            uint8_t *base = g.base;
+            uint64_t *ro = (uint64_t *)(base + g.b_ro), *ap = (uint64_t *)(base + g.b_ap),
+                     *lo = (uint64_t *)(base + g.b_lo), *es = (uint64_t *)(base + g.b_es),
+                     *rec = (uint64_t *)(base + g.b_rec);
+            MhTxHeader *hd = (MhTxHeader *)(base + g.b_h);
+            if (!g.fetched)
+                MH_HIP(launch_fetch_host(st, HostRuns{{g.pro, g.pap, g.plo}, {ro, ap, lo}, {nt, nt, nt + 1}}));
             MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, db, ro, hd, es));
-            MH_HIP(launch_txe_index(st, c->tm(), nt, db, hd, es, lo, (uint64_t *)(base + b_rec),
-                                    base + b_ver));
+            MH_HIP(launch_txe_index(st, c->tm(), nt, db, hd, es, lo, rec, base + g.b_ver));
             if (npe + nph)
-                MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, (uint64_t *)(base + b_rec), nph,
-                                          pl + 2 * npe, pl + 2 * npe + nph, (MhTxHeader *)(base + b_h)));
-            MH_HIP(launch_txe_leaf(st, c->tm(), eg, db, (const uint64_t *)(base + b_rec) + e0,
-                                   base + b_ver + e0, small, base + b_lv + e0 * 32));
-            if (small) {
-                MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + b_lv + e0 * 32,
-                                          base + b_eh + t0 * 32, wmax));
-            } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), P, nt, eg, base + b_lv + e0 * 32,
-                                                base + b_eh + t0 * 32,
-                                                reinterpret_cast<uint8_t *>(pro) + idx_bytes)) {
+                MH_HIP(launch_txlog_patch(st, npe, pl, pl + npe, rec, nph, pl + 2 * npe,
+                                          pl + 2 * npe + nph, hd));
+            MH_HIP(launch_txe_leaf(st, c->tm(), g.E, db, rec, base + g.b_ver, g.small, base + g.b_lv));
+            if (g.small) {
+                MH_HIP(launch_small_roots(st, c->tm(), nt, lo, base + g.b_lv, base + g.b_eh, g.wmax));
+            } else if (int e = run_tree_plan_on(c->s_tree, st, c->tm(), g.P, nt, g.E, base + g.b_lv,
+                                                base + g.b_eh,
+                                                reinterpret_cast<uint8_t *>(g.pro) + g.idx_bytes)) {
                 return e;
             }
-            MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, db, base + b_eh + t0 * 32,
-                                 base + b_s + t0 * kTxInnerStride, db,
-                                 (const uint64_t *)(base + b_ap) + t0, nullptr, base + b_a + t0 * 32,
-                                 (int32_t *)(base + b_st) + t0));
+            MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, db, base + g.b_eh, base + g.b_s, db, ap, nullptr,
+                                 base + g.b_a, (int32_t *)(base + g.b_st)));
             if (hdrs_out)  // the device headers with the rebuilt Eh
-                MH_HIP(launch_put_eh(st, nt, base + b_eh + t0 * 32, hd));
-            if (ds != st) {
-                MH_HIP(hipEventRecord(c->ev_done[1], st));
-                MH_HIP(hipStreamWaitEvent(ds, c->ev_done[1], 0));
+                MH_HIP(launch_put_eh(st, nt, base + g.b_eh, hd));
+            return MH_OK;
+        };
+        // ---- its results down to the caller's arrays at record t0: by kernel
+        // stores when they are pinned host memory (on the results stream,
+        // beside the next group's kernels; a D2H copy would wait behind the
+        // log chunks on the DMA engine), else by D2H copies.  After event ev.
+        auto results = [&](const Grp &g, hipEvent_t ev) -> int {
+            const uint64_t nt = g.t1 - g.t0, t0 = g.t0;
+            hipStream_t ds = c->d2h_stream;
+            MH_HIP(hipStreamWaitEvent(ds, ev, 0));
+            uint32_t *hs = status_out ? host_words(status_out + t0, nt * 4) : nullptr;
+            uint32_t *ha = alh_out ? host_words(alh_out + t0 * 32, nt * 32) : nullptr;
+            uint32_t *hh = hdrs_out ? host_words(hdrs_out + t0, nt * sizeof(mh_tx_header)) : nullptr;
+            if ((!status_out || hs) && (!alh_out || ha) && (!hdrs_out || hh)) {
+                MH_HIP(launch_store_host(
+                    ds, HostWordRuns{{(const uint32_t *)(g.base + g.b_st), (const uint32_t *)(g.base + g.b_a),
+                                      (const uint32_t *)(g.base + g.b_h)},
+                                     {hs, ha, hh},
+                                     {hs ? nt : 0, ha ? nt * 8 : 0, hh ? nt * sizeof(mh_tx_header) / 4 : 0}}));
+                return MH_OK;
             }
             if (status_out)
-                MH_HIP(hipMemcpyAsync(status_out + t0, base + b_st + t0 * 4, nt * 4,
-                                      hipMemcpyDeviceToHost, ds));
+                MH_HIP(hipMemcpyAsync(status_out + t0, g.base + g.b_st, nt * 4, hipMemcpyDeviceToHost, ds));
             if (alh_out)
-                MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, base + b_a + t0 * 32, nt * 32,
-                                      hipMemcpyDeviceToHost, ds));
+                MH_HIP(hipMemcpyAsync(alh_out + t0 * 32, g.base + g.b_a, nt * 32, hipMemcpyDeviceToHost, ds));
             if (hdrs_out)
-                MH_HIP(hipMemcpyAsync(hdrs_out + t0, hd, nt * sizeof(mh_tx_header),
+                MH_HIP(hipMemcpyAsync(hdrs_out + t0, g.base + g.b_h, nt * sizeof(mh_tx_header),
                                       hipMemcpyDeviceToHost, ds));
             return MH_OK;
         };
-        if (phases) {
-            hop_all(buf, chunk, max_txs, lim, hop, false);
-            tr.mark("hop1");
-            nA = hop.R.size();
-            uint64_t w1 = 0;
-            for (const HopRec &r : hop.R) {
-                eA += r.nent;
-                w1 = std::max<uint64_t>(w1, r.nent);
+
+        // ---- host hop (tx.go:419-603): record structure and limits only.  Per
+        // entry the host reads the two lengths it needs to find the next entry
+        // (parked helper threads over a long stretch, hop_all); the per-entry
+        // index (record offsets, versions, message lengths) is rebuilt on the
+        // device from each tx's first entry (k_txe_index).
+        //
+        // It runs in one phase per copy chunk: phase k parses the records
+        // that end inside chunk k, from where phase k-1 stopped (a record
+        // crossing the chunk's end reads as truncated there and is parsed
+        // again by the next phase), and their device work is queued at once
+        // behind the chunk's event.  The records and the return code are the
+        // one-pass parse's either way: every check of hop_record reads only
+        // bytes it has bounds-checked, so a shorter buffer can only end a
+        // parse early with TRUNCATED or a short-id EOF.  A phase with
+        // non-canonical metadata or a wide tx stops the early groups: the
+        // rest goes as one group once the whole log is in.
+        // an early group behind the event of its chunk, results on their stream
+        auto launch = [&](Grp &g) -> int {
+            // the index arrays do not need the chunk: fetched before its event
+            const uint64_t nt = g.t1 - g.t0;
+            MH_HIP(launch_fetch_host(
+                st, HostRuns{{g.pro, g.pap, g.plo},
+                             {(uint64_t *)(g.base + g.b_ro), (uint64_t *)(g.base + g.b_ap),
+                              (uint64_t *)(g.base + g.b_lo)},
+                             {nt, nt, nt + 1}}));
+            g.fetched = true;
+            if (hipError_t e = cc.wait(g.k)) return -(int)e;
+            MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[g.k], 0));
+            if (int e = run(g, dbuf, nullptr, 0, 0)) return e;
+            MH_HIP(hipEventRecord(c->ev_chunks[nck + g.k], st));
+            return results(g, c->ev_chunks[nck + g.k]);
+        };
+        size_t deferred = 0;  // gs[0, deferred) are queued
+        uint64_t pos = 0, e_done = 0;
+        // (a log past 4 GiB is parsed in one phase: hop_record's 32-bit
+        // metadata-offset check depends on where the parse starts)
+        const uint64_t nphase = len <= 0xffffffffull ? nck : 1;
+        bool early = nphase > 1;
+        for (uint64_t k = 0; k < nphase; k++) {
+            const uint64_t end = k + 1 < nphase ? cut[k + 1] : len;
+            const uint64_t r0 = hop.R.size();
+            HopOut h;
+            hop_all(buf + pos, end - pos, max_txs - r0, lim, h, false);
+            for (const HopRec &r : h.R) hop.R.push_back(HopRec{r.rec + pos, r.alh + pos, r.nent, 0});
+            for (HopPatch &pt : h.P) {
+                pt.rec += r0;
+                hop.P.push_back(std::move(pt));
             }
-            const bool more = nA < max_txs && (hop.rc == MH_ERR_TRUNCATED ||
-                                               (hop.rc == MH_OK && hop.end + 8 > chunk));
-            // the early group: small trees, nothing to patch, and more to come
-            if (more && nA && hop.P.empty() && small_roots_fit(nA, w1)) {
-                // sized for the most records / entries the log can hold (a
-                // record is >= 124 bytes, an entry >= 48)
-                if (int e = alloc(std::min<uint64_t>(max_txs, len / 124 + 1), len / 48 + 1)) return e;
-                if (hipError_t e = cc.wait(0)) return -(int)e;
-                MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[0], 0));
-                if (int e = group(0, nA, 0, dbuf, c->d2h_stream, nullptr, 0, 0)) return e;
-                tr.mark("group_a");
-            } else {
-                nA = eA = 0;
-            }
-            if (more) {
-                const uint64_t p2 = hop.end, r0 = hop.R.size();
-                HopOut h2;
-                hop_all(buf + p2, len - p2, max_txs - r0, lim, h2, false);
-                for (const HopRec &r : h2.R) hop.R.push_back(HopRec{r.rec + p2, r.alh + p2, r.nent, 0});
-                for (HopPatch &pt : h2.P) {
-                    pt.rec += r0;
-                    hop.P.push_back(std::move(pt));
-                }
-                hop.rc = h2.rc;
-                hop.end = p2 + h2.end;
-                tr.mark("hop2");
-            }
-        } else {
-            hop_all(buf, len, max_txs, lim, hop, false);
+            hop.rc = h.rc;
+            hop.end = pos + h.end;
             tr.mark("hop");
+            const bool more = k + 1 < nphase && hop.R.size() < max_txs &&
+                              (h.rc == MH_ERR_TRUNCATED || (h.rc == MH_OK && hop.end + 8 > end));
+            if (early && h.P.empty() && hop.R.size() > r0) {
+                gs.emplace_back();
+                Grp &g = gs.back();
+                if (int e = prepare(g, gs.size() - 1, r0, hop.R.size(), e_done)) return e;
+                if (!g.small) {
+                    gs.pop_back();
+                    early = false;
+                } else {
+                    g.k = k;
+                    e_done += g.E;
+                    // queued now if its chunk's copy is (a pageable log's copy
+                    // calls block their thread: the remaining phases of the
+                    // hop go first, and these groups after them)
+                    if (deferred == gs.size() - 1 && cc.issued(k)) {
+                        if (int e = launch(g)) return e;
+                        deferred++;
+                        tr.mark("group");
+                    }
+                }
+            } else if (!h.P.empty()) {
+                early = false;
+            }
+            if (!more) break;
+            pos = hop.end;
+        }
+        if (!nck) hop_all(buf, len, max_txs, lim, hop, false);  // empty log
+        for (; deferred < gs.size(); deferred++) {
+            if (int e = launch(gs[deferred])) return e;
+            tr.mark("group");
         }
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
@@ -1194,69 +1371,71 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         if (consumed_out) *consumed_out = hop.end;
         if (int e = join_copies()) return e;
         tr.mark("joined");
-        if (!ntx) {
-            // buf stays the caller's once we return
+        const uint64_t t_rest = gs.empty() ? 0 : gs.back().t1;
+        if (t_rest < ntx) {
+            // ---- the rest as one group once the whole log is in
+            if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
+            gs.emplace_back();
+            Grp &g = gs.back();
+            if (int e = prepare(g, gs.size() - 1, t_rest, ntx, e_done)) return e;
+            // metadata that parses but is not in canonical form (a log not
+            // written by immudb): Go hashes KVMetadata.Bytes() /
+            // TxMetadata.Bytes(), so the canonical entry records / tx metadata
+            // go after the log bytes in a copy of the log on the device, and
+            // the group's entry index / headers point at them
+            const uint8_t *db = dbuf;
+            const uint64_t *pl = nullptr;
+            uint64_t npe = 0, nph = 0;
+            if (!hop.P.empty()) {
+                std::vector<uint64_t> first_leaf(ntx - t_rest);  // group-local entry index
+                for (uint64_t t = t_rest, acc = 0; t < ntx; t++) {
+                    first_leaf[t - t_rest] = acc;
+                    acc += hop.R[t].nent;
+                }
+                uint64_t side = 0;
+                for (const HopPatch &pt : hop.P) {
+                    side += pt.bytes.size();
+                    (pt.kind == 0 ? npe : nph)++;
+                }
+                if (len + side > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
+                std::vector<uint8_t> sbuf;
+                sbuf.reserve(side);
+                std::vector<uint64_t> patch(2 * (npe + nph));  // [ne idx][ne off][nh idx][nh off | len << 32]
+                uint64_t ie = 0, ih = 0;
+                for (const HopPatch &pt : hop.P) {
+                    if (pt.rec < t_rest) return MH_ERR_ILLEGAL_STATE;  // early groups have none
+                    const uint64_t off = len + sbuf.size();
+                    if (pt.kind == 0) {
+                        patch[ie] = first_leaf[pt.rec - t_rest] + pt.entry;
+                        patch[npe + ie++] = off;
+                    } else {
+                        patch[2 * npe + ih] = pt.rec - t_rest;
+                        patch[2 * npe + nph + ih++] = off | ((uint64_t)pt.bytes.size() << 32);
+                    }
+                    sbuf.insert(sbuf.end(), pt.bytes.begin(), pt.bytes.end());
+                }
+                const uint64_t po = (len + side + 7) & ~7ull;
+                MH_HIP(c->s_txpatch.ensure(po + patch.size() * 8));
+                uint8_t *nb = c->s_txpatch.as<uint8_t>();
+                MH_HIP(hipMemcpyAsync(nb, dbuf, len, hipMemcpyDeviceToDevice, st));
+                MH_HIP(hipMemcpyAsync(nb + len, sbuf.data(), side, hipMemcpyHostToDevice, st));
+                MH_HIP(hipMemcpyAsync(nb + po, patch.data(), patch.size() * 8, hipMemcpyHostToDevice, st));
+                MH_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
+                db = nb;
+                pl = reinterpret_cast<const uint64_t *>(nb + po);
+            }
+            if (int e = run(g, db, pl, npe, nph)) return e;
+            MH_HIP(hipEventRecord(c->ev_done[1], st));
+            if (int e = results(g, c->ev_done[1])) return e;
+        }
+        tr.mark("enqueued");
+        MH_HIP(hipStreamSynchronize(c->d2h_stream));
+        MH_HIP(hipStreamSynchronize(st));
+        // buf stays the caller's once we return
+        if (nck) {
             MH_HIP(hipStreamSynchronize(c->copy_stream));
             MH_HIP(hipStreamSynchronize(c->copy_stream2));
-            return rc;
         }
-        if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));  // the whole log in
-        uint64_t E = 0;
-        for (const HopRec &r : hop.R) E += r.nent;
-        if (nA) {
-            if (ntx > ntx_cap || E > E_cap) return MH_ERR_ILLEGAL_STATE;  // cannot happen: bounds
-        } else if (int e = alloc(ntx, E)) {
-            return e;
-        }
-        // ---- metadata that parses but is not in canonical form (a log not
-        // written by immudb): Go hashes KVMetadata.Bytes() / TxMetadata.Bytes(),
-        // so the canonical entry records / tx metadata go after the log bytes
-        // in a copy of the log on the device, and the entry index / headers
-        // point at them.  (The early group never has any.)
-        const uint8_t *db = dbuf;
-        const uint64_t *pl = nullptr;
-        uint64_t npe = 0, nph = 0;
-        if (!hop.P.empty()) {
-            std::vector<uint64_t> first_leaf(ntx);
-            for (uint64_t k = 0, acc = 0; k < ntx; k++) {
-                first_leaf[k] = acc;
-                acc += hop.R[k].nent;
-            }
-            uint64_t side = 0;
-            for (const HopPatch &pt : hop.P) {
-                side += pt.bytes.size();
-                (pt.kind == 0 ? npe : nph)++;
-            }
-            if (len + side > 0xffffffffull) return MH_ERR_ILLEGAL_ARGUMENTS;
-            std::vector<uint8_t> sbuf;
-            sbuf.reserve(side);
-            std::vector<uint64_t> patch(2 * (npe + nph));  // [ne idx][ne off][nh idx][nh off | len << 32]
-            uint64_t ie = 0, ih = 0;
-            for (const HopPatch &pt : hop.P) {
-                const uint64_t off = len + sbuf.size();
-                if (pt.kind == 0) {
-                    patch[ie] = first_leaf[pt.rec] + pt.entry;
-                    patch[npe + ie++] = off;
-                } else {
-                    patch[2 * npe + ih] = pt.rec;
-                    patch[2 * npe + nph + ih++] = off | ((uint64_t)pt.bytes.size() << 32);
-                }
-                sbuf.insert(sbuf.end(), pt.bytes.begin(), pt.bytes.end());
-            }
-            const uint64_t po = (len + side + 7) & ~7ull;
-            MH_HIP(c->s_txpatch.ensure(po + patch.size() * 8));
-            uint8_t *nb = c->s_txpatch.as<uint8_t>();
-            MH_HIP(hipMemcpyAsync(nb, dbuf, len, hipMemcpyDeviceToDevice, st));
-            MH_HIP(hipMemcpyAsync(nb + len, sbuf.data(), side, hipMemcpyHostToDevice, st));
-            MH_HIP(hipMemcpyAsync(nb + po, patch.data(), patch.size() * 8, hipMemcpyHostToDevice, st));
-            MH_HIP(hipStreamSynchronize(st));  // the host vectors go out of scope
-            db = nb;
-            pl = reinterpret_cast<const uint64_t *>(nb + po);
-        }
-        if (int e = group(nA, ntx, eA, db, st, pl, npe, nph)) return e;
-        tr.mark("enqueued");
-        if (nA) MH_HIP(hipStreamSynchronize(c->d2h_stream));
-        MH_HIP(hipStreamSynchronize(st));
         tr.mark("done");
         return rc;
     });

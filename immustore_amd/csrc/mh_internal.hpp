@@ -256,6 +256,20 @@ hipError_t launch_txlog_patch(hipStream_t st, uint64_t ne, const uint64_t *e_idx
                               const uint64_t *e_off, uint64_t *rec_off, uint64_t nh,
                               const uint64_t *h_idx, const uint64_t *h_val, MhTxHeader *hdrs);
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
+// up to three runs of words pinned host memory -> HBM by a kernel (k_fetch_host)
+struct HostRuns {
+    const uint64_t *src[3];
+    uint64_t *dst[3];
+    uint64_t n[3];
+};
+hipError_t launch_fetch_host(hipStream_t st, const HostRuns &r);
+// up to three runs of 32-bit words HBM -> pinned host memory by a kernel (k_store_host)
+struct HostWordRuns {
+    const uint32_t *src[3];
+    uint32_t *dst[3];
+    uint64_t n[3];
+};
+hipError_t launch_store_host(hipStream_t st, const HostWordRuns &r);
 hipError_t launch_txe_index(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                             const MhTxHeader *hdrs, const uint64_t *ent_start,
                             const uint64_t *leaf_off, uint64_t *rec_off, uint8_t *ver);

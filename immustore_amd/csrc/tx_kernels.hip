@@ -279,6 +279,53 @@ hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const
     return hipGetLastError();
 }
 
+// Up to three runs of 64-bit words from pinned host memory into HBM, read by
+// the kernel over PCIe: a small upload that does not queue behind the large
+// host-to-device copies the DMA engine is busy with (the tx-log chunks).
+__global__ __launch_bounds__(256) void k_fetch_host(HostRuns r) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < 3; k++)
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n[k]; i += stride)
+            r.dst[k][i] = r.src[k][i];
+}
+
+hipError_t launch_fetch_host(hipStream_t st, const HostRuns &r) {
+    const uint64_t m = std::max(r.n[0], std::max(r.n[1], r.n[2]));
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_fetch_host, dim3((unsigned)std::min<uint64_t>(grid_for(m, 256), 1024)),
+                       dim3(256), 0, st, r);
+    return hipGetLastError();
+}
+
+// Up to three runs of 32-bit words from HBM into pinned host memory by
+// kernel stores over PCIe: results that do not wait for the DMA engine.  A
+// run whose ends are 16-byte aligned goes in 16-byte stores (4-byte stores
+// reach only ~25 GB/s over the link).
+__global__ __launch_bounds__(256) void k_store_host(HostWordRuns r) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < 3; k++) {
+        const uint64_t n = r.n[k];
+        if ((((uintptr_t)r.src[k] | (uintptr_t)r.dst[k]) & 15) == 0) {
+            const uint4 *s = reinterpret_cast<const uint4 *>(r.src[k]);
+            uint4 *d = reinterpret_cast<uint4 *>(r.dst[k]);
+            for (uint64_t i = tid; i < n / 4; i += stride) d[i] = s[i];
+            for (uint64_t i = (n & ~3ull) + tid; i < n; i += stride) r.dst[k][i] = r.src[k][i];
+        } else {
+            for (uint64_t i = tid; i < n; i += stride) r.dst[k][i] = r.src[k][i];
+        }
+    }
+    __threadfence_system();
+}
+
+hipError_t launch_store_host(hipStream_t st, const HostWordRuns &r) {
+    const uint64_t m = std::max(r.n[0], std::max(r.n[1], r.n[2]));
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_store_host, dim3((unsigned)std::min<uint64_t>(grid_for(m / 4 + 1, 256), 1024)),
+                       dim3(256), 0, st, r);
+    return hipGetLastError();
+}
+
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_put_eh, dim3(grid_for(n, 256)), dim3(256), 0, st, n, eh, hdrs);

@@ -223,6 +223,52 @@ def test_commit_queue_30_threads_vs_oracle(m, ctx, orc):
     q.close()
 
 
+def test_commit_queue_small_batches_and_large_txs(m, ctx, orc):
+    """Committers copy their own txs into the open batch's arena and their
+    results out of it: max_txs 4 under 12 threads (several batches in flight
+    over the two workers, arenas reused as soon as every committer has read),
+    and txs larger than the default arena (5000 entries; a 20 MiB value; 2 MiB
+    of keys) that open a batch of their own -- every result equal to the
+    oracle's."""
+    import threading
+    from immustore_amd.commit import CommitQueue, EntrySpec
+    q = CommitQueue(ctx, version=1, max_width=0, max_txs=4, wait_us=30)
+    rng = np.random.default_rng(31)
+    txs = []
+    for k in range(96):
+        if k == 17:
+            es = [EntrySpec(b"w%d" % e, bytes([e % 251]) * 8) for e in range(5000)]
+        elif k == 40:
+            es = [EntrySpec(b"big", orc.fill_random(20 << 20, 3).tobytes(), b"\x02")]
+        elif k == 63:
+            es = [EntrySpec(bytes([e % 256, e // 256]) * 500, b"v") for e in range(2100)]
+        else:
+            es = [EntrySpec(b"k%d/%d" % (k, e), bytes(rng.integers(0, 256, int(rng.integers(0, 2000)),
+                                                                    dtype=np.uint8)),
+                            [b"", b"\x00"][e % 2]) for e in range(int(rng.integers(0, 9)))]
+        txs.append(es)
+    out = [None] * len(txs)
+
+    def run(t):
+        for k in range(t, len(txs), 12):
+            out[k] = q.submit(txs[k])
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(12)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    for k, es in enumerate(txs):
+        st, hv, eh = out[k]
+        s2, ehv, _, root = orc.build_entries(1, [e.key for e in es], [e.md for e in es],
+                                             [e.value for e in es])
+        assert st == 0 and eh == root, k
+        assert np.array_equal(hv, ehv.reshape(-1, 32)), k
+    batches, n = q.stats()
+    assert n == len(txs) and batches >= len(txs) // 4
+    q.close()
+
+
 def test_commit_queue_v0_metadata_and_free(m, ctx, orc):
     from immustore_amd.commit import CommitQueue, EntrySpec
     q = CommitQueue(ctx, version=0)

@@ -204,13 +204,20 @@ def test_txlog_validate_parallel_hop(m, ctx, orc):
     same(raw, max_txs=4321)
 
 
-def test_txlog_validate_two_phase_split(m, ctx, orc):
-    """From 16 MiB the log goes up in two copy chunks and the hop runs in two
-    phases (the records inside the first chunk are validated while the rest
-    is parsed): errors on either side of the split and in the record that
-    straddles it, max_txs at the split, non-canonical metadata (patched
-    records) and wide txs (tree plan) before or after it -- all equal the
-    one-pass oracle."""
+def _chunk_cuts(n, K=4):
+    """mh_txlog_validate's copy chunks of an n-byte log (from 16 MiB, K of
+    them, sizes K : K-1 : ... : 1, cut at 4 KiB multiples)."""
+    w = K * (K + 1) // 2
+    return [int(n * (k * K - k * (k - 1) // 2) / w) & ~4095 for k in range(1, K)]
+
+
+def test_txlog_validate_chunk_phases(m, ctx, orc):
+    """From 16 MiB the log goes up in 4 copy chunks and the hop runs in one
+    phase per chunk (the records ending inside a chunk are validated while the
+    rest is copied and parsed): errors on either side of every cut and in the
+    records that straddle them, max_txs at a cut, a cut short of a record,
+    non-canonical metadata (patched records) and wide txs (tree plan) in the
+    first or the last chunk -- all equal to the one-pass oracle."""
     from tx_util import metadata_logs
     rng = np.random.default_rng(5)
     raw, starts = _bulk_txlog(rng, 9000)
@@ -223,29 +230,61 @@ def test_txlog_validate_two_phase_split(m, ctx, orc):
         assert list(a[5]) == list(b[4]) and np.array_equal(a[4], b[3]), kw
         return a
 
-    chunk = (len(raw) // 4 * 3) & ~4095
-    j = max(k for k in range(len(starts)) if starts[k] < chunk)  # straddles the split
-    for k in (j - 1, j, j + 1):
-        bad = bytearray(raw)
-        bad[starts[k] + 89] = 7  # unknown header version
-        a = same(bytes(bad))
-        assert (a[0], a[1], a[2]) == (17, k, starts[k])
-    bad = bytearray(raw)  # hVal of the straddling record's last entry
-    bad[starts[j + 1] - 33] ^= 1
-    same(bytes(bad))
-    for mt in (j - 1, j, j + 1):
-        a = same(raw, max_txs=mt)
-        assert a[1] == mt
-    same(raw[:chunk + 5])
-    same(raw[:starts[j + 1]] + bytes(len(raw) - starts[j + 1]))
-    # patched records after the split only / before it only
+    for cut in _chunk_cuts(len(raw)):
+        j = max(k for k in range(len(starts)) if starts[k] < cut)  # straddles the cut
+        for k in (j - 1, j, j + 1):
+            bad = bytearray(raw)
+            bad[starts[k] + 89] = 7  # unknown header version
+            a = same(bytes(bad))
+            assert (a[0], a[1], a[2]) == (17, k, starts[k])
+        bad = bytearray(raw)  # hVal of the straddling record's last entry
+        bad[starts[j + 1] - 33] ^= 1
+        same(bytes(bad))
+        for mt in (j - 1, j, j + 1):
+            a = same(raw, max_txs=mt)
+            assert a[1] == mt
+    cut = _chunk_cuts(len(raw))[0]
+    j = max(k for k in range(len(starts)) if starts[k] < cut)
+    same(raw[:starts[j + 1]] + bytes(len(raw) - starts[j + 1]))  # zero tail from the first cut
+    same(raw[:len(raw) - 5])
+    # patched records / wide txs at the start or the end
     md = b"".join(r for name, r in metadata_logs(orc) if name == "noncanonical_sealed_canonical")
     same(raw + md * 50)
     same(md * 50 + raw)
-    # wide txs after the split only / before it only
     wide = _synthetic_txlog(rng, 20, orc, max_entries=300)
     same(raw + wide)
     same(wide + raw)
+
+
+@pytest.mark.parametrize("hdrs", [True, False])
+def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
+    """The log and the outputs in pinned host memory (as the cgo shim's arena
+    holds them): the index arrays go up and the results come down by kernel
+    loads / stores over PCIe instead of DMA copies.  Equal to the oracle and
+    to the pageable call, for a clean log, one with corrupted records in every
+    copy chunk, and an output arena larger than the result."""
+    import torch
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(8)
+    raw, starts = _bulk_txlog(rng, 9000)
+    bad = bytearray(raw)
+    for k in (3, 2500, 4700, 7000, 8999):
+        bad[starts[k] + 100] ^= 1  # inside the record: an Alh mismatch
+    for buf in (raw, bytes(bad)):
+        pin = torch.empty(len(buf), dtype=torch.uint8).pin_memory()
+        pin.numpy()[:] = np.frombuffer(buf, np.uint8)
+        cap = 9100
+        outs = (torch.empty(cap * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy()
+                .view(TX_HEADER) if hdrs else None,
+                torch.empty(cap * 32, dtype=torch.uint8).pin_memory().numpy().reshape(cap, 32),
+                torch.empty(cap, dtype=torch.int32).pin_memory().numpy())
+        a = m.txlog_validate(pin.numpy(), ctx=ctx, out=outs)
+        b = orc.txlog_validate(buf)
+        c = m.txlog_validate(buf, ctx=ctx)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]) == (c[0], c[1], c[2])
+        assert np.array_equal(a[4], b[3]) and list(a[5]) == list(b[4])
+        if hdrs:
+            assert np.array_equal(a[3], c[3])
 
 
 def test_dual_proof_v2_fixture_cases(m, ctx, orc, fixtures):
