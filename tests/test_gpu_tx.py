@@ -256,6 +256,40 @@ def test_txlog_validate_chunk_phases(m, ctx, orc):
     same(wide + raw)
 
 
+def test_txlog_validate_chunked_mutants(m, ctx, orc):
+    """Random damage to a ~24 MiB log (chunked copy, one hop phase per chunk):
+    byte flips anywhere, bursts of zeros, a cut at a random length -- status,
+    count, consumed bytes, every Alh and per-tx status equal to the oracle's
+    one-pass parse, with pageable and with pinned outputs."""
+    import torch
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(21)
+    raw, starts = _bulk_txlog(rng, 11000)
+    assert len(raw) >= (16 << 20)
+    cap = 11100
+    outs = (torch.empty(cap * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy().view(TX_HEADER),
+            torch.empty(cap * 32, dtype=torch.uint8).pin_memory().numpy().reshape(cap, 32),
+            torch.empty(cap, dtype=torch.int32).pin_memory().numpy())
+    for case in range(24):
+        b = bytearray(raw)
+        kind = case % 3
+        if kind == 0:
+            for p in rng.integers(0, len(b), int(rng.integers(1, 40))):
+                b[int(p)] ^= int(rng.integers(1, 256))
+        elif kind == 1:
+            p = int(rng.integers(0, len(b) - 4096))
+            w = int(rng.integers(8, 4096))
+            b[p:p + w] = bytes(w)
+        else:
+            b = b[:int(rng.integers(len(b) // 2, len(b)))]
+        buf = bytes(b)
+        o = orc.txlog_validate(buf)
+        for out in (None, outs):
+            a = m.txlog_validate(buf, ctx=ctx, out=out)
+            assert (a[0], a[1], a[2]) == (o[0], o[1], o[2]), (case, out is None)
+            assert np.array_equal(a[4], o[3]) and list(a[5]) == list(o[4]), (case, out is None)
+
+
 @pytest.mark.parametrize("hdrs", [True, False])
 def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
     """The log and the outputs in pinned host memory (as the cgo shim's arena
