@@ -1256,21 +1256,13 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // stores when they are pinned host memory (on the results stream,
         // beside the next group's kernels; a D2H copy would wait behind the
         // log chunks on the DMA engine), else by D2H copies.  After event ev.
-        auto results = [&](const Grp &g, hipEvent_t ev) -> int {
+        // D2H copies into pageable memory return only when done: those of the
+        // early groups are issued once every group is queued (late)
+        std::vector<std::pair<const Grp *, hipEvent_t>> late;
+        auto results_dma = [&](const Grp &g, hipEvent_t ev) -> int {
             const uint64_t nt = g.t1 - g.t0, t0 = g.t0;
             hipStream_t ds = c->d2h_stream;
             MH_HIP(hipStreamWaitEvent(ds, ev, 0));
-            uint32_t *hs = status_out ? host_words(status_out + t0, nt * 4) : nullptr;
-            uint32_t *ha = alh_out ? host_words(alh_out + t0 * 32, nt * 32) : nullptr;
-            uint32_t *hh = hdrs_out ? host_words(hdrs_out + t0, nt * sizeof(mh_tx_header)) : nullptr;
-            if ((!status_out || hs) && (!alh_out || ha) && (!hdrs_out || hh)) {
-                MH_HIP(launch_store_host(
-                    ds, HostWordRuns{{(const uint32_t *)(g.base + g.b_st), (const uint32_t *)(g.base + g.b_a),
-                                      (const uint32_t *)(g.base + g.b_h)},
-                                     {hs, ha, hh},
-                                     {hs ? nt : 0, ha ? nt * 8 : 0, hh ? nt * sizeof(mh_tx_header) / 4 : 0}}));
-                return MH_OK;
-            }
             if (status_out)
                 MH_HIP(hipMemcpyAsync(status_out + t0, g.base + g.b_st, nt * 4, hipMemcpyDeviceToHost, ds));
             if (alh_out)
@@ -1278,6 +1270,24 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             if (hdrs_out)
                 MH_HIP(hipMemcpyAsync(hdrs_out + t0, g.base + g.b_h, nt * sizeof(mh_tx_header),
                                       hipMemcpyDeviceToHost, ds));
+            return MH_OK;
+        };
+        auto results = [&](const Grp &g, hipEvent_t ev) -> int {
+            const uint64_t nt = g.t1 - g.t0, t0 = g.t0;
+            hipStream_t ds = c->d2h_stream;
+            uint32_t *hs = status_out ? host_words(status_out + t0, nt * 4) : nullptr;
+            uint32_t *ha = alh_out ? host_words(alh_out + t0 * 32, nt * 32) : nullptr;
+            uint32_t *hh = hdrs_out ? host_words(hdrs_out + t0, nt * sizeof(mh_tx_header)) : nullptr;
+            if ((!status_out || hs) && (!alh_out || ha) && (!hdrs_out || hh)) {
+                MH_HIP(hipStreamWaitEvent(ds, ev, 0));
+                MH_HIP(launch_store_host(
+                    ds, HostWordRuns{{(const uint32_t *)(g.base + g.b_st), (const uint32_t *)(g.base + g.b_a),
+                                      (const uint32_t *)(g.base + g.b_h)},
+                                     {hs, ha, hh},
+                                     {hs ? nt : 0, ha ? nt * 8 : 0, hh ? nt * sizeof(mh_tx_header) / 4 : 0}}));
+                return MH_OK;
+            }
+            late.emplace_back(&g, ev);
             return MH_OK;
         };
 
@@ -1428,6 +1438,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             MH_HIP(hipEventRecord(c->ev_done[1], st));
             if (int e = results(g, c->ev_done[1])) return e;
         }
+        for (const auto &r : late)
+            if (int e = results_dma(*r.first, r.second)) return e;
         tr.mark("enqueued");
         MH_HIP(hipStreamSynchronize(c->d2h_stream));
         MH_HIP(hipStreamSynchronize(st));
