@@ -1054,6 +1054,18 @@ static uint32_t *host_words(void *p, uint64_t bytes) {
     return (uint32_t *)a.devicePointer;
 }
 
+// a and b in the same pinned host allocation (device addresses as far apart)
+static bool same_alloc(const void *a, const void *b) {
+    hipPointerAttribute_t x, y;
+    if (hipPointerGetAttributes(&x, a) != hipSuccess || hipPointerGetAttributes(&y, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return x.type == hipMemoryTypeHost && y.type == hipMemoryTypeHost && x.devicePointer &&
+           (const uint8_t *)y.devicePointer - (const uint8_t *)x.devicePointer ==
+               (const uint8_t *)b - (const uint8_t *)a;
+}
+
 // copy chunks of a long tx log: MH_TXLOG_CHUNKS (1..16, read once), default 4
 static uint64_t txlog_chunks() {
     static const uint64_t k = [] {
@@ -1115,12 +1127,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 const char *e = getenv("MH_TXLOG_INLINE_COPY");
                 return e ? atoi(e) : 1;
             }();
-            hipPointerAttribute_t a;
-            if (len && hipPointerGetAttributes(&a, buf) == hipSuccess)
-                pinned = a.type == hipMemoryTypeHost;
-            else
-                (void)hipGetLastError();
-            pinned = pinned && inl;
+            // the whole range in one pinned allocation (first and last byte)
+            pinned = inl && len && same_alloc(buf, buf + len - 1);
         }
         const uint64_t K = len < (16ull << 20) ? 1 : pinned ? txlog_chunks() : 2;
         std::vector<uint64_t> cut(K + 1, 0);
