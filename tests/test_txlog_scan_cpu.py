@@ -93,6 +93,35 @@ def test_scan_parallel_hop_matches_sequential(txl, orc):
     same(txl, orc, recs[:len(recs) // 2], max_entries=1 << 20)
 
 
+def test_scan_concurrent_callers(txl, orc):
+    """The hop's parked helper threads serve one call at a time; concurrent
+    callers (other contexts, other goroutines) start their own threads. Six
+    threads scanning different logs at once (some 1-8 MiB: the pool's smaller
+    chunks) all get the sequential parse's result."""
+    import threading
+    rng = np.random.default_rng(91)
+    raw, starts = _bulk_txlog(rng, 6000)
+    bad = bytearray(raw)
+    bad[starts[3333] + 89] = 9
+    cases = [(raw, {}), (bytes(bad), {}), (raw[:len(raw) - 77], {}), (raw[:starts[700]], {}),
+             (raw, {"max_txs": 2500}), (raw[:(3 << 20) + 5], {})]
+    want = [orc.txlog_validate(b, **kw)[:3] for b, kw in cases]
+    got = [None] * len(cases)
+
+    def run(i):
+        b, kw = cases[i]
+        for _ in range(5):
+            a = txl.txlog_scan(b, **kw)
+            got[i] = (a[0], a[1], a[2]) if got[i] in (None, (a[0], a[1], a[2])) else "mismatch"
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(cases))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert got == [tuple(w) for w in want]
+
+
 def test_scan_v0_entry_with_kv_metadata(txl, orc):
     """A v0 record whose entry carries KV metadata: TxEntryDigest_v1_1 fails
     the read with ErrMetadataUnsupported (tx.go:690-693 via readEntry,
