@@ -1109,8 +1109,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // it has landed, under the copy of the rest.
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
-        hipStream_t st = c->stream;
         MH_HIP(c->copy_lane());
+        hipStream_t st = c->stream;
         if (len) MH_HIP(c->s_txlog.ensure(len));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
         // A pinned log: K chunks from 16 MiB up (MH_TXLOG_CHUNKS, default 4)
