@@ -77,6 +77,19 @@ def timed(step, steps, warmup, sync):
     return (time.perf_counter() - t0) / steps
 
 
+def timed_k(ctx, fn, steps, warmup, sync):
+    """timed() with the context's per-kernel timing events off, then the same
+    steps again with them on for the kernel times (ctx.timing: steps + warmup
+    launches): the events add a few microseconds per launch, which a timed
+    region of many small launches would otherwise carry."""
+    t = timed(fn, steps, warmup, sync)
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    timed(fn, steps, warmup, sync)
+    ctx.set_timing(False)
+    return t
+
+
 def prewarm(step, sync, seconds):
     """Run `step` untimed for `seconds` so the GPU clock reaches its sustained
     value before the timed region (the headline bench's 2000 steps do the same;
@@ -298,10 +311,7 @@ def c5_ahtree(a, m, N, L, ctx, dev, sync):
                                                  bv.data_ptr(), ok.data_ptr(), None))
 
         prewarm(step, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        t = timed(step, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        t = timed_k(ctx, step, a.steps, a.warmup, sync)
         kms = ctx.timing("ahtree_verify")[0] / (a.steps + a.warmup)
         okh = ok.cpu().numpy().astype(bool)
         res[name] = {"M_proofs_per_s": round(P / t / 1e6, 1), "ms_per_step": round(t * 1e3, 3),
@@ -350,10 +360,7 @@ def ragged(a, m, N, L, ctx, dev, sync):
                                              lv.data_ptr(), root.data_ptr()))
 
     prewarm(step, sync, a.prewarm)
-    ctx.timing_reset()
-    ctx.set_timing(True)
-    t = timed(step, a.steps, a.warmup, sync)
-    ctx.set_timing(False)
+    t = timed_k(ctx, step, a.steps, a.warmup, sync)
     runs = a.steps + a.warmup
     tm = {k: round(ctx.timing(k)[0] / runs, 4) for k in ("varlen_sort", "entries_varlen", "reduce")}
     sha_ms = tm["entries_varlen"]
@@ -523,10 +530,7 @@ def values(a, m, N, L, ctx, dev, sync):
                                              dl.data_ptr(), dh.data_ptr(), ds.data_ptr()))
 
     prewarm(step, sync, a.prewarm)
-    ctx.timing_reset()
-    ctx.set_timing(True)
-    t = timed(step, a.steps, a.warmup, sync)
-    ctx.set_timing(False)
+    t = timed_k(ctx, step, a.steps, a.warmup, sync)
     runs = a.steps + a.warmup
     kms = ctx.timing("verify_values")[0] / runs
     sort_ms = ctx.timing("varlen_sort")[0] / runs
@@ -665,10 +669,7 @@ def run_single(a):
                                                      pay.data_ptr(), M, 32, None))
 
         prewarm(step, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        t = timed(step, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        t = timed_k(ctx, step, a.steps, a.warmup, sync)
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("aht_leaves", "aht_perfect",
                                                                    "aht_spine")}
         comps = M + 2 * (nd - M)
@@ -742,10 +743,7 @@ def run_single(a):
                 nterms.data_ptr(), pst.data_ptr()))
 
         prewarm(gen, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        tgen = timed(gen, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        tgen = timed_k(ctx, gen, a.steps, a.warmup, sync)
         assert int(pst.abs().sum().item()) == 0 and int((nterms != D).sum().item()) == 0
         gen_ms = ctx.timing("htree_proof")[0] / (a.steps + a.warmup)
         tamper = rng.random(P) < 0.10
@@ -762,10 +760,7 @@ def run_single(a):
                 terms.data_ptr(), digests.data_ptr(), roots.data_ptr(), ok.data_ptr()))
 
         prewarm(step, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        t = timed(step, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        t = timed_k(ctx, step, a.steps, a.warmup, sync)
         kms = ctx.timing("htree_verify")[0] / (a.steps + a.warmup)
         nok = int(ok.sum().item())
         exp = int((~tamper).sum())
@@ -838,14 +833,8 @@ def run_single(a):
 
         t_pageable = timed(step_pageable, a.steps, a.warmup, sync)
         prewarm(step, sync, a.prewarm)
-        t = timed(step, a.steps, a.warmup, sync)
-        # kernel times from a second pass with the per-kernel timing events on
-        # (they add ~0.15 ms per call over the call's ~25 launches, so the
-        # timed pass above runs without them)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        timed(step, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        # (the call's ~25 launches would carry ~0.15 ms of timing events)
+        t = timed_k(ctx, step, a.steps, a.warmup, sync)
         names = ("tx_hdr_from_raw", "txe_index", "txe_leaf", "small_roots", "seg_level", "tx_alh")
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
         # breakdown: the host hop alone (mh_txlog_scan, no headers out) and a
@@ -1050,10 +1039,7 @@ def run_single(a):
                                                     st.data_ptr(), scratch.data_ptr()))
 
         prewarm(step_dual, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        td = timed(step_dual, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        td = timed_k(ctx, step_dual, a.steps, a.warmup, sync)
         kd = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("pb_dual_size",
                                                                    "pb_dual_write")}
         assert int(st.abs().sum().item()) == 0
@@ -1097,10 +1083,7 @@ def run_single(a):
                 off2.data_ptr(), st.data_ptr(), scratch.data_ptr()))
 
         prewarm(step_incl, sync, a.prewarm)
-        ctx.timing_reset()
-        ctx.set_timing(True)
-        ti = timed(step_incl, a.steps, a.warmup, sync)
-        ctx.set_timing(False)
+        ti = timed_k(ctx, step_incl, a.steps, a.warmup, sync)
         ki = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("pb_incl_size",
                                                                    "pb_incl_write")}
         assert int(st.abs().sum().item()) == 0
