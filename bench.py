@@ -334,13 +334,18 @@ def cabi_main(a):
         step()
     md.synchronize()
     c0 = md.ctx_handle(0)
-    N.check(L.mh_ctx_timing_reset(c0))
-    N.check(L.mh_ctx_set_timing(c0, 1))
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     md.synchronize()
     elapsed = time.perf_counter() - t0
+    # device 0's kernel time from a pass after the timed region (the timing
+    # events stay out of it)
+    N.check(L.mh_ctx_timing_reset(c0))
+    N.check(L.mh_ctx_set_timing(c0, 1))
+    for _ in range(min(a.steps, 50)):
+        step()
+    md.synchronize()
     N.check(L.mh_ctx_set_timing(c0, 0))
     import ctypes as C
     ms, cnt = C.c_double(), C.c_uint64()
@@ -373,8 +378,8 @@ def cabi_main(a):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "k_entries_fixed", "kernel_ms": round(kern_ms, 4),
-                     "kernel_ms_source": "device 0's launches inside the timed region (one "
-                                         "build at a time: not contended)",
+                     "kernel_ms_source": "device 0's launches in a pass after the timed region "
+                                         "(one build at a time: not contended)",
                      "alg_bytes_per_launch": alg_bytes,
                      "per_step": {"achieved": round(step_achieved, 2),
                                   "frac": round(step_achieved / HBM_PEAK_GBS, 4)}},
