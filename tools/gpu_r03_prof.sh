@@ -5,7 +5,7 @@
 # beside --pmc).
 set -eo pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/prof_r03
+O=$R/gpurun_out/prof_r03b
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 2000 --warmup 3 --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/trace.log
