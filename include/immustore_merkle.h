@@ -38,6 +38,11 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* the library is built with hidden visibility: only these entry points are
+ * exported */
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility push(default)
+#endif
 
 #define MH_ABI_VERSION 1
 
@@ -815,6 +820,9 @@ int mh_dev_dual_proof_v2_pb_batch(mh_ctx *ctx, int phase, const uint8_t *dlog, u
                                   const uint8_t *md_blob, uint8_t *out, uint64_t out_cap,
                                   uint64_t *off, int32_t *status, void *scratch);
 
+#if defined(__GNUC__) || defined(__clang__)
+#pragma GCC visibility pop
+#endif
 #ifdef __cplusplus
 }
 #endif
