@@ -1162,7 +1162,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // and pinned index staging, all indexed from the group's first record
         struct Grp {
             uint64_t t0 = 0, t1 = 0, e0 = 0, E = 0, wmax = 0, k = 0;
-            bool small = true, fetched = false;
+            bool small = true, fetched = false, host_done = false;
             uint8_t *base = nullptr;
             uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
             uint64_t b_rec, b_ver, b_lv, b_h, b_es, b_ro, b_ap, b_lo, b_eh, b_s, b_a, b_st, idx_bytes;
@@ -1241,6 +1241,28 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             MhTxHeader *hd = (MhTxHeader *)(base + g.b_h);
             if (!g.fetched)
                 MH_HIP(launch_fetch_host(st, HostRuns{{g.pro, g.pap, g.plo}, {ro, ap, lo}, {nt, nt, nt + 1}}));
+            static const bool fused = [] {
+                const char *e = getenv("MH_TXLOG_FUSED");
+                return !e || atoi(e) != 0;
+            }();
+            if (fused && g.small && npe + nph == 0) {  // the whole chain in one launch
+                // pinned outputs: the kernel writes the results there itself
+                TxlogHostOut ho;
+                uint32_t *hs = status_out ? host_words(status_out + g.t0, nt * 4) : nullptr;
+                uint32_t *ha = alh_out ? host_words(alh_out + g.t0 * 32, nt * 32) : nullptr;
+                uint32_t *hh = hdrs_out ? host_words(hdrs_out + g.t0, nt * sizeof(mh_tx_header)) : nullptr;
+                if ((!status_out || hs) && (!alh_out || ha) && (!hdrs_out || hh) &&
+                    ((uintptr_t)hh & 7) == 0) {
+                    ho.status = hs;
+                    ho.alh = ha;
+                    ho.hdrs = reinterpret_cast<uint64_t *>(hh);
+                    g.host_done = true;
+                }
+                MH_HIP(launch_txlog_group(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_s,
+                                          base + g.b_eh, base + g.b_a,
+                                          (int32_t *)(base + g.b_st), ho, g.wmax));
+                return MH_OK;
+            }
             MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, db, ro, hd, es));
             MH_HIP(launch_txe_index(st, c->tm(), nt, db, hd, es, lo, rec, base + g.b_ver));
             if (npe + nph)
@@ -1281,6 +1303,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             return MH_OK;
         };
         auto results = [&](const Grp &g, hipEvent_t ev) -> int {
+            if (g.host_done) return MH_OK;  // stored by the group's kernel
             const uint64_t nt = g.t1 - g.t0, t0 = g.t0;
             hipStream_t ds = c->d2h_stream;
             uint32_t *hs = status_out ? host_words(status_out + t0, nt * 4) : nullptr;

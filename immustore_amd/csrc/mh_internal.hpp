@@ -256,6 +256,23 @@ hipError_t launch_txlog_patch(hipStream_t st, uint64_t ne, const uint64_t *e_idx
                               const uint64_t *e_off, uint64_t *rec_off, uint64_t nh,
                               const uint64_t *h_idx, const uint64_t *h_val, MhTxHeader *hdrs);
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
+// a14 for a group of records whose trees have <= 64 leaves, one launch:
+// headers, entry walk, entry digests + leaves, tx trees, Eh into hdrs and
+// eh_out, Alh vs the stored one (statuses).  Arrays are indexed from the
+// group's first record; leaf_off has ntx + 1 entries.
+// ho (device addresses of pinned host arrays, each member nullable, indexed
+// from the group's first record like the device arrays): results written
+// there by the kernel too.  hdrs 8-byte aligned, alh / status 4-byte.
+struct TxlogHostOut {
+    uint32_t *status = nullptr;
+    uint32_t *alh = nullptr;
+    uint64_t *hdrs = nullptr;
+};
+hipError_t launch_txlog_group(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                              const uint64_t *rec_off, const uint64_t *alh_off,
+                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *scratch,
+                              uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
+                              const TxlogHostOut &ho, uint64_t wmax);
 // up to three runs of words pinned host memory -> HBM by a kernel (k_fetch_host)
 struct HostRuns {
     const uint64_t *src[3];

@@ -60,6 +60,47 @@ __device__ __forceinline__ void put_be(uint8_t *&o, uint64_t v, int n) {
 // One header per lane: innerHash (message assembled in the lane's scratch
 // slot, <= 356 bytes) then Alh.  eh_src (nullable) replaces hdrs[p].eh;
 // expect (nullable) turns the Alh into a pass / MH_ERR_CORRUPTED_DATA status.
+// e: the stored Alh to compare against (nullable).
+__device__ __forceinline__ void tx_alh_one(uint64_t p, const MhTxHeader &h,
+                                           const uint8_t *__restrict__ md_blob,
+                                           const uint8_t *__restrict__ eh, uint8_t *__restrict__ msg,
+                                           const uint8_t *__restrict__ e,
+                                           uint8_t *__restrict__ inner_out,
+                                           uint8_t *__restrict__ alh_out,
+                                           int32_t *__restrict__ status) {
+    uint8_t *o = msg;
+    put_be(o, (uint64_t)h.ts, 8);
+    put_be(o, h.version, 2);
+    if (h.version == 0) {
+        put_be(o, h.nentries, 2);
+    } else {
+        put_be(o, h.md_len, 2);
+        const uint8_t *md = md_blob + h.md_off;
+        for (uint32_t k = 0; k < h.md_len; k++) *o++ = md[k];
+        put_be(o, h.nentries, 4);
+    }
+    for (int k = 0; k < 32; k++) *o++ = eh[k];
+    put_be(o, h.bl_tx_id, 8);
+    for (int k = 0; k < 32; k++) *o++ = h.bl_root[k];
+    uint32_t inner[8], prev[8], a[8];
+    sha256_bytes(msg, (uint64_t)(o - msg), -1, inner);
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = ld_be32_aligned(h.prev_alh + 4 * j);
+    alh_hash(h.id, prev, inner, a);
+    if (inner_out) store_digest(inner_out + p * 32, inner);
+    if (alh_out) store_digest(alh_out + p * 32, a);
+    if (status) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t v = ((uint32_t)e[4 * j] << 24) | ((uint32_t)e[4 * j + 1] << 16) |
+                               ((uint32_t)e[4 * j + 2] << 8) | e[4 * j + 3];
+            x |= v ^ a[j];
+        }
+        status[p] = x ? MH_ERR_CORRUPTED_DATA : MH_OK;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_tx_alh(uint64_t n, const MhTxHeader *__restrict__ hdrs,
                                                 const uint8_t *__restrict__ md_blob,
                                                 const uint8_t *__restrict__ eh_src,
@@ -72,40 +113,9 @@ __global__ __launch_bounds__(256) void k_tx_alh(uint64_t n, const MhTxHeader *__
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const MhTxHeader &h = hdrs[p];
-    uint8_t *msg = scratch + p * kTxInnerStride;
-    uint8_t *o = msg;
-    put_be(o, (uint64_t)h.ts, 8);
-    put_be(o, h.version, 2);
-    if (h.version == 0) {
-        put_be(o, h.nentries, 2);
-    } else {
-        put_be(o, h.md_len, 2);
-        const uint8_t *md = md_blob + h.md_off;
-        for (uint32_t k = 0; k < h.md_len; k++) *o++ = md[k];
-        put_be(o, h.nentries, 4);
-    }
-    const uint8_t *eh = eh_src ? eh_src + p * 32 : h.eh;
-    for (int k = 0; k < 32; k++) *o++ = eh[k];
-    put_be(o, h.bl_tx_id, 8);
-    for (int k = 0; k < 32; k++) *o++ = h.bl_root[k];
-    uint32_t inner[8], prev[8], a[8];
-    sha256_bytes(msg, (uint64_t)(o - msg), -1, inner);
-#pragma unroll
-    for (int j = 0; j < 8; j++) prev[j] = ld_be32_aligned(h.prev_alh + 4 * j);
-    alh_hash(h.id, prev, inner, a);
-    if (inner_out) store_digest(inner_out + p * 32, inner);
-    if (alh_out) store_digest(alh_out + p * 32, a);
-    if (status) {
-        const uint8_t *e = expect + (expect_off ? expect_off[p] : p * 32);
-        uint32_t x = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t v = ((uint32_t)e[4 * j] << 24) | ((uint32_t)e[4 * j + 1] << 16) |
-                               ((uint32_t)e[4 * j + 2] << 8) | e[4 * j + 3];
-            x |= v ^ a[j];
-        }
-        status[p] = x ? MH_ERR_CORRUPTED_DATA : MH_OK;
-    }
+    tx_alh_one(p, h, md_blob, eh_src ? eh_src + p * 32 : h.eh, scratch + p * kTxInnerStride,
+               status ? expect + (expect_off ? expect_off[p] : p * 32) : nullptr, inner_out,
+               alh_out, status);
 }
 
 // leafFor(d) = SHA256(0x00 || d)  (verification.go:237-242, ahtree.go:288-292)
@@ -198,20 +208,24 @@ __global__ __launch_bounds__(256) void k_advance_chain(
 // Entry digest (tx.go:690-731) -- and, with leaf != 0, its htree leaf
 // SHA256(0x00 || digest) (htree.go:79-83) -- hashed in place from the raw
 // tx-log entry record (sha256_skip12): no message buffer, no offsets scan.
+__device__ __forceinline__ void txe_digest_one(const uint8_t *__restrict__ r, uint8_t ver,
+                                               uint32_t d[8]) {
+    const uint32_t ml = ((uint32_t)r[0] << 8) | r[1];
+    const uint32_t kl = ((uint32_t)r[2 + ml] << 8) | r[3 + ml];
+    if (ver == 1)
+        sha256_skip12(r, 4 + ml + kl, d);
+    else
+        sha256_skip12(r + 4 + ml, kl, d);
+}
+
 __global__ __launch_bounds__(256) void k_txe_leaf(uint64_t n, const uint8_t *__restrict__ buf,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint8_t *__restrict__ ver, int leaf,
                                                   uint8_t *__restrict__ out) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
-    const uint8_t *r = buf + rec_off[e];
-    const uint32_t ml = ((uint32_t)r[0] << 8) | r[1];
-    const uint32_t kl = ((uint32_t)r[2 + ml] << 8) | r[3 + ml];
     uint32_t d[8];
-    if (ver[e] == 1)
-        sha256_skip12(r, 4 + ml + kl, d);
-    else
-        sha256_skip12(r + 4 + ml, kl, d);
+    txe_digest_one(buf + rec_off[e], ver[e], d);
     if (leaf) {
         uint32_t h[8];
         leaf_hash(d, h);
@@ -224,20 +238,15 @@ __global__ __launch_bounds__(256) void k_txe_leaf(uint64_t n, const uint8_t *__r
 // TxHeader of each record from the raw tx-log bytes (the fields readHeader
 // reads, tx.go:419-518; the host hop already validated the structure), plus
 // the offset of its first entry.  md_off is relative to the log buffer.
-__global__ __launch_bounds__(256) void k_tx_hdr_from_raw(uint64_t ntx, const uint8_t *__restrict__ buf,
-                                                         const uint64_t *__restrict__ rec_off,
-                                                         MhTxHeader *__restrict__ hdrs,
-                                                         uint64_t *__restrict__ ent_start) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntx) return;
-    const uint64_t p = rec_off[t];
+// returns the offset of the record's first entry
+__device__ __forceinline__ uint64_t tx_hdr_one(const uint8_t *__restrict__ buf, uint64_t p,
+                                               MhTxHeader &h) {
     const uint8_t *r = buf + p;
     auto be = [&](int o, int n) {
         uint64_t v = 0;
         for (int k = 0; k < n; k++) v = v << 8 | r[o + k];
         return v;
     };
-    MhTxHeader h;
     h.id = be(0, 8);
     h.ts = (int64_t)be(8, 8);
     h.bl_tx_id = be(16, 8);
@@ -259,8 +268,18 @@ __global__ __launch_bounds__(256) void k_tx_hdr_from_raw(uint64_t ntx, const uin
         h.nentries = (uint32_t)be(92 + h.md_len, 4);
         q = 96 + h.md_len;
     }
+    return p + q;
+}
+
+__global__ __launch_bounds__(256) void k_tx_hdr_from_raw(uint64_t ntx, const uint8_t *__restrict__ buf,
+                                                         const uint64_t *__restrict__ rec_off,
+                                                         MhTxHeader *__restrict__ hdrs,
+                                                         uint64_t *__restrict__ ent_start) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx) return;
+    MhTxHeader h;
+    ent_start[t] = tx_hdr_one(buf, rec_off[t], h);
     hdrs[t] = h;
-    ent_start[t] = p + q;
 }
 
 __global__ __launch_bounds__(256) void k_put_eh(uint64_t n, const uint8_t *__restrict__ eh,
@@ -595,6 +614,169 @@ hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const 
         hipLaunchKernelGGL(k_small_roots, dim3(grid_for(ntrees, 256)), dim3(256), kNodeTabBytes, st,
                            ntrees, leaf_off, nodes, roots);
     }
+    return hipGetLastError();
+}
+
+// The whole a14 check of a group of tx-log records whose trees are small, in
+// ONE launch (tx.go:533-630 per record: header, entry walk, entry digests and
+// leaves, the tx's htree, innerHash + Alh against the stored Alh).  A
+// 256-thread workgroup takes TPW = 512 >> lgp consecutive records (every tx
+// <= P = 1 << lgp entries, P <= 64): lane k < TPW parses record k's header
+// and walks its entries into LDS; every thread then hashes entry digests and
+// leaves (two entry slots per thread), the trees are reduced level-parallel in
+// LDS exactly as k_small_roots_pack does (htree.go:85-110), and lane k ends
+// with innerHash + Alh (tx.go:249-319).  Replaces the six dependent launches
+// of a group (header, entry index, leaves, small roots, Alh, Eh copy), whose
+// latencies added up after the last chunk of the log had landed.  Groups with
+// metadata patches (a header or entry whose metadata the host re-encoded)
+// keep the multi-launch path.
+static_assert(sizeof(MhTxHeader) == 17 * 8, "headers are staged as 17 words");
+
+__global__ __launch_bounds__(256) void k_txlog_group(
+    uint64_t ntx, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ rec_off,
+    const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
+    MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ scratch, uint8_t *__restrict__ eh_out,
+    uint8_t *__restrict__ alh_out, int32_t *__restrict__ status, TxlogHostOut ho, int lgp,
+    int warm) {
+    __shared__ uint32_t nb[2][512][9];  // +1 word pad, as k_small_roots_pack; headers staged here last
+    __shared__ uint64_t erec[1024];     // entry record offsets (tree k at k * P); Alh staged here last
+    __shared__ uint8_t tver[256];
+    const int P = 1 << lgp, TPW = 512 >> lgp;
+    const int tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TPW;
+    const uint64_t nmine = min((uint64_t)TPW, ntx - t0);  // records of this workgroup
+    const bool mine = (uint64_t)tid < nmine;            // this lane owns record t0 + tid
+    if (warm) {
+        // The workgroup's records are contiguous in the log (record t ends
+        // with its stored Alh at alh_off[t]): every thread touches 16-byte
+        // pieces of that range at once, so the serial header / entry walks
+        // below hit L2 instead of paying an HBM round trip per dependent load.
+        const uint64_t lo = rec_off[t0] & ~15ull, hi = alh_off[t0 + nmine - 1] + 32;
+        uint32_t acc = 0;
+        for (uint64_t p = lo + 16 * (uint64_t)tid; p < hi; p += 16 * 256)
+            acc ^= reinterpret_cast<const uint4 *>(buf + p)->x;
+        asm volatile("" ::"v"(acc));
+    }
+    if (mine) {
+        const uint64_t t = t0 + tid;
+        MhTxHeader h;
+        uint64_t q = tx_hdr_one(buf, rec_off[t], h);  // tx.go:419-518
+        hdrs[t] = h;
+        tver[tid] = (uint8_t)h.version;
+        const uint64_t w = leaf_off[t + 1] - leaf_off[t];
+        for (uint64_t j = 0; j < w; j++) {  // tx.go:578-585 (lengths validated by the hop)
+            const uint32_t ml = ((uint32_t)buf[q] << 8) | buf[q + 1];
+            const uint32_t kl = ((uint32_t)buf[q + 2 + ml] << 8) | buf[q + 3 + ml];
+            erec[tid * P + j] = q;
+            q += 4 + ml + kl + 12 + 32;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < TPW * P; i += 256) {  // entry digest + leaf (tx.go:690-731, htree.go:79-83)
+        const int k = i >> lgp, j = i & (P - 1);
+        const uint64_t t = t0 + k;
+        if (t < ntx && (uint64_t)j < leaf_off[t + 1] - leaf_off[t]) {
+            uint32_t d[8], h[8];
+            txe_digest_one(buf + erec[i], tver[k], d);
+            leaf_hash(d, h);
+#pragma unroll
+            for (int q = 0; q < 8; q++) nb[0][i][q] = h[q];
+        }
+    }
+    int cur = 0;
+    for (int l = 1; l <= lgp; l++) {  // htree.go:85-110, every tree of the workgroup at once
+        __syncthreads();
+        const int S = P >> l;
+        if (tid < TPW * S) {
+            const int k = tid / S, j = tid - k * S;
+            const uint64_t t = t0 + k;
+            if (t < ntx) {
+                const uint64_t w = leaf_off[t + 1] - leaf_off[t];
+                const uint64_t wp = (w + (1ull << (l - 1)) - 1) >> (l - 1);
+                const int a = k * P + 2 * j;
+                if ((uint64_t)(2 * j + 1) < wp) {
+                    uint32_t x[8], y[8], h[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        x[q] = nb[cur][a][q];
+                        y[q] = nb[cur][a + 1][q];
+                    }
+                    node_hash_g(x, y, h);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) nb[cur ^ 1][k * P + j][q] = h[q];
+                } else if ((uint64_t)(2 * j) < wp) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) nb[cur ^ 1][k * P + j][q] = nb[cur][a][q];
+                }
+            }
+        }
+        cur ^= 1;
+    }
+    __syncthreads();
+    const uint64_t t = t0 + tid;
+    uint32_t eh[8];
+    if (mine) {
+        if (leaf_off[t + 1] == leaf_off[t]) {  // no entries: SHA256(nil), htree.go:73-77
+            load_digest(kEmptyRootDev, eh);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) eh[q] = nb[cur][tid * P][q];
+        }
+    }
+    __syncthreads();  // nb and erec are free: results are staged there
+    uint64_t *hst = reinterpret_cast<uint64_t *>(&nb[0][0][0]);  // nmine headers, 17 words each
+    uint32_t *ast = reinterpret_cast<uint32_t *>(erec);          // nmine Alh, 8 words each
+    if (mine) {
+        store_digest(eh_out + t * 32, eh);
+        uint32_t *he = reinterpret_cast<uint32_t *>(hdrs[t].eh);  // 8-byte aligned field
+#pragma unroll
+        for (int q = 0; q < 8; q++) he[q] = bswap(eh[q]);
+        tx_alh_one(t, hdrs[t], buf, eh_out + t * 32, scratch + t * kTxInnerStride,
+                   buf + alh_off[t], nullptr, alh_out, status);
+        // results straight into the caller's pinned arrays (no store kernel
+        // after the group): the lane's own status, the workgroup's Alh and
+        // headers staged in LDS and written below as contiguous runs
+        if (ho.status) ho.status[t] = (uint32_t)status[t];
+        if (ho.alh) {
+            const uint32_t *a = reinterpret_cast<const uint32_t *>(alh_out + t * 32);
+#pragma unroll
+            for (int q = 0; q < 8; q++) ast[tid * 8 + q] = a[q];
+        }
+        if (ho.hdrs) {
+            const uint64_t *hw = reinterpret_cast<const uint64_t *>(hdrs + t);
+#pragma unroll
+            for (int q = 0; q < 17; q++) hst[tid * 17 + q] = hw[q];
+        }
+    }
+    if (ho.alh || ho.hdrs) {  // kernel arguments: uniform
+        __syncthreads();
+        if (ho.alh)
+            for (uint64_t i = tid; i < nmine * 8; i += 256) ho.alh[t0 * 8 + i] = ast[i];
+        if (ho.hdrs)
+            for (uint64_t i = tid; i < nmine * 17; i += 256) ho.hdrs[t0 * 17 + i] = hst[i];
+    }
+    if (ho.status || ho.alh || ho.hdrs) __threadfence_system();
+}
+
+hipError_t launch_txlog_group(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                              const uint64_t *rec_off, const uint64_t *alh_off,
+                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *scratch,
+                              uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
+                              const TxlogHostOut &ho, uint64_t wmax) {
+    if (!ntx) return hipSuccess;
+    if (wmax > 64 || ((uintptr_t)ho.hdrs & 7) || ((uintptr_t)ho.alh & 3) || ((uintptr_t)ho.status & 3))
+        return hipErrorInvalidValue;
+    int lgp = 1;
+    while ((1ull << lgp) < wmax) lgp++;
+    const uint64_t tpw = 512 >> lgp;
+    static const int warm = [] {
+        const char *e = getenv("MH_TXLOG_WARM");
+        return e ? atoi(e) : 1;
+    }();
+    TimerScope ts(tm, "txlog_group", st);
+    hipLaunchKernelGGL(k_txlog_group, dim3(grid_for(ntx, (unsigned)tpw)), dim3(256), 0, st, ntx,
+                       buf, rec_off, alh_off, leaf_off, hdrs, scratch, eh_out, alh_out, status, ho,
+                       lgp, warm);
     return hipGetLastError();
 }
 
