@@ -321,6 +321,57 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
             assert np.array_equal(a[3], c[3])
 
 
+def test_txlog_validate_pinned_last_chunk(m, ctx, orc):
+    """A pinned log's last chunk is not DMA'd when its records form a
+    small-tree group: that group's kernel fetches them over PCIe itself.  Ends
+    that are not 16-byte multiples, errors / max_txs / a corrupted hVal inside
+    the last chunk, and a wide tx or re-encoded metadata at the end (the copy
+    is then issued after all) -- equal to the oracle and to the pageable call,
+    headers included."""
+    import torch
+    from tx_util import metadata_logs
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(31)
+    raw, starts = _bulk_txlog(rng, 9500)
+    assert len(raw) >= (16 << 20)
+    last_cut = _chunk_cuts(len(raw))[-1]
+    late = [k for k in range(len(starts)) if starts[k] > last_cut + 4096]
+    assert len(late) > 50
+    cap = 20000
+    outs = (torch.empty(cap * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy().view(TX_HEADER),
+            torch.empty(cap * 32, dtype=torch.uint8).pin_memory().numpy().reshape(cap, 32),
+            torch.empty(cap, dtype=torch.int32).pin_memory().numpy())
+
+    def same(buf, **kw):
+        pin = torch.empty(len(buf), dtype=torch.uint8).pin_memory()
+        pin.numpy()[:] = np.frombuffer(buf, np.uint8)
+        a = m.txlog_validate(pin.numpy(), ctx=ctx, out=outs, **kw)
+        b = orc.txlog_validate(buf, **kw)
+        c = m.txlog_validate(buf, ctx=ctx, **kw)
+        assert (a[0], a[1], a[2]) == (b[0], b[1], b[2]) == (c[0], c[1], c[2]), kw
+        assert np.array_equal(a[4], b[3]) and list(a[5]) == list(b[4]), kw
+        assert np.array_equal(a[3], c[3]), kw
+        return a
+
+    same(raw)
+    odd = [k for k in late if starts[k] % 16][-1]
+    a = same(raw[:starts[odd]])  # ends mid 16-byte piece
+    assert a[1] == odd
+    k = late[len(late) // 2]
+    bad = bytearray(raw)
+    bad[starts[k] + 89] = 7  # unknown header version inside the last chunk
+    a = same(bytes(bad))
+    assert (a[0], a[1], a[2]) == (17, k, starts[k])
+    bad = bytearray(raw)
+    bad[starts[k + 1] - 33] ^= 1  # the last hVal of record k
+    a = same(bytes(bad))
+    same(raw, max_txs=k)
+    same(raw[:len(raw) - 7])
+    md = b"".join(r for name, r in metadata_logs(orc) if name == "noncanonical_sealed_canonical")
+    same(raw + md * 50)
+    same(raw + _synthetic_txlog(rng, 20, orc, max_entries=300))
+
+
 def test_dual_proof_v2_fixture_cases(m, ctx, orc, fixtures):
     seen = set()
     for name, fx in fixtures.items():
