@@ -322,12 +322,12 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
 
 
 def test_txlog_validate_pinned_last_chunk(m, ctx, orc):
-    """A pinned log's last chunk is not DMA'd when its records form a
-    small-tree group: that group's kernel fetches them over PCIe itself.  Ends
-    that are not 16-byte multiples, errors / max_txs / a corrupted hVal inside
-    the last chunk, and a wide tx or re-encoded metadata at the end (the copy
-    is then issued after all) -- equal to the oracle and to the pageable call,
-    headers included."""
+    """The last copy chunk of a pinned log (its group's kernel runs right
+    after it lands and stores the results into the pinned outputs itself):
+    ends that are not 16-byte multiples, errors / max_txs / a corrupted hVal
+    inside the last chunk, and a wide tx or re-encoded metadata at the end (the
+    rest-group path) -- equal to the oracle and to the pageable call, headers
+    included."""
     import torch
     from tx_util import metadata_logs
     from immustore_amd.txlayer import TX_HEADER
