@@ -78,7 +78,11 @@ __global__ __launch_bounds__(512) void k_htree_verify(uint64_t np, const uint64_
 // over term h is up to two hashes: "A" (ci = H(h, ci), only when the first
 // tree's path turns here) and "B" (cj = H(h, cj) or H(cj, h)); `phase`
 // walks them in order.
-__global__ __launch_bounds__(512) void k_ahtree_verify(int kind, uint64_t np,
+// KIND is a template argument so that each kind is compiled on its own: the
+// two inclusion kinds (one hash per term, no consistency state) then have the
+// registers to load the next term under the current step's hash.
+template <int KIND>
+__global__ __launch_bounds__(512) void k_ahtree_verify(uint64_t np,
                                                        const uint64_t *__restrict__ vi,
                                                        const uint64_t *__restrict__ vj,
                                                        const uint64_t *__restrict__ term_off,
@@ -89,7 +93,8 @@ __global__ __launch_bounds__(512) void k_ahtree_verify(int kind, uint64_t np,
                                                        uint8_t *__restrict__ eval_out) {
     extern __shared__ uint32_t tab[];
     node_tab_init(tab);
-    const bool cons = kind == MH_AHT_CONSISTENCY;
+    constexpr int kind = KIND;
+    constexpr bool cons = kind == MH_AHT_CONSISTENCY;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np;
          p += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t i = vi[p], j = vj[p];
@@ -123,9 +128,23 @@ __global__ __launch_bounds__(512) void k_ahtree_verify(int kind, uint64_t np,
             }
         }
         int phase = 0;
+        uint4 na = make_uint4(0, 0, 0, 0), nb = na;  // inclusion: term t, loaded one step ahead
+        if (!cons && run && t < t1) {
+            na = reinterpret_cast<const uint4 *>(terms + t * 32)[0];
+            nb = reinterpret_cast<const uint4 *>(terms + t * 32)[1];
+        }
         while (run && t < t1) {
             uint32_t h[8], L[8], R[8], o[8];
-            load_digest(terms + t * 32, h);
+            if (cons) {
+                load_digest(terms + t * 32, h);
+            } else {
+                h[0] = bswap(na.x); h[1] = bswap(na.y); h[2] = bswap(na.z); h[3] = bswap(na.w);
+                h[4] = bswap(nb.x); h[5] = bswap(nb.y); h[6] = bswap(nb.z); h[7] = bswap(nb.w);
+                if (t + 1 < t1) {
+                    na = reinterpret_cast<const uint4 *>(terms + (t + 1) * 32)[0];
+                    nb = reinterpret_cast<const uint4 *>(terms + (t + 1) * 32)[1];
+                }
+            }
             bool h_left, to_c;
             const bool both = (x % 2 == 1) || (x == y);
             if (!cons) {
@@ -225,9 +244,13 @@ hipError_t launch_ahtree_verify(hipStream_t st, Timer *tm, int kind, uint64_t np
                                 uint8_t *ok, uint8_t *eval_out) {
     if (!np) return hipSuccess;
     if (tm) tm->begin("ahtree_verify", st);
-    hipLaunchKernelGGL(k_ahtree_verify, dim3(resident_grid((const void *)k_ahtree_verify, 512, np)),
-                       dim3(512), kNodeTabBytes, st, kind, np, i, j,
-                       term_off, terms, a, b, ok, eval_out);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(resident_grid((const void *)kern, 512, np)), dim3(512),
+                           kNodeTabBytes, st, np, i, j, term_off, terms, a, b, ok, eval_out);
+    };
+    if (kind == MH_AHT_INCLUSION) go(k_ahtree_verify<MH_AHT_INCLUSION>);
+    else if (kind == MH_AHT_CONSISTENCY) go(k_ahtree_verify<MH_AHT_CONSISTENCY>);
+    else go(k_ahtree_verify<MH_AHT_LAST_INCLUSION>);
     if (tm) tm->end(st);
     return hipGetLastError();
 }
