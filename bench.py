@@ -71,7 +71,10 @@ def parse():
                         "configs[3], 2^23 x 4 KiB per GPU (2^26 entries at 8 GPUs); c3: "
                         "configs[2] ahtree append of 10^7; c5: configs[4] proof re-hash "
                         "(c3 / c5: one GPU, GPU part from bench_workloads.py)")
-    p.add_argument("--entries", type=int, default=None, help="override entries per GPU")
+    p.add_argument("--entries", type=int, default=None,
+                   help="override entries per GPU (--api cabi --config c3: total appends)")
+    p.add_argument("--n0", type=int, default=10 ** 6 + 3,
+                   help="--api cabi --config c3: size of the tree the batch is appended onto")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-check", action="store_true",
                    help="only bring up the N-rank process group (gloo, no GPU work) and print "
@@ -92,14 +95,117 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(seconds):
-    """Oracle (C restatement, oracle/) on the host, SHA-NI if present: one thread
-    (the Go reference builds a tx's tree in one goroutine) and all the host
-    threads this process may use (capped at 16, the GPU box's CPU share),
-    splitting the leaves into power-of-two chunks as the GPU path does."""
+# ------------------------------------------------------------------ root check
+# After the timed region every multi-GPU (and single-GPU) line proves its own
+# result: the oracle (oracle/, the CPU restatement of htree.go:68-113 and
+# tx.go:332-355 pinned by the Go-written stores) rebuilds each shard from the
+# same splitmix64 stream and BE64 keys the devices generated, and the top
+# levels over the shard roots; the device roots must equal it bit for bit.
+# The oracle is the checker here, never the thing measured.
+SPLITMIX_G = 0x9E3779B97F4A7C15
+CHECK_BLOCK_BITS = 14      # sampled mode: 2^14-entry blocks = level-14 nodes
+FULL_CHECK_BYTES = 2 << 30  # shards up to this many value bytes: rebuilt whole
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as orc
     orc.use_shani(True)
+    return orc
+
+
+def host_threads(share=1):
+    """Host threads this process may use, split over `share` processes."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return max(1, avail // max(share, 1))
+
+
+def shard_block(orc, seed, key0, e0, cnt, val):
+    """Entries [e0, e0 + cnt) of a shard whose values came from
+    mh_dev_fill_random(seed) and keys from mh_dev_fill_keys_be64(key0): the
+    splitmix64 stream from word e0 * val / 8 (word w = mix(seed + (w+1) G))."""
+    s = (seed + (e0 * val // 8) * SPLITMIX_G) & 0xFFFFFFFFFFFFFFFF
+    vals = orc.fill_random(cnt * val, s).reshape(cnt, val)
+    keys = np.frombuffer(np.arange(key0 + e0, key0 + e0 + cnt, dtype=">u8").tobytes(),
+                         np.uint8).reshape(cnt, KEY_LEN)
+    return keys, vals
+
+
+def oracle_shard_root(orc, n, val, seed, key0, levels_dev, threads):
+    """The oracle's root of one shard (v1 entries, keys BE64(key0 + i)).
+    full: every entry rebuilt (C2: 1 GiB per shard).  sampled (C4, 32 GiB per
+    shard): three 2^14-entry blocks rebuilt and compared with the device's
+    level-14 nodes, and the levels above rebuilt by the oracle from those
+    nodes.  -> (root, blocks_ok, mode)."""
+    if n * val <= FULL_CHECK_BYTES or n <= (1 << CHECK_BLOCK_BITS):
+        keys, vals = shard_block(orc, seed, key0, 0, n, val)
+        _, _, r = orc.build_entries_fixed(1, keys, vals, nthreads=threads, want_levels=False)
+        return r, True, "full"
+    import immustore_amd as m
+    b, B = CHECK_BLOCK_BITS, 1 << CHECK_BLOCK_BITS
+    nb = -(-n // B)
+    off = m.level_offset(n, b)
+    nodes = levels_dev[off * 32:(off + nb) * 32].cpu().numpy().reshape(nb, 32)
+    rng = np.random.default_rng(seed)
+    picks = sorted({0, nb - 1, int(rng.integers(0, nb))})
+    ok = True
+    for i in picks:
+        e0 = i * B
+        keys, vals = shard_block(orc, seed, key0, e0, min(B, n - e0), val)
+        _, _, r = orc.build_entries_fixed(1, keys, vals, nthreads=threads, want_levels=False)
+        ok &= r == nodes[i].tobytes()
+    r = reduce_nodes(orc, [bytes(x) for x in nodes])
+    return r, ok, "sampled: level-%d blocks %s rebuilt + levels above" % (b, picks)
+
+
+def corrupt_hook(vals, who):
+    """Test-only (MH_BENCH_CORRUPT=<rank or device>): flip one value byte of
+    that shard after it was generated, so the root check must fail."""
+    if os.environ.get("MH_BENCH_CORRUPT", "") == str(who):
+        vals[100:101].bitwise_xor_(1)
+        return True
+    return False
+
+
+def reduce_nodes(orc, nodes):
+    """The levels above a row of inner nodes with htree's pairing rule
+    (htree.go:85-110: h = SHA256(0x01 || l || r), an odd last node moves up
+    unchanged) -- no leaf hashing."""
+    lvl = list(nodes)
+    while len(lvl) > 1:
+        nxt = [orc.sha256(b"\x01" + lvl[i] + lvl[i + 1]) for i in range(0, len(lvl) - 1, 2)]
+        if len(lvl) % 2:
+            nxt.append(lvl[-1])
+        lvl = nxt
+    return lvl[0]
+
+
+def global_expected(orc, shard_roots):
+    """Root over the shard roots = the root of the whole tree when every shard
+    holds a power-of-two count (SURVEY.md finding 3)."""
+    return reduce_nodes(orc, shard_roots)
+
+
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cpu.max), or None if unlimited /
+    unreadable: the box's CPU share can be far below what affinity shows."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(seconds):
+    """Oracle (C restatement, oracle/) on the host, SHA-NI if present: one thread
+    (the Go reference builds a tx's tree in one goroutine), every host thread
+    this process may use (sched_getaffinity, SURVEY 8(d) "all cores") and 16
+    threads (the GPU box's CPU share), splitting the leaves into power-of-two
+    chunks as the GPU path does."""
+    orc = _oracle()
 
     def run(n, threads, reps=5):
         """1 warm-up, then the median of `reps` timed builds."""
@@ -120,12 +226,10 @@ def cpu_baseline(seconds):
     n = int(min(N_ENTRIES, max(probe, probe * seconds / 6 / max(dt, 1e-6))))
     n = 1 << (n.bit_length() - 1)
     dt1 = run(n, 1)
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))
-    dtm = run(N_ENTRIES, threads)
+    avail = host_threads()
+    dta = run(N_ENTRIES, avail)
+    t16 = min(16, avail)
+    dt16 = dta if t16 == avail else run(N_ENTRIES, t16)
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -134,14 +238,22 @@ def cpu_baseline(seconds):
                 break
     except OSError:
         pass
+    gib = lambda t: round(N_ENTRIES * VAL_LEN / t / 2 ** 30, 4)  # noqa: E731
     return {
-        "value": round(N_ENTRIES * VAL_LEN / dtm / 2 ** 30, 4),
+        "value": gib(dta),
         "unit": "GiB/s",
-        "cores": threads,
+        "cores": avail,
+        "cores_available": avail,
+        "cgroup_cpu_quota": cgroup_cpus(),
+        "cpu_model": model,
         "kind": "port",
         "sample": "htree build over all 2^20 x 1 KiB entries (key BE64(i), v1, seed 2), %d "
-                  "threads over power-of-two leaf chunks, median of 5 = %.3f s; SHA-NI=%s; CPU: %s"
-                  % (threads, dtm, orc.has_shani(), model),
+                  "threads (every CPU in this process's affinity mask) over power-of-two leaf "
+                  "chunks, median of 5 = %.3f s; SHA-NI=%s; CPU: %s"
+                  % (avail, dta, orc.has_shani(), model),
+        "threads_16": {"value": gib(dt16), "unit": "GiB/s", "cores": t16,
+                       "sample": "same build on %d threads (the GPU box's CPU share), median of "
+                                 "5 = %.3f s" % (t16, dt16)},
         "single_thread": {"value": round(n * VAL_LEN / dt1 / 2 ** 30, 4), "unit": "GiB/s",
                           "cores": 1, "sample": "first %d entries, median of 5 = %.2f s" % (n, dt1)},
     }
@@ -311,6 +423,9 @@ def cabi_main(a):
         N.check(L.mh_dev_fill_random(md.ctx_handle(d), vals[d].data_ptr(), vals[d].numel(), 2 + d))
         N.check(L.mh_dev_fill_keys_be64(md.ctx_handle(d), keys[d].data_ptr(), n, d * n))
     md.synchronize()
+    corrupted = [d for d in range(K) if corrupt_hook(vals[d], d)]
+    for d in devs:
+        torch.cuda.synchronize(d)
     lv = [torch.empty(m.levels_len(n) * 32, dtype=torch.uint8, device=d) for d in devs]
     top = [torch.empty(max(m.levels_len(K), 1) * 32, dtype=torch.uint8, device=d) for d in devs]
     rt = [torch.empty(32, dtype=torch.uint8, device=d) for d in devs]
@@ -351,8 +466,28 @@ def cabi_main(a):
     ms, cnt = C.c_double(), C.c_uint64()
     N.check(L.mh_ctx_timing(c0, b"entries_fixed", C.byref(ms), C.byref(cnt)))
     kern_ms = ms.value / max(cnt.value, 1)
-    roots = {bytes(r.cpu().numpy().tobytes()) for r in rt}
-    assert len(roots) == 1, "devices disagree on the global root"
+    # the root check: every device's subtree (top of its levels) vs the
+    # oracle's rebuild of its shard, every device's global root vs the
+    # oracle's root over those (after the timed region)
+    tc = time.perf_counter()
+    orc = _oracle()
+    threads = host_threads()
+    depth = (n - 1).bit_length()
+    o_subs, blocks_ok, sub_ok, mode = [], True, True, None
+    for d in range(K):
+        r, bo, mode = oracle_shard_root(orc, n, VAL, 2 + d, d * n, lv[d], threads)
+        o_subs.append(r)
+        blocks_ok &= bo
+        top_off = m.level_offset(n, depth)
+        sub_ok &= lv[d][top_off * 32:(top_off + 1) * 32].cpu().numpy().tobytes() == r
+    want = global_expected(orc, o_subs)
+    glob_ok = all(r.cpu().numpy().tobytes() == want for r in rt)
+    exact = K == 1 or (n & (n - 1)) == 0
+    rcheck = {"vs": "oracle", "ok": bool(exact and blocks_ok and sub_ok and glob_ok),
+              "n": K * n, "shards": K, "mode": mode, "root": want.hex(),
+              "subtree_roots_ok": bool(sub_ok), "global_roots_ok": bool(glob_ok),
+              "host_threads": threads, "corrupted_shards": corrupted,
+              "seconds": round(time.perf_counter() - tc, 2)}
     lpl = int(os.environ.get("MH_LPL", "2" if n >= 2 * 262144 else "1"))
     wgl = int(os.environ.get("MH_WG_LEVELS", "1"))
     ltop = min({1: 0, 2: 1, 4: 2}[lpl] + wgl, (n - 1).bit_length())
@@ -384,9 +519,212 @@ def cabi_main(a):
                      "per_step": {"achieved": round(step_achieved, 2),
                                   "frac": round(step_achieved / HBM_PEAK_GBS, 4)}},
         "cpu_baseline": None,
+        "root_check": rcheck,
     }
     print(json.dumps(out), flush=True)
     md.close()
+    if not rcheck["ok"]:
+        print("root_check FAILED: %s" % json.dumps(rcheck), file=sys.stderr, flush=True)
+        raise SystemExit(1)
+
+
+def root_check_ranks(a, n, val, rank, world, dist, backend, dev, levels_dev, sub_root_dev,
+                     glob_root_dev, corrupted):
+    """Every rank rebuilds its own shard with the oracle on its share of the
+    host cores; the 128-byte records (device subtree root, device global
+    root, oracle shard root, block verdict) are all-gathered and rank 0
+    compares every device root with the oracle's whole-tree root; the verdict
+    is shared so every rank exits with the same status."""
+    import torch
+    t0 = time.perf_counter()
+    orc = _oracle()
+    threads = host_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    o_sub, blocks_ok, mode = oracle_shard_root(orc, n, val, 2 + rank, rank * n, levels_dev,
+                                               threads)
+    rec = np.zeros(128, np.uint8)
+    rec[0:32] = sub_root_dev.cpu().numpy()
+    rec[32:64] = glob_root_dev.cpu().numpy()
+    rec[64:96] = np.frombuffer(o_sub, np.uint8)
+    rec[96] = int(blocks_ok)
+    rec[97] = int(corrupted)
+    if dist:
+        on = torch.device("cpu") if backend == "gloo" else dev
+        g = torch.empty(world * 128, dtype=torch.uint8, device=on)
+        dist.all_gather_into_tensor(g, torch.from_numpy(rec).to(on))
+        recs = g.cpu().numpy().reshape(world, 128)
+    else:
+        recs = rec.reshape(1, 128)
+    exact = world == 1 or (n & (n - 1)) == 0  # top levels exact for power-of-two shards
+    want = global_expected(orc, [recs[r, 64:96].tobytes() for r in range(world)])
+    ok = exact and all(recs[r, 96] == 1 for r in range(world)) and \
+        all(recs[r, 0:32].tobytes() == recs[r, 64:96].tobytes() for r in range(world)) and \
+        all(recs[r, 32:64].tobytes() == want for r in range(world))
+    if dist:
+        f = torch.tensor([int(ok)], dtype=torch.int64,
+                         device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(f.item())
+    return {"vs": "oracle", "ok": bool(ok), "n": world * n, "shards": world, "mode": mode,
+            "root": want.hex(), "host_threads_per_rank": threads,
+            "corrupted_shards": [r for r in range(world) if recs[r, 97]],
+            "seconds": round(time.perf_counter() - t0, 2),
+            "what": "each rank's subtree root and global root vs the oracle's rebuild of the "
+                    "same splitmix64 values / BE64 keys (embedded/htree/htree.go:68-113); "
+                    "after the timed region"}
+
+
+def cabi_c3(a):
+    """--api cabi --config c3: syncBinaryLinking's replay (immustore.go:
+    1198-1232, reached from :686-693) the way a Go process drives the node's
+    GPUs: mh_multi_dev_ahtree_append_batch of `total` payloads (default 10^7
+    x 32 B, BASELINE configs[2]) onto a tree of n0 = 10^6 + 3 whose peaks
+    were read back with mh_dev_ahtree_peaks, cut into ranges over devices
+    0..N-1 (one RCCL clique), each device keeping only its range's digests.
+    One step = the whole batch appended again onto the same old tree.  After
+    the timed region: RootAt(n0 + total) and sampled digests / roots of every
+    range vs the oracle's append of all n0 + total payloads."""
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        raise SystemExit("--api cabi is one process: run it without torch.distributed.run")
+    import torch
+    K = a.gpus
+    if torch.cuda.device_count() < K:
+        raise SystemExit("--api cabi --gpus %d: only %d device(s) visible"
+                         % (K, torch.cuda.device_count()))
+    from immustore_amd import _native as N
+    from immustore_amd.multi import MultiDevice, ahtree_range_plan
+    L = N.load()
+    up = L.mh_ahtree_nodes_upto
+    n0, total, plen, seed = a.n0, a.entries or 10 ** 7, 32, 3
+    md = MultiDevice(list(range(K)))
+    devs = [torch.device("cuda", d) for d in range(K)]
+    # the old tree: its n0 appends on device 0, only its peaks kept
+    c0 = md.ctx_handle(0)
+    pk = np.zeros(32 * bin(n0).count("1"), np.uint8)
+    if n0:
+        p0 = torch.empty(n0 * plen, dtype=torch.uint8, device=devs[0])
+        d0 = torch.empty(up(n0) * 32, dtype=torch.uint8, device=devs[0])
+        torch.cuda.synchronize(devs[0])
+        N.check(L.mh_dev_fill_random(c0, p0.data_ptr(), p0.numel(), seed))
+        N.check(L.mh_dev_ahtree_append_batch(c0, d0.data_ptr(), 0, p0.data_ptr(), n0, plen, None))
+        N.check(L.mh_dev_ahtree_peaks(c0, d0.data_ptr(), n0, pk.ctypes.data))
+        md.synchronize()
+        del p0, d0
+    shard_bits, b = ahtree_range_plan(n0, total, K)
+    G = len(b) - 1
+    # range d = appends (b[d], b[d+1]]: payloads b[d] .. b[d+1]-1 of the one
+    # splitmix64 stream (word offset 4 b[d])
+    pay, dl, ro = [None] * K, [None] * K, [None] * K
+    for d in range(G):
+        cnt = b[d + 1] - b[d]
+        pay[d] = torch.empty(cnt * plen, dtype=torch.uint8, device=devs[d])
+        dl[d] = torch.empty((up(b[d + 1]) - up(b[d])) * 32, dtype=torch.uint8, device=devs[d])
+        ro[d] = torch.empty(cnt * 32, dtype=torch.uint8, device=devs[d])
+        torch.cuda.synchronize(devs[d])
+        sd = (seed + b[d] * (plen // 8) * SPLITMIX_G) & 0xFFFFFFFFFFFFFFFF
+        N.check(L.mh_dev_fill_random(md.ctx_handle(d), pay[d].data_ptr(), pay[d].numel(), sd))
+    md.synchronize()
+    corrupted = [d for d in range(G) if corrupt_hook(pay[d], d)]
+    for d in devs:
+        torch.cuda.synchronize(d)
+    ptr = lambda ts: [t.data_ptr() if t is not None else None for t in ts]  # noqa: E731
+    pp, pd, pr = ptr(pay), ptr(dl), ptr(ro)
+    pkb = pk.tobytes() if n0 else None
+
+    def step():
+        md.dev_ahtree_append_batch(total, pp, plen, pd, pr, n0=n0, peaks=pkb)
+
+    pre = 0
+    if a.prewarm > 0:
+        tp = time.perf_counter()
+        while time.perf_counter() - tp < a.prewarm:
+            for _ in range(4):
+                step()
+                pre += 1
+            md.synchronize()
+    for _ in range(a.warmup):
+        step()
+    md.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    md.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / a.steps * 1e3
+    # device 0's kernels in a pass after the timed region
+    N.check(L.mh_ctx_timing_reset(c0))
+    N.check(L.mh_ctx_set_timing(c0, 1))
+    kp = min(a.steps, 10)
+    for _ in range(kp):
+        step()
+    md.synchronize()
+    N.check(L.mh_ctx_set_timing(c0, 0))
+    import ctypes as C
+    kms = {}
+    for k in ("aht_leaves", "aht_perfect", "aht_spine", "aht_top", "aht_gather"):
+        t, c = C.c_double(), C.c_uint64()
+        N.check(L.mh_ctx_timing(c0, k.encode(), C.byref(t), C.byref(c)))
+        if c.value:
+            kms[k] = round(t.value / kp, 3)
+    # ---- check vs the oracle's append of every payload
+    tc = time.perf_counter()
+    orc = _oracle()
+    allp = orc.fill_random((n0 + total) * plen, seed).reshape(n0 + total, plen)
+    o = orc.AHtree(n0 + total)
+    o.append_batch(allp)
+    ref = o.dlog  # (>= nodesUpto(n0 + total), 32), no copy
+    ok = True
+    rng = np.random.default_rng(7)
+    for d in range(G):
+        g = dl[d].view(-1, 32)
+        nd = g.shape[0]
+        idx = np.unique(np.concatenate([np.arange(min(nd, 512)), np.arange(max(nd - 512, 0), nd),
+                                        rng.integers(0, nd, 2048)]))
+        got = g[torch.from_numpy(idx).to(g.device)].cpu().numpy()
+        ok &= bool(np.array_equal(got, ref[up(b[d]) + idx]))
+        r = ro[d].view(-1, 32)
+        cnt = b[d + 1] - b[d]
+        for j in sorted({0, cnt // 2, cnt - 1, int(rng.integers(0, cnt))}):
+            ok &= r[j].cpu().numpy().tobytes() == bytes(o.root_at(b[d] + j + 1)[1])
+    want = bytes(o.root_at(n0 + total)[1])
+    last = ro[G - 1].view(-1, 32)[-1].cpu().numpy().tobytes()
+    ok &= last == want
+    rcheck = {"vs": "oracle", "ok": bool(ok), "n": n0 + total, "root": want.hex(),
+              "what": "RootAt(n0 + total) and, per range, its first / last 512 and 2048 random "
+                      "digests and 4 RootAt values vs orc.AHtree over all n0 + total payloads "
+                      "(embedded/ahtree/ahtree.go:246-373, 727-771)",
+              "corrupted_ranges": corrupted, "seconds": round(time.perf_counter() - tc, 2)}
+    new_digests = up(n0 + total) - up(n0)
+    alg = total * plen + 32 * new_digests
+    out = {"metric": "ahtree replay append (syncBinaryLinking), %d x %d B payloads onto a tree of "
+                     "%d, through the C ABI across %d device(s)" % (total, plen, n0, K),
+           "value": round(total / elapsed * a.steps / 1e6, 3), "unit": "M appends/s",
+           "n_gpus": K, "api": "cabi", "rccl_ranks": K if (md.uses_rccl() and G > 1) else 0,
+           "steps": a.steps, "warmup": a.warmup,
+           "clock_prewarm": {"seconds": a.prewarm, "appends_batches": pre},
+           "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic (splitmix64 payloads generated in HBM)",
+           "config": {"workload": "mh_multi_dev_ahtree_append_batch onto old peaks from "
+                                  "mh_dev_ahtree_peaks", "n0": n0, "appends": total,
+                      "payload_len": plen, "ranges": G, "range_bounds": b,
+                      "shard_bits": shard_bits,
+                      "dlog_bytes_per_device": [int(t.numel()) if t is not None else 0
+                                                for t in dl]},
+           "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 2),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "alg_bytes_per_step": alg,
+                        "note": "payloads read + new dLog digests written, whole job per step",
+                        "kernel_ms_device0": kms,
+                        "sha": {"gcomp_per_s": round((total + 2 * (new_digests - total)) /
+                                                     (ms * 1e-3) / 1e9, 2),
+                                "peak_gcomp_per_s": SHA_PEAK_GCOMPS}},
+           "cpu_baseline": None, "root_check": rcheck}
+    print(json.dumps(out), flush=True)
+    md.close()
+    if not ok:
+        print("root_check FAILED: %s" % json.dumps(rcheck), file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 def main():
@@ -394,7 +732,7 @@ def main():
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if a.api == "cabi":
-        return cabi_main(a)
+        return cabi_c3(a) if a.config == "c3" else cabi_main(a)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(relaunch_ranks(a))
     if a.launch_check:
@@ -453,6 +791,7 @@ def main():
     with torch.cuda.stream(streams[0]):
         N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 2 + rank))
         N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, rank * n))
+        corrupted = corrupt_hook(vals, rank)
     torch.cuda.synchronize(dev)
     nlv = m.levels_len(n)
     levels = [torch.empty(nlv * 32, dtype=torch.uint8, device=dev) for _ in range(D)]
@@ -572,6 +911,8 @@ def main():
     # every build's root must be the same tree root (same input each step)
     r0 = root[0].cpu()
     assert all(torch.equal(r0, r.cpu()) for r in root), "in-flight builds disagree"
+    rcheck = root_check_ranks(a, n, VAL, rank, world, dist, backend, dev, levels[0], root[0],
+                              groot[0] if world > 1 else root[0], corrupted)
 
     k_ms = sum(c.timing("entries_fixed")[0] for c in ctxs[1:]) + k_ms0
     k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
@@ -678,6 +1019,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None
+    out["root_check"] = rcheck
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm_ctx is not ctx:
@@ -686,6 +1028,9 @@ def main():
         c.close()
     if dist:
         dist.destroy_process_group()
+    if not rcheck["ok"]:
+        print("root_check FAILED: %s" % json.dumps(rcheck), file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

@@ -89,9 +89,11 @@ func (t *AHtree) peaks(n uint64) ([]byte, error) {
 }
 
 // AppendBatch appends every payload of ds (32-byte Alh values on the replay
-// path; any equal length works) exactly as len(ds) calls of Append would:
-// the same pLog records, dLog digests (the tree/*.sha stream) and cLog
-// entries, and returns RootAt(size) after the batch.
+// path; any lengths) exactly as len(ds) calls of Append would: the same pLog
+// records, dLog digests (the tree/*.sha stream) and cLog entries, and returns
+// RootAt(size) after the batch.  Like Append (ahtree.go:260-263) it rejects
+// only a nil payload; the C ABI takes one payload length per call, so each
+// maximal run of equal-length payloads is one device batch.
 func (t *AHtree) AppendBatch(ds [][]byte) (n uint64, root [sha256.Size]byte, err error) {
 	t.mutex.Lock()
 	defer t.mutex.Unlock()
@@ -101,16 +103,31 @@ func (t *AHtree) AppendBatch(ds [][]byte) (n uint64, root [sha256.Size]byte, err
 	if t.readOnly {
 		return 0, root, ErrReadOnly
 	}
-	m := len(ds)
-	if m == 0 {
+	if len(ds) == 0 {
 		return t.size(), root, ErrIllegalArguments
 	}
-	plen := len(ds[0])
 	for _, d := range ds {
-		if d == nil || len(d) != plen {
+		if d == nil {
 			return 0, root, ErrIllegalArguments
 		}
 	}
+	for i := 0; i < len(ds); {
+		j := i + 1
+		for j < len(ds) && len(ds[j]) == len(ds[i]) {
+			j++
+		}
+		if n, root, err = t.appendRun(ds[i:j]); err != nil {
+			return 0, root, err
+		}
+		i = j
+	}
+	return n, root, nil
+}
+
+// appendRun: one device batch of equal-length payloads (t.mutex held).
+func (t *AHtree) appendRun(ds [][]byte) (n uint64, root [sha256.Size]byte, err error) {
+	m := len(ds)
+	plen := len(ds[0])
 	mm, err := devices()
 	if err != nil {
 		return 0, root, err
@@ -143,8 +160,14 @@ func (t *AHtree) AppendBatch(ds [][]byte) (n uint64, root [sha256.Size]byte, err
 	if len(pk) > 0 {
 		pkp = (*C.uint8_t)(unsafe.Pointer(&pk[0]))
 	}
+	// zero-length payloads (Append accepts them, ahtree.go:279 only skips
+	// the pLog bytes): no payload buffer, which the C side allows for plen 0
+	var pp *C.uint8_t
+	if plen > 0 {
+		pp = (*C.uint8_t)(unsafe.Pointer(&payloads[0]))
+	}
 	st := C.mh_multi_ahtree_append_batch(mm, C.uint64_t(n0), pkp,
-		(*C.uint8_t)(unsafe.Pointer(&payloads[0])), C.uint64_t(m), C.uint32_t(plen),
+		pp, C.uint64_t(m), C.uint32_t(plen),
 		(*C.uint8_t)(unsafe.Pointer(&dlog[0])), (*C.uint8_t)(unsafe.Pointer(&root[0])))
 	if st != C.MH_OK {
 		return 0, root, mapErr(st)

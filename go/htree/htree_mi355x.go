@@ -121,40 +121,58 @@ func (t *HTree) InclusionProof(i int) (*InclusionProof, error) {
 
 // VerifyInclusionBatch checks many proofs at once (htree.go:166-195 per
 // proof); a single proof stays the reference's VerifyInclusion (one proof is
-// cheaper on a host core than a PCIe round trip).  ok[p] is the verdict.
+// cheaper on a host core than a PCIe round trip).  ok[p] is the verdict; a
+// nil proof is false without reaching the device, as VerifyInclusion returns
+// false for it (htree.go:167-169).  digests and roots hold one entry per
+// proof: anything else is ErrIllegalArguments before C reads n x 32 bytes.
 func VerifyInclusionBatch(proofs []*InclusionProof, digests, roots [][sha256.Size]byte) ([]bool, error) {
 	n := len(proofs)
+	if len(digests) != n || len(roots) != n {
+		return nil, ErrIllegalArguments
+	}
 	ok := make([]bool, n)
-	if n == 0 {
+	// the non-nil proofs, packed (idx[q] = their position in proofs)
+	idx := make([]int, 0, n)
+	for k, pr := range proofs {
+		if pr != nil {
+			idx = append(idx, k)
+		}
+	}
+	m := len(idx)
+	if m == 0 {
 		return ok, nil
 	}
 	p, err := mi355x.Context()
 	if err != nil {
 		return nil, err
 	}
-	leaf := make([]uint64, n)
-	width := make([]uint64, n)
-	off := make([]uint64, n+1)
+	leaf := make([]uint64, m)
+	width := make([]uint64, m)
+	off := make([]uint64, m+1)
+	dig := make([][sha256.Size]byte, m)
+	rts := make([][sha256.Size]byte, m)
 	var terms [][sha256.Size]byte
-	for k, pr := range proofs {
-		leaf[k], width[k] = uint64(pr.Leaf), uint64(pr.Width)
+	for q, k := range idx {
+		pr := proofs[k]
+		leaf[q], width[q] = uint64(pr.Leaf), uint64(pr.Width)
+		dig[q], rts[q] = digests[k], roots[k]
 		terms = append(terms, pr.Terms...)
-		off[k+1] = uint64(len(terms))
+		off[q+1] = uint64(len(terms))
 	}
 	if len(terms) == 0 {
 		terms = make([][sha256.Size]byte, 1)
 	}
-	res := make([]uint8, n)
-	st := C.mh_htree_verify_inclusion_batch((*C.mh_ctx)(p), C.uint64_t(n),
+	res := make([]uint8, m)
+	st := C.mh_htree_verify_inclusion_batch((*C.mh_ctx)(p), C.uint64_t(m),
 		(*C.uint64_t)(unsafe.Pointer(&leaf[0])), (*C.uint64_t)(unsafe.Pointer(&width[0])),
 		(*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint8_t)(unsafe.Pointer(&terms[0][0])),
-		(*C.uint8_t)(unsafe.Pointer(&digests[0][0])), (*C.uint8_t)(unsafe.Pointer(&roots[0][0])),
+		(*C.uint8_t)(unsafe.Pointer(&dig[0][0])), (*C.uint8_t)(unsafe.Pointer(&rts[0][0])),
 		(*C.uint8_t)(unsafe.Pointer(&res[0])))
 	if st != C.MH_OK {
 		return nil, mapErr(st)
 	}
-	for k := range res {
-		ok[k] = res[k] != 0
+	for q, k := range idx {
+		ok[k] = res[q] != 0
 	}
 	return ok, nil
 }

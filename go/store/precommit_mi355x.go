@@ -177,6 +177,10 @@ func (b *PrecommitBatch) Run(version int, maxTxEntries int, txs [][]*EntrySpec,
 // digest mismatch") or nil.  For a scrub or an export of many values.
 func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error, error) {
 	n := len(vals)
+	// one length and one digest per value: C reads n of each
+	if len(vLen) != n || len(hVal) != n {
+		return nil, ErrIllegalArguments
+	}
 	if n == 0 {
 		return nil, nil
 	}

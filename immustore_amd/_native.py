@@ -12,6 +12,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MH_LIB_PATH") or os.path.join(_HERE, "libimmustore_merkle.so")
 
 MH_OK = 0
+# test-only fault sites of mh_debug_fail_at
+MH_FAULT_RCCL_GROUP = 1
+MH_FAULT_TXLOG_AFTER_GROUP = 2
 MH_ERR_MAX_WIDTH_EXCEEDED = 1
 MH_ERR_ILLEGAL_ARGUMENTS = 2
 MH_ERR_ILLEGAL_STATE = 3
@@ -195,6 +198,7 @@ SIGNATURES = {
     "mh_ctx_set_timing": (i32, [vp, i32]),
     "mh_ctx_timing": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(u64)]),
     "mh_ctx_timing_reset": (i32, [vp]),
+    "mh_debug_fail_at": (i32, [i32, i32]),
     "mh_dev_alloc": (i32, [vp, u64, C.POINTER(vp)]),
     "mh_dev_free": (i32, [vp, vp]),
     "mh_host_alloc_pinned": (i32, [u64, C.POINTER(vp)]),

@@ -7,6 +7,7 @@
 // here only moves bytes, computes indices and reports errors.  There is no
 // CPU hashing fallback: without a usable device every entry point returns
 // MH_ERR_NO_DEVICE.
+#include <atomic>
 #include <algorithm>
 #include <functional>
 #include <cstdio>
@@ -26,6 +27,21 @@ hipError_t launch_copy_nodes(hipStream_t st, const uint8_t *src, uint64_t n, uin
 
 // ------------------------------------------------------------------ misc
 extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
+
+namespace {
+std::atomic<int> g_fault[3];
+}
+
+bool mh_fault(int site) {
+    if (site <= 0 || site >= 3 || g_fault[site].load(std::memory_order_relaxed) <= 0) return false;
+    return g_fault[site].fetch_sub(1) == 1;
+}
+
+extern "C" int mh_debug_fail_at(int site, int countdown) {
+    if (site <= 0 || site >= 3 || countdown < 0) return MH_ERR_ILLEGAL_ARGUMENTS;
+    g_fault[site].store(countdown);
+    return MH_OK;
+}
 
 extern "C" const char *mh_status_string(int st) {
     switch (st) {

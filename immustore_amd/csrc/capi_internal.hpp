@@ -36,6 +36,10 @@ inline int mh_guard(F &&f) noexcept {
         if (e_ != hipSuccess) return -(int)e_;              \
     } while (0)
 
+// Test-only fault sites (mh_debug_fail_at, include/immustore_merkle.h):
+// true exactly once, when the armed countdown of `site` reaches zero.
+bool mh_fault(int site);
+
 // CSR offsets off[0..n] never run backwards (checked before a host wrapper
 // rebases them and sizes the device copies from off[n] - off[0])
 inline bool monotonic(const uint64_t *off, uint64_t n) {

@@ -56,6 +56,20 @@ const Rccl &rccl() {
         if ((expr) != ncclSuccess) return MH_ERR_COLLECTIVE; \
     } while (0)
 
+// Ends an open RCCL group on scope exit unless end() already did.
+struct RcclGroup {
+    const Rccl &r;
+    bool open = true;
+    explicit RcclGroup(const Rccl &rr) : r(rr) {}
+    ncclResult_t end() {
+        open = false;
+        return r.group_end();
+    }
+    ~RcclGroup() {
+        if (open) r.group_end();
+    }
+};
+
 uint64_t next_pow2(uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
@@ -242,15 +256,15 @@ int gather_bytes(mh_multi *m, const std::vector<const uint8_t *> &send,
     }
     const Rccl &R = rccl();
     MH_NCCL(R.group_start());
+    // every exit after ncclGroupStart ends the group: an open group would
+    // defer every later RCCL call of this thread into it (the next build
+    // would hang instead of failing)
+    RcclGroup group(R);
     for (int d = 0; d < m->K; d++) {
-        MH_HIP(hipSetDevice(m->dev[d]));
-        if (R.all_gather(send[d], recv[d], bytes, ncclUint8, m->comm[d], m->ctx[d]->stream) !=
-            ncclSuccess) {
-            R.group_end();
-            return MH_ERR_COLLECTIVE;
-        }
+        MH_HIP(mh_fault(MH_FAULT_RCCL_GROUP) ? hipErrorInvalidDevice : hipSetDevice(m->dev[d]));
+        MH_NCCL(R.all_gather(send[d], recv[d], bytes, ncclUint8, m->comm[d], m->ctx[d]->stream));
     }
-    MH_NCCL(R.group_end());
+    MH_NCCL(group.end());
     return MH_OK;
 }
 

@@ -1143,6 +1143,16 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         cut[K] = len;
         const uint64_t nck = len ? K : 0;
         MH_HIP(ensure_chunk_events(c, 2 * nck));
+        // once a group's kernels are queued they may store into the caller's
+        // pinned status / alh / header arrays: every exit (errors included)
+        // waits for both streams, so nothing writes caller memory after return
+        struct StreamGuard {
+            hipStream_t a, b;
+            ~StreamGuard() {
+                hipStreamSynchronize(a);
+                hipStreamSynchronize(b);
+            }
+        } stream_guard{st, c->d2h_stream};
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
         for (uint64_t k = 0; k < nck; k++)
@@ -1405,6 +1415,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             if (int e = launch(gs[deferred])) return e;
             tr.mark("group");
         }
+        if (!gs.empty() && mh_fault(MH_FAULT_TXLOG_AFTER_GROUP)) return -(int)hipErrorOutOfMemory;
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
         // on an error hop.end is the failing record's offset = the end of the last good one

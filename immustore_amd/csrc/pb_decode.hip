@@ -918,9 +918,10 @@ extern "C" int mh_verify_dual_proof_v2_pb_batch(mh_ctx *c, uint64_t n, const uin
                        b_leaf = L.add(n * 32), b_ca = L.add(n * 32), b_oki = L.add(n), b_okc = L.add(n);
         MH_HIP(c->s_tx.ensure(L.total));
         // term area reused chunk after chunk: a well-formed term costs >= 34
-        // message bytes (tag, length, 32-byte digest), so this rarely grows
+        // message bytes (tag, length, 32-byte digest), so this rarely grows;
+        // sized from the batch itself when it is smaller than one chunk
         DevBuf &tb = c->s_tree;
-        MH_HIP(tb.ensure(std::max<uint64_t>(chunk_bytes / 34 + 64, 1) * 32));
+        MH_HIP(tb.ensure(std::max<uint64_t>(std::min(mb, chunk_bytes) / 34 + 64, 1) * 32));
         uint8_t *base = c->s_tx.as<uint8_t>();
         // the copies, one helper thread: chunk 0 = the per-message arrays
         // whole (offsets, ids, Alh values: few large copies -- each copy call

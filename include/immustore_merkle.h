@@ -121,6 +121,17 @@ int mh_ctx_set_timing(mh_ctx *ctx, int enable);
 int mh_ctx_timing(mh_ctx *ctx, const char *prefix, double *total_ms, uint64_t *launches);
 int mh_ctx_timing_reset(mh_ctx *ctx);
 
+/* TEST ONLY: fault injection for error-path tests.  The next `countdown`-th
+ * time (1 = the next time) the library passes fault site `site`, it fails
+ * there as if the HIP / RCCL call at that point had failed.  countdown 0
+ * disarms the site.  Sites: MH_FAULT_RCCL_GROUP (inside the RCCL group of a
+ * multi-device all-gather, after ncclGroupStart), MH_FAULT_TXLOG_AFTER_GROUP
+ * (mh_txlog_validate, after the first chunk group's kernels were queued).
+ * No reference counterpart: production callers never arm it. */
+#define MH_FAULT_RCCL_GROUP 1
+#define MH_FAULT_TXLOG_AFTER_GROUP 2
+int mh_debug_fail_at(int site, int countdown);
+
 /* device memory helpers, so that a cgo caller needs no HIP headers */
 int mh_dev_alloc(mh_ctx *ctx, uint64_t bytes, void **dptr);
 int mh_dev_free(mh_ctx *ctx, void *dptr);

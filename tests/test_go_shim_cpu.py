@@ -123,3 +123,45 @@ def test_bound_functions_are_exported():
     L = ctypes.CDLL(lib)
     for _, name, _ in go_calls():
         assert hasattr(L, name), name
+
+
+def _func_body(path, name):
+    """Source of Go function `name` (from its `func` line to the closing brace
+    at column 0)."""
+    src = open(os.path.join(GO, path)).read()
+    m = re.search(r"^func (\([^)]*\) )?%s\(" % re.escape(name), src, flags=re.M)
+    assert m, "%s not in %s" % (name, path)
+    end = src.index("\n}\n", m.start())
+    return src[m.start():end + 2]
+
+
+def test_verify_inclusion_batch_guards():
+    """htree.VerifyInclusion returns false for a nil proof (htree.go:167-169):
+    the batch shim skips nil proofs without touching C, and checks that
+    digests / roots hold one entry per proof before C reads n x 32 bytes."""
+    b = _func_body("htree/htree_mi355x.go", "VerifyInclusionBatch")
+    assert re.search(r"len\(digests\) != n \|\| len\(roots\) != n", b)
+    assert re.search(r"if pr != nil", b)
+    # only the packed non-nil proofs reach the C call
+    call = b[b.index("C.mh_htree_verify_inclusion_batch"):]
+    assert "C.uint64_t(m)" in call and "&dig[0][0]" in call and "&rts[0][0]" in call
+    assert b.index("if pr != nil") < b.index("mi355x.Context()")
+
+
+def test_ahtree_append_batch_accepts_mixed_lengths():
+    """Append accepts any non-nil payload (ahtree.go:260-263): AppendBatch
+    rejects only nil, cuts runs of equal length, and passes no payload
+    pointer for zero-length payloads."""
+    b = _func_body("ahtree/ahtree_mi355x.go", "AppendBatch")
+    assert "len(d) != plen" not in b
+    assert re.search(r"if d == nil \{\s*return 0, root, ErrIllegalArguments", b)
+    assert "t.appendRun(ds[i:j])" in b
+    r = _func_body("ahtree/ahtree_mi355x.go", "appendRun")
+    assert re.search(r"if plen > 0 \{\s*pp = ", r)
+    assert "pp, C.uint64_t(m), C.uint32_t(plen)" in r
+
+
+def test_verify_values_length_guards():
+    b = _func_body("store/precommit_mi355x.go", "VerifyValues")
+    assert re.search(r"len\(vLen\) != n \|\| len\(hVal\) != n", b)
+    assert b.index("len(vLen) != n") < b.index("C.mh_verify_values_batch")
