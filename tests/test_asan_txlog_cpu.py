@@ -9,7 +9,7 @@ the multi-threaded hop (bit flips, extreme BE16 / BE32 length fields,
 truncation, splices).  Each mutant sits in an allocation of its exact length;
 the library's host code and the oracle are both built with ASan (host only,
 tools/asan/Makefile), and the two parses must agree on (status, ntx,
-consumed) for every mutant.  (tools/gpu_fuzz.sh runs the same fuzzer on a GPU
+consumed) for every mutant.  (tools/gpu_run.sh fuzz runs the same fuzzer on a GPU
 box with the device path, mh_txlog_validate, compared in full:
 profiles/fuzz_txlog_device_r02.log.)"""
 import os

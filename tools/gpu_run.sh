@@ -18,6 +18,13 @@
 #   txlog            tools/txlog_bench (a14 through the C ABI)
 #   workloads        bench_workloads.py: every secondary workload line
 #   ab:<VARIANTS>    tools/ab_env.sh rotation, e.g. ab:base,MH_LPL=1
+#   txab:<VARIANTS>  tools/txlog_bench rotation (ROUNDS x), e.g. txab:base;MH_TXLOG_KERNEL=group
+#   txtl:<VARIANTS>  a14 kernel + copy timeline of the last call per variant -> txtl.txt
+#   workload:<name>  bench_workloads.py --workload <name>
+#   fuzz             host-ASan tx-log fuzzer with the device path (FUZZ_ITERS, FUZZ_SEED)
+#   queue            tools/queue_bench: group commit, 30 committers (QWAIT us, QMAXTXS)
+#   traffic          tools/gpu_pmc.sh: the counter passes behind traffic_r*.json (PMC_CMD overrides)
+#   pmctx            tools/gpu_pmc_txlog.sh (PMC_MATCH=kernel name) -> gpurun_out/pmctx/table.txt
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -58,6 +65,34 @@ for s in "$@"; do
       step prof 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
     txlog) step txlog 300 ./tools/txlog_bench || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;
+    txab:*)  # interleaved A/B of tools/txlog_bench over env variants, e.g. txab:base;MH_TXLOG_KERNEL=group
+      vs="$(echo "${s#txab:}" | tr ';' ' ')"
+      for i in $(seq ${ROUNDS:-3}); do
+        for v in $vs; do
+          envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
+          env $envs timeout -k 10 200 ./tools/txlog_bench ${TXB_ARGS:-200} > "$O/txab.json" 2> "$O/txab.err" || { cat "$O/txab.err"; exit 1; }
+          echo "$v $(cat "$O/txab.json")" | tee -a "$O/txab.txt"
+        done
+      done ;;
+    txtl:*)  # a14 timeline per env variant: kernel + memory-copy trace of the last call (tools/trace_window.py)
+      vs="$(echo "${s#txtl:}" | tr ';' ' ')"
+      for v in $vs; do
+        envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
+        rm -rf "$O/txtl"
+        env $envs timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/txtl" -o run -- python3 tools/txlog_timeline.py > "$O/txtl.out" 2>&1 || { tail -5 "$O/txtl.out"; exit 1; }
+        { echo "# variant $v"; python3 tools/trace_window.py "$O/txtl" 2500; } | tee -a "$O/txtl.txt"
+      done
+      rm -rf "$O/txtl" ;;
+    fuzz)  # host-ASan tx-log fuzzer with the device path (tools/asan/; built on the box, ~30 s)
+      { [ -x build/asan/txlog_fuzz ] || make -s -j16 -C tools/asan > "$O/asan_build.log" 2>&1; } || { tail -5 "$O/asan_build.log"; exit 1; }
+      python3 tools/asan/make_corpus.py "$O/corpus" > /dev/null || exit 1
+      ASAN_OPTIONS=detect_leaks=0 MH_FUZZ_DEVICE=1 step fuzz ${FUZZ_TIMEOUT:-500} \
+        build/asan/txlog_fuzz ${FUZZ_ITERS:-2000} ${FUZZ_SEED:-20261016} "$O"/corpus/*.log
+      rc=$?; rm -rf "$O/corpus"; [ $rc -eq 0 ] || exit 1 ;;
+    queue) step queue 300 ./tools/queue_bench 30 2000 16 1024 ${QWAIT:-20} ${QMAXTXS:-64} || exit 1 ;;
+    traffic) step traffic 1200 bash tools/gpu_pmc.sh || exit 1 ;;
+    workload:*) w="${s#workload:}"; step "wl_$w" 600 python bench_workloads.py --workload "$w" || exit 1 ;;
+    pmctx) step pmctx 900 bash tools/gpu_pmc_txlog.sh || exit 1; cat "gpurun_out/pmctx${PMC_TAG:-}/table.txt" ;;
     ab:*) VARIANTS="$(echo "${s#ab:}" | tr ';' ' ')" step ab 900 bash tools/ab_env.sh || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
