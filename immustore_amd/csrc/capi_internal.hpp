@@ -200,6 +200,7 @@ struct mh_ctx {
     hipStream_t copy_stream = nullptr;
     hipStream_t copy_stream2 = nullptr;  // a second copy lane (ChunkCopier)
     hipStream_t d2h_stream = nullptr;  // device->host results of an early part of a call
+    hipStream_t stream2 = nullptr;     // a second compute stream (tx-log groups)
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf s_chunk[2];
     std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call
@@ -210,6 +211,7 @@ struct mh_ctx {
         hipError_t e = hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&copy_stream2, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&d2h_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking);
         for (int k = 0; k < 2 && e == hipSuccess; k++) {
             e = hipEventCreateWithFlags(&ev_copied[k], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming);
@@ -225,6 +227,7 @@ struct mh_ctx {
         if (copy_stream) hipStreamDestroy(copy_stream);
         if (copy_stream2) hipStreamDestroy(copy_stream2);
         if (d2h_stream) hipStreamDestroy(d2h_stream);
+        if (stream2) hipStreamDestroy(stream2);
     }
 };
 

@@ -1147,18 +1147,33 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // pinned status / alh / header arrays: every exit (errors included)
         // waits for both streams, so nothing writes caller memory after return
         struct StreamGuard {
-            hipStream_t a, b;
+            hipStream_t a, b, c2;
             ~StreamGuard() {
                 hipStreamSynchronize(a);
                 hipStreamSynchronize(b);
+                hipStreamSynchronize(c2);
             }
-        } stream_guard{st, c->d2h_stream};
+        } stream_guard{st, c->d2h_stream, c->stream2};
+        // early groups alternate between the context's stream and a second
+        // compute stream, so a group's kernel never waits behind the previous
+        // group's (the last chunk's group starts as soon as its chunk lands);
+        // MH_TXLOG_STREAMS=1: one stream (A/B, read per call)
+        const char *nse = getenv("MH_TXLOG_STREAMS");
+        const bool two_streams = !(nse && atoi(nse) == 1);
+        auto gstream = [&](uint64_t k) { return two_streams && (k & 1) ? c->stream2 : st; };
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
         for (uint64_t k = 0; k < nck; k++)
             cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], cut[k + 1] - cut[k]}};
         cc.inline_issue = pinned;
+        {  // MH_TXLOG_COPY_LANES=2: chunk k on copy stream k % 2 (A/B, read per call)
+            const char *cl = getenv("MH_TXLOG_COPY_LANES");
+            if (cl && atoi(cl) == 2 && pinned) cc.lanes = 2;
+        }
         MH_HIP(cc.start());
+        // the second compute stream starts after everything queued on the
+        // context's stream before this call too (cc.start() recorded ev_done[0])
+        MH_HIP(hipStreamWaitEvent(c->stream2, c->ev_done[0], 0));
         auto join_copies = [&]() -> int {
             hipError_t e = cc.join();
             return e == hipSuccess ? MH_OK : -(int)e;
@@ -1242,7 +1257,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // host tree plan), Alh with the rebuilt Eh vs the stored one
         // (tx.go:623-627).  pl: the group's metadata patch lists (below).
         auto run = [&](Grp &g, const uint8_t *db, const uint64_t *pl, uint64_t npe,
-                       uint64_t nph) -> int {
+                       uint64_t nph, hipStream_t st) -> int {
             const uint64_t nt = g.t1 - g.t0;
             uint8_t *base = g.base;
             uint64_t *ro = (uint64_t *)(base + g.b_ro), *ap = (uint64_t *)(base + g.b_ap),
@@ -1268,9 +1283,17 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                     ho.hdrs = reinterpret_cast<uint64_t *>(hh);
                     g.host_done = true;
                 }
-                MH_HIP(launch_txlog_group(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_s,
-                                          base + g.b_eh, base + g.b_a,
-                                          (int32_t *)(base + g.b_st), ho, g.wmax));
+                // MH_TXLOG_KERNEL=group: the workgroup kernel (read per call: A/B tests)
+                const char *kn = getenv("MH_TXLOG_KERNEL");
+                const bool wave = !(kn && strcmp(kn, "group") == 0);
+                if (wave)
+                    MH_HIP(launch_txlog_wave(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
+                                             base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
+                                             g.pro, g.pap));
+                else
+                    MH_HIP(launch_txlog_group(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_s,
+                                              base + g.b_eh, base + g.b_a,
+                                              (int32_t *)(base + g.b_st), ho, g.wmax));
                 return MH_OK;
             }
             MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, db, ro, hd, es));
@@ -1352,6 +1375,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         auto launch = [&](Grp &g) -> int {
             // the index arrays do not need the chunk: fetched before its event
             const uint64_t nt = g.t1 - g.t0;
+            hipStream_t st = gstream(g.k);
             MH_HIP(launch_fetch_host(
                 st, HostRuns{{g.pro, g.pap, g.plo},
                              {(uint64_t *)(g.base + g.b_ro), (uint64_t *)(g.base + g.b_ap),
@@ -1360,7 +1384,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             g.fetched = true;
             if (hipError_t e = cc.wait(g.k)) return -(int)e;
             MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[g.k], 0));
-            if (int e = run(g, dbuf, nullptr, 0, 0)) return e;
+            if (int e = run(g, dbuf, nullptr, 0, 0, st)) return e;
             MH_HIP(hipEventRecord(c->ev_chunks[nck + g.k], st));
             return results(g, c->ev_chunks[nck + g.k]);
         };
@@ -1476,7 +1500,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 db = nb;
                 pl = reinterpret_cast<const uint64_t *>(nb + po);
             }
-            if (int e = run(g, db, pl, npe, nph)) return e;
+            if (int e = run(g, db, pl, npe, nph, st)) return e;
             MH_HIP(hipEventRecord(c->ev_done[1], st));
             if (int e = results(g, c->ev_done[1])) return e;
         }
@@ -1485,12 +1509,14 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         tr.mark("enqueued");
         MH_HIP(hipStreamSynchronize(c->d2h_stream));
         MH_HIP(hipStreamSynchronize(st));
+        MH_HIP(hipStreamSynchronize(c->stream2));
         // buf stays the caller's once we return
         if (nck) {
             MH_HIP(hipStreamSynchronize(c->copy_stream));
             MH_HIP(hipStreamSynchronize(c->copy_stream2));
         }
         tr.mark("done");
+        txlog_probe_report();
         return rc;
     });
 }

@@ -273,6 +273,17 @@ hipError_t launch_txlog_group(hipStream_t st, Timer *tm, uint64_t ntx, const uin
                               const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *scratch,
                               uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
                               const TxlogHostOut &ho, uint64_t wmax);
+// the same with one wave per 64 / L records (k_txlog_wave); h_rec_off /
+// h_alh_off: host-readable copies of rec_off / alh_off (the wave's LDS
+// staging is sized from them)
+hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                             const uint64_t *rec_off, const uint64_t *alh_off,
+                             const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
+                             uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
+                             uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off);
+// MH_TXLOG_PROBE=1: per-phase wave timings of the last call's k_txlog_wave
+// launches on stderr (call after the call's final sync)
+void txlog_probe_report();
 // up to three runs of words pinned host memory -> HBM by a kernel (k_fetch_host)
 struct HostRuns {
     const uint64_t *src[3];

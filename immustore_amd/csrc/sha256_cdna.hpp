@@ -300,6 +300,29 @@ __device__ __forceinline__ void node_hash_tab(const uint32_t l[8], const uint32_
     for (int j = 0; j < 8; j++) out[j] = s.h[j];
 }
 
+// Second block of SHA256(0x01 || l || r) given r's last word, its K+W row
+// read from the table in GLOBAL memory (L2-resident): the node hash's
+// padding block without the ~480-instruction schedule expansion.
+__device__ __forceinline__ void compress_node_tail_g(State &s, uint32_t r7) {
+    const uint4 *row = (const uint4 *)(g_node_tab.w + (r7 & 0xffu) * kNodeTabStride);
+    uint4 kw[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) kw[q] = row[q];
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6],
+             h = s.h[7];
+    MH_ROUNDS8(MH_K(0) + ((r7 << 24) | 0x00800000u), MH_K(1), MH_K(2), MH_K(3), MH_K(4), MH_K(5),
+               MH_K(6), MH_K(7));
+    MH_ROUNDS8(MH_K(8), MH_K(9), MH_K(10), MH_K(11), MH_K(12), MH_K(13), MH_K(14),
+               MH_K(15) + 65u * 8u);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint4 x = kw[2 * q], y = kw[2 * q + 1];
+        MH_ROUNDS8(x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w);
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
 // node = SHA256(0x01 || l || r) with the second block's K+W row read from
 // the table in GLOBAL memory (L2-resident): for latency-bound lone waves at
 // the top of a tree, where a workgroup cannot afford the 53 KB LDS copy.  The

@@ -576,3 +576,72 @@ def test_txlog_validate_metadata_parse_vs_oracle(m, ctx, orc):
         assert np.array_equal(alh, o[3][:n]) and np.array_equal(sts, o[4][:n]), name
     rc, n, _, _, _, sts = m.txlog_validate(big, ctx=ctx)
     assert rc == 0 and n == 42000 and not sts.any()
+
+
+def _record_heads(raw, n):
+    """The TxHeader fields of the first n records, parsed in Python from the
+    raw log (tx.go:419-518) -- what mh_txlog_validate returns besides Eh."""
+    out, p = [], 0
+    for _ in range(n):
+        tid, ts, bl = struct.unpack_from(">QQQ", raw, p)
+        ver, = struct.unpack_from(">H", raw, p + 88)
+        if ver == 0:
+            ne, = struct.unpack_from(">H", raw, p + 90)
+            ml, mo, q = 0, 0, p + 92
+        else:
+            ml, = struct.unpack_from(">H", raw, p + 90)
+            ne, = struct.unpack_from(">I", raw, p + 92 + ml)
+            mo, q = p + 92, p + 96 + ml
+        out.append((tid, ts, bl, raw[p + 24:p + 56], raw[p + 56:p + 88], ver, ne, ml, mo))
+        for _ in range(ne):
+            m_, = struct.unpack_from(">H", raw, q)
+            k_, = struct.unpack_from(">H", raw, q + 2 + m_)
+            q += 4 + m_ + k_ + 44
+        p = q + 32
+    return out
+
+
+@pytest.mark.parametrize("max_entries", [1, 2, 3, 5, 8, 16, 17, 40, 64])
+def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries):
+    """k_txlog_wave (one wave per 64 / L records, L lanes per record: every
+    lane-count the widest tx can pick) with the records staged in LDS and
+    read from HBM, against the workgroup kernel (MH_TXLOG_KERNEL=group), the
+    oracle and the record heads parsed in Python: headers (every field, Eh
+    included), Alh and per-tx statuses, clean and with corrupted records,
+    with pageable and pinned outputs."""
+    import torch
+    from immustore_amd.txlayer import TX_HEADER
+    rng = np.random.default_rng(100 + max_entries)
+    raw = _synthetic_txlog(rng, 700, orc, max_entries=max_entries)
+    bad = bytearray(raw)
+    for p in rng.integers(0, len(raw), 25):
+        bad[int(p)] ^= 0x40
+    cap = 800
+    pin = (torch.empty(cap * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy().view(TX_HEADER),
+           torch.empty(cap * 32, dtype=torch.uint8).pin_memory().numpy().reshape(cap, 32),
+           torch.empty(cap, dtype=torch.int32).pin_memory().numpy())
+    for buf in (raw, bytes(bad)):
+        o = orc.txlog_validate(buf)
+        res = {}
+        for kern, smax in (("group", None), ("wave", None), ("wave", "0")):
+            monkeypatch.setenv("MH_TXLOG_KERNEL", kern)
+            if smax is None:
+                monkeypatch.delenv("MH_TXLOG_STAGE_MAX", raising=False)
+            else:
+                monkeypatch.setenv("MH_TXLOG_STAGE_MAX", smax)
+            for out in (None, pin):
+                a = m.txlog_validate(buf, ctx=ctx, out=out)
+                assert (a[0], a[1], a[2]) == (o[0], o[1], o[2]), (kern, smax)
+                assert np.array_equal(a[4], o[3]) and list(a[5]) == list(o[4]), (kern, smax)
+                res[(kern, smax, out is None)] = a[3][:a[1]].copy()
+        ref = res[("group", None, True)]
+        for key, h in res.items():
+            assert np.array_equal(h, ref), key
+        if buf is raw:
+            heads = _record_heads(buf, o[1])
+            for h, x in zip(ref, heads):
+                got = (int(h["id"]), int(h["ts"]), int(h["bl_tx_id"]), h["bl_root"].tobytes(),
+                       h["prev_alh"].tobytes(), int(h["version"]), int(h["nentries"]),
+                       int(h["md_len"]), int(h["md_off"]))
+                assert got == x
+    monkeypatch.delenv("MH_TXLOG_KERNEL", raising=False)

@@ -20,6 +20,7 @@
 #   ab:<VARIANTS>    tools/ab_env.sh rotation, e.g. ab:base,MH_LPL=1
 #   txab:<VARIANTS>  tools/txlog_bench rotation (ROUNDS x), e.g. txab:base;MH_TXLOG_KERNEL=group
 #   txtl:<VARIANTS>  a14 kernel + copy timeline of the last call per variant -> txtl.txt
+#   txprobe:<VARS>   MH_TXLOG_PROBE=1 per-phase wave cycles of the a14 launches -> txprobe.txt
 #   workload:<name>  bench_workloads.py --workload <name>
 #   fuzz             host-ASan tx-log fuzzer with the device path (FUZZ_ITERS, FUZZ_SEED)
 #   queue            tools/queue_bench: group commit, 30 committers (QWAIT us, QMAXTXS)
@@ -91,6 +92,13 @@ for s in "$@"; do
       rc=$?; rm -rf "$O/corpus"; [ $rc -eq 0 ] || exit 1 ;;
     queue) step queue 300 ./tools/queue_bench 30 2000 16 1024 ${QWAIT:-20} ${QMAXTXS:-64} || exit 1 ;;
     traffic) step traffic 1200 bash tools/gpu_pmc.sh || exit 1 ;;
+    txprobe:*)  # MH_TXLOG_PROBE=1 per-phase wave timings of the a14 launches (last call), per variant
+      vs="$(echo "${s#txprobe:}" | tr ';' ' ')"
+      for v in $vs; do
+        envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
+        env MH_TXLOG_PROBE=1 $envs timeout -k 10 200 python3 tools/txlog_timeline.py > "$O/txprobe.out" 2> "$O/txprobe.err" || { tail -5 "$O/txprobe.err"; exit 1; }
+        { echo "# variant $v"; grep txlog_probe "$O/txprobe.err" | tail -4; tail -1 "$O/txprobe.out"; } | tee -a "$O/txprobe.txt"
+      done ;;
     workload:*) w="${s#workload:}"; step "wl_$w" 600 python bench_workloads.py --workload "$w" || exit 1 ;;
     pmctx) step pmctx 900 bash tools/gpu_pmc_txlog.sh || exit 1; cat "gpurun_out/pmctx${PMC_TAG:-}/table.txt" ;;
     ab:*) VARIANTS="$(echo "${s#ab:}" | tr ';' ' ')" step ab 900 bash tools/ab_env.sh || exit 1 ;;

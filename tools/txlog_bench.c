@@ -48,6 +48,8 @@ static int cmp(const void *a, const void *b) {
     } while (0)
 
 int main(int argc, char **argv) {
+    /* TXB_NO_HDRS=1: no header output (validation only: Alh + statuses) */
+    const int nohdr = getenv("TXB_NO_HDRS") && atoi(getenv("TXB_NO_HDRS"));
     const int K = argc > 1 ? atoi(argv[1]) : 50;
     const uint64_t ntx = argc > 2 ? strtoull(argv[2], 0, 10) : 65536;
     const uint64_t ne = argc > 3 ? strtoull(argv[3], 0, 10) : 16;
@@ -88,10 +90,10 @@ int main(int argc, char **argv) {
     double *ms = malloc(sizeof(double) * (size_t)K);
     /* clock pre-warm: calls for 2 s first (as bench_workloads.py --prewarm) */
     for (const double tw = now(); now() - tw < 2.0;)
-        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, hd, alh, st));
+        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, nohdr ? NULL : hd, alh, st));
     for (int k = 0; k < K; k++) {
         const double t0 = now();
-        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, hd, alh, st));
+        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, nohdr ? NULL : hd, alh, st));
         ms[k] = (now() - t0) * 1e3;
     }
     int bad = 0;
@@ -102,10 +104,10 @@ int main(int argc, char **argv) {
     printf("{\"metric\": \"tx-log read-path validation (a14) through the C ABI\", \"records\": %llu, "
            "\"entries_per_record\": %llu, \"log_bytes\": %llu, \"calls\": %d, \"ms_median\": %.4f, "
            "\"ms_min\": %.4f, \"ms_mean\": %.4f, \"M_tx_per_s_median\": %.3f, \"ntx\": %llu, "
-           "\"consumed\": %llu, \"invalid\": %d, \"pinned\": true}\n",
+           "\"consumed\": %llu, \"invalid\": %d, \"pinned\": true, \"headers_out\": %s}\n",
            (unsigned long long)ntx, (unsigned long long)ne, (unsigned long long)len, K, ms[K / 2],
            ms[0], sum / K, ntx / (ms[K / 2] * 1e-3) / 1e6, (unsigned long long)n,
-           (unsigned long long)used, bad);
+           (unsigned long long)used, bad, nohdr ? "false" : "true");
     free(ms);
     mh_host_free_pinned(log);
     mh_host_free_pinned(alh);
