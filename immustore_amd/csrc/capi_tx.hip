@@ -1154,12 +1154,14 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 hipStreamSynchronize(c2);
             }
         } stream_guard{st, c->d2h_stream, c->stream2};
-        // early groups alternate between the context's stream and a second
-        // compute stream, so a group's kernel never waits behind the previous
-        // group's (the last chunk's group starts as soon as its chunk lands);
-        // MH_TXLOG_STREAMS=1: one stream (A/B, read per call)
+        // MH_TXLOG_STREAMS=2 (A/B, read per call): early groups alternate
+        // between the context's stream and a second compute stream, so a
+        // group's kernel never waits behind the previous group's.  Off by
+        // default: with k_txlog_wave a group's kernel ends before the next
+        // chunk lands, and two groups sharing the CUs slowed the last one
+        // (profiles/ab_txlog_streams_r04.txt)
         const char *nse = getenv("MH_TXLOG_STREAMS");
-        const bool two_streams = !(nse && atoi(nse) == 1);
+        const bool two_streams = nse && atoi(nse) == 2;
         auto gstream = [&](uint64_t k) { return two_streams && (k & 1) ? c->stream2 : st; };
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
