@@ -1111,7 +1111,10 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         hipSetDevice(c->device);
         MH_HIP(c->copy_lane());
         hipStream_t st = c->stream;
-        if (len) MH_HIP(c->s_txlog.ensure(len));
+        // + 256: k_txlog_wave's staging of a wave's records reads up to 128
+        // bytes past the last record's stored Alh (16-byte pieces + its
+        // unguarded block over-read pad), inside the allocation
+        if (len) MH_HIP(c->s_txlog.ensure(len + 256));
         uint8_t *dbuf = c->s_txlog.as<uint8_t>();
         // A pinned log: K chunks from 16 MiB up (MH_TXLOG_CHUNKS, default 4)
         // of decreasing size, K : K-1 : ... : 1 (the last chunk's device work
@@ -1130,6 +1133,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             // the whole range in one pinned allocation (first and last byte)
             pinned = inl && len && same_alloc(buf, buf + len - 1);
         }
+        tr.mark("attrs");
         const uint64_t K = len < (16ull << 20) ? 1 : pinned ? txlog_chunks() : 2;
         std::vector<uint64_t> cut(K + 1, 0);
         for (uint64_t k = 1; k < K; k++) {
@@ -1143,6 +1147,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         cut[K] = len;
         const uint64_t nck = len ? K : 0;
         MH_HIP(ensure_chunk_events(c, 2 * nck));
+        tr.mark("events");
         // once a group's kernels are queued they may store into the caller's
         // pinned status / alh / header arrays: every exit (errors included)
         // waits for both streams, so nothing writes caller memory after return

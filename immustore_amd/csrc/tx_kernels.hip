@@ -14,6 +14,8 @@
 // roofline shaped, and they exist so that no hashing of this layer runs on
 // the host.
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "digest_io.hpp"
 #include "mh_internal.hpp"
@@ -1236,6 +1238,7 @@ namespace {
 struct TxwProbe {
     std::vector<std::pair<uint64_t *, unsigned>> bufs;  // (device stamps, waves)
     size_t used = 0;
+    std::mutex mu;  // contexts validating concurrently share the slots
 };
 TxwProbe &txw_probe() {
     static TxwProbe p;
@@ -1250,6 +1253,7 @@ bool txw_probe_on() {
 static uint64_t *txlog_probe_slot(unsigned waves) {
     if (!txw_probe_on()) return nullptr;
     TxwProbe &p = txw_probe();
+    std::lock_guard<std::mutex> lk(p.mu);
     if (p.used == p.bufs.size()) p.bufs.push_back({nullptr, 0});
     auto &b = p.bufs[p.used++];
     if (b.second < waves) {
@@ -1269,6 +1273,7 @@ static uint64_t *txlog_probe_slot(unsigned waves) {
 void txlog_probe_report() {
     if (!txw_probe_on()) return;
     TxwProbe &p = txw_probe();
+    std::lock_guard<std::mutex> lk(p.mu);
     for (size_t l = 0; l < p.used; l++) {
         const unsigned n = p.bufs[l].second;
         std::vector<uint64_t> h((size_t)n * 16);
