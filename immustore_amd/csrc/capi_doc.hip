@@ -194,21 +194,22 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
             !B->ehval || !B->src_hdr || !B->tgt_hdr || !B->incl_off || !B->cons_off ||
             !B->known_tx_id || !B->known_alh)
             return MH_ERR_ILLEGAL_ARGUMENTS;
+        // the extents first: every copy below reads [first, last) of an
+        // array; that every offset in between is in order is checked on the
+        // host while the copies run, before any kernel reads through them
+        if (B->doc_off[n] < B->doc_off[0] || B->doc_key_off[n] < B->doc_key_off[0] ||
+            B->ent_off[n] < B->ent_off[0] || B->incl_off[n] < B->incl_off[0] ||
+            B->cons_off[n] < B->cons_off[0])
+            return MH_ERR_ILLEGAL_ARGUMENTS;
         const uint64_t E = B->ent_off[n] - B->ent_off[0];
+        if (E && (B->ekey_off[B->ent_off[n]] < B->ekey_off[B->ent_off[0]] ||
+                  (B->emd_off && B->emd_off[B->ent_off[n]] < B->emd_off[B->ent_off[0]])))
+            return MH_ERR_ILLEGAL_ARGUMENTS;
         if ((B->doc_off[n] > B->doc_off[0] && !B->doc) ||
             (B->doc_key_off[n] > B->doc_key_off[0] && !B->doc_key) ||
             (E && B->ekey_off[B->ent_off[n]] > B->ekey_off[B->ent_off[0]] && !B->ekeys) ||
             (B->emd_off && E && B->emd_off[B->ent_off[n]] > B->emd_off[B->ent_off[0]] && !B->emd))
             return MH_ERR_ILLEGAL_ARGUMENTS;
-        for (uint64_t d = 0; d < n; d++)
-            if (B->doc_off[d + 1] < B->doc_off[d] || B->doc_key_off[d + 1] < B->doc_key_off[d] ||
-                B->ent_off[d + 1] < B->ent_off[d] || B->incl_off[d + 1] < B->incl_off[d] ||
-                B->cons_off[d + 1] < B->cons_off[d])
-                return MH_ERR_ILLEGAL_ARGUMENTS;
-        for (uint64_t e = B->ent_off[0]; e < B->ent_off[n]; e++)
-            if (B->ekey_off[e + 1] < B->ekey_off[e] ||
-                (B->emd_off && B->emd_off[e + 1] < B->emd_off[e]))
-                return MH_ERR_ILLEGAL_ARGUMENTS;
         MH_HIP(hipSetDevice(c->device));
         const uint64_t e0 = B->ent_off[0];
 
@@ -232,20 +233,6 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
         //  5. VerifyDualProofV2 (:185-194)
         bool any_v0 = false;
         for (uint64_t d = 0; d < n && !any_v0; d++) any_v0 = B->tx_hdr[d].version == 0;
-        std::vector<uint64_t> leaf_off(n + 1);
-        for (uint64_t d = 0; d <= n; d++) leaf_off[d] = B->ent_off[d] - e0;
-        std::vector<uint8_t> ov, ver;
-        if (any_v0 && E) {
-            ov.resize(E * 32);
-            ver.resize(E);
-            for (uint64_t d = 0; d < n; d++) {
-                const uint8_t v = B->tx_hdr[d].version == 0 ? 0 : 1;
-                for (uint64_t e = B->ent_off[d]; e < B->ent_off[d + 1]; e++) {
-                    ver[e - e0] = v;
-                    memcpy(&ov[32 * (e - e0)], v ? B->ehval + 32 * e : kEmptyRoot, 32);
-                }
-            }
-        }
         const uint64_t k0 = E ? B->ekey_off[e0] : 0, kb = E ? B->ekey_off[e0 + E] - k0 : 0;
         const bool has_md = B->emd_off != nullptr;
         const uint64_t m0 = (has_md && E) ? B->emd_off[e0] : 0,
@@ -279,71 +266,139 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
                        b_sel = L.add(n), b_sbl = L.add(n * 32), b_tbl = L.add(n * 32),
                        b_leaf = L.add(n * 32), b_ca = L.add(n * 32), b_oki = L.add(n),
                        b_okc = L.add(n), b_ta = L.add(n * 32);
+        // the caller's arrays: one copy each, or -- when they all lie in one
+        // pinned allocation (the shim's packing arena) with little between
+        // them -- ONE copy of the whole span, each array then addressed inside
+        // it (MH_DOC_ARENA=0: per-array copies, A/B)
+        struct Up {
+            uint64_t off;
+            const uint8_t *src;
+            uint64_t bytes;
+        };
+        std::vector<Up> ups;
+        auto add = [&](uint64_t off, const void *src, uint64_t bytes) {
+            ups.push_back(Up{off, static_cast<const uint8_t *>(src), src ? bytes : 0});
+        };
+        add(b_doc, B->doc + dc0, dcb);
+        add(b_doff, B->doc_off, (n + 1) * 8);
+        add(b_dk, B->doc_key + dk0, dkb);
+        add(b_dko, B->doc_key_off, (n + 1) * 8);
+        add(b_eo, B->ent_off, (n + 1) * 8);
+        if (E) {
+            add(b_k, B->ekeys + k0, kb);
+            add(b_m, B->emd + m0, mb);
+            add(b_ko, B->ekey_off + e0, (E + 1) * 8);
+            if (has_md) add(b_mo, B->emd_off + e0, (E + 1) * 8);
+            add(b_hv, B->ehval + 32 * e0, E * 32);
+        }
+        add(b_h3r, B->tx_hdr, hb);
+        add(b_h3r + hb, B->src_hdr, hb);
+        add(b_h3r + 2 * hb, B->tgt_hdr, hb);
+        add(b_md, B->md_blob, mdl);
+        add(b_kid, B->known_tx_id, n * 8);
+        add(b_kalh, B->known_alh, n * 32);
+        add(b_io, B->incl_off, (n + 1) * 8);
+        add(b_co, B->cons_off, (n + 1) * 8);
+        add(b_it, B->incl_terms ? B->incl_terms + 32 * i0 : nullptr, ni * 32);
+        add(b_ct, B->cons_terms ? B->cons_terms + 32 * c0 : nullptr, nc * 32);
+        const uint8_t *lo = nullptr, *hi = nullptr;
+        uint64_t sum = 0;
+        for (const Up &u : ups)
+            if (u.bytes) {
+                lo = lo ? std::min(lo, u.src) : u.src;
+                hi = hi ? std::max(hi, u.src + u.bytes) : u.src + u.bytes;
+                sum += u.bytes;
+            }
+        static const bool arena_on = [] {
+            const char *e = getenv("MH_DOC_ARENA");
+            return !(e && e[0] == '0');
+        }();
+        const uint8_t *alo = lo ? reinterpret_cast<const uint8_t *>((uintptr_t)lo & ~(uintptr_t)255) : nullptr;
+        const bool arena = arena_on && lo && (uint64_t)(hi - alo) <= sum + sum / 4 + (1u << 20) &&
+                           pinned_same_alloc(alo, hi - 1);
+        const uint64_t b_span = L.add(arena ? (uint64_t)(hi - alo) : 0);
         MH_HIP(c->s_msgs.ensure(L.total));
         uint8_t *base = c->s_msgs.as<uint8_t>();
-        auto up = [&](uint64_t off, const void *src, uint64_t bytes) -> hipError_t {
-            return bytes ? hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, st)
-                         : hipSuccess;
+        // the device address of the array uploaded to layout slot off
+        auto dp = [&](uint64_t off) -> uint8_t * {
+            if (arena)
+                for (const Up &u : ups)
+                    if (u.off == off && u.bytes) return base + b_span + (u.src - alo);
+            return base + off;
         };
-        MH_HIP(up(b_doc, B->doc + dc0, dcb));
-        MH_HIP(up(b_doff, B->doc_off, (n + 1) * 8));
-        MH_HIP(up(b_dk, B->doc_key + dk0, dkb));
-        MH_HIP(up(b_dko, B->doc_key_off, (n + 1) * 8));
-        MH_HIP(up(b_eo, B->ent_off, (n + 1) * 8));
-        if (E) {
-            MH_HIP(up(b_k, B->ekeys + k0, kb));
-            MH_HIP(up(b_m, B->emd + m0, mb));
-            MH_HIP(up(b_ko, B->ekey_off + e0, (E + 1) * 8));
-            if (has_md) MH_HIP(up(b_mo, B->emd_off + e0, (E + 1) * 8));
-            MH_HIP(up(b_hv, B->ehval + 32 * e0, E * 32));
-            if (any_v0) {
-                MH_HIP(up(b_ov, ov.data(), E * 32));
-                MH_HIP(up(b_ver, ver.data(), E));
+        if (arena) {
+            MH_HIP(hipMemcpyAsync(base + b_span, alo, (uint64_t)(hi - alo), hipMemcpyHostToDevice, st));
+        } else {
+            for (const Up &u : ups)
+                if (u.bytes) MH_HIP(hipMemcpyAsync(base + u.off, u.src, u.bytes, hipMemcpyHostToDevice, st));
+        }
+        // every offset in order (host, under the copies; branch-free loops)
+        {
+            bool bad = false;
+            for (uint64_t d = 0; d < n; d++)
+                bad |= (B->doc_off[d + 1] < B->doc_off[d]) | (B->doc_key_off[d + 1] < B->doc_key_off[d]) |
+                       (B->ent_off[d + 1] < B->ent_off[d]) | (B->incl_off[d + 1] < B->incl_off[d]) |
+                       (B->cons_off[d + 1] < B->cons_off[d]);
+            const uint64_t *ko = B->ekey_off, *mo = B->emd_off;
+            for (uint64_t e = e0; e < e0 + E; e++) bad |= ko[e + 1] < ko[e];
+            if (mo)
+                for (uint64_t e = e0; e < e0 + E; e++) bad |= mo[e + 1] < mo[e];
+            if (bad) {
+                MH_HIP(hipStreamSynchronize(st));  // the copies read the caller's arrays
+                return MH_ERR_ILLEGAL_ARGUMENTS;
             }
         }
-        MH_HIP(up(b_h3r, B->tx_hdr, hb));
-        MH_HIP(up(b_h3r + hb, B->src_hdr, hb));
-        MH_HIP(up(b_h3r + 2 * hb, B->tgt_hdr, hb));
-        MH_HIP(up(b_md, B->md_blob, mdl));
-        MH_HIP(up(b_kid, B->known_tx_id, n * 8));
-        MH_HIP(up(b_kalh, B->known_alh, n * 32));
-        MH_HIP(up(b_io, B->incl_off, (n + 1) * 8));
-        MH_HIP(up(b_co, B->cons_off, (n + 1) * 8));
-        MH_HIP(up(b_it, B->incl_terms ? B->incl_terms + 32 * i0 : nullptr, ni * 32));
-        MH_HIP(up(b_ct, B->cons_terms ? B->cons_terms + 32 * c0 : nullptr, nc * 32));
+        std::vector<uint64_t> leaf_off(n + 1);
+        for (uint64_t d = 0; d <= n; d++) leaf_off[d] = B->ent_off[d] - e0;
+        std::vector<uint8_t> ov, ver;
+        if (any_v0 && E) {
+            ov.resize(E * 32);
+            ver.resize(E);
+            for (uint64_t d = 0; d < n; d++) {
+                const uint8_t v = B->tx_hdr[d].version == 0 ? 0 : 1;
+                for (uint64_t e = B->ent_off[d]; e < B->ent_off[d + 1]; e++) {
+                    ver[e - e0] = v;
+                    memcpy(&ov[32 * (e - e0)], v ? B->ehval + 32 * e : kEmptyRoot, 32);
+                }
+            }
+            MH_HIP(hipMemcpyAsync(base + b_ov, ov.data(), E * 32, hipMemcpyHostToDevice, st));
+            MH_HIP(hipMemcpyAsync(base + b_ver, ver.data(), E, hipMemcpyHostToDevice, st));
+        }
         const unsigned g1 = (unsigned)((n + 255) / 256), g3 = (unsigned)((3 * n + 255) / 256);
         // 1.
-        MH_HIP(launch_sha256_csr(st, c->tm(), base + b_doc - dc0, (const uint64_t *)(base + b_doff),
+        MH_HIP(launch_sha256_csr(st, c->tm(), dp(b_doc) - dc0, (const uint64_t *)dp(b_doff),
                                  n, nullptr, nullptr, base + b_hdoc, base + b_sort));
         hipLaunchKernelGGL(k_doc_find, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n,
-                           (const uint64_t *)(base + b_eo), base + b_dk - dk0,
-                           (const uint64_t *)(base + b_dko), base + b_k - k0,
-                           (const uint64_t *)(base + b_ko) - e0, base + b_hv, base + b_hdoc,
+                           (const uint64_t *)dp(b_eo), dp(b_dk) - dk0,
+                           (const uint64_t *)dp(b_dko), dp(b_k) - k0,
+                           (const uint64_t *)dp(b_ko) - e0, dp(b_hv), base + b_hdoc,
                            (int32_t *)(base + b_st));
         MH_HIP(hipGetLastError());
         // 3.
         if (E)
-            MH_HIP(launch_entries_varlen(st, c->tm(), 1, E, base + b_k - k0,
-                                         (const uint64_t *)(base + b_ko),
-                                         has_md ? base + b_m - m0 : nullptr,
-                                         has_md ? (const uint64_t *)(base + b_mo) : nullptr,
-                                         nullptr, nullptr, any_v0 ? base + b_ov : base + b_hv,
+            MH_HIP(launch_entries_varlen(st, c->tm(), 1, E, dp(b_k) - k0,
+                                         (const uint64_t *)dp(b_ko),
+                                         has_md ? dp(b_m) - m0 : nullptr,
+                                         has_md ? (const uint64_t *)dp(b_mo) : nullptr,
+                                         nullptr, nullptr, any_v0 ? base + b_ov : dp(b_hv),
                                          nullptr, nullptr, base + b_dig, false, nullptr,
                                          any_v0 ? base + b_ver : nullptr));
         if (int e = build_many_dev(c, st, n, leaf_off.data(), base + b_dig, base + b_r,
                                    c->s_digests, c->s_offs))
             return e;
         // 4.
-        const mh_tx_header *h3r = reinterpret_cast<const mh_tx_header *>(base + b_h3r);
+        const mh_tx_header *htx = reinterpret_cast<const mh_tx_header *>(dp(b_h3r)),
+                           *hsrc = reinterpret_cast<const mh_tx_header *>(dp(b_h3r + hb)),
+                           *htgt = reinterpret_cast<const mh_tx_header *>(dp(b_h3r + 2 * hb));
         mh_tx_header *h3 = reinterpret_cast<mh_tx_header *>(base + b_h3);
-        hipLaunchKernelGGL(k_doc_hdr_prep, dim3(g3), dim3(256), 0, st, n, h3r, h3r + n, h3r + 2 * n,
+        hipLaunchKernelGGL(k_doc_hdr_prep, dim3(g3), dim3(256), 0, st, n, htx, hsrc, htgt,
                            mdl, B->md_blob != nullptr ? 1 : 0, h3, base + b_hok);
         MH_HIP(hipGetLastError());
-        MH_HIP(launch_tx_alh(st, c->tm(), 3 * n, h3, base + b_md, nullptr, base + b_hs, nullptr,
+        MH_HIP(launch_tx_alh(st, c->tm(), 3 * n, h3, dp(b_md), nullptr, base + b_hs, nullptr,
                              nullptr, nullptr, base + b_alh, nullptr));
-        hipLaunchKernelGGL(k_doc_state, dim3(g1), dim3(256), 0, st, n, h3r, h3, base + b_hok,
-                           base + b_alh, base + b_r, (const uint64_t *)(base + b_kid),
-                           base + b_kalh, (int32_t *)(base + b_st), (uint64_t *)(base + b_ii),
+        hipLaunchKernelGGL(k_doc_state, dim3(g1), dim3(256), 0, st, n, htx, h3, base + b_hok,
+                           base + b_alh, base + b_r, (const uint64_t *)dp(b_kid),
+                           dp(b_kalh), (int32_t *)(base + b_st), (uint64_t *)(base + b_ii),
                            (uint64_t *)(base + b_ij), (uint64_t *)(base + b_ci), base + b_sel,
                            base + b_sbl, base + b_tbl);
         MH_HIP(hipGetLastError());
@@ -352,13 +407,13 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
         //    the caller's term offsets, the terms' base shifted by the first
         MH_HIP(launch_leaf_for(st, c->tm(), n, base + b_alh + 32 * n, base + b_leaf));
         MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_INCLUSION, n, (const uint64_t *)(base + b_ii),
-                                    (const uint64_t *)(base + b_ij), (const uint64_t *)(base + b_io),
-                                    base + b_it - 32 * i0, base + b_leaf, base + b_tbl,
+                                    (const uint64_t *)(base + b_ij), (const uint64_t *)dp(b_io),
+                                    dp(b_it) - 32 * i0, base + b_leaf, base + b_tbl,
                                     base + b_oki, nullptr));
         MH_HIP(launch_select32(st, n, base + b_sel, base + b_leaf, base + b_sbl, base + b_ca));
         MH_HIP(launch_ahtree_verify(st, c->tm(), MH_AHT_CONSISTENCY, n,
                                     (const uint64_t *)(base + b_ci), (const uint64_t *)(base + b_ij),
-                                    (const uint64_t *)(base + b_co), base + b_ct - 32 * c0,
+                                    (const uint64_t *)dp(b_co), dp(b_ct) - 32 * c0,
                                     base + b_ca, base + b_tbl, base + b_okc, nullptr));
         hipLaunchKernelGGL(k_doc_final, dim3(g1), dim3(256), 0, st, n, h3, base + b_alh,
                            base + b_oki, base + b_okc, (int32_t *)(base + b_st), base + b_ta);

@@ -335,6 +335,18 @@ struct ChunkCopier {
     }
 };
 
+// a and b in the same pinned host allocation (device addresses as far apart)
+inline bool pinned_same_alloc(const void *a, const void *b) {
+    hipPointerAttribute_t x, y;
+    if (hipPointerGetAttributes(&x, a) != hipSuccess || hipPointerGetAttributes(&y, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return x.type == hipMemoryTypeHost && y.type == hipMemoryTypeHost && x.devicePointer &&
+           (const uint8_t *)y.devicePointer - (const uint8_t *)x.devicePointer ==
+               (const uint8_t *)b - (const uint8_t *)a;
+}
+
 // events for n chunks in c->ev_chunks
 inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
     while (c->ev_chunks.size() < n) {

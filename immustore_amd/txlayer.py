@@ -261,14 +261,43 @@ class _Pinned:
             self.p = None
 
 
-def pack_document_batch(docs, pinned: bool = False):
+class _Arena:
+    """Arrays packed back to back (256-byte aligned) in ONE pinned host
+    allocation, as a cgo shim's packing arena holds a batch."""
+
+    def __init__(self, arrays):
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        offs, o = [], 0
+        for a in arrays:
+            offs.append(o)
+            o += (max(a.nbytes, 1) + 255) & ~255
+        self.p = C.c_void_p()
+        N.check(N.load().mh_host_alloc_pinned(max(o, 1), C.byref(self.p)))
+        self.addrs = []
+        for a, off in zip(arrays, offs):
+            if a.nbytes:
+                C.memmove(self.p.value + off, a.ctypes.data, a.nbytes)
+            self.addrs.append(self.p.value + off)
+
+    def __del__(self):
+        if self.p:
+            N.load().mh_host_free_pinned(self.p)
+            self.p = None
+
+
+def pack_document_batch(docs, pinned=False):
     """The mh_document_batch of verify_document_batch's docs -> (struct, the
-    arrays it points into, to be kept alive while it is used).  pinned: the
-    arrays in pinned host memory, as a cgo shim's packing arena would be."""
+    arrays it points into, to be kept alive while it is used).  pinned: True
+    puts every array in its own pinned allocation; "arena" packs them all into
+    one pinned allocation, as a cgo shim's packing arena would."""
     n = len(docs)
     keep = []
+    arena = []
 
     def k(a):
+        if pinned == "arena":
+            arena.append(np.ascontiguousarray(a))
+            return len(arena) - 1  # an index until the arena exists
         if pinned:
             a = _Pinned(a)
             keep.append(a)
@@ -293,10 +322,14 @@ def pack_document_batch(docs, pinned: bool = False):
     co, ct = _terms_csr([d["cons"] for d in docs])
     kid = np.array([d.get("known_tx_id", 0) for d in docs], np.uint64)
     kalh = _d32([d.get("known_alh", bytes(32)) for d in docs], n)
-    b = _DocumentBatch(n, k(dbuf), k(doff), k(kbuf), k(koff), k(txh), k(ent_off), k(ekbuf),
-                       k(ekoff), k(embuf), k(emoff), k(ehv), k(sh), k(th),
-                       k(mb) if mb is not None else None, ml, k(io), k(it), k(co), k(ct), k(kid),
-                       k(kalh))
+    ptrs = [k(dbuf), k(doff), k(kbuf), k(koff), k(txh), k(ent_off), k(ekbuf), k(ekoff), k(embuf),
+            k(emoff), k(ehv), k(sh), k(th), k(mb) if mb is not None else None, ml, k(io), k(it),
+            k(co), k(ct), k(kid), k(kalh)]
+    if pinned == "arena":
+        ar = _Arena(arena)
+        keep.append(ar)
+        ptrs = [p if i == 14 or p is None else ar.addrs[p] for i, p in enumerate(ptrs)]
+    b = _DocumentBatch(n, *ptrs)
     return b, keep
 
 

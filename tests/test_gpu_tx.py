@@ -488,6 +488,27 @@ def test_verify_document_batch_vs_oracle(m, ctx, orc, fixtures):
     assert (st == 0).sum() >= 40
 
 
+@pytest.mark.parametrize("pinned", [True, "arena"])
+def test_verify_document_batch_pinned_and_arena(m, ctx, orc, fixtures, pinned):
+    """The same document cases packed in pinned memory, one allocation per
+    array or every array in ONE pinned allocation (the shim's arena: one
+    upload of the whole span, each array addressed inside it) -- per-document
+    status and Alh equal to the oracle and to the pageable call."""
+    from immustore_amd import txlayer
+    from tx_util import document_cases
+    docs, blob = document_cases(fixtures, orc)
+    docs[0]["md_blob"] = blob
+    ref = txlayer.verify_document_batch(docs, ctx=ctx)
+    b, keep = txlayer.pack_document_batch(docs, pinned=pinned)
+    st, alh = txlayer.call_document_batch(b, len(docs), ctx)
+    assert np.array_equal(st, ref[0]) and np.array_equal(alh, ref[1])
+    for k, d in enumerate(docs):
+        ost, oalh = orc.verify_document(d, blob)
+        assert int(st[k]) == ost, k
+        assert alh[k].tobytes() == (oalh if ost == 0 else bytes(32)), k
+    del keep
+
+
 def test_verify_document_batch_offsets_running_backwards(m, ctx, orc, fixtures):
     """Offsets that run backwards (document, key, entry and proof-term CSR)
     are rejected with ErrIllegalArguments before anything is read through
