@@ -1173,6 +1173,10 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         for (uint64_t k = 0; k < nck; k++)
             cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], cut[k + 1] - cut[k]}};
         cc.inline_issue = pinned;
+        {  // MH_TXLOG_FLAGS=1: chunk arrival by stream-written words (A/B, read per call)
+            const char *fl = getenv("MH_TXLOG_FLAGS");
+            if (fl && atoi(fl) == 1 && nck) MH_HIP(cc.use_flags());
+        }
         {  // MH_TXLOG_COPY_LANES=2: chunk k on copy stream k % 2 (A/B, read per call)
             const char *cl = getenv("MH_TXLOG_COPY_LANES");
             if (cl && atoi(cl) == 2 && pinned) cc.lanes = 2;
@@ -1390,7 +1394,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                              {nt, nt, nt + 1}}));
             g.fetched = true;
             if (hipError_t e = cc.wait(g.k)) return -(int)e;
-            MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[g.k], 0));
+            MH_HIP(cc.stream_wait(st, g.k));
             if (int e = run(g, dbuf, nullptr, 0, 0, st)) return e;
             MH_HIP(hipEventRecord(c->ev_chunks[nck + g.k], st));
             return results(g, c->ev_chunks[nck + g.k]);
@@ -1457,7 +1461,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         const uint64_t t_rest = gs.empty() ? 0 : gs.back().t1;
         if (t_rest < ntx) {
             // ---- the rest as one group once the whole log is in
-            if (nck) MH_HIP(hipStreamWaitEvent(st, c->ev_chunks[nck - 1], 0));
+            if (nck) MH_HIP(cc.stream_wait(st, nck - 1));
             gs.emplace_back();
             Grp &g = gs.back();
             if (int e = prepare(g, gs.size() - 1, t_rest, ntx, e_done)) return e;

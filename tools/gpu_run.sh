@@ -16,6 +16,7 @@
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
 #   txlog            tools/txlog_bench (a14 through the C ABI)
+#   copyprobe        tools/copy_probe: chunked pinned H2D pipeline costs (host wall time)
 #   workloads        bench_workloads.py: every secondary workload line
 #   ab:<VARIANTS>    tools/ab_env.sh rotation, e.g. ab:base,MH_LPL=1
 #   txab:<VARIANTS>  tools/txlog_bench rotation (ROUNDS x), e.g. txab:base;MH_TXLOG_KERNEL=group
@@ -65,6 +66,7 @@ for s in "$@"; do
       rm -rf "$O/prof"
       step prof 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
     txlog) step txlog 300 ./tools/txlog_bench || exit 1 ;;
+    copyprobe) step copyprobe 200 ./tools/copy_probe || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;
     txab:*)  # interleaved A/B of tools/txlog_bench over env variants, e.g. txab:base;MH_TXLOG_KERNEL=group
       vs="$(echo "${s#txab:}" | tr ';' ' ')"
