@@ -204,11 +204,6 @@ struct mh_ctx {
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf s_chunk[2];
     std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call
-    // chunk-arrival flags (ChunkCopier::flags): one word per chunk, written by
-    // the copy stream after the chunk, waited on by value; flag_seq numbers
-    // the calls so a stale word never matches
-    DevBuf s_flags;
-    uint32_t flag_seq = 0;
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
     // creates copy_stream and the events on first use (c->mu held)
     hipError_t copy_lane() {
@@ -260,9 +255,6 @@ struct ChunkCopier {
     std::thread th[2];
     int lanes = 1;  // 1: one helper thread / copy stream; 2: two
     bool inline_issue = false;  // issue every copy from the caller (pinned sources: no blocking)
-    // chunk arrival as a stream-written word instead of an event (use_flags())
-    uint32_t *flags = nullptr;
-    uint32_t seq = 0;
 
     bool started = false;
     explicit ChunkCopier(mh_ctx *ctx) : c(ctx) {}
@@ -301,9 +293,7 @@ struct ChunkCopier {
                 for (size_t k = (size_t)j; k < chunks.size(); k += (size_t)lanes) {
                     for (const Piece &p : chunks[k])
                         if (!e && p.bytes) e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, s);
-                    if (!e)
-                        e = flags ? hipStreamWriteValue32(s, flags + k, seq, 0)
-                                  : hipEventRecord(c->ev_chunks[k], s);
+                    if (!e) e = hipEventRecord(c->ev_chunks[k], s);
                     std::lock_guard<std::mutex> g(m);
                     if (e) {
                         err = e;
@@ -332,24 +322,11 @@ struct ChunkCopier {
         cv.wait(g, [&] { return done[k] || err != hipSuccess; });
         return err;
     }
-    // arrival of chunk k as flag words (at most 64 chunks) for this call
-    hipError_t use_flags() {
-        if (chunks.size() > 64) return hipErrorInvalidValue;
-        if (!c->s_flags.p) {
-            if (hipError_t e = c->s_flags.ensure(64 * 4)) return e;
-            if (hipError_t e = hipMemset(c->s_flags.p, 0, 64 * 4)) return e;
-        }
-        if (++c->flag_seq == 0) c->flag_seq = 1;
-        flags = c->s_flags.as<uint32_t>();
-        seq = c->flag_seq;
-        return hipSuccess;
-    }
     // stream st waits until chunk k has landed (after wait(k) succeeded: its
-    // copies and marker are enqueued, so the wait always ends)
-    hipError_t stream_wait(hipStream_t st, size_t k) {
-        if (flags) return hipStreamWaitValue32(st, flags + k, seq, hipStreamWaitValueEq, 0xffffffffu);
-        return hipStreamWaitEvent(st, c->ev_chunks[k], 0);
-    }
+    // copies and event are enqueued).  Events, not stream-written words:
+    // ROCclr runs hipStreamWriteValue32 / WaitValue32 as blit kernels, no
+    // faster (profiles/ab_txlog_wait0_flags_r04.txt)
+    hipError_t stream_wait(hipStream_t st, size_t k) { return hipStreamWaitEvent(st, c->ev_chunks[k], 0); }
     // chunk k's copies and event are enqueued already (no waiting)
     bool issued(size_t k) {
         std::lock_guard<std::mutex> g(m);

@@ -1173,10 +1173,6 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         for (uint64_t k = 0; k < nck; k++)
             cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], cut[k + 1] - cut[k]}};
         cc.inline_issue = pinned;
-        {  // MH_TXLOG_FLAGS=1: chunk arrival by stream-written words (A/B, read per call)
-            const char *fl = getenv("MH_TXLOG_FLAGS");
-            if (fl && atoi(fl) == 1 && nck) MH_HIP(cc.use_flags());
-        }
         {  // MH_TXLOG_COPY_LANES=2: chunk k on copy stream k % 2 (A/B, read per call)
             const char *cl = getenv("MH_TXLOG_COPY_LANES");
             if (cl && atoi(cl) == 2 && pinned) cc.lanes = 2;

@@ -321,17 +321,14 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
             assert np.array_equal(a[3], c[3])
 
 
-@pytest.mark.parametrize("flags", ["0", "1"])
-def test_txlog_validate_pinned_last_chunk(m, ctx, orc, monkeypatch, flags):
+def test_txlog_validate_pinned_last_chunk(m, ctx, orc):
     """The last copy chunk of a pinned log (its group's kernel runs right
     after it lands and stores the results into the pinned outputs itself):
     ends that are not 16-byte multiples, errors / max_txs / a corrupted hVal
     inside the last chunk, and a wide tx or re-encoded metadata at the end (the
     rest-group path) -- equal to the oracle and to the pageable call, headers
-    included.  flags=1: chunk arrival signalled by stream-written words
-    (MH_TXLOG_FLAGS) instead of events."""
+    included."""
     import torch
-    monkeypatch.setenv("MH_TXLOG_FLAGS", flags)
     from tx_util import metadata_logs
     from immustore_amd.txlayer import TX_HEADER
     rng = np.random.default_rng(31)
