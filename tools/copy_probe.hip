@@ -9,6 +9,8 @@
 //   k<K>kern0   + the copy stream first waits on an event of the (idle)
 //               compute stream (what every a14 call does today)
 //   single+k    one copy, then one kernel on the SAME stream
+//   *-spin      the host polls hipStreamQuery instead of hipStreamSynchronize
+//   small       a 4 KiB copy: the fixed round trip of one copy and its wait
 //   k<K>wv      chunk flags by hipStreamWriteValue32 on the copy stream,
 //               the compute stream waits by hipStreamWaitValue32
 // Diagnosis only; nothing on the product path uses it.
@@ -82,6 +84,18 @@ int main(int argc, char **argv) {
     vs.push_back({"single", [&] {
                       CK(hipMemcpyAsync(d, h, len, hipMemcpyHostToDevice, cs));
                       CK(hipStreamSynchronize(cs));
+                  }});
+    vs.push_back({"single-spin", [&] {  // the same, the host polling the stream
+                      CK(hipMemcpyAsync(d, h, len, hipMemcpyHostToDevice, cs));
+                      while (hipStreamQuery(cs) == hipErrorNotReady) (void)hipGetLastError();
+                  }});
+    vs.push_back({"small", [&] {  // 4 KiB: the round trip of one copy + wait
+                      CK(hipMemcpyAsync(d, h, 4096, hipMemcpyHostToDevice, cs));
+                      CK(hipStreamSynchronize(cs));
+                  }});
+    vs.push_back({"small-spin", [&] {
+                      CK(hipMemcpyAsync(d, h, 4096, hipMemcpyHostToDevice, cs));
+                      while (hipStreamQuery(cs) == hipErrorNotReady) (void)hipGetLastError();
                   }});
     vs.push_back({"single+k", [&] {
                       CK(hipMemcpyAsync(d, h, len, hipMemcpyHostToDevice, cs));
