@@ -351,27 +351,6 @@ inline bool pinned_same_alloc(const void *a, const void *b) {
                (const uint8_t *)b - (const uint8_t *)a;
 }
 
-// The end of a latency-bound call: wait for stream s by polling it from this
-// thread instead of hipStreamSynchronize, whose wait may sleep until an
-// interrupt wakes it (tens of us after the last kernel ends).  MH_SYNC_SPIN
-// (read once): 1 polls, 0 = hipStreamSynchronize (A/B).
-inline bool sync_spin_on() {
-    static const bool on = [] {
-        const char *e = getenv("MH_SYNC_SPIN");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-inline hipError_t wait_stream(hipStream_t s) {
-    if (!sync_spin_on()) return hipStreamSynchronize(s);
-    for (;;) {
-        const hipError_t e = hipStreamQuery(s);
-        if (e != hipErrorNotReady) return e;
-        (void)hipGetLastError();  // not ready is not an error
-        for (int k = 0; k < 32; k++) __builtin_ia32_pause();
-    }
-}
-
 // events for n chunks in c->ev_chunks
 inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
     while (c->ev_chunks.size() < n) {

@@ -1514,7 +1514,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         for (const auto &r : late)
             if (int e = results_dma(*r.first, r.second)) return e;
         tr.mark("enqueued");
-        MH_HIP(wait_stream(st));
+        MH_HIP(hipStreamSynchronize(st));
         MH_HIP(hipStreamSynchronize(c->d2h_stream));
         MH_HIP(hipStreamSynchronize(c->stream2));
         // buf stays the caller's once we return
