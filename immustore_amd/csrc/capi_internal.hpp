@@ -256,13 +256,25 @@ struct ChunkCopier {
     int lanes = 1;  // 1: one helper thread / copy stream; 2: two
     bool inline_issue = false;  // issue every copy from the caller (pinned sources: no blocking)
 
-    bool started = false;
+    bool started = false, synced = false;
     explicit ChunkCopier(mh_ctx *ctx) : c(ctx) {}
+    // every copy is complete: none reads the caller's host memory any more
+    // (the second lane's stream holds copies only with lanes == 2)
+    hipError_t sync() {
+        if (hipError_t e = join()) return e;
+        if (started) {
+            if (hipError_t e = hipStreamSynchronize(c->copy_stream)) return e;
+            if (lanes == 2)
+                if (hipError_t e = hipStreamSynchronize(c->copy_stream2)) return e;
+        }
+        synced = true;
+        return hipSuccess;
+    }
     // on every way out of the call: no copy may still read the caller's
     // host memory once it returns (an error path skips the final sync)
     ~ChunkCopier() {
         join();
-        if (started) {
+        if (started && !synced) {
             hipStreamSynchronize(c->copy_stream);
             hipStreamSynchronize(c->copy_stream2);
         }
@@ -352,10 +364,19 @@ inline bool pinned_same_alloc(const void *a, const void *b) {
 }
 
 // events for n chunks in c->ev_chunks
+// Without the system-scope fence: every waiter on these events is a device
+// stream (the host waits on streams), and the fence held each chunk's
+// consumer ~4 us longer (-12..-19 us per a14 call in three interleaved
+// rounds, profiles/ab_txlog_evfence_r04.txt).  MH_EV_NOFENCE=0 (read once)
+// restores it.
 inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
+    static const unsigned flags = [] {
+        const char *e = getenv("MH_EV_NOFENCE");
+        return e && !atoi(e) ? hipEventDisableTiming : hipEventDisableTiming | hipEventDisableSystemFence;
+    }();
     while (c->ev_chunks.size() < n) {
         hipEvent_t e;
-        if (hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming)) return r;
+        if (hipError_t r = hipEventCreateWithFlags(&e, flags)) return r;
         c->ev_chunks.push_back(e);
     }
     return hipSuccess;

@@ -1153,7 +1153,9 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // waits for both streams, so nothing writes caller memory after return
         struct StreamGuard {
             hipStream_t a, b, c2;
+            bool armed = true;  // cleared once the call's own final waits ran
             ~StreamGuard() {
+                if (!armed) return;
                 hipStreamSynchronize(a);
                 hipStreamSynchronize(b);
                 hipStreamSynchronize(c2);
@@ -1180,7 +1182,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         MH_HIP(cc.start());
         // the second compute stream starts after everything queued on the
         // context's stream before this call too (cc.start() recorded ev_done[0])
-        MH_HIP(hipStreamWaitEvent(c->stream2, c->ev_done[0], 0));
+        if (two_streams) MH_HIP(hipStreamWaitEvent(c->stream2, c->ev_done[0], 0));
         auto join_copies = [&]() -> int {
             hipError_t e = cc.join();
             return e == hipSuccess ? MH_OK : -(int)e;
@@ -1329,9 +1331,11 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // D2H copies into pageable memory return only when done: those of the
         // early groups are issued once every group is queued (late)
         std::vector<std::pair<const Grp *, hipEvent_t>> late;
+        bool d2h_used = false;  // anything queued on c->d2h_stream this call
         auto results_dma = [&](const Grp &g, hipEvent_t ev) -> int {
             const uint64_t nt = g.t1 - g.t0, t0 = g.t0;
             hipStream_t ds = c->d2h_stream;
+            d2h_used = true;
             MH_HIP(hipStreamWaitEvent(ds, ev, 0));
             if (status_out)
                 MH_HIP(hipMemcpyAsync(status_out + t0, g.base + g.b_st, nt * 4, hipMemcpyDeviceToHost, ds));
@@ -1350,6 +1354,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             uint32_t *ha = alh_out ? host_words(alh_out + t0 * 32, nt * 32) : nullptr;
             uint32_t *hh = hdrs_out ? host_words(hdrs_out + t0, nt * sizeof(mh_tx_header)) : nullptr;
             if ((!status_out || hs) && (!alh_out || ha) && (!hdrs_out || hh)) {
+                d2h_used = true;
                 MH_HIP(hipStreamWaitEvent(ds, ev, 0));
                 MH_HIP(launch_store_host(
                     ds, HostWordRuns{{(const uint32_t *)(g.base + g.b_st), (const uint32_t *)(g.base + g.b_a),
@@ -1514,14 +1519,14 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         for (const auto &r : late)
             if (int e = results_dma(*r.first, r.second)) return e;
         tr.mark("enqueued");
+        // only the streams this call queued work on (every wait is an API
+        // round trip on the critical path of the call)
         MH_HIP(hipStreamSynchronize(st));
-        MH_HIP(hipStreamSynchronize(c->d2h_stream));
-        MH_HIP(hipStreamSynchronize(c->stream2));
+        if (d2h_used) MH_HIP(hipStreamSynchronize(c->d2h_stream));
+        if (two_streams) MH_HIP(hipStreamSynchronize(c->stream2));
+        stream_guard.armed = false;
         // buf stays the caller's once we return
-        if (nck) {
-            MH_HIP(hipStreamSynchronize(c->copy_stream));
-            MH_HIP(hipStreamSynchronize(c->copy_stream2));
-        }
+        if (nck) MH_HIP(cc.sync());
         tr.mark("done");
         txlog_probe_report();
         return rc;

@@ -11,6 +11,7 @@
 //   single+k    one copy, then one kernel on the SAME stream
 //   *-spin      the host polls hipStreamQuery instead of hipStreamSynchronize
 //   small       a 4 KiB copy: the fixed round trip of one copy and its wait
+//   k<K>kernnf  k<K>kern with hipEventDisableSystemFence events
 //   k<K>wv      chunk flags by hipStreamWriteValue32 on the copy stream,
 //               the compute stream waits by hipStreamWaitValue32
 // Diagnosis only; nothing on the product path uses it.
@@ -62,8 +63,9 @@ int main(int argc, char **argv) {
     hipStream_t cs, ks;
     CK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&ks, hipStreamNonBlocking));
-    std::vector<hipEvent_t> ev(17);
+    std::vector<hipEvent_t> ev(17), evn(17);
     for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : evn) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
     uint32_t seq = 0;
 
     auto cuts = [&](int K) {
@@ -136,6 +138,19 @@ int main(int argc, char **argv) {
                               CK(hipStreamSynchronize(ks));
                               CK(hipStreamSynchronize(cs));
                           }});
+        vs.push_back({k + "kernnf", [&, K] {  // k<K>kern with events without the system fence
+                          auto c = cuts(K);
+                          for (int j = 0; j < K; j++) {
+                              CK(hipMemcpyAsync(d + c[j], h + c[j], c[j + 1] - c[j], hipMemcpyHostToDevice, cs));
+                              CK(hipEventRecord(evn[j], cs));
+                          }
+                          for (int j = 0; j < K; j++) {
+                              CK(hipStreamWaitEvent(ks, evn[j], 0));
+                              hipLaunchKernelGGL(k_touch, dim3(1), dim3(256), 0, ks, d + c[j], c[j + 1] - c[j], dout);
+                          }
+                          CK(hipStreamSynchronize(ks));
+                          CK(hipStreamSynchronize(cs));
+                      }});
         vs.push_back({k + "wv", [&, K] {
                           auto c = cuts(K);
                           seq++;

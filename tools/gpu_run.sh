@@ -82,7 +82,8 @@ for s in "$@"; do
       for v in $vs; do
         envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
         rm -rf "$O/txtl"
-        env $envs timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/txtl" -o run -- python3 tools/txlog_timeline.py > "$O/txtl.out" 2>&1 || { tail -5 "$O/txtl.out"; exit 1; }
+        api=""; [ -n "${TXTL_API:-}" ] && api="--hip-runtime-trace"  # TXTL_API=1: host HIP calls too
+        env $envs timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace $api --output-format csv -d "$O/txtl" -o run -- python3 tools/txlog_timeline.py > "$O/txtl.out" 2>&1 || { tail -5 "$O/txtl.out"; exit 1; }
         { echo "# variant $v"; python3 tools/trace_window.py "$O/txtl" 2500; } | tee -a "$O/txtl.txt"
       done
       rm -rf "$O/txtl" ;;
