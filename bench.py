@@ -63,9 +63,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--prewarm", type=float, default=2.0,
+    p.add_argument("--prewarm", type=float, default=5.0,
                    help="seconds of untimed builds before the warmup steps, so the GPU "
-                        "clock is at its sustained value when timing starts (0 = off)")
+                        "clock is at its sustained value when timing starts (0 = off); "
+                        "5 s rather than 2 also spans a utilisation sampler's 5 s period, "
+                        "which saw the round-3 runs' GPU idle")
     p.add_argument("--config", choices=["c2", "c4", "c3", "c5"], default="c2",
                    help="c2: BASELINE configs[1], 2^20 x 1 KiB per GPU (headline); c4: "
                         "configs[3], 2^23 x 4 KiB per GPU (2^26 entries at 8 GPUs); c3: "
