@@ -109,9 +109,12 @@ def _rank(rank, world, port, n, val, bad_rank, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bad_rank", [-1, 1])
-def test_root_check_ranks_gloo(orc, bad_rank):
-    world, n, val = 2, 1 << 9, 64
+@pytest.mark.parametrize("world,bad_rank", [(2, -1), (2, 1), (8, -1), (8, 5)])
+def test_root_check_ranks_gloo(orc, world, bad_rank):
+    """bench.py's post-timing root check over `world` gloo ranks -- 8 is the
+    driver's largest --gpus: the same all-gather of 128-byte records, verdict
+    and all-reduce it runs over RCCL on an 8-GPU node."""
+    n, val = 1 << 9, 64
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -52,7 +52,8 @@ def _worker(rank, world, port, n, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 1 << 12), (2, 1000), (3, 1025), (4, 4097), (2, 1)])
+@pytest.mark.parametrize("world,n", [(2, 1 << 12), (2, 1000), (3, 1025), (4, 4097), (2, 1),
+                                     (8, 1 << 13), (8, 5001)])
 def test_sharded_build_equals_single_tree(world, n, orc):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
