@@ -13,6 +13,7 @@
 #   corrupt_cabi     the same through --api cabi
 #   c3cabi           bench.py --api cabi --config c3 (replay append onto n0)
 #   dist2            2 gloo ranks sharing GPU 0 (bench.py --gpus 2 rehearsal)
+#   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
 #   txlog            tools/txlog_bench (a14 through the C ABI)
@@ -61,6 +62,10 @@ for s in "$@"; do
       MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist2 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 \
         bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
+    dist8)  # 8 gloo ranks sharing GPU 0: the driver's N = 8 path (root check over 8 ranks) rehearsed
+      MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist8 500 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 \
+        bench.py --gpus 8 --steps 20 --warmup 3 --prewarm 1 --no-cpu-baseline || exit 1 ;;
     c4) step c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1 ;;
     prof)
       rm -rf "$O/prof"
