@@ -1076,6 +1076,26 @@ static uint64_t txlog_chunks() {
     return k;
 }
 
+// relative sizes of a pinned log's copy chunks, first to last: K : K-1 : ... : 1
+// (K = txlog_chunks()), or MH_TXLOG_WEIGHTS="w0:w1:..." (read per call, A/B;
+// up to 16 positive numbers separated by ':' or ',')
+static std::vector<double> txlog_weights() {
+    std::vector<double> w;
+    if (const char *e = getenv("MH_TXLOG_WEIGHTS")) {
+        for (const char *p = e; *p && w.size() < 16;) {
+            char *q = nullptr;
+            const double v = strtod(p, &q);
+            if (q == p || !(v > 0)) break;
+            w.push_back(v);
+            if (*q != ',' && *q != ':') break;
+            p = q + 1;
+        }
+    }
+    if (w.empty())
+        for (uint64_t k = txlog_chunks(); k >= 1; k--) w.push_back((double)k);
+    return w;
+}
+
 // MH_TXLOG_TRACE=1: host timestamps of the call's phases on stderr (A/B
 // measurements of the copy / hop / device overlap)
 namespace {
@@ -1134,15 +1154,14 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             pinned = inl && len && same_alloc(buf, buf + len - 1);
         }
         tr.mark("attrs");
-        const uint64_t K = len < (16ull << 20) ? 1 : pinned ? txlog_chunks() : 2;
+        const std::vector<double> wts = pinned ? txlog_weights() : std::vector<double>{3, 1};
+        const uint64_t K = len < (16ull << 20) ? 1 : wts.size();
         std::vector<uint64_t> cut(K + 1, 0);
+        double wsum = 0, pre = 0;
+        for (uint64_t k = 0; k < K; k++) wsum += wts[k];
         for (uint64_t k = 1; k < K; k++) {
-            if (!pinned) {
-                cut[k] = (len / 4 * 3) & ~4095ull;
-                continue;
-            }
-            const uint64_t w = K * (K + 1) / 2, pre = k * K - k * (k - 1) / 2;  // sum of the first k weights
-            cut[k] = (uint64_t)((double)len * pre / w) & ~4095ull;
+            pre += wts[k - 1];  // the first k weights
+            cut[k] = std::max<uint64_t>(cut[k - 1], (uint64_t)((double)len * pre / wsum) & ~4095ull);
         }
         cut[K] = len;
         const uint64_t nck = len ? K : 0;
