@@ -321,14 +321,17 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
             assert np.array_equal(a[3], c[3])
 
 
-def test_txlog_validate_pinned_last_chunk(m, ctx, orc):
+@pytest.mark.parametrize("bulk", ["", "chain"])
+def test_txlog_validate_pinned_last_chunk(m, ctx, orc, monkeypatch, bulk):
     """The last copy chunk of a pinned log (its group's kernel runs right
     after it lands and stores the results into the pinned outputs itself):
     ends that are not 16-byte multiples, errors / max_txs / a corrupted hVal
     inside the last chunk, and a wide tx or re-encoded metadata at the end (the
     rest-group path) -- equal to the oracle and to the pageable call, headers
-    included."""
+    included.  bulk=chain: the early groups through the six-launch chain
+    (MH_TXLOG_BULK), the last through the fused kernel."""
     import torch
+    monkeypatch.setenv("MH_TXLOG_BULK", bulk)
     from tx_util import metadata_logs
     from immustore_amd.txlayer import TX_HEADER
     rng = np.random.default_rng(31)
