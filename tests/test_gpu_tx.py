@@ -204,11 +204,14 @@ def test_txlog_validate_parallel_hop(m, ctx, orc):
     same(raw, max_txs=4321)
 
 
-def _chunk_cuts(n, K=4):
-    """mh_txlog_validate's copy chunks of an n-byte log (from 16 MiB, K of
-    them, sizes K : K-1 : ... : 1, cut at 4 KiB multiples)."""
-    w = K * (K + 1) // 2
-    return [int(n * (k * K - k * (k - 1) // 2) / w) & ~4095 for k in range(1, K)]
+def _chunk_cuts(n, weights=(4, 2, 1, 1)):
+    """mh_txlog_validate's copy chunks of a pinned n-byte log (from 16 MiB,
+    sizes 4 : 2 : 1 : 1 by default, cut at 4 KiB multiples)."""
+    tot, pre, cuts = float(sum(weights)), 0.0, []
+    for w in weights[:-1]:
+        pre += w
+        cuts.append(max(cuts[-1] if cuts else 0, int(float(n) * pre / tot) & ~4095))
+    return cuts
 
 
 def test_txlog_validate_chunk_phases(m, ctx, orc):
