@@ -1101,6 +1101,33 @@ static std::vector<double> txlog_weights() {
     return w;
 }
 
+// The mh_tx_header words of the record at buf + rec other than Eh (words
+// 11-14), exactly as k_txlog_wave stores them: id, ts, blTxID (BE64), blRoot
+// and prevAlh (raw), version | nentries << 32, v1: mdLen | (rec + 92) << 32.
+// The hop has bounds-checked the record.
+static void fill_header_host(const uint8_t *buf, uint64_t rec, uint64_t *h) {
+    const uint8_t *p = buf + rec;
+    auto be = [](const uint8_t *q, int n) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; i++) v = v << 8 | q[i];
+        return v;
+    };
+    h[0] = be(p, 8);
+    h[1] = be(p + 8, 8);
+    h[2] = be(p + 16, 8);
+    memcpy(h + 3, p + 24, 64);
+    const uint32_t ver = (uint32_t)be(p + 88, 2);
+    uint32_t nent, ml = 0;
+    if (ver == 0) {
+        nent = (uint32_t)be(p + 90, 2);
+    } else {
+        ml = (uint32_t)be(p + 90, 2);
+        nent = (uint32_t)be(p + 92 + ml, 4);
+    }
+    h[15] = (uint64_t)ver | ((uint64_t)nent << 32);
+    h[16] = ver ? (uint64_t)ml | ((uint64_t)(uint32_t)(rec + 92) << 32) : 0;
+}
+
 // MH_TXLOG_TRACE=1: host timestamps of the call's phases on stderr (A/B
 // measurements of the copy / hop / device overlap)
 namespace {
@@ -1220,7 +1247,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // and pinned index staging, all indexed from the group's first record
         struct Grp {
             uint64_t t0 = 0, t1 = 0, e0 = 0, E = 0, wmax = 0, k = 0;
-            bool small = true, fetched = false, host_done = false, early = false;
+            bool small = true, fetched = false, host_done = false, early = false, host_hdrs = false;
             uint8_t *base = nullptr;
             uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
             uint64_t b_rec, b_ver, b_lv, b_h, b_es, b_ro, b_ap, b_lo, b_eh, b_s, b_a, b_st, idx_bytes;
@@ -1325,6 +1352,15 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 // MH_TXLOG_KERNEL=group: the workgroup kernel (read per call: A/B tests)
                 const char *kn = getenv("MH_TXLOG_KERNEL");
                 const bool wave = !(kn && strcmp(kn, "group") == 0);
+                // MH_TXLOG_HOST_HDRS=1 (read per call, A/B): the last chunk's
+                // group -- its kernel is the tail of the call -- writes only
+                // the Eh words of the caller's pinned headers; the host fills
+                // the other fields from the log while that kernel runs
+                const char *hh_env = getenv("MH_TXLOG_HOST_HDRS");
+                if (wave && ho.hdrs && hh_env && atoi(hh_env) == 1 && g.early && g.k + 1 == nck) {
+                    ho.eh_only = 1;
+                    g.host_hdrs = true;
+                }
                 if (wave)
                     MH_HIP(launch_txlog_wave(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
                                              base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
@@ -1482,6 +1518,13 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             if (int e = launch(gs[deferred])) return e;
             tr.mark("group");
         }
+        // header fields other than Eh of a host_hdrs group (readHeader,
+        // tx.go:419-518, as k_txlog_wave lays them out: 17 words per record)
+        for (const Grp &g : gs)
+            if (g.host_hdrs)
+                for (uint64_t t = g.t0; t < g.t1; t++)
+                    fill_header_host(buf, hop.R[t].rec, reinterpret_cast<uint64_t *>(hdrs_out + t));
+        tr.mark("host_hdrs");
         if (!gs.empty() && mh_fault(MH_FAULT_TXLOG_AFTER_GROUP)) return -(int)hipErrorOutOfMemory;
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;

@@ -267,6 +267,7 @@ struct TxlogHostOut {
     uint32_t *status = nullptr;
     uint32_t *alh = nullptr;
     uint64_t *hdrs = nullptr;
+    int eh_only = 0;  // k_txlog_wave: of hdrs, only the Eh words (the host writes the rest)
 };
 hipError_t launch_txlog_group(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                               const uint64_t *rec_off, const uint64_t *alh_off,

@@ -1208,9 +1208,16 @@ __global__ __launch_bounds__(256) void k_txlog_wave(
     // the device headers only when the caller's are not written here (they
     // are what a D2H copy takes to pageable outputs)
     uint64_t *hd = ho.hdrs ? ho.hdrs + T0 * 17 : reinterpret_cast<uint64_t *>(hdrs) + T0 * 17;
-    for (uint32_t k = threadIdx.x; k < nb * 17; k += 256) {
-        const uint32_t rec = k / 17, j = k - rec * 17;
-        hd[k] = reinterpret_cast<const uint64_t *>(m0 + (rec >> lgr) * wwords)[(rec & (R - 1)) * 17 + j];
+    if (ho.hdrs && ho.eh_only) {  // words 11-14 of each record's header (Eh); the host fills the rest
+        for (uint32_t k = threadIdx.x; k < nb * 4; k += 256) {
+            const uint32_t rec = k >> 2, j = 11 + (k & 3);
+            hd[rec * 17 + j] = reinterpret_cast<const uint64_t *>(m0 + (rec >> lgr) * wwords)[(rec & (R - 1)) * 17 + j];
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < nb * 17; k += 256) {
+            const uint32_t rec = k / 17, j = k - rec * 17;
+            hd[k] = reinterpret_cast<const uint64_t *>(m0 + (rec >> lgr) * wwords)[(rec & (R - 1)) * 17 + j];
+        }
     }
     if (ho.alh)
         for (uint32_t k = threadIdx.x; k < nb * 8; k += 256) {

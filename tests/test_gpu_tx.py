@@ -324,17 +324,19 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
             assert np.array_equal(a[3], c[3])
 
 
-@pytest.mark.parametrize("bulk", ["", "chain"])
-def test_txlog_validate_pinned_last_chunk(m, ctx, orc, monkeypatch, bulk):
+@pytest.mark.parametrize("bulk,host_hdrs", [("", "0"), ("chain", "0"), ("", "1")])
+def test_txlog_validate_pinned_last_chunk(m, ctx, orc, monkeypatch, bulk, host_hdrs):
     """The last copy chunk of a pinned log (its group's kernel runs right
     after it lands and stores the results into the pinned outputs itself):
     ends that are not 16-byte multiples, errors / max_txs / a corrupted hVal
     inside the last chunk, and a wide tx or re-encoded metadata at the end (the
     rest-group path) -- equal to the oracle and to the pageable call, headers
     included.  bulk=chain: the early groups through the six-launch chain
-    (MH_TXLOG_BULK), the last through the fused kernel."""
+    (MH_TXLOG_BULK), the last through the fused kernel; host_hdrs=1: the last
+    group's header fields other than Eh filled by the host (MH_TXLOG_HOST_HDRS)."""
     import torch
     monkeypatch.setenv("MH_TXLOG_BULK", bulk)
+    monkeypatch.setenv("MH_TXLOG_HOST_HDRS", host_hdrs)
     from tx_util import metadata_logs
     from immustore_amd.txlayer import TX_HEADER
     rng = np.random.default_rng(31)
