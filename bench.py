@@ -735,7 +735,11 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     if a.api == "cabi":
         return cabi_c3(a) if a.config == "c3" else cabi_main(a)
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    # MH_DIST_FORCE_PG=1: the --gpus N code path (process group, comm stream,
+    # all-gather of the roots over RCCL, the top levels, the root-check
+    # records) even at N = 1, launched as one torch.distributed.run rank
+    force_pg = os.environ.get("MH_DIST_FORCE_PG", "") == "1"
+    if (a.gpus > 1 or force_pg) and "WORLD_SIZE" not in os.environ:
         raise SystemExit(relaunch_ranks(a))
     if a.launch_check:
         return launch_check(a)
@@ -764,7 +768,7 @@ def main():
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     local = dev.index
-    if world > 1:
+    if world > 1 or force_pg:
         import torch.distributed as dist
         if backend == "gloo":
             dist.init_process_group("gloo")
@@ -804,7 +808,7 @@ def main():
 
     # collectives of all in-flight builds go through ONE stream, in issue
     # order, so every rank runs its RCCL kernels in the same order
-    comm = torch.cuda.Stream(dev) if (world > 1 and D > 1) else streams[0]
+    comm = torch.cuda.Stream(dev) if (dist and D > 1) else streams[0]
     comm_ctx = ctx if comm is streams[0] else m.Context(local, comm.cuda_stream)
 
     def step(k):
@@ -813,7 +817,7 @@ def main():
             N.check(L.mh_dev_htree_build_entries_fixed(ctxs[j].handle, 1, n, keys.data_ptr(),
                                                        KEY_LEN, vals.data_ptr(), VAL, None,
                                                        levels[j].data_ptr(), root[j].data_ptr()))
-        if world > 1:
+        if dist:
             # 32 B per rank over RCCL, then the top log2(world) levels locally
             # (immustore_amd/sharding.py; exact by SURVEY.md finding 3)
             comm.wait_stream(streams[j])
@@ -914,7 +918,7 @@ def main():
     r0 = root[0].cpu()
     assert all(torch.equal(r0, r.cpu()) for r in root), "in-flight builds disagree"
     rcheck = root_check_ranks(a, n, VAL, rank, world, dist, backend, dev, levels[0], root[0],
-                              groot[0] if world > 1 else root[0], corrupted)
+                              groot[0] if dist else root[0], corrupted)
 
     k_ms = sum(c.timing("entries_fixed")[0] for c in ctxs[1:]) + k_ms0
     k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
@@ -978,8 +982,8 @@ def main():
         "config": {"workload": "htree build (value SHA-256 + TxEntryDigest_v1_2 + leaf + all "
                                "levels), %d x %d B entries per GPU, %d B keys" % (n, VAL, KEY_LEN),
                    "entries_per_gpu": n, "value_len": VAL, "key_len": KEY_LEN,
-                   "parallelism": "subtree shard per GPU + RCCL all-gather of roots"
-                   if world > 1 else "single GPU", "lanes_per_leaf_group": lpl,
+                   "parallelism": "subtree shard per GPU + %s all-gather of roots"
+                   % ("RCCL" if backend != "gloo" else "gloo") if dist else "single GPU", "lanes_per_leaf_group": lpl,
                    "builds_in_flight": D, "wg_subtree_levels": wgl},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -100,7 +100,105 @@ def prewarm(step, sync, seconds):
         sync()
 
 
+SPLITMIX_G = 0x9E3779B97F4A7C15
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as orc
+    orc.use_shani(True)
+    return orc
+
+
+def host_threads(share=1):
+    """Host threads this process may use, split over `share` processes."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return max(1, avail // max(share, 1))
+
+
+def corrupt_hook(buf, who, at=100):
+    """Test-only (MH_BENCH_CORRUPT=<rank>): flip byte `at` of this rank's
+    inputs after they were generated, so its result check must fail."""
+    if os.environ.get("MH_BENCH_CORRUPT", "") == str(who):
+        buf[at:at + 1].bitwise_xor_(1)
+        return True
+    return False
+
+
+def aht_samples(lo, hi, rng, edge=64, rand=256):
+    """Appends of the range (lo, hi] the check looks at: the first and last
+    `edge` and `rand` random ones (the last is always included: RootAt(hi))."""
+    import numpy as np
+    cnt = hi - lo
+    s = set(range(lo + 1, lo + 1 + min(edge, cnt))) | set(range(max(lo + 1, hi - edge + 1), hi + 1))
+    s |= set(int(x) for x in rng.integers(lo + 1, hi + 1, rand))
+    return np.array(sorted(s), np.uint64)
+
+
+def c3_rank_check(orc, seed, plen, lo, hi, dlog_rows, root_rows, samples, threads):
+    """One rank's ahtree range (lo, hi] against the oracle without rebuilding
+    the tree: the peaks of lo from the payload stream in blocks
+    (orc.ahtree_peaks_streamed), then the range streamed from them
+    (orc.ahtree_stream, ahtree.go:287-322), every digest each sampled append
+    wrote and its RootAt compared.  dlog_rows(idx) / root_rows(idx) return the
+    device's rows at range-relative indices as (len, 32) host arrays.
+    -> (ok, RootAt(hi) of the oracle)."""
+    import numpy as np
+    up = orc.nodes_upto
+    pk = orc.ahtree_peaks_streamed(seed, plen, lo, threads=threads) if lo else None
+    ref, _ = orc.ahtree_stream(seed, plen, lo, hi, samples, peaks_in=pk)
+    base = up(lo)
+    idx, want = [], []
+    for n in (int(x) for x in samples):
+        first = up(n - 1) - base  # nodesUntil(n), range-relative
+        idx.extend(range(first, first + len(ref[n])))
+        want.extend(ref[n])
+    got = dlog_rows(np.array(idx, np.int64))
+    ok = bool(np.array_equal(got, np.frombuffer(b"".join(want), np.uint8).reshape(-1, 32)))
+    r = root_rows(samples.astype(np.int64) - lo - 1)
+    ok &= bool(np.array_equal(r, np.frombuffer(b"".join(ref[int(n)][-1] for n in samples),
+                                               np.uint8).reshape(-1, 32)))
+    return ok, ref[int(hi)][-1]
+
+
+def c5_rank_check(orc, leaf, W, terms, digests, root, ok_dev, tamper, sample):
+    """One rank's VerifyInclusion bitmap: every verdict equals the expected
+    one (~tamper), and on `sample` the oracle's htree.VerifyInclusion
+    (htree.go:166-195) over the very same terms / digests / root gives the
+    device's verdicts.  terms (s, D, 32), digests (s, 32) host arrays of the
+    sampled proofs.  -> (ok, sampled verdicts agreeing)."""
+    import numpy as np
+    exact = bool((ok_dev.astype(bool) == ~tamper).all())
+    _, ok_o = orc.htree_verify_batch(leaf[sample].astype(np.uint64), W, terms, digests, root)
+    agree = bool((ok_o.astype(bool) == ok_dev[sample].astype(bool)).all())
+    return exact and agree, int(len(sample))
+
+
+def share_verdict(dist, backend, dev, ok, corrupted, payload=b""):
+    """All-gather a 64-byte record per rank (verdict, corrupted flag, 32 B
+    payload) -> (every rank ok, corrupted ranks, payloads in rank order)."""
+    import numpy as np
+    import torch
+    rec = np.zeros(64, np.uint8)
+    rec[0], rec[1] = int(ok), int(corrupted)
+    rec[32:32 + len(payload)] = np.frombuffer(payload, np.uint8)
+    on = torch.device("cpu") if backend == "gloo" else dev
+    world = dist.get_world_size()
+    g = torch.empty(world * 64, dtype=torch.uint8, device=on)
+    dist.all_gather_into_tensor(g, torch.from_numpy(rec).to(on))
+    recs = g.cpu().numpy().reshape(world, 64)
+    return (bool(all(recs[:, 0] == 1)), [r for r in range(world) if recs[r, 1]],
+            [recs[r, 32:64].tobytes() for r in range(world)])
+
+
 def distributed_main(a):
+    """One process per GPU (torch.distributed.run; MH_DIST_FORCE_PG=1 runs the
+    same code as one rank over a real process group).  c3 / c5 in their
+    SURVEY.md 8(e) multi-GPU forms, weak scaling; every line checks its result
+    against the oracle after the timed region and exits 1 on a mismatch."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -121,6 +219,8 @@ def distributed_main(a):
     stream = torch.cuda.current_stream(dev)
     ctx = m.Context(dev.index, stream.cuda_stream)
     L = N.load()
+    on = torch.device("cpu") if backend == "gloo" else dev
+    threads = host_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
 
     def sync_all():
         torch.cuda.synchronize(dev)
@@ -135,48 +235,87 @@ def distributed_main(a):
         for _ in range(a.steps):
             step()
         sync_all()
-        t = torch.tensor([(time.perf_counter() - t0) / a.steps], dtype=torch.float64,
-                         device="cpu" if backend == "gloo" else dev)
+        t = torch.tensor([(time.perf_counter() - t0) / a.steps], dtype=torch.float64, device=on)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     if a.workload == "c3":
-        k = 23
-        S = 1 << k
-        m_total = world * S
-        pay = torch.empty(S * 32, dtype=torch.uint8, device=dev)
-        N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), 3 + rank))
-        nd = m.nodes_upto(m_total)
-        dlog = torch.empty(nd * 32, dtype=torch.uint8, device=dev)  # globally indexed
+        # every rank appends 2^23 payloads of one global batch onto an empty
+        # tree, keeping ONLY its own dLog range (the ranged
+        # form of mh_multi_dev_ahtree_append_batch): leaves + perfect levels,
+        # one all-gather of its pieces' level-k roots, the piece tree, spines
+        from immustore_amd.multi import ahtree_range_plan
+        up = L.mh_ahtree_nodes_upto
+        seed, plen, n0 = 3, 32, 0
+        total = world * a.per_rank
+        k, b = ahtree_range_plan(n0, total, world)
+        G = len(b) - 1
+        send_b, work_b = sharding.ahtree_range_sizes(n0, total, world)
+        lo, hi = (b[rank], b[rank + 1]) if rank < G else (b[G], b[G])
+        cnt = hi - lo
+        pay = torch.empty(max(cnt, 1) * plen, dtype=torch.uint8, device=dev)
+        sd = (seed + lo * (plen // 8) * SPLITMIX_G) & 0xFFFFFFFFFFFFFFFF  # payload lo of the stream
+        N.check(L.mh_dev_fill_random(ctx.handle, pay.data_ptr(), pay.numel(), sd))
+        torch.cuda.synchronize(dev)
+        corrupted = corrupt_hook(pay, rank)
+        dlog = torch.empty(max(up(hi) - up(lo), 1) * 32, dtype=torch.uint8, device=dev)
+        ro = torch.empty(max(cnt, 1) * 32, dtype=torch.uint8, device=dev)
+        work = torch.empty(work_b, dtype=torch.uint8, device=dev)
+        send = torch.zeros(send_b, dtype=torch.uint8, device=dev)
+        recv = torch.empty(world * send_b, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
 
-        def allgather(ptr):
-            off = ptr - dlog.data_ptr()
-            src = dlog[off:off + 32]
+        def exchange():
             if backend == "gloo":
-                out = torch.empty(world * 32, dtype=torch.uint8)
-                dist.all_gather_into_tensor(out, src.cpu())
-                out = out.to(dev)
+                r = torch.empty(world * send_b, dtype=torch.uint8)
+                dist.all_gather_into_tensor(r, send.cpu())
+                recv.copy_(r)
             else:
-                out = torch.empty(world * 32, dtype=torch.uint8, device=dev)
-                dist.all_gather_into_tensor(out, src)
-            allgather.keep = out
-            return out.data_ptr()
+                dist.all_gather_into_tensor(recv, send)
 
         def step():
-            sharding.ahtree_sharded_append(ctx, dlog.data_ptr(), pay.data_ptr(), rank, world, k,
-                                           m_total, allgather)
+            sharding.ahtree_range_append(ctx, n0, None, total, world, rank, pay.data_ptr(), plen,
+                                         dlog.data_ptr(), work.data_ptr(), send.data_ptr(),
+                                         recv.data_ptr(), exchange if G > 1 else None,
+                                         ro.data_ptr())
 
         t = timed_max(step)
-        # the last append's root, on the last rank, vs an independent recurrence
-        # over this rank's own dLog range is checked by tests/test_gpu_sharded.py
-        out = {"metric": "ahtree batch append, sharded, 2^23 payloads per GPU (configs[2] at scale)",
-               "value": round(m_total / t / 1e6, 3), "unit": "M appends/s", "n_gpus": world,
-               "ms_per_step": round(t * 1e3, 3), "scaling": "weak", "appends_total": m_total,
-               "exchange": "all-gather of 32 B per rank (%s)" % backend}
+        # ---- check vs the oracle, after the timed region
+        tc = time.perf_counter()
+        orc = _oracle()
+        ok, root_o = True, b"\0" * 32
+        samples = np.zeros(0, np.uint64)
+        if cnt:
+            samples = aht_samples(lo, hi, np.random.default_rng(7 + rank))
+            dl, rr = dlog.view(-1, 32), ro.view(-1, 32)
+            rows = lambda t_, i: t_[torch.from_numpy(i).to(dev)].cpu().numpy()  # noqa: E731
+            ok, root_o = c3_rank_check(orc, seed, plen, lo, hi, lambda i: rows(dl, i),
+                                       lambda i: rows(rr, i), samples, threads)
+        ok_all, bad, roots = share_verdict(dist, backend, dev, ok, corrupted, root_o)
+        rcheck = {"vs": "oracle", "ok": ok_all, "n": total, "ranges": G, "shard_bits": k,
+                  "root": roots[G - 1].hex(), "samples_per_rank": int(len(samples)),
+                  "corrupted_ranks": bad, "host_threads_per_rank": threads,
+                  "seconds": round(time.perf_counter() - tc, 2),
+                  "what": "per rank: the oracle's peaks of its range start (payload stream "
+                          "hashed block by block) and its range streamed from them "
+                          "(oracle/orc_ahtree_stream, ahtree.go:287-322); every dLog digest "
+                          "and RootAt of 64 first, 64 last and 256 random appends compared "
+                          "(RootAt(n) of the last rank = the batch's root)"}
+        new_digests = up(n0 + total) - up(n0)
+        out = {"metric": "ahtree batch append, sharded, %d payloads per GPU (configs[2] at scale)"
+                         % a.per_rank,
+               "value": round(total / t / 1e6, 3), "unit": "M appends/s", "n_gpus": world,
+               "ms_per_step": round(t * 1e3, 3), "scaling": "weak", "appends_total": total,
+               "dlog_bytes_this_rank": int(dlog.numel()),
+               "dlog_bytes_whole_tree": int(new_digests * 32),
+               "exchange": "all-gather of %d B per rank (%s)" % (send_b, backend),
+               "root_check": rcheck}
     elif a.workload == "c5":
-        D = a.depth
+        # proofs are independent: every rank re-hashes its own share (split by
+        # index, its own seed) against the replicated 2^D-leaf tree, with no
+        # collective in the timed region
+        D, P = a.depth, a.proofs
         W = 1 << D
-        P = a.proofs
         dig = torch.empty(W * 32, dtype=torch.uint8, device=dev)
         N.check(L.mh_dev_fill_random(ctx.handle, dig.data_ptr(), dig.numel(), 5))
         levels = torch.empty(m.levels_len(W) * 32, dtype=torch.uint8, device=dev)
@@ -185,14 +324,26 @@ def distributed_main(a):
                                              root.data_ptr()))
         rng = np.random.default_rng(5 + rank)  # this rank's share of the proofs
         leaf = rng.integers(0, W, P, dtype=np.int64)
-        offs = np.array([m.level_offset(W, lv) for lv in range(D)], np.int64)
-        idx = offs[None, :] + ((leaf[:, None] >> np.arange(D)[None, :]) ^ 1)
-        terms = levels.view(-1, 32)[torch.from_numpy(idx.reshape(-1)).to(dev)].contiguous()
-        digests = dig.view(-1, 32)[torch.from_numpy(leaf).to(dev)].contiguous()
+        leaf_t = torch.from_numpy(leaf).to(dev)
+        terms = torch.empty(P * D * 32, dtype=torch.uint8, device=dev)
+        nterms = torch.empty(P, dtype=torch.int32, device=dev)
+        pst = torch.empty(P, dtype=torch.int32, device=dev)
+        N.check(L.mh_dev_htree_inclusion_proof_batch(ctx.handle, levels.data_ptr(), W, P,
+                                                     leaf_t.data_ptr(), terms.data_ptr(), D,
+                                                     nterms.data_ptr(), pst.data_ptr()))
+        torch.cuda.synchronize(dev)
+        assert int(pst.abs().sum().item()) == 0 and int((nterms != D).sum().item()) == 0
+        tamper = rng.random(P) < 0.10
+        src = np.where(tamper, (leaf + 1) % W, leaf)  # a wrong digest for 10 %
+        digests = dig.view(-1, 32)[torch.from_numpy(src).to(dev)].contiguous()
         roots = root.view(1, 32).expand(P, 32).contiguous()
         width_t = torch.full((P,), W, dtype=torch.int64, device=dev)
         toff = torch.arange(0, (P + 1) * D, D, dtype=torch.int64, device=dev)
         ok = torch.zeros(P, dtype=torch.uint8, device=dev)
+        # test hook: one term of the first untampered proof flipped
+        first_good = int(np.nonzero(~tamper)[0][0])
+        corrupted = corrupt_hook(terms, rank, at=first_good * D * 32 + 5)
+        torch.cuda.synchronize(dev)
 
         def step():
             N.check(L.mh_dev_htree_verify_inclusion_batch(
@@ -200,20 +351,44 @@ def distributed_main(a):
                 terms.data_ptr(), digests.data_ptr(), roots.data_ptr(), ok.data_ptr()))
 
         t = timed_max(step)
-        nok = torch.tensor([int(ok.sum().item())], dtype=torch.int64,
-                           device="cpu" if backend == "gloo" else dev)
-        dist.all_reduce(nok)
-        out = {"metric": "htree inclusion-proof re-hash, 10^6 proofs x depth 24 per GPU",
+        tc = time.perf_counter()
+        orc = _oracle()
+        okh = ok.cpu().numpy()
+        srng = np.random.default_rng(11 + rank)
+        sample = np.unique(np.concatenate([np.arange(min(P, 1 << 13)),
+                                           srng.integers(0, P, 1 << 13)]))
+        if corrupted:
+            sample = np.unique(np.concatenate([sample, [first_good]]))
+        st = torch.from_numpy(sample).to(dev)
+        th = terms.view(P, D, 32)[st].cpu().numpy()
+        dh = digests[st].cpu().numpy()
+        rk_ok, ns = c5_rank_check(orc, leaf, W, th, dh, root.cpu().numpy().tobytes(), okh, tamper,
+                                  sample)
+        nver = int(okh.astype(bool).sum())
+        ok_all, bad, _ = share_verdict(dist, backend, dev, rk_ok, corrupted)
+        tot = torch.tensor([nver], dtype=torch.int64, device=on)
+        dist.all_reduce(tot)
+        rcheck = {"vs": "oracle", "ok": ok_all, "proofs": world * P, "verified": int(tot.item()),
+                  "sampled_per_rank": ns, "corrupted_ranks": bad,
+                  "seconds": round(time.perf_counter() - tc, 2),
+                  "what": "per rank: every verdict equals the expected bitmap (10 % tampered "
+                          "digests false, the rest true), and the oracle's VerifyInclusion "
+                          "(htree.go:166-195) over the same terms / digests / root of >= 2^13 "
+                          "proofs gives the device's verdicts"}
+        out = {"metric": "htree inclusion-proof re-hash, %d proofs x depth %d per GPU" % (P, D),
                "value": round(world * P / t / 1e6, 3), "unit": "M proofs/s", "n_gpus": world,
-               "ms_per_step": round(t * 1e3, 3), "scaling": "weak",
-               "all_verified": int(nok.item()) == world * P}
+               "ms_per_step": round(t * 1e3, 3), "scaling": "weak", "root_check": rcheck}
     else:
         raise SystemExit("multi-GPU mode covers --workload c3 / c5")
     out["workload"] = a.workload
+    out["process_group"] = {"backend": backend, "world_size": dist.get_world_size()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
     dist.destroy_process_group()
+    if not out["root_check"]["ok"]:
+        print("root_check FAILED: %s" % json.dumps(out["root_check"]), file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 def make_parser():
@@ -232,6 +407,8 @@ def make_parser():
     p.add_argument("--prewarm", type=float, default=0.5,
                    help="seconds of untimed steps before each device-resident timed region")
     p.add_argument("--m", type=int, default=10 ** 7, help="c3 appends")
+    p.add_argument("--per-rank", type=int, default=1 << 23,
+                   help="c3 under torch.distributed: appends per rank (weak scaling)")
     p.add_argument("--proofs", type=int, default=10 ** 6, help="c5 proofs")
     p.add_argument("--depth", type=int, default=24, help="c5 tree depth")
     p.add_argument("--no-ahtree", action="store_true", help="c5: htree proofs only")
@@ -1197,9 +1374,29 @@ def run_single(a):
     return out
 
 
+def relaunch_one_rank():
+    """MH_DIST_FORCE_PG=1 without a launcher: start this command as ONE rank
+    under torch.distributed.run (a CHILD process, before anything here touches
+    the GPU) and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = make_parser().parse_args()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    force = os.environ.get("MH_DIST_FORCE_PG", "") == "1"
+    if force and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(relaunch_one_rank())
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or force:
         return distributed_main(a)
     print(json.dumps(run_single(a)), flush=True)
 

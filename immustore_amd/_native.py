@@ -297,6 +297,9 @@ SIGNATURES = {
     "mh_multi_dev_ahtree_append_batch": (i32, [vp, u64, u8p, u64, vp, u32, vp, vp]),
     "mh_multi_ahtree_append_batch": (i32, [vp, u64, u8p, u8p, u64, u32, u8p, u8p]),
     "mh_ahtree_range_plan": (i32, [u64, u64, i32, C.POINTER(i32), vp, C.POINTER(i32)]),
+    "mh_ahtree_range_sizes": (i32, [u64, u64, i32, C.POINTER(u64), C.POINTER(u64)]),
+    "mh_dev_ahtree_range_local": (i32, [vp, u64, u8p, u64, i32, i32, u8p, u32, u8p, u8p, u8p]),
+    "mh_dev_ahtree_range_finish": (i32, [vp, u64, u8p, u64, i32, i32, u8p, u8p, u8p, u8p]),
     "mh_dev_ahtree_append_range": (i32, [vp, u8p, u64, u8p, u8p, u64, u32, u8p]),
     "mh_dev_ahtree_peaks": (i32, [vp, u8p, u64, u8p]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,

@@ -582,13 +582,10 @@ inline uint8_t *range_base(uint8_t *buf, uint64_t lo) {
     return reinterpret_cast<uint8_t *>((uintptr_t)buf - (uintptr_t)(ahtree_nodes_upto(lo) * 32));
 }
 
-// Phases 1-4 for ranges already planned; payload[d] / dlog[d] are device
-// pointers of range d (dlog[d] holds nodesUpto(b[d+1]) - nodesUpto(b[d])
-// digests), slots = the old peaks of n0 in the 64-slot layout (host).
-int aht_multi_run(mh_multi *m, const AhtPlan &p, const AhtSlots &slots,
-                  const std::vector<const uint8_t *> &payload, uint32_t plen,
-                  const std::vector<uint8_t *> &dlog, const std::vector<uint8_t *> &roots_out) {
-    const int K = m->K, G = p.G, k = p.k;
+// The piece-tree geometry of a plan (shared by every range): send slots per
+// device (Pmax) and the slot count of the replicated top buffer.
+AhtTopArgs aht_top_args(const AhtPlan &p, uint64_t *top_slots) {
+    const int G = p.G, k = p.k;
     const uint64_t n0 = p.b[0];
     uint64_t Pmax = 1;
     AhtTopArgs ta;
@@ -600,73 +597,127 @@ int aht_multi_run(mh_multi *m, const AhtPlan &p, const AhtSlots &slots,
     for (int d = 0; d <= G; d++) ta.pe0[d] = p.b[d] >> k;
     for (int d = 0; d < G; d++) Pmax = std::max<uint64_t>(Pmax, ta.pe0[d + 1] - ta.pe0[d]);
     ta.Pmax = Pmax;
-    uint64_t top_slots = 0;
+    uint64_t slots = 0;
     ta.nlev = 0;
     while (ta.nlev < 64 - k && (ta.Pend >> ta.nlev) != 0) {
-        ta.lev_off[ta.nlev] = top_slots;
-        top_slots += (ta.Pend >> ta.nlev) - (ta.N0 >> ta.nlev) + 1;
+        ta.lev_off[ta.nlev] = slots;
+        slots += (ta.Pend >> ta.nlev) - (ta.N0 >> ta.nlev) + 1;
         ta.nlev++;
     }
-    // 1. leaves + perfect levels (all of them when one range holds the batch)
-    for (int d = 0; d < G; d++) {
+    *top_slots = slots;
+    return ta;
+}
+
+// Device buffers of one range: the old peaks of n0 (pk) and the frontier of
+// its left end (fr), 64 slots each, the spine work queue and the top tree.
+struct AhtRangeBufs {
+    uint8_t *pk = nullptr, *fr = nullptr, *top = nullptr;
+    uint32_t *ctr = nullptr;
+};
+
+// Phase 1 of range d on its context's stream: the old peaks in, leaves +
+// perfect levels (all of them when one range holds the batch), then -- with
+// more than one range -- the level-k roots of its complete pieces into send
+// (Pmax slots).
+int aht_range_local(mh_ctx *c, const AhtPlan &p, const AhtTopArgs &ta, int d,
+                    const AhtSlots &slots, const uint8_t *payload, uint32_t plen, uint8_t *dlog,
+                    const AhtRangeBufs &B, uint8_t *send) {
+    hipStream_t st = c->stream;
+    // by value through the kernel arguments: nothing host-side to outlive
+    MH_HIP(launch_ahtree_put_slots(st, slots, B.pk));
+    const uint64_t lo = p.b[d], hi = p.b[d + 1];
+    uint8_t *vb = range_base(dlog, lo);
+    AhtEdge edge;
+    edge.fr = d ? B.fr : B.pk;
+    edge.lo = lo;
+    MH_HIP(launch_ahtree_leaves(st, c->tm(), vb, lo, payload, hi - lo, plen));
+    MH_HIP(launch_ahtree_perfect(st, c->tm(), vb, lo, hi, 1, p.G == 1 ? 63 : p.k, edge));
+    if (p.G > 1 && send)
+        MH_HIP(launch_ahtree_gather_pieces(st, vb, p.k, ta.pe0[d] + 1, ta.pe0[d + 1] - ta.pe0[d],
+                                           send));
+    return MH_OK;
+}
+
+// Phases 3-4 of range d once recv holds every range's piece roots (range r
+// at r * Pmax slots): the piece tree, its nodes ending in the range, the
+// frontier, then the spines.
+int aht_range_finish(mh_ctx *c, const AhtPlan &p, const AhtTopArgs &ta, int d,
+                     const uint8_t *recv, uint8_t *dlog, const AhtRangeBufs &B,
+                     uint8_t *roots_out) {
+    hipStream_t st = c->stream;
+    uint8_t *vb = range_base(dlog, p.b[d]);
+    if (p.G > 1) {
+        AhtTopArgs a = ta;
+        a.lo = p.b[d];
+        a.hi = p.b[d + 1];
+        MH_HIP(launch_ahtree_top(st, a, recv, B.pk, B.top, vb, B.fr));
+    }
+    AhtEdge edge;
+    edge.fr = d ? B.fr : B.pk;
+    edge.lo = p.b[d];
+    MH_HIP(launch_ahtree_spine(st, c->tm(), vb, p.b[d], p.b[d + 1] - p.b[d], roots_out, B.ctr,
+                               edge));
+    return MH_OK;
+}
+
+// Phases 1-4 for ranges already planned; payload[d] / dlog[d] are device
+// pointers of range d (dlog[d] holds nodesUpto(b[d+1]) - nodesUpto(b[d])
+// digests), slots = the old peaks of n0 in the 64-slot layout (host).
+int aht_multi_run(mh_multi *m, const AhtPlan &p, const AhtSlots &slots,
+                  const std::vector<const uint8_t *> &payload, uint32_t plen,
+                  const std::vector<uint8_t *> &dlog, const std::vector<uint8_t *> &roots_out) {
+    const int K = m->K, G = p.G;
+    uint64_t top_slots = 0;
+    const AhtTopArgs ta = aht_top_args(p, &top_slots);
+    const uint64_t Pmax = ta.Pmax;
+    std::vector<AhtRangeBufs> rb(K);
+    std::vector<const uint8_t *> send(K);
+    std::vector<uint8_t *> recv(K);
+    for (int d = 0; d < K; d++) {
         mh_multi::Dev &B = *m->buf[d];
         MH_HIP(hipSetDevice(m->dev[d]));
-        hipStream_t st = m->ctx[d]->stream;
         MH_HIP(B.pk.ensure(64 * 32));
         MH_HIP(B.fr.ensure(64 * 32));
         MH_HIP(B.ctr.ensure(256));
-        // by value through the kernel arguments: nothing host-side to outlive
-        MH_HIP(launch_ahtree_put_slots(st, slots, B.pk.as<uint8_t>()));
-        const uint64_t lo = p.b[d], hi = p.b[d + 1];
-        uint8_t *vb = range_base(dlog[d], lo);
-        AhtEdge edge;
-        edge.fr = d ? B.fr.as<uint8_t>() : B.pk.as<uint8_t>();
-        edge.lo = lo;
-        MH_HIP(launch_ahtree_leaves(st, m->ctx[d]->tm(), vb, lo, payload[d], hi - lo, plen));
-        MH_HIP(launch_ahtree_perfect(st, m->ctx[d]->tm(), vb, lo, hi, 1, G == 1 ? 63 : k, edge));
+        MH_HIP(B.top.ensure(top_slots * 32));
+        MH_HIP(B.send.ensure(Pmax * 32));
+        MH_HIP(B.recv.ensure((uint64_t)K * Pmax * 32));
+        rb[d].pk = B.pk.as<uint8_t>();
+        rb[d].fr = B.fr.as<uint8_t>();
+        rb[d].top = B.top.as<uint8_t>();
+        rb[d].ctr = B.ctr.as<uint32_t>();
+        send[d] = B.send.as<uint8_t>();
+        recv[d] = B.recv.as<uint8_t>();
     }
-    if (G > 1) {
-        // 2. the complete pieces' level-k roots, Pmax slots per device
-        std::vector<const uint8_t *> send(K);
-        std::vector<uint8_t *> recv(K);
-        for (int d = 0; d < K; d++) {
-            mh_multi::Dev &B = *m->buf[d];
-            MH_HIP(hipSetDevice(m->dev[d]));
-            MH_HIP(B.send.ensure(Pmax * 32));
-            MH_HIP(B.recv.ensure((uint64_t)K * Pmax * 32));
-            if (d < G)
-                MH_HIP(launch_ahtree_gather_pieces(m->ctx[d]->stream, range_base(dlog[d], p.b[d]),
-                                                   k, ta.pe0[d] + 1, ta.pe0[d + 1] - ta.pe0[d],
-                                                   B.send.as<uint8_t>()));
-            send[d] = B.send.as<uint8_t>();
-            recv[d] = B.recv.as<uint8_t>();
-        }
-        if (int st = gather_bytes(m, send, recv, Pmax * 32)) return st;
-        // 3. piece tree, the device's nodes above level k, its frontier
-        for (int d = 0; d < G; d++) {
-            mh_multi::Dev &B = *m->buf[d];
-            MH_HIP(hipSetDevice(m->dev[d]));
-            MH_HIP(B.top.ensure(top_slots * 32));
-            AhtTopArgs a = ta;
-            a.lo = p.b[d];
-            a.hi = p.b[d + 1];
-            MH_HIP(launch_ahtree_top(m->ctx[d]->stream, a, recv[d], B.pk.as<uint8_t>(),
-                                     B.top.as<uint8_t>(), range_base(dlog[d], p.b[d]),
-                                     B.fr.as<uint8_t>()));
-        }
-    }
-    // 4. spines
+    // 1. leaves + perfect levels, the pieces' level-k roots into send
     for (int d = 0; d < G; d++) {
-        mh_multi::Dev &B = *m->buf[d];
         MH_HIP(hipSetDevice(m->dev[d]));
-        AhtEdge edge;
-        edge.fr = d ? B.fr.as<uint8_t>() : B.pk.as<uint8_t>();
-        edge.lo = p.b[d];
-        MH_HIP(launch_ahtree_spine(m->ctx[d]->stream, m->ctx[d]->tm(), range_base(dlog[d], p.b[d]),
-                                   p.b[d], p.b[d + 1] - p.b[d], roots_out[d],
-                                   B.ctr.as<uint32_t>(), edge));
+        if (int st = aht_range_local(m->ctx[d], p, ta, d, slots, payload[d], plen, dlog[d], rb[d],
+                                     m->buf[d]->send.as<uint8_t>()))
+            return st;
+    }
+    // 2. all-gather of Pmax slots per device
+    if (G > 1)
+        if (int st = gather_bytes(m, send, recv, Pmax * 32)) return st;
+    // 3-4. piece tree, the device's nodes above level k, its frontier; spines
+    for (int d = 0; d < G; d++) {
+        MH_HIP(hipSetDevice(m->dev[d]));
+        if (int st = aht_range_finish(m->ctx[d], p, ta, d, recv[d], dlog[d], rb[d], roots_out[d]))
+            return st;
     }
     return MH_OK;
+}
+
+// The work buffer of the one-range-per-process form: pk | fr | ctr | top.
+constexpr uint64_t kAhtWorkHead = 64 * 32 * 2 + 256;
+
+AhtRangeBufs aht_work_bufs(uint8_t *work) {
+    AhtRangeBufs B;
+    B.pk = work;
+    B.fr = work + 64 * 32;
+    B.ctr = reinterpret_cast<uint32_t *>(work + 64 * 32 * 2);
+    B.top = work + kAhtWorkHead;
+    return B;
 }
 
 int peaks_ok(uint64_t n0, const uint8_t *peaks) { return n0 == 0 || peaks != nullptr; }
@@ -683,6 +734,77 @@ extern "C" int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *
         *nranges = p.G;
         for (int d = 0; d <= p.G; d++) bounds[d] = p.b[d];
         return MH_OK;
+    });
+}
+
+extern "C" int mh_ahtree_range_sizes(uint64_t n0, uint64_t total, int ndev, uint64_t *send_bytes,
+                                     uint64_t *work_bytes) {
+    return mh_guard([&]() -> int {
+        if (!send_bytes || !work_bytes) return MH_ERR_ILLEGAL_ARGUMENTS;
+        AhtPlan p;
+        if (int st = aht_plan(n0, total, ndev, p)) return st;
+        uint64_t top_slots = 0;
+        const AhtTopArgs ta = aht_top_args(p, &top_slots);
+        *send_bytes = ta.Pmax * 32;
+        *work_bytes = kAhtWorkHead + top_slots * 32;
+        return MH_OK;
+    });
+}
+
+namespace {
+
+// Arguments shared by the two per-rank calls: the plan, the range, the old
+// peaks and the work buffer.
+int aht_rank_setup(uint64_t n0, const uint8_t *peaks, uint64_t total, int world, int rank,
+                   uint8_t *dlog_range, uint8_t *work, AhtPlan &p, AhtTopArgs &ta) {
+    if (!peaks_ok(n0, peaks) || !work || world < 1 || rank < 0 || rank >= world || total == 0)
+        return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (((uintptr_t)work & 15) || ((uintptr_t)dlog_range & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (int st = aht_plan(n0, total, world, p)) return st;
+    uint64_t top_slots = 0;
+    ta = aht_top_args(p, &top_slots);
+    if (rank < p.G && !dlog_range) return MH_ERR_ILLEGAL_ARGUMENTS;
+    return MH_OK;
+}
+
+}  // namespace
+
+extern "C" int mh_dev_ahtree_range_local(mh_ctx *c, uint64_t n0, const uint8_t *peaks,
+                                         uint64_t total, int world, int rank,
+                                         const uint8_t *payloads, uint32_t plen,
+                                         uint8_t *dlog_range, uint8_t *work, uint8_t *send) {
+    return mh_guard([&]() -> int {
+        if (!c || !send) return MH_ERR_ILLEGAL_ARGUMENTS;
+        AhtPlan p;
+        AhtTopArgs ta;
+        if (int st = aht_rank_setup(n0, peaks, total, world, rank, dlog_range, work, p, ta))
+            return st;
+        if (rank >= p.G) return MH_OK;  // no range: its send slots are never read
+        if (plen && !payloads) return MH_ERR_ILLEGAL_ARGUMENTS;
+        AhtSlots slots;
+        expand_peaks(n0, peaks, slots);
+        MH_HIP(hipSetDevice(c->device));
+        std::lock_guard<std::mutex> lk(c->mu);
+        return aht_range_local(c, p, ta, rank, slots, payloads, plen, dlog_range,
+                               aht_work_bufs(work), send);
+    });
+}
+
+extern "C" int mh_dev_ahtree_range_finish(mh_ctx *c, uint64_t n0, const uint8_t *peaks,
+                                          uint64_t total, int world, int rank,
+                                          const uint8_t *recv, uint8_t *dlog_range, uint8_t *work,
+                                          uint8_t *roots_out) {
+    return mh_guard([&]() -> int {
+        if (!c) return MH_ERR_ILLEGAL_ARGUMENTS;
+        AhtPlan p;
+        AhtTopArgs ta;
+        if (int st = aht_rank_setup(n0, peaks, total, world, rank, dlog_range, work, p, ta))
+            return st;
+        if (rank >= p.G) return MH_OK;
+        if (p.G > 1 && !recv) return MH_ERR_ILLEGAL_ARGUMENTS;
+        MH_HIP(hipSetDevice(c->device));
+        std::lock_guard<std::mutex> lk(c->mu);
+        return aht_range_finish(c, p, ta, rank, recv, dlog_range, aht_work_bufs(work), roots_out);
     });
 }
 

@@ -93,3 +93,36 @@ def ahtree_sharded_append(ctx, dlog_ptr: int, payloads_ptr: int, rank: int, worl
                                             min(complete, world), gathered))
     N.check(L.mh_dev_ahtree_append_spine(ctx.handle, dlog_ptr, n0, m, roots_out_ptr))
     return n0, m
+
+
+def ahtree_range_sizes(n0: int, total: int, world: int) -> Tuple[int, int]:
+    """(send_bytes, work_bytes) of one rank's ranged append (mh_ahtree_range_sizes)."""
+    import ctypes as C
+    from . import _native as N
+    s, w = C.c_uint64(), C.c_uint64()
+    N.check(N.load().mh_ahtree_range_sizes(n0, total, world, C.byref(s), C.byref(w)))
+    return s.value, w.value
+
+
+def ahtree_range_append(ctx, n0: int, peaks, total: int, world: int, rank: int, payloads_ptr: int,
+                        plen: int, dlog_ptr: int, work_ptr: int, send_ptr: int, recv_ptr: int,
+                        exchange, roots_out_ptr=None):
+    """This rank's range of appending `total` payloads onto a tree of n0
+    (peaks: host bytes of the old tree's popcount(n0) peaks, None for n0 = 0),
+    keeping only its own dLog range (range `rank` of mh_ahtree_range_plan):
+    local phase -> exchange() (the caller's all-gather of send_bytes per rank
+    from send into recv, rank order; None when the plan has one range) ->
+    piece tree + spines.  Every pointer is a device address on ctx's device;
+    asynchronous on ctx's stream, the exchange ordered after the local phase
+    by the caller (torch's collectives wait on the current stream)."""
+    import numpy as np
+    from . import _native as N
+    from .merkle import _addr
+    L = N.load()
+    pk = np.frombuffer(peaks, np.uint8) if peaks else None
+    N.check(L.mh_dev_ahtree_range_local(ctx.handle, n0, _addr(pk), total, world, rank,
+                                        payloads_ptr, plen, dlog_ptr, work_ptr, send_ptr))
+    if exchange is not None:
+        exchange()
+    N.check(L.mh_dev_ahtree_range_finish(ctx.handle, n0, _addr(pk), total, world, rank, recv_ptr,
+                                         dlog_ptr, work_ptr, roots_out_ptr))

@@ -735,6 +735,32 @@ int mh_multi_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint8_t *peaks,
  * ndev <= 64. */
 int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *shard_bits, uint64_t *bounds,
                          int *nranges);
+/* The same ranged append with ONE PROCESS PER DEVICE (torch.distributed /
+ * any launcher whose ranks exchange bytes themselves): rank r of `world`
+ * appends range r of mh_ahtree_range_plan(n0, total, world) -- the same
+ * digests mh_multi_dev_ahtree_append_batch leaves on device r -- in two calls
+ * around one all-gather the caller runs (ahtree.go:246-373):
+ *  1. mh_dev_ahtree_range_local: leaves + perfect nodes of the range and its
+ *     pieces' level-k roots into `send` (device, send_bytes);
+ *  2. the caller all-gathers send_bytes from every rank, in rank order, into
+ *     `recv` (device, world x send_bytes; skipped when the plan has one range);
+ *  3. mh_dev_ahtree_range_finish: the piece tree above level k, the rank's
+ *     frontier and its spines; roots_out (may be NULL) gets RootAt after each
+ *     append of the range.
+ * send_bytes / work_bytes from mh_ahtree_range_sizes; `work` (device,
+ * 16-byte aligned) is this rank's scratch and must be kept between the two
+ * calls; payloads / dlog_range as for the device variant above (range r's
+ * payloads, room for its new digests).  peaks (host) on EVERY rank when
+ * n0 > 0.  A rank past the plan's ranges (r >= nranges) does nothing but
+ * still joins the all-gather.  Asynchronous on the context stream. */
+int mh_ahtree_range_sizes(uint64_t n0, uint64_t total, int ndev, uint64_t *send_bytes,
+                          uint64_t *work_bytes);
+int mh_dev_ahtree_range_local(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
+                              int world, int rank, const uint8_t *payloads, uint32_t plen,
+                              uint8_t *dlog_range, uint8_t *work, uint8_t *send);
+int mh_dev_ahtree_range_finish(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
+                               int world, int rank, const uint8_t *recv, uint8_t *dlog_range,
+                               uint8_t *work, uint8_t *roots_out);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

@@ -745,6 +745,25 @@ int orc_ahtree_consistency_proof(const uint8_t *dlog, uint64_t size, uint64_t i,
     return finish_proof(&s, terms, nterms);
 }
 
+/* Many InclusionProof (kind 0) / ConsistencyProof (kind 1) calls over one
+ * dLog (ahtree.go:525-651): proof p into terms + p * cap * 32, its length
+ * into nterms[p], the call's status into st[p] (a proof longer than cap:
+ * ERR_ILLEGAL_ARGS).  The checker of the device's batch proof generation. */
+void orc_ahtree_proof_batch(const uint8_t *dlog, uint64_t size, int kind, uint64_t n,
+                            const uint64_t *i, const uint64_t *j, uint8_t *terms, uint32_t cap,
+                            uint32_t *nterms, int32_t *st) {
+    uint8_t tmp[192 * 32];
+    for (uint64_t p = 0; p < n; p++) {
+        uint32_t nt = 0;
+        int r = kind == 0 ? orc_ahtree_inclusion_proof(dlog, size, i[p], j[p], tmp, &nt)
+                          : orc_ahtree_consistency_proof(dlog, size, i[p], j[p], tmp, &nt);
+        if (r == OK && nt > cap) r = ERR_ILLEGAL_ARGS;
+        st[p] = r;
+        nterms[p] = r == OK ? nt : 0;
+        if (r == OK) memcpy(terms + p * (uint64_t)cap * 32, tmp, (size_t)nt * 32);
+    }
+}
+
 void orc_ahtree_eval_inclusion(const uint8_t *terms, uint32_t nterms, uint64_t i, uint64_t j,
                                const uint8_t leaf[32], uint8_t out[32]) {
     /* ahtree/verification.go:32-56 */
@@ -879,6 +898,75 @@ uint64_t orc_ahtree_verify_batch(int kind, uint64_t n, const uint64_t *i, const 
         cnt += jobs[t].cnt;
     }
     return cnt;
+}
+
+/* ------------------------------------------------ streamed ahtree (checker) */
+static uint64_t splitmix_word(uint64_t seed, uint64_t w) {
+    /* word w of orc_fill_random(seed): splitmix64 output number w+1 */
+    uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+/* The ahtree appends (n_start, n_end] of plen-byte payloads drawn from the
+ * orc_fill_random(seed) stream -- append n_start + 1 + x takes payload
+ * pay0 + x, i.e. stream bytes [(pay0 + x) plen, (pay0 + x + 1) plen) -- kept
+ * as the 64 PEAKS of the current size only, no dLog: peak l of a tree of
+ * size n is node(n with the bits below l cleared, l) (ahtree.go:460-462) for
+ * every set bit l of n.  Append n (ahtree.go:287-322) hashes the leaf
+ * SHA256(0x00 || payload) and then, for every set bit l of n-1 from low to
+ * high, h = SHA256(0x01 || node(k, l) || h) with node(k, l) = peak l of n-1;
+ * the first tz(n) of those are the perfect nodes ending at n, so the peaks of
+ * n are those of n-1 with levels < tz(n) dropped and level tz(n) = h after
+ * tz(n) steps.  For each sampled n (strictly ascending, in (n_start, n_end])
+ * all 1 + popcount(n-1) digests append n writes to the dLog go to
+ * out + s * 65 * 32 and their count to cnt[s] (the last one is RootAt(n)).
+ * peaks_in / peaks_out: 64 x 32 B, slot l meaningful for set bits l of
+ * n_start / n_end (peaks_in may be NULL when n_start == 0; peaks_out may be
+ * NULL).  Test infrastructure: checks device dLogs too large to rebuild. */
+int orc_ahtree_stream(uint64_t seed, uint32_t plen, uint64_t pay0, uint64_t n_start,
+                      const uint8_t *peaks_in, uint64_t n_end, const uint64_t *samples,
+                      uint64_t ns, uint8_t *out, uint32_t *cnt, uint8_t *peaks_out) {
+    if (plen % 8 || plen > 1024 || n_end < n_start || (n_start && !peaks_in) ||
+        (ns && (!samples || !out || !cnt)))
+        return ERR_ILLEGAL_ARGS;
+    for (uint64_t s = 0; s < ns; s++)
+        if (samples[s] <= n_start || samples[s] > n_end || (s && samples[s] <= samples[s - 1]))
+            return ERR_ILLEGAL_ARGS;
+    uint8_t pk[64][32];
+    memset(pk, 0, sizeof pk);
+    if (n_start) memcpy(pk, peaks_in, sizeof pk);
+    uint8_t msg[1 + 1024];
+    msg[0] = 0;
+    const uint32_t words = plen / 8;
+    uint64_t s = 0;
+    for (uint64_t n = n_start + 1; n <= n_end; n++) {
+        const uint64_t w0 = (pay0 + (n - n_start - 1)) * words;
+        for (uint32_t q = 0; q < words; q++) {
+            const uint64_t z = splitmix_word(seed, w0 + q);
+            memcpy(msg + 1 + 8 * q, &z, 8); /* little-endian words, as orc_fill_random */
+        }
+        uint8_t h[32];
+        orc_sha256(msg, 1 + (size_t)plen, h);
+        const int sampled = s < ns && samples[s] == n;
+        uint8_t *o = sampled ? out + s * 65 * 32 : NULL;
+        uint32_t c = 0;
+        if (o) memcpy(o + 32 * c++, h, 32);
+        const int tz = __builtin_ctzll(n);
+        if (tz == 0) memcpy(pk[0], h, 32); /* n odd: the leaf is the level-0 peak */
+        const uint64_t prev = n - 1;
+        for (int l = 0; l < 64 && (prev >> l); l++) {
+            if (!((prev >> l) & 1)) continue;
+            if (l >= tz && !o) break; /* past the perfect nodes: only samples need the rest */
+            node_hash(pk[l], h, h);
+            if (o) memcpy(o + 32 * c++, h, 32);
+            if (l == tz - 1) memcpy(pk[tz], h, 32); /* the perfect node ending at n */
+        }
+        if (o) cnt[s++] = c;
+    }
+    if (peaks_out) memcpy(peaks_out, pk, sizeof pk);
+    return OK;
 }
 
 /* ------------------------------------------------------------ synthetic */

@@ -196,6 +196,19 @@ int orc_ahtree_verify_last_inclusion(const uint8_t *terms, uint32_t nterms, uint
  * little-endian words): identical to immustore_amd's device generator. */
 void orc_fill_random(uint8_t *dst, uint64_t nbytes, uint64_t seed);
 
+/* n InclusionProof (kind 0) / ConsistencyProof (kind 1) calls, proof p at
+ * terms + p * cap * 32 (ahtree.go:525-651). */
+void orc_ahtree_proof_batch(const uint8_t *dlog, uint64_t size, int kind, uint64_t n,
+                            const uint64_t *i, const uint64_t *j, uint8_t *terms, uint32_t cap,
+                            uint32_t *nterms, int32_t *st);
+
+/* ahtree appends (n_start, n_end] of orc_fill_random(seed) payloads kept as
+ * the 64 peaks only (no dLog): the dLog digests of sampled appends and the
+ * peaks of n_end.  See merkle_oracle.c. */
+int orc_ahtree_stream(uint64_t seed, uint32_t plen, uint64_t pay0, uint64_t n_start,
+                      const uint8_t *peaks_in, uint64_t n_end, const uint64_t *samples,
+                      uint64_t ns, uint8_t *out, uint32_t *cnt, uint8_t *peaks_out);
+
 #ifdef __cplusplus
 }
 #endif

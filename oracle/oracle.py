@@ -91,6 +91,11 @@ def lib():
         L.orc_txlog_validate.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64,
                                          u64p, u64p, u8p, C.POINTER(C.c_int32)]
         L.orc_sha256_use_shani.argtypes = [C.c_int]
+        L.orc_ahtree_proof_batch.argtypes = [u8p, C.c_uint64, C.c_int, C.c_uint64, u64p, u64p,
+                                             u8p, C.c_uint32, u32p, C.POINTER(C.c_int32)]
+        L.orc_ahtree_proof_batch.restype = None
+        L.orc_ahtree_stream.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, u8p,
+                                        C.c_uint64, u64p, C.c_uint64, u8p, u32p, u8p]
         L.orc_precommit_batch.argtypes = [C.c_int, C.c_uint64, C.c_uint64, u64p, u8p, u64p, u8p,
                                           u64p, u8p, u64p, u8p, u8p, u8p, u8p, u8p,
                                           C.POINTER(C.c_int32), C.c_int]
@@ -309,6 +314,19 @@ class AHtree:
         st = lib().orc_ahtree_consistency_proof(_p(self.dlog), self.size, i, j, _p(t), C.byref(nt))
         return st, t[:nt.value].copy()
 
+    def proof_batch(self, kind, i, j, cap=64):
+        """kind 0 / 1: InclusionProof / ConsistencyProof for every (i[p], j[p])
+        -> (terms (n, cap, 32), nterms (n,), status (n,))."""
+        i = np.ascontiguousarray(i, np.uint64)
+        j = np.ascontiguousarray(j, np.uint64)
+        n = len(i)
+        t = np.zeros((max(n, 1), cap, 32), np.uint8)
+        nt = np.zeros(max(n, 1), np.uint32)
+        st = np.zeros(max(n, 1), np.int32)
+        lib().orc_ahtree_proof_batch(_p(self.dlog), self.size, kind, n, _p(i, u64p), _p(j, u64p),
+                                     _p(t), cap, _p(nt, u32p), st.ctypes.data_as(C.POINTER(C.c_int32)))
+        return t[:n], nt[:n], st[:n]
+
 
 def _terms(t):
     if not isinstance(t, np.ndarray):
@@ -372,6 +390,65 @@ def verify_values(vals, off, hvals, vlen=None, nthreads=1):
 def fill_random(nbytes, seed):
     out = np.zeros(nbytes, np.uint8)
     lib().orc_fill_random(_p(out), nbytes, seed)
+    return out
+
+
+def ahtree_stream(seed, plen, n_start, n_end, samples=(), peaks_in=None, pay0=None):
+    """orc_ahtree_stream: appends (n_start, n_end] of fill_random(seed)
+    payloads (append n takes payload pay0 + n - n_start - 1; pay0 defaults to
+    n_start, i.e. payload n-1 of the one stream) kept as peaks only ->
+    ({n: [digests append n writes to the dLog]}, peaks of n_end as a (64, 32)
+    array, slot l meaningful for set bits l of n_end)."""
+    L = lib()
+    s = np.ascontiguousarray(sorted(set(int(x) for x in samples)), np.uint64)
+    out = np.zeros((max(len(s), 1), 65, 32), np.uint8)
+    cnt = np.zeros(max(len(s), 1), np.uint32)
+    pk = np.zeros((64, 32), np.uint8)
+    pin = None if peaks_in is None else np.ascontiguousarray(peaks_in, np.uint8).reshape(64, 32)
+    st = L.orc_ahtree_stream(seed, plen, n_start if pay0 is None else pay0, n_start,
+                             _p(pin) if pin is not None else None, n_end,
+                             _p(s, u64p) if len(s) else None, len(s), _p(out), _p(cnt, u32p),
+                             _p(pk))
+    if st:
+        raise ValueError("orc_ahtree_stream: status %d" % st)
+    return {int(n): [bytes(out[i, c]) for c in range(cnt[i])] for i, n in enumerate(s)}, pk
+
+
+def ahtree_peaks_streamed(seed, plen, n, threads=1, block_bits=20):
+    """The peaks of a tree of n appends of fill_random(seed) payloads, as a
+    (64, 32) array, without its dLog: peak l (set bit l of n) is the perfect
+    subtree over the aligned block of 2^l appends ending at n with the bits
+    below l cleared (ahtree.go:460-462); a block of 2^l payloads is the root
+    of the perfect tree over them alone, so every block is cut into
+    sub-blocks of <= 2^block_bits payloads streamed on `threads` host threads
+    (orc_ahtree_stream, GIL released) and their roots paired
+    SHA256(0x01 || left || right) up to level l."""
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = []  # (level, first payload, sub-block bits)
+    for l in range(64):
+        if (n >> l) & 1:
+            a = (n >> (l + 1)) << (l + 1)
+            sb = min(l, block_bits)
+            for j in range(1 << (l - sb)):
+                jobs.append((l, a + (j << sb), sb))
+
+    def root_of(job):
+        _, first, sb = job
+        _, pk = ahtree_stream(seed, plen, 0, 1 << sb, pay0=first)
+        return bytes(pk[sb])
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        roots = list(ex.map(root_of, jobs))
+    out = np.zeros((64, 32), np.uint8)
+    k = 0
+    for l in range(64):
+        if (n >> l) & 1:
+            sb = min(l, block_bits)
+            row = roots[k:k + (1 << (l - sb))]
+            k += len(row)
+            while len(row) > 1:
+                row = [sha256(b"\x01" + row[i] + row[i + 1]) for i in range(0, len(row), 2)]
+            out[l] = np.frombuffer(row[0], np.uint8)
     return out
 
 

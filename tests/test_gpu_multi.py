@@ -212,6 +212,76 @@ def test_multi_dev_ahtree_append_vs_oracle(m, orc, aht_ref, devices, total, n0):
         md.close()
 
 
+@pytest.mark.parametrize("world,total", [(1, 1 << 14), (2, 1 << 16), (3, 3 * (1 << 14) + 5),
+                                         (4, 1000), (8, 100003), (8, 5)])
+@pytest.mark.parametrize("n0", _AHT_N0S)
+def test_rank_ahtree_range_append_vs_oracle(m, orc, aht_ref, world, total, n0):
+    """The one-process-per-GPU form (mh_dev_ahtree_range_local / _finish,
+    what bench_workloads.py --workload c3 runs under torch.distributed): the
+    `world` ranks played one after the other on one device, each with its own
+    context, work buffer and range, the all-gather done by hand in rank order
+    between the two calls -- every rank's range and roots equal the oracle's
+    single AppendBatch (ahtree.go:246-373); ranks past the plan's ranges
+    (total = 5 over 8 ranks) do nothing."""
+    import torch
+    from immustore_amd import _native as N
+    from immustore_amd import sharding
+    from immustore_amd.multi import ahtree_range_plan, peaks_of
+    L = N.load()
+    up = L.mh_ahtree_nodes_upto
+    pay, o, ref = aht_ref
+    _, b = ahtree_range_plan(n0, total, world)
+    G = len(b) - 1
+    send_b, work_b = sharding.ahtree_range_sizes(n0, total, world)
+    pk = peaks_of(ref, n0) if n0 else None
+    ctxs = [m.Context(0) for _ in range(world)]
+    try:
+        rng = lambda r: (b[r], b[r + 1]) if r < G else (b[G], b[G])  # noqa: E731
+        dp = [torch.from_numpy(pay[rng(r)[0]:rng(r)[1]].reshape(-1).copy()).cuda()
+              if r < G else torch.empty(32, dtype=torch.uint8, device="cuda") for r in range(world)]
+        dl = [torch.empty(max(up(rng(r)[1]) - up(rng(r)[0]), 1) * 32, dtype=torch.uint8,
+                          device="cuda") for r in range(world)]
+        ro = [torch.empty(max(rng(r)[1] - rng(r)[0], 1) * 32, dtype=torch.uint8, device="cuda")
+              for r in range(world)]
+        work = [torch.empty(work_b, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        send = [torch.zeros(send_b, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        recv = [torch.empty(world * send_b, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        pkb = np.frombuffer(pk, np.uint8) if pk else None
+        pkp = pkb.ctypes.data if pk else None
+        torch.cuda.synchronize()
+        for _rep in range(2):  # a second append of the same batch reuses the work buffers
+            for r in range(world):
+                N.check(L.mh_dev_ahtree_range_local(ctxs[r].handle, n0, pkp, total, world, r,
+                                                    dp[r].data_ptr(), 32, dl[r].data_ptr(),
+                                                    work[r].data_ptr(), send[r].data_ptr()))
+            for c in ctxs:
+                c.synchronize()
+            gathered = torch.cat(send)
+            for r in range(world):
+                recv[r].copy_(gathered)
+            torch.cuda.synchronize()
+            for r in range(world):
+                N.check(L.mh_dev_ahtree_range_finish(ctxs[r].handle, n0, pkp, total, world, r,
+                                                     recv[r].data_ptr(), dl[r].data_ptr(),
+                                                     work[r].data_ptr(), ro[r].data_ptr()))
+            for c in ctxs:
+                c.synchronize()
+            for r in range(G):
+                lo, hi = b[r], b[r + 1]
+                got = dl[r].cpu().numpy().reshape(-1, 32)
+                assert np.array_equal(got, ref[up(lo):up(hi)]), (world, n0, total, r)
+                rr = ro[r].cpu().numpy().reshape(-1, 32)
+                assert all(rr[j].tobytes() == bytes(o.root_at(lo + j + 1)[1])
+                           for j in (0, (hi - lo) // 2, hi - lo - 1)), (world, n0, total, r)
+        with pytest.raises(N.MerkleError):  # n0 > 0 needs the old peaks on every rank
+            N.check(L.mh_dev_ahtree_range_local(ctxs[0].handle, 7, None, total, world, 0,
+                                                dp[0].data_ptr(), 32, dl[0].data_ptr(),
+                                                work[0].data_ptr(), send[0].data_ptr()))
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("n0", _AHT_N0S + (2 ** 20, 2 ** 20 - 1))
 def test_dev_ahtree_append_range_vs_oracle(m, orc, aht_ref, n0):
     """One device, the dLog kept as a range (mh_dev_ahtree_append_range):

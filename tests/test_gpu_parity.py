@@ -688,6 +688,53 @@ def test_ahtree_reset_reference_sequence(m, ctx):
     assert list(np.nonzero(ok)[0] + 1) == [n]
 
 
+def test_ahtree_reference_suite_full_size(m, ctx, orc):
+    """The reference's own ahtree suite at ITS size (N = 1024, payload
+    {byte(i)}) on the device: TestIntegrity (ahtree_test.go:579-612) and
+    TestInclusionAndConsistencyProofs (:647-715).  Every InclusionProof and
+    ConsistencyProof for 1 <= i <= j <= 1024 (524,800 pairs each) generated by
+    k_ahtree_proof is byte-equal to the oracle's (ahtree.go:525-651) and
+    verifies on the device (k_ahtree_verify, ahtree/verification.go:21-109)
+    against RootAt; VerifyLastInclusion(InclusionProof(i, N), i, leaf_i,
+    RootAt(i)) holds only for i = N; InclusionProof(2, 1) / ConsistencyProof(2,
+    1) are ErrIllegalArguments."""
+    from immustore_amd import _native as N
+    n = 1024
+    pay = (np.arange(1, n + 1) & 0xFF).astype(np.uint8).reshape(n, 1)  # Go: []byte{byte(i)}
+    t = m.AHtree(ctx)
+    t.append_batch(pay)
+    o = orc.AHtree(n)
+    o.append_batch(pay)
+    assert t.dlog() == o.dlog_bytes()
+    leaf = np.stack([np.zeros(32, np.uint8)] + [np.frombuffer(H(b"\x00" + bytes([i & 0xFF])), np.uint8)
+                                               for i in range(1, n + 1)])
+    root = np.stack([np.zeros(32, np.uint8)] +
+                    [np.frombuffer(t.root_at(k), np.uint8) for k in range(1, n + 1)])
+    assert all(root[k].tobytes() == o.root_at(k)[1] for k in range(1, n + 1))
+    I, J = np.triu_indices(n, 0)
+    I = (I + 1).astype(np.uint64)
+    J = (J + 1).astype(np.uint64)
+    for kind, a in ((N.MH_AHT_INCLUSION, leaf[I]), (N.MH_AHT_CONSISTENCY, root[I])):
+        terms, nt, st = t.proof_batch(kind, I, J, max_terms=32)
+        assert (st == 0).all()
+        ot, ont, ost = o.proof_batch(kind, I, J, cap=32)
+        assert (ost == 0).all() and np.array_equal(nt, ont)
+        mask = np.arange(32)[None, :] < nt[:, None]
+        assert np.array_equal(terms[mask], ot[mask]), kind  # every proof byte-equal
+        ok = _aht_verify_csr(m, ctx, kind, I, J, terms, nt, a, root[J])
+        assert ok.all(), (kind, int((~ok).sum()))
+        del terms, ot
+    K = np.arange(1, n + 1, dtype=np.uint64)
+    terms, nt, st = t.proof_batch(N.MH_AHT_INCLUSION, K, np.full(n, n, np.uint64), max_terms=32)
+    assert (st == 0).all()
+    ok = _aht_verify_csr(m, ctx, N.MH_AHT_LAST_INCLUSION, K, K, terms, nt, leaf[K], root[K])
+    assert list(np.nonzero(ok)[0] + 1) == [n]
+    for kind in (N.MH_AHT_INCLUSION, N.MH_AHT_CONSISTENCY):
+        _, _, st = t.proof_batch(kind, [2], [1])
+        assert list(st) == [N.MH_ERR_ILLEGAL_ARGUMENTS]
+    t.close()
+
+
 # ------------------------------------------ upper levels (k_entries_fixed + k_reduce)
 @pytest.mark.parametrize("wgl", ["0", "2", "4", "8"])
 def test_entries_fixed_wg_levels_vs_oracle(m, ctx, orc, lpl, wgl):

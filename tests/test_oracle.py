@@ -262,3 +262,61 @@ def test_verify_values_oracle_vs_hashlib(orc):
         # no lengths: only the digest decides (a long vLen alone passes)
         c2, st2 = orc.verify_values(vb, off, hv, None)
         assert np.all(st2[~bad] == 0) and c2 <= c
+
+
+@pytest.mark.parametrize("n_start", [0, 1, 5, 64, 1000, 1023, 1024])
+def test_ahtree_stream_equals_dlog(orc, n_start):
+    """orc_ahtree_stream (peaks only, no dLog; the checker of the multi-rank
+    C3 bench line) gives the digests append n writes (ahtree.go:287-322) and
+    the peaks (ahtree.go:460-462) of the full-dLog restatement, from any
+    starting size with the peaks handed over."""
+    M = 3000
+    raw = orc.fill_random(32 * M, 9).reshape(M, 32)
+    t = orc.AHtree()
+    t.append_batch(raw)
+    dl = t.dlog
+    pin = orc.ahtree_stream(9, 32, 0, n_start)[1] if n_start else None
+    rng = np.random.default_rng(n_start)
+    samples = sorted(set(int(x) for x in rng.integers(n_start + 1, M + 1, 300)) | {n_start + 1, M})
+    res, pk = orc.ahtree_stream(9, 32, n_start, M, samples, peaks_in=pin)
+    assert sorted(res) == samples
+    for n, ds in res.items():
+        base = orc.nodes_until(n)
+        assert ds == [bytes(dl[base + c]) for c in range(1 + bin(n - 1).count("1"))], n
+        assert ds[-1] == t.root_at(n)[1]
+    for l in range(64):
+        if (M >> l) & 1:
+            assert bytes(pk[l]) == bytes(dl[orc.nodes_until((M >> l) << l) + l]), l
+
+
+def test_ahtree_peaks_streamed_in_blocks(orc):
+    """The peaks rebuilt block by block on several threads equal the dLog's."""
+    M = 3000
+    t = orc.AHtree()
+    t.append_batch(orc.fill_random(32 * M, 9).reshape(M, 32))
+    for n in (1, 2, 3, 1000, 2047, 2048, 3000):
+        for bb in (0, 3, 20):
+            pk = orc.ahtree_peaks_streamed(9, 32, n, threads=4, block_bits=bb)
+            for l in range(64):
+                if (n >> l) & 1:
+                    assert bytes(pk[l]) == bytes(t.dlog[orc.nodes_until((n >> l) << l) + l]), (n, l)
+    with pytest.raises(ValueError):
+        orc.ahtree_stream(9, 31, 0, 4)  # payloads must be whole splitmix64 words
+
+
+def test_ahtree_proof_batch_equals_single_calls(orc):
+    """orc_ahtree_proof_batch (the checker of the device's batch proof
+    generation at the reference suite's N = 1024) = one call per pair."""
+    n = 200
+    t = orc.AHtree(n)
+    t.append_batch((np.arange(1, n + 1) & 0xFF).astype(np.uint8).reshape(n, 1))
+    I, J = np.triu_indices(n, 0)
+    I, J = I + 1, J + 1
+    for kind, fn in ((0, t.inclusion_proof), (1, t.consistency_proof)):
+        terms, nt, st = t.proof_batch(kind, I, J, cap=32)
+        assert not st.any()
+        for p in range(0, len(I), 7):
+            _, o = fn(int(I[p]), int(J[p]))
+            assert nt[p] == len(o) and terms[p, :nt[p]].tobytes() == o.tobytes()
+        assert list(t.proof_batch(kind, [2, 1], [1, n + 1])[2]) == [2, 5]
+        assert list(t.proof_batch(kind, [1], [n], cap=2)[2]) == [2]  # longer than cap

@@ -15,6 +15,10 @@
 #   dist2            2 gloo ranks sharing GPU 0 (bench.py --gpus 2 rehearsal)
 #   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
+#   wdist:<w>:<N>    bench_workloads.py --workload <w> (c3 / c5) as N gloo ranks sharing GPU 0
+#   wcorrupt:<w>:<N> the same with MH_BENCH_CORRUPT=1 (N >= 2): must exit 1 (result check)
+#   forcepg          MH_DIST_FORCE_PG=1: the multi-rank code paths as ONE nccl (RCCL) rank:
+#                    bench.py (C2), bench.py --config c4, bench_workloads.py c3 and c5
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
 #   txlog            tools/txlog_bench (a14 through the C ABI)
 #   copyprobe        tools/copy_probe: chunked pinned H2D pipeline costs (host wall time)
@@ -66,6 +70,20 @@ for s in "$@"; do
       MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist8 500 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 \
         bench.py --gpus 8 --steps 20 --warmup 3 --prewarm 1 --no-cpu-baseline || exit 1 ;;
+    wdist:*|wcorrupt:*)  # bench_workloads.py multi-rank lines, N gloo ranks sharing GPU 0
+      w=$(echo "$s" | cut -d: -f2); n=$(echo "$s" | cut -d: -f3); kind=${s%%:*}
+      corrupt=""; [ "$kind" = wcorrupt ] && corrupt="MH_BENCH_CORRUPT=1"
+      env $corrupt MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 timeout -k 10 600 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29541 \
+        bench_workloads.py --workload "$w" --steps 5 --warmup 1 > "$O/${kind}_${w}_$n.out" 2> "$O/${kind}_${w}_$n.err"
+      rc=$?; tail -2 "$O/${kind}_${w}_$n.out"; grep -v amdgpu.ids "$O/${kind}_${w}_$n.err" | grep -i "fail\|error" | tail -2
+      if [ "$kind" = wcorrupt ]; then echo "$s exit $rc (want 1)"; [ $rc -eq 1 ] || exit 1
+      else [ $rc -eq 0 ] || exit 1; fi ;;
+    forcepg)  # the torch.distributed / RCCL code paths executed as one nccl rank
+      MH_DIST_FORCE_PG=1 step forcepg_c2 400 python bench.py --steps 200 --warmup 5 --no-cpu-baseline || exit 1
+      MH_DIST_FORCE_PG=1 step forcepg_c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1
+      MH_DIST_FORCE_PG=1 step forcepg_wc3 600 python bench_workloads.py --workload c3 --steps 5 --warmup 1 || exit 1
+      MH_DIST_FORCE_PG=1 step forcepg_wc5 600 python bench_workloads.py --workload c5 --steps 5 --warmup 1 || exit 1 ;;
     c4) step c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1 ;;
     prof)
       rm -rf "$O/prof"
