@@ -41,21 +41,24 @@ N_ENTRIES = 1 << 20
 VAL_LEN = 1024
 KEY_LEN = 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# int32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (same lanes/clk as the
-# 157.3 TFLOPS fp32 vector peak without the FMA factor of 2).
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 # VALU instructions per 64-byte compression of the generic compress() in the
 # gfx950 ISA of this build (counted in profiles/isa_counts_r01.txt); the
 # constant-schedule padding block (compress_kw) needs fewer.
 OPS_PER_COMP = 1388
 OPS_PER_COMP_KW = 901
 # Measured SHA-256 compression ceiling of this chip with this round function:
-# tools/microbench_sha.hip, registers only, >= 2 waves/SIMD (profiles/
-# microbench_r01.txt).  v_alignbit_b32 / v_add3_u32 / v_perm_b32 issue at
-# about half the rate of v_add_u32 / v_bitop3_b32 on gfx950
-# (tools/microbench_valu.hip), so the nominal VALU peak above over-states
-# what a SHA-256 round can reach.
+# tools/microbench_sha.hip, registers only, 8 waves/SIMD, 30.9 G compressions/s
+# (profiles/microbench_r01.txt, line "waves/SIMD 8").
 SHA_PEAK_GCOMPS = 30.9
+# VALU peak FOR THIS INSTRUCTION MIX (lane-ops/s): the measured compression
+# ceiling above x the 1388 VALU instructions of one compression x 64 lanes / 64
+# (one wave-instruction = 64 lane-ops per compression lane) = 42.9 T.  Not the
+# nominal 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T: on gfx950
+# v_alignbit_b32 and v_add3_u32 -- 805 of the 1388 -- issue at 1.93 / 2.04 ns
+# per wave-instruction per SIMD against 1.26-1.33 for add / xor / bitop3
+# (profiles/microbench_r01.txt, microbench_valu rows), so no SHA-256 round
+# reaches the nominal figure.
+VALU_PEAK_OPS = SHA_PEAK_GCOMPS * 1e9 * OPS_PER_COMP
 
 
 def parse():
@@ -784,8 +787,15 @@ def main():
     # MaxConcurrency precommits, embedded/store/options.go:35).  D = 1 is
     # strictly sequential.
     D = max(1, a.inflight)
+    # With a process group the build streams are high-priority streams: HIP
+    # gives those a hardware-queue pool of their own, so the three builds keep
+    # three queues next to the process group's streams (with the normal pool of
+    # GPU_MAX_HW_QUEUES = 4 two builds shared one queue and ran back to back:
+    # one nccl rank 1154 -> 1264 GiB/s, >= 2 leaf kernels running 4 -> 85 % of
+    # the time, profiles/pgprof_r05.txt).  MH_BENCH_STREAM_PRIO overrides.
+    prio = int(os.environ.get("MH_BENCH_STREAM_PRIO", "-1" if dist else "0"))
     streams = [torch.cuda.current_stream(dev)] if D == 1 else \
-        [torch.cuda.Stream(dev) for _ in range(D)]
+        [torch.cuda.Stream(dev, priority=prio) for _ in range(D)]
     ctxs = [m.Context(local, s.cuda_stream) for s in streams]
     ctx = ctxs[0]
     L = N.load()
@@ -806,10 +816,17 @@ def main():
                   for _ in range(D)]
     groot = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(D)]
 
-    # collectives of all in-flight builds go through ONE stream, in issue
-    # order, so every rank runs its RCCL kernels in the same order
-    comm = torch.cuda.Stream(dev) if (dist and D > 1) else streams[0]
-    comm_ctx = ctx if comm is streams[0] else m.Context(local, comm.cuda_stream)
+    # the all-gather + top levels of build j run on build j's own stream:
+    # torch issues every collective of the process group on its one internal
+    # stream in host order, so all ranks run their RCCL kernels in the same
+    # order without a stream of ours.  A separate comm stream (the round-4
+    # form, MH_BENCH_COMM_STREAM=1) costs a HIP hardware queue: with 4 per
+    # process (GPU_MAX_HW_QUEUES) three build streams, the PG's stream and a
+    # comm stream share them, so two builds end up in one queue and stop
+    # overlapping (profiles/pgprof_r05.txt: 1132 vs 1298 GiB/s as one rank).
+    sep_comm = dist is not None and D > 1 and os.environ.get("MH_BENCH_COMM_STREAM", "") == "1"
+    comm = torch.cuda.Stream(dev) if sep_comm else None
+    comm_ctx = m.Context(local, comm.cuda_stream) if sep_comm else None
 
     def step(k):
         j = k % D
@@ -820,12 +837,15 @@ def main():
         if dist:
             # 32 B per rank over RCCL, then the top log2(world) levels locally
             # (immustore_amd/sharding.py; exact by SURVEY.md finding 3)
-            comm.wait_stream(streams[j])
-            with torch.cuda.stream(comm):
+            s_, c_ = (comm, comm_ctx) if sep_comm else (streams[j], ctxs[j])
+            if sep_comm:
+                comm.wait_stream(streams[j])
+            with torch.cuda.stream(s_):
                 g = sharding.allgather_roots(root[j], world)
-                N.check(L.mh_dev_htree_reduce_nodes(comm_ctx.handle, g.data_ptr(), world,
+                N.check(L.mh_dev_htree_reduce_nodes(c_.handle, g.data_ptr(), world,
                                                     top_levels[j].data_ptr(), groot[j].data_ptr()))
-            streams[j].wait_stream(comm)
+            if sep_comm:
+                streams[j].wait_stream(comm)
 
     # clock pre-warm: full builds (same inputs, every level recomputed, nothing
     # kept) for a fixed wall time before the W warmup steps -- with the
@@ -984,7 +1004,7 @@ def main():
                    "entries_per_gpu": n, "value_len": VAL, "key_len": KEY_LEN,
                    "parallelism": "subtree shard per GPU + %s all-gather of roots"
                    % ("RCCL" if backend != "gloo" else "gloo") if dist else "single GPU", "lanes_per_leaf_group": lpl,
-                   "builds_in_flight": D, "wg_subtree_levels": wgl},
+                   "builds_in_flight": D, "wg_subtree_levels": wgl, "stream_priority": prio},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": "k_entries_fixed",
@@ -996,7 +1016,13 @@ def main():
                                           "achieved / frac"},
                      "valu": {"achieved_tops": round(valu / 1e12, 2),
                               "peak_tops": round(VALU_PEAK_OPS / 1e12, 2),
-                              "frac": round(valu / VALU_PEAK_OPS, 4)},
+                              "frac": round(valu / VALU_PEAK_OPS, 4),
+                              "peak_source": "measured SHA-256 register loop 30.9 G comp/s "
+                                             "(profiles/microbench_r01.txt) x 1388 VALU "
+                                             "instructions per compression (profiles/"
+                                             "isa_counts_r01.txt): the issue-weighted peak of "
+                                             "this instruction mix; achieved counts the "
+                                             "constant-schedule blocks at 901"},
                      "sha": {"gcomp_per_s": round(comp_rate / 1e9, 2),
                              "peak_gcomp_per_s": SHA_PEAK_GCOMPS,
                              "frac": round(comp_rate / 1e9 / SHA_PEAK_GCOMPS, 4),
@@ -1028,7 +1054,7 @@ def main():
     out["root_check"] = rcheck
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if comm_ctx is not ctx:
+    if comm_ctx is not None:
         comm_ctx.close()
     for c in ctxs:
         c.close()

@@ -94,6 +94,13 @@ func (t *AHtree) peaks(n uint64) ([]byte, error) {
 // RootAt(size) after the batch.  Like Append (ahtree.go:260-263) it rejects
 // only a nil payload; the C ABI takes one payload length per call, so each
 // maximal run of equal-length payloads is one device batch.
+//
+// Partial failure: the runs are committed one after the other.  If run k
+// fails, runs 0..k-1 are already in pLog, dLog and cLog (as len(ds) single
+// Appends would have left them up to the failing one), so the error comes
+// with n = the tree size after the last run that succeeded and root =
+// RootAt(n) -- the state the caller resumes from (n = the size before the
+// call and a zero root when the first run fails).
 func (t *AHtree) AppendBatch(ds [][]byte) (n uint64, root [sha256.Size]byte, err error) {
 	t.mutex.Lock()
 	defer t.mutex.Unlock()
@@ -111,14 +118,18 @@ func (t *AHtree) AppendBatch(ds [][]byte) (n uint64, root [sha256.Size]byte, err
 			return 0, root, ErrIllegalArguments
 		}
 	}
+	n = t.size()
 	for i := 0; i < len(ds); {
 		j := i + 1
 		for j < len(ds) && len(ds[j]) == len(ds[i]) {
 			j++
 		}
-		if n, root, err = t.appendRun(ds[i:j]); err != nil {
-			return 0, root, err
+		rn, rroot, rerr := t.appendRun(ds[i:j])
+		if rerr != nil {
+			// n / root: what the runs before this one committed
+			return n, root, rerr
 		}
+		n, root = rn, rroot
 		i = j
 	}
 	return n, root, nil

@@ -395,6 +395,10 @@ extern "C" int mh_dev_htree_reduce_nodes(mh_ctx *c, const uint8_t *nodes, uint64
         if (!c || (w && (!nodes || !levels))) return MH_ERR_ILLEGAL_ARGUMENTS;
         MH_HIP(hipSetDevice(c->device));
         if (((uintptr_t)nodes & 15) || ((uintptr_t)levels & 15)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (w >= 1 && w <= kSmallTreeMax) {  // one launch (every multi-GPU step)
+            MH_HIP(launch_reduce_small(c->stream, nodes, w, levels, root));
+            return MH_OK;
+        }
         LevelGeom g;
         g.init(w);
         if (w) {

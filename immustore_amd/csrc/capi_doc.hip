@@ -326,11 +326,16 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
                     if (u.off == off && u.bytes) return base + b_span + (u.src - alo);
             return base + off;
         };
-        if (arena) {
-            MH_HIP(hipMemcpyAsync(base + b_span, alo, (uint64_t)(hi - alo), hipMemcpyHostToDevice, st));
-        } else {
-            for (const Up &u : ups)
-                if (u.bytes) MH_HIP(hipMemcpyAsync(base + u.off, u.src, u.bytes, hipMemcpyHostToDevice, st));
+        {
+            // which upload ran shows in the context's timing records
+            // (mh_ctx_timing "doc_upload_arena" / "doc_upload_arrays")
+            TimerScope ts(c->tm(), arena ? "doc_upload_arena" : "doc_upload_arrays", st);
+            if (arena) {
+                MH_HIP(hipMemcpyAsync(base + b_span, alo, (uint64_t)(hi - alo), hipMemcpyHostToDevice, st));
+            } else {
+                for (const Up &u : ups)
+                    if (u.bytes) MH_HIP(hipMemcpyAsync(base + u.off, u.src, u.bytes, hipMemcpyHostToDevice, st));
+            }
         }
         // every offset in order (host, under the copies; branch-free loops)
         {

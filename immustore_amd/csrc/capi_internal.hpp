@@ -203,7 +203,8 @@ struct mh_ctx {
     hipStream_t stream2 = nullptr;     // a second compute stream (tx-log groups)
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
     DevBuf s_chunk[2];
-    std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call
+    std::vector<hipEvent_t> ev_chunks;  // one per chunk of a pipelined call (arrivals)
+    std::vector<hipEvent_t> ev_results; // one per group: its results are complete
     Timer *tm() { return timer.enabled ? &timer : nullptr; }
     // creates copy_stream and the events on first use (c->mu held)
     hipError_t copy_lane() {
@@ -224,6 +225,7 @@ struct mh_ctx {
             if (ev_done[k]) hipEventDestroy(ev_done[k]);
         }
         for (hipEvent_t e : ev_chunks) hipEventDestroy(e);
+        for (hipEvent_t e : ev_results) hipEventDestroy(e);
         if (copy_stream) hipStreamDestroy(copy_stream);
         if (copy_stream2) hipStreamDestroy(copy_stream2);
         if (d2h_stream) hipStreamDestroy(d2h_stream);
@@ -351,16 +353,37 @@ struct ChunkCopier {
     }
 };
 
-// a and b in the same pinned host allocation (device addresses as far apart)
+// [a, b] (b >= a) lies inside ONE pinned host allocation: the allocation's
+// address range as the runtime reports it for a (HIP_POINTER_ATTRIBUTE_
+// RANGE_START_ADDR / _RANGE_SIZE, in the host or the device view of the
+// allocation) must hold both ends.  Two separate hipHostMalloc blocks are not
+// one allocation even when their device addresses are as far apart as their
+// host addresses (on ROCm they usually are: same virtual address), and a copy
+// of a span crossing them could read a gap.  Any query that
+// fails means "no", i.e. one copy per array.
 inline bool pinned_same_alloc(const void *a, const void *b) {
-    hipPointerAttribute_t x, y;
-    if (hipPointerGetAttributes(&x, a) != hipSuccess || hipPointerGetAttributes(&y, b) != hipSuccess) {
+    hipPointerAttribute_t x;
+    void *start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttributes(&x, a) != hipSuccess || x.type != hipMemoryTypeHost ||
+        hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)a) !=
+            hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)a) !=
+            hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return x.type == hipMemoryTypeHost && y.type == hipMemoryTypeHost && x.devicePointer &&
-           (const uint8_t *)y.devicePointer - (const uint8_t *)x.devicePointer ==
-               (const uint8_t *)b - (const uint8_t *)a;
+    const uintptr_t s = (uintptr_t)start, ua = (uintptr_t)a, ub = (uintptr_t)b,
+                    ud = (uintptr_t)x.devicePointer;
+    if (ub < ua || !size) return false;
+    uintptr_t off;
+    if (ua >= s && ua - s < size)
+        off = ua - s;
+    else if (ud && ud >= s && ud - s < size)
+        off = ud - s;
+    else
+        return false;
+    return ub - ua < size - off;
 }
 
 // events for n chunks in c->ev_chunks
@@ -378,6 +401,18 @@ inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
         hipEvent_t e;
         if (hipError_t r = hipEventCreateWithFlags(&e, flags)) return r;
         c->ev_chunks.push_back(e);
+    }
+    return hipSuccess;
+}
+
+// events for the results of n groups in c->ev_results: default flags, i.e.
+// WITH the system-scope release -- the copies that wait on them may read the
+// results through a DMA engine rather than a kernel
+inline hipError_t ensure_result_events(mh_ctx *c, size_t n) {
+    while (c->ev_results.size() < n) {
+        hipEvent_t e;
+        if (hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming)) return r;
+        c->ev_results.push_back(e);
     }
     return hipSuccess;
 }

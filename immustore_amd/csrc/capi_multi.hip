@@ -32,6 +32,7 @@ struct Rccl {
                                hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*abort)(ncclComm_t) = nullptr;
 };
 
 const Rccl &rccl() {
@@ -46,7 +47,8 @@ const Rccl &rccl() {
         r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
         r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
         r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
-        r.ok = r.init_all && r.destroy && r.all_gather && r.group_start && r.group_end;
+        r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
+        r.ok = r.init_all && r.destroy && r.all_gather && r.group_start && r.group_end && r.abort;
     });
     return r;
 }
@@ -87,6 +89,9 @@ struct mh_multi {
     // devices): RCCL wants one rank per device, so the 32-byte roots are then
     // gathered with device-to-device copies instead
     bool use_rccl = true;
+    // the clique was aborted (a collective failed after others of the same
+    // group were queued): every later collective returns MH_ERR_COLLECTIVE
+    bool broken = false;
     struct Dev {
         DevBuf keys, vals, hv, levels, send, recv, top, dlog, ovr;
         DevBuf fr, pk, ctr;  // ranged ahtree append: frontier, old peaks, work queue
@@ -157,7 +162,7 @@ extern "C" int mh_multi_destroy(mh_multi *m) {
             if (m->ctx[d]) mh_ctx_synchronize(m->ctx[d]);
         const Rccl &R = rccl();
         for (ncclComm_t c : m->comm)
-            if (c && R.ok) R.destroy(c);
+            if (c && R.ok && !m->broken) R.destroy(c);  // aborted comms are gone
         for (int d = 0; d < (int)m->buf.size(); d++) {
             hipSetDevice(m->dev[d]);
             m->buf[d].reset();  // frees on the owning device
@@ -255,17 +260,36 @@ int gather_bytes(mh_multi *m, const std::vector<const uint8_t *> &send,
         return MH_OK;
     }
     const Rccl &R = rccl();
+    if (m->broken) return MH_ERR_COLLECTIVE;
+    // every device selectable before the group opens, so a plain HIP error
+    // cannot stop the loop below half way
+    for (int d = 0; d < m->K; d++) MH_HIP(hipSetDevice(m->dev[d]));
     MH_NCCL(R.group_start());
     // every exit after ncclGroupStart ends the group: an open group would
     // defer every later RCCL call of this thread into it (the next build
     // would hang instead of failing)
     RcclGroup group(R);
-    for (int d = 0; d < m->K; d++) {
-        MH_HIP(mh_fault(MH_FAULT_RCCL_GROUP) ? hipErrorInvalidDevice : hipSetDevice(m->dev[d]));
-        MH_NCCL(R.all_gather(send[d], recv[d], bytes, ncclUint8, m->comm[d], m->ctx[d]->stream));
+    int queued = 0, st = MH_OK;
+    for (int d = 0; d < m->K && st == MH_OK; d++) {
+        if (mh_fault(MH_FAULT_RCCL_GROUP) || hipSetDevice(m->dev[d]) != hipSuccess ||
+            R.all_gather(send[d], recv[d], bytes, ncclUint8, m->comm[d], m->ctx[d]->stream) !=
+                ncclSuccess)
+            st = MH_ERR_COLLECTIVE;
+        else
+            queued++;
     }
-    MH_NCCL(group.end());
-    return MH_OK;
+    const ncclResult_t ge = group.end();
+    if (st == MH_OK && ge == ncclSuccess) return MH_OK;
+    if (queued > 0) {
+        // the collectives queued for devices 0..queued-1 were launched by
+        // ncclGroupEnd and wait for peers that never join: abort the clique
+        // (ncclCommAbort ends its pending operations) so those streams drain,
+        // and refuse every later collective on this handle
+        m->broken = true;
+        for (ncclComm_t c : m->comm)
+            if (c) R.abort(c);
+    }
+    return MH_ERR_COLLECTIVE;
 }
 
 int gather_roots(mh_multi *m, const std::vector<const uint8_t *> &send,

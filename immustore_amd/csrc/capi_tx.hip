@@ -1054,18 +1054,6 @@ static uint32_t *host_words(void *p, uint64_t bytes) {
     return (uint32_t *)a.devicePointer;
 }
 
-// a and b in the same pinned host allocation (device addresses as far apart)
-static bool same_alloc(const void *a, const void *b) {
-    hipPointerAttribute_t x, y;
-    if (hipPointerGetAttributes(&x, a) != hipSuccess || hipPointerGetAttributes(&y, b) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return x.type == hipMemoryTypeHost && y.type == hipMemoryTypeHost && x.devicePointer &&
-           (const uint8_t *)y.devicePointer - (const uint8_t *)x.devicePointer ==
-               (const uint8_t *)b - (const uint8_t *)a;
-}
-
 // copy chunks of a long tx log: MH_TXLOG_CHUNKS (1..16, read once), default 4
 static uint64_t txlog_chunks() {
     static const uint64_t k = [] {
@@ -1174,8 +1162,10 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // pageable one is staged by the runtime inside each copy call, so a
         // helper thread (ChunkCopier) issues those under the hop, in two
         // chunks (3/4 + 1/4: every staged call has its own setup).  Events
-        // ev_chunks[0, K) mark the chunks' arrival, ev_chunks[K, 2K) the end
-        // of each group's kernels.
+        // ev_chunks[0, K) mark the chunks' arrival (no system-scope fence: their
+        // waiters are device streams), ev_results[0, K) the end of each
+        // group's kernels (with the fence: c->d2h_stream's copies of a
+        // group's results may run on a DMA engine).
         bool pinned = false;
         {
             static const int inl = [] {
@@ -1183,7 +1173,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 return e ? atoi(e) : 1;
             }();
             // the whole range in one pinned allocation (first and last byte)
-            pinned = inl && len && same_alloc(buf, buf + len - 1);
+            pinned = inl && len && pinned_same_alloc(buf, buf + len - 1);
         }
         tr.mark("attrs");
         const std::vector<double> wts = pinned ? txlog_weights() : std::vector<double>{3, 1};
@@ -1197,7 +1187,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         }
         cut[K] = len;
         const uint64_t nck = len ? K : 0;
-        MH_HIP(ensure_chunk_events(c, 2 * nck));
+        MH_HIP(ensure_chunk_events(c, nck));
+        MH_HIP(ensure_result_events(c, nck));
         tr.mark("events");
         // once a group's kernels are queued they may store into the caller's
         // pinned status / alh / header arrays: every exit (errors included)
@@ -1464,8 +1455,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
             if (hipError_t e = cc.wait(g.k)) return -(int)e;
             MH_HIP(cc.stream_wait(st, g.k));
             if (int e = run(g, dbuf, nullptr, 0, 0, st)) return e;
-            MH_HIP(hipEventRecord(c->ev_chunks[nck + g.k], st));
-            return results(g, c->ev_chunks[nck + g.k]);
+            MH_HIP(hipEventRecord(c->ev_results[g.k], st));
+            return results(g, c->ev_results[g.k]);
         };
         size_t deferred = 0;  // gs[0, deferred) are queued
         uint64_t pos = 0, e_done = 0;

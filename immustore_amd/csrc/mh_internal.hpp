@@ -247,6 +247,10 @@ inline bool small_roots_fit(uint64_t ntrees, uint64_t wmax) {
 // for many trees)
 hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const uint64_t *leaf_off,
                               uint8_t *nodes, uint8_t *roots, uint64_t wmax);
+// the levels above a row of 1 <= w <= 64 nodes (flat level-major, level 0 =
+// the row) and their root, one single-wave launch
+hipError_t launch_reduce_small(hipStream_t st, const uint8_t *nodes, uint64_t w, uint8_t *levels,
+                               uint8_t *root);
 // headers + first-entry offsets of tx records from the raw log (md_off relative to buf)
 hipError_t launch_tx_hdr_from_raw(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                                   const uint64_t *rec_off, MhTxHeader *hdrs, uint64_t *ent_start);

@@ -619,6 +619,70 @@ hipError_t launch_small_roots(hipStream_t st, Timer *tm, uint64_t ntrees, const 
     return hipGetLastError();
 }
 
+// The levels above a row of w <= 64 inner nodes in ONE launch
+// (mh_dev_htree_reduce_nodes for the all-gathered shard roots of a multi-GPU
+// build, w = ranks): one wave, node k of the current level on lane k in LDS,
+// every level's nodes hashed at once (htree.go:85-110: pairs, an odd last
+// node promoted) and written to levels in the flat level-major layout
+// (level 0 = the input row), the root to root.  Replaces a copy kernel, the
+// level launches and a device-to-device copy per build.
+__global__ __launch_bounds__(64) void k_reduce_small(const uint8_t *__restrict__ nodes, uint32_t w,
+                                                     uint8_t *__restrict__ levels,
+                                                     uint8_t *__restrict__ root) {
+    __shared__ uint32_t L[64][9];
+    const uint32_t lane = threadIdx.x;
+    if (lane < w) {
+        uint32_t d[8];
+        load_digest(nodes + 32 * lane, d);
+#pragma unroll
+        for (int j = 0; j < 8; j++) L[lane][j] = d[j];
+        store_digest(levels + 32 * lane, d);
+    }
+    uint64_t off = w;
+    while (w > 1) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t half = w / 2;
+        uint32_t a[8], b[8], h[8];
+        const bool hash = lane < half, promote = (w & 1) && lane == half;
+        if (hash || promote) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = L[promote ? w - 1 : 2 * lane][j];
+        }
+        if (hash) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) b[j] = L[2 * lane + 1][j];
+            node_hash_g(a, b, h);
+        } else {
+            copy8(h, a);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (hash || promote) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) L[lane][j] = h[j];
+            store_digest(levels + 32 * (off + lane), h);
+        }
+        w = (w + 1) / 2;
+        off += w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0 && root) {
+        uint32_t r[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) r[j] = L[0][j];
+        store_digest(root, r);
+    }
+}
+
+hipError_t launch_reduce_small(hipStream_t st, const uint8_t *nodes, uint64_t w, uint8_t *levels,
+                               uint8_t *root) {
+    if (w == 0 || w > kSmallTreeMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_reduce_small, dim3(1), dim3(64), 0, st, nodes, (uint32_t)w, levels, root);
+    return hipGetLastError();
+}
+
 // The whole a14 check of a group of tx-log records whose trees are small, in
 // ONE launch (tx.go:533-630 per record: header, entry walk, entry digests and
 // leaves, the tx's htree, innerHash + Alh against the stored Alh).  A

@@ -396,6 +396,32 @@ def test_reduce_nodes_matches_sharded_build(m, ctx, orc):
         assert dr.to_host().tobytes() == orc.htree_build(d)[1]
 
 
+def test_reduce_nodes_levels_every_small_width(m, ctx, orc):
+    """mh_dev_htree_reduce_nodes for every width 1..70 (the single-wave
+    k_reduce_small up to 64, the level kernels above): every level above the
+    row (htree.go:85-110 without the leaf step: pairs hashed, an odd last node
+    promoted unchanged) and the root, against a host restatement over the
+    oracle's SHA-256."""
+    from immustore_amd import _native as N
+    rng = np.random.default_rng(81)
+    for w in list(range(1, 71)) + [127, 128, 129]:
+        row = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(w)]
+        want, lvl = list(row), list(row)
+        while len(lvl) > 1:
+            nxt = [orc.sha256(b"\x01" + lvl[i] + lvl[i + 1]) for i in range(0, len(lvl) - 1, 2)]
+            if len(lvl) % 2:
+                nxt.append(lvl[-1])
+            want += nxt
+            lvl = nxt
+        dn = DevBuf.from_host(ctx, np.frombuffer(b"".join(row), np.uint8))
+        dl = DevBuf(ctx, m.levels_len(w) * 32)
+        dr = DevBuf(ctx, 32)
+        N.check(N.load().mh_dev_htree_reduce_nodes(ctx.handle, dn.ptr, w, dl.ptr, dr.ptr))
+        assert len(want) == m.levels_len(w)
+        assert dl.to_host().tobytes() == b"".join(want), w
+        assert dr.to_host().tobytes() == lvl[0], w
+
+
 # ------------------------------------------------------------------ ahtree
 def test_ahtree_golden_small(m, ctx, synthetic):
     a = synthetic["ahtree"]

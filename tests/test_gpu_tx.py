@@ -508,8 +508,17 @@ def test_verify_document_batch_pinned_and_arena(m, ctx, orc, fixtures, pinned):
     docs[0]["md_blob"] = blob
     ref = txlayer.verify_document_batch(docs, ctx=ctx)
     b, keep = txlayer.pack_document_batch(docs, pinned=pinned)
+    ctx.timing_reset()
+    ctx.set_timing(True)
     st, alh = txlayer.call_document_batch(b, len(docs), ctx)
+    ctx.set_timing(False)
     assert np.array_equal(st, ref[0]) and np.array_equal(alh, ref[1])
+    # one upload of the arena's span only when every array is inside ONE
+    # pinned allocation; separately pinned arrays (adjacent or not) go one
+    # copy per array, never one span across allocations
+    n_arena, n_arrays = ctx.timing("doc_upload_arena")[1], ctx.timing("doc_upload_arrays")[1]
+    assert (n_arena > 0 and n_arrays == 0) if pinned == "arena" else (n_arena == 0 and n_arrays > 0), \
+        (pinned, n_arena, n_arrays)
     for k, d in enumerate(docs):
         ost, oalh = orc.verify_document(d, blob)
         assert int(st[k]) == ost, k

@@ -17,6 +17,7 @@
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   wdist:<w>:<N>    bench_workloads.py --workload <w> (c3 / c5) as N gloo ranks sharing GPU 0
 #   wcorrupt:<w>:<N> the same with MH_BENCH_CORRUPT=1 (N >= 2): must exit 1 (result check)
+#   pgprof:<VARS>    rocprofv3 kernel trace of bench.py per env variant -> queue map + overlap
 #   forcepg          MH_DIST_FORCE_PG=1: the multi-rank code paths as ONE nccl (RCCL) rank:
 #                    bench.py (C2), bench.py --config c4, bench_workloads.py c3 and c5
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
@@ -84,6 +85,15 @@ for s in "$@"; do
       MH_DIST_FORCE_PG=1 step forcepg_c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1
       MH_DIST_FORCE_PG=1 step forcepg_wc3 600 python bench_workloads.py --workload c3 --steps 5 --warmup 1 || exit 1
       MH_DIST_FORCE_PG=1 step forcepg_wc5 600 python bench_workloads.py --workload c5 --steps 5 --warmup 1 || exit 1 ;;
+    pgprof:*)  # kernel traces of bench.py per env variant (e.g. pgprof:base;MH_DIST_FORCE_PG=1) -> queue map
+      vs="$(echo "${s#pgprof:}" | tr ';' ' ')"; i=0
+      for v in $vs; do
+        i=$((i+1)); envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
+        rm -rf "$O/pgprof_$i"
+        env $envs timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/pgprof_$i" -o run -- python3 bench.py --steps ${PG_STEPS:-200} --warmup 5 --no-cpu-baseline > "$O/pgprof_$i.out" 2> "$O/pgprof_$i.err" || { tail -5 "$O/pgprof_$i.err"; exit 1; }
+        { echo "# variant $v: $(tail -1 "$O/pgprof_$i.out" | cut -c1-160)"; python3 tools/queue_map.py "$O/pgprof_$i"; } | tee -a "$O/pgprof.txt"
+        rm -rf "$O/pgprof_$i"
+      done ;;
     c4) step c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1 ;;
     prof)
       rm -rf "$O/prof"
