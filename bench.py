@@ -71,11 +71,12 @@ def parse():
                         "clock is at its sustained value when timing starts (0 = off); "
                         "5 s rather than 2 also spans a utilisation sampler's 5 s period, "
                         "which saw the round-3 runs' GPU idle")
-    p.add_argument("--config", choices=["c2", "c4", "c3", "c5"], default="c2",
+    p.add_argument("--config", choices=["c2", "c4", "c3", "c5", "txlog"], default="c2",
                    help="c2: BASELINE configs[1], 2^20 x 1 KiB per GPU (headline); c4: "
                         "configs[3], 2^23 x 4 KiB per GPU (2^26 entries at 8 GPUs); c3: "
                         "configs[2] ahtree append of 10^7; c5: configs[4] proof re-hash "
-                        "(c3 / c5: one GPU, GPU part from bench_workloads.py)")
+                        "(c3 / c5: one GPU, GPU part from bench_workloads.py); txlog: "
+                        "SURVEY 8(a) a14 through the C ABI (--api cabi only)")
     p.add_argument("--entries", type=int, default=None,
                    help="override entries per GPU (--api cabi --config c3: total appends)")
     p.add_argument("--n0", type=int, default=10 ** 6 + 3,
@@ -732,12 +733,104 @@ def cabi_c3(a):
         raise SystemExit(1)
 
 
+def cabi_txlog(a):
+    """--api cabi --config txlog: SURVEY.md 8(a) a14 / 8(f) row 2, the read
+    path's re-hash of a tx log (tx.go:388-630; the replay of
+    immustore.go:1198-1223 and the indexer's readTx, indexer.go:570) the way a
+    Go process drives the node's GPUs: mh_multi_txlog_validate over devices
+    0..N-1 -- the log (2^16 records x 16 entries, 75.5 MB, pinned as the cgo
+    shim's arena) cut at record boundaries, every part copied over its own
+    PCIe link and validated on its device.  After the timed region every Alh
+    and status is checked against the oracle's (oracle/, which also sealed the
+    log); MH_BENCH_CORRUPT=0 flips one stored hVal so the check must fail."""
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        raise SystemExit("--api cabi is one process: run it without torch.distributed.run")
+    import torch
+    K = a.gpus
+    if torch.cuda.device_count() < K:
+        raise SystemExit("--api cabi --gpus %d: only %d device(s) visible"
+                         % (K, torch.cuda.device_count()))
+    import bench_workloads as bw
+    from immustore_amd.multi import MultiDevice
+    from immustore_amd.txlayer import TX_HEADER
+    orc = _oracle()
+    ntx, ne, kl = a.entries or (1 << 16), 16, 16
+    buf = bw.txlog_records(ntx, ne, kl)
+    rec = buf.shape[1]
+    _, n, _, alh_o, _ = orc.txlog_validate(buf.reshape(-1))  # sealed by the oracle
+    assert n == ntx
+    buf[:, rec - 32:] = alh_o
+    corrupted = os.environ.get("MH_BENCH_CORRUPT", "") == "0"
+    if corrupted:
+        buf[ntx // 2, rec - 33] ^= 1  # the last entry's hVal of the middle record
+    pin = torch.empty(buf.size, dtype=torch.uint8).pin_memory()
+    raw = pin.numpy()
+    raw[:] = buf.reshape(-1)
+    outs = (torch.empty(ntx * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy()
+            .view(TX_HEADER),
+            torch.empty(ntx * 32, dtype=torch.uint8).pin_memory().numpy().reshape(ntx, 32),
+            torch.empty(ntx, dtype=torch.int32).pin_memory().numpy())
+    md = MultiDevice(list(range(K)))
+
+    def step():
+        r = md.txlog_validate(raw, out=outs)
+        assert r[0] == 0 and r[1] == ntx
+
+    pre = 0
+    tp = time.perf_counter()
+    while time.perf_counter() - tp < a.prewarm:
+        step()
+        pre += 1
+    for _ in range(a.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / a.steps * 1e3
+    # ---- check vs the oracle (the log's own stored Alh values, recomputed)
+    tc = time.perf_counter()
+    r = md.txlog_validate(raw, out=outs)
+    o = orc.txlog_validate(raw)
+    ok = r[:3] == (o[0], o[1], o[2]) and bool(np.array_equal(r[4], o[3])) and \
+        list(r[5]) == list(o[4]) and not r[5].any()
+    rcheck = {"vs": "oracle", "ok": bool(ok), "records": ntx,
+              "bad_records": [int(x) for x in np.nonzero(r[5])[0][:8]],
+              "what": "every record's recomputed Alh and per-tx status vs orc.txlog_validate "
+                      "(tx.go:388-630) over the same log, all valid",
+              "corrupted": corrupted, "seconds": round(time.perf_counter() - tc, 2)}
+    md.close()
+    out = {"metric": "tx-log read-path validation (a14), %d records x %d entries, through the C "
+                     "ABI across %d device(s)" % (ntx, ne, K),
+           "value": round(ntx / (ms * 1e-3) / 1e6, 3), "unit": "M tx/s", "n_gpus": K, "api": "cabi",
+           "steps": a.steps, "warmup": a.warmup, "clock_prewarm": {"seconds": a.prewarm,
+                                                                   "calls": pre},
+           "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic v1 records (bench_workloads.txlog_records), sealed by the oracle, "
+                   "pinned host log and outputs",
+           "config": {"workload": "mh_multi_txlog_validate: the log cut at record boundaries, "
+                                  "one part per device over its own PCIe link",
+                      "log_bytes": int(raw.size), "records": ntx, "entries_per_record": ne},
+           "log_GBps_incl_parse_and_h2d": round(raw.size / (ms * 1e-3) / 1e9, 2),
+           "cpu_baseline": None, "root_check": rcheck}
+    print(json.dumps(out), flush=True)
+    if not ok:
+        print("root_check FAILED: %s" % json.dumps(rcheck), file=sys.stderr, flush=True)
+        raise SystemExit(1)
+
+
 def main():
     a = parse()
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if a.api == "cabi":
+        if a.config == "txlog":
+            return cabi_txlog(a)
         return cabi_c3(a) if a.config == "c3" else cabi_main(a)
+    if a.config == "txlog":
+        raise SystemExit("--config txlog runs through --api cabi (one process over N devices); "
+                         "one GPU: bench_workloads.py --workload txlog")
     # MH_DIST_FORCE_PG=1: the --gpus N code path (process group, comm stream,
     # all-gather of the roots over RCCL, the top levels, the root-check
     # records) even at N = 1, launched as one torch.distributed.run rank

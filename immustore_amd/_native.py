@@ -298,12 +298,19 @@ SIGNATURES = {
     "mh_multi_ahtree_append_batch": (i32, [vp, u64, u8p, u8p, u64, u32, u8p, u8p]),
     "mh_ahtree_range_plan": (i32, [u64, u64, i32, C.POINTER(i32), vp, C.POINTER(i32)]),
     "mh_ahtree_range_sizes": (i32, [u64, u64, i32, C.POINTER(u64), C.POINTER(u64)]),
+    "mh_multi_htree_verify_inclusion_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u8p]),
+    "mh_multi_verify_dual_proof_v2_batch": (i32, [vp, u64, vp, vp, u8p, u64, u8p, u8p, u8p, u8p,
+                                                  u8p, u8p, u8p, u8p, vp]),
+    "mh_multi_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64),
+                                      C.POINTER(u64), vp, u8p, vp]),
     "mh_dev_ahtree_range_local": (i32, [vp, u64, u8p, u64, i32, i32, u8p, u32, u8p, u8p, u8p]),
     "mh_dev_ahtree_range_finish": (i32, [vp, u64, u8p, u64, i32, i32, u8p, u8p, u8p, u8p]),
     "mh_dev_ahtree_append_range": (i32, [vp, u8p, u64, u8p, u8p, u64, u32, u8p]),
     "mh_dev_ahtree_peaks": (i32, [vp, u8p, u64, u8p]),
     "mh_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64), C.POINTER(u64), vp,
                                 u8p, vp]),
+    "mh_txlog_validate_resident": (i32, [vp, u8p, u8p, u64, u32, u32, u64, C.POINTER(u64),
+                                         C.POINTER(u64), vp, u8p, vp]),
     "mh_commit_pipe_new": (i32, [vp, u64, C.POINTER(vp)]),
     "mh_commit_pipe_free": (i32, [vp]),
     "mh_precommit_batch": (i32, [vp, i32, u64, u64, vp, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p,

@@ -911,3 +911,135 @@ extern "C" int mh_multi_ahtree_append_batch(mh_multi *m, uint64_t n0, const uint
         return MH_OK;
     });
 }
+
+// ============================================================================
+// The PCIe-bound batch paths over the node's GPUs (one Go process = one
+// process: only mh_multi gives it more than one device).  Each call cuts its
+// batch into K contiguous parts -- by index for proofs, at record boundaries
+// for a tx log -- and runs the single-context call of part d on device d from
+// its own thread, so every part crosses its own PCIe link; the outputs are the
+// parts' outputs side by side, byte-equal to one single-context call over the
+// whole batch.  K = 1 is that call.
+// ============================================================================
+namespace {
+
+// [lo, hi) of part d of n items over K parts (nearly equal)
+inline void split_part(uint64_t n, int K, int d, uint64_t &lo, uint64_t &hi) {
+    lo = (uint64_t)((unsigned __int128)n * (unsigned)d / (unsigned)K);
+    hi = (uint64_t)((unsigned __int128)n * (unsigned)(d + 1) / (unsigned)K);
+}
+
+}  // namespace
+
+// htree.VerifyInclusion over n proofs (htree.go:166-195), split by index.
+extern "C" int mh_multi_htree_verify_inclusion_batch(mh_multi *m, uint64_t n, const uint64_t *leaf,
+                                                     const uint64_t *width, const uint64_t *term_off,
+                                                     const uint8_t *terms, const uint8_t *digests,
+                                                     const uint8_t *roots, uint8_t *ok) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (m->K == 1 || n < (uint64_t)m->K)
+            return mh_htree_verify_inclusion_batch(m->ctx[0], n, leaf, width, term_off, terms,
+                                                   digests, roots, ok);
+        if (!leaf || !width || !term_off || !digests || !roots || !ok) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(term_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;  // before any part writes ok
+        std::lock_guard<std::mutex> lk(m->mu);
+        return per_device(m->K, [&](int d) -> int {
+            uint64_t lo, hi;
+            split_part(n, m->K, d, lo, hi);
+            return mh_htree_verify_inclusion_batch(m->ctx[d], hi - lo, leaf + lo, width + lo,
+                                                   term_off + lo, terms, digests + 32 * lo,
+                                                   roots + 32 * lo, ok + lo);
+        });
+    });
+}
+
+// store.VerifyDualProofV2 over n proofs (verification.go:303-372), split by index.
+extern "C" int mh_multi_verify_dual_proof_v2_batch(
+    mh_multi *m, uint64_t n, const mh_tx_header *src_hdr, const mh_tx_header *tgt_hdr,
+    const uint8_t *md_blob, uint64_t md_blob_len, const uint64_t *incl_off,
+    const uint8_t *incl_terms, const uint64_t *cons_off, const uint8_t *cons_terms,
+    const uint64_t *src, const uint64_t *tgt, const uint8_t *src_alh, const uint8_t *tgt_alh,
+    int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (m->K == 1 || n < (uint64_t)m->K)
+            return mh_verify_dual_proof_v2_batch(m->ctx[0], n, src_hdr, tgt_hdr, md_blob,
+                                                 md_blob_len, incl_off, incl_terms, cons_off,
+                                                 cons_terms, src, tgt, src_alh, tgt_alh, status);
+        if (!src_hdr || !tgt_hdr || !incl_off || !cons_off || !src || !tgt || !src_alh ||
+            !tgt_alh || !status)
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(incl_off, n) || !monotonic(cons_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(m->mu);
+        return per_device(m->K, [&](int d) -> int {
+            uint64_t lo, hi;
+            split_part(n, m->K, d, lo, hi);
+            return mh_verify_dual_proof_v2_batch(m->ctx[d], hi - lo, src_hdr + lo, tgt_hdr + lo,
+                                                 md_blob, md_blob_len, incl_off + lo, incl_terms,
+                                                 cons_off + lo, cons_terms, src + lo, tgt + lo,
+                                                 src_alh + 32 * lo, tgt_alh + 32 * lo, status + lo);
+        });
+    });
+}
+
+// The read path's re-hash of a tx log (tx.go:388-630: replay,
+// immustore.go:1198-1223; the indexer's readTx, indexer.go:570) over the
+// devices: the host hop finds the record boundaries once (mh_txlog_scan, the
+// call's structural status), the records are cut into K parts of nearly equal
+// bytes at record boundaries -- every record carries its prevAlh, so the parts
+// are independent -- and part d is validated by device d (mh_txlog_validate
+// on its bytes: its own copy over its own link).  A v1 header's md_off is
+// relative to buf, as in the single call.
+extern "C" int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t len,
+                                       uint32_t max_entries, uint32_t max_key_len,
+                                       uint64_t max_txs, uint64_t *ntx_out,
+                                       uint64_t *consumed_out, mh_tx_header *hdrs_out,
+                                       uint8_t *alh_out, int32_t *status_out) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (m->K == 1)
+            return mh_txlog_validate(m->ctx[0], buf, len, max_entries, max_key_len, max_txs,
+                                     ntx_out, consumed_out, hdrs_out, alh_out, status_out);
+        if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // a record is >= 122 bytes (90-byte head + 32-byte Alh)
+        const uint64_t cap = std::min<uint64_t>(max_txs, len / 122 + 1);
+        std::vector<uint64_t> aoff(cap ? cap : 1);
+        uint64_t cnt = 0, used = 0;
+        const int rc = mh_txlog_scan(buf, len, max_entries, max_key_len, cap, &cnt, &used, nullptr,
+                                     aoff.data());
+        if (rc < 0) return rc;
+        if (ntx_out) *ntx_out = cnt;
+        if (consumed_out) *consumed_out = used;
+        if (!cnt) return rc;
+        // part d: records [t[d], t[d+1]), bytes [start(t[d]), start(t[d+1]))
+        const int K = m->K;
+        auto start = [&](uint64_t t) -> uint64_t { return t ? aoff[t - 1] + 32 : 0; };
+        std::vector<uint64_t> t(K + 1, 0);
+        t[K] = cnt;
+        for (int d = 1; d < K; d++) {
+            const uint64_t want = (uint64_t)((unsigned __int128)used * (unsigned)d / (unsigned)K);
+            uint64_t x = (uint64_t)(std::lower_bound(aoff.begin(), aoff.begin() + cnt, want) - aoff.begin());
+            t[d] = std::max(t[d - 1], std::min(x, cnt));  // the first record ending at or after want
+        }
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int st = per_device(K, [&](int d) -> int {
+            const uint64_t t0 = t[d], t1 = t[d + 1];
+            if (t1 == t0) return MH_OK;
+            const uint64_t b0 = start(t0), b1 = start(t1);
+            uint64_t n = 0, u = 0;
+            int r = mh_txlog_validate(m->ctx[d], buf + b0, b1 - b0, max_entries, max_key_len,
+                                      t1 - t0, &n, &u, hdrs_out ? hdrs_out + t0 : nullptr,
+                                      alh_out ? alh_out + 32 * t0 : nullptr,
+                                      status_out ? status_out + t0 : nullptr);
+            if (r < 0) return r;
+            // the part's records parsed as in the whole-log scan
+            if (r != MH_OK || n != t1 - t0 || u != b1 - b0) return MH_ERR_ILLEGAL_STATE;
+            if (hdrs_out)
+                for (uint64_t k = t0; k < t1; k++)
+                    if (hdrs_out[k].version == 1) hdrs_out[k].md_off += (uint32_t)b0;
+            return MH_OK;
+        });
+        return st ? st : rc;
+    });
+}

@@ -1136,10 +1136,12 @@ struct PhaseTrace {
 };
 }  // namespace
 
-extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
-                                 uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
-                                 uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
-                                 int32_t *status_out) {
+// buf: the log in host memory (the hop parses it); dlog: the same bytes
+// already resident on the device (no copy; nullptr: copied from buf in chunks)
+static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlog, uint64_t len,
+                               uint32_t max_entries, uint32_t max_key_len, uint64_t max_txs,
+                               uint64_t *ntx_out, uint64_t *consumed_out, mh_tx_header *hdrs_out,
+                               uint8_t *alh_out, int32_t *status_out) {
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
         PhaseTrace tr;
@@ -1154,8 +1156,8 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         // + 256: k_txlog_wave's staging of a wave's records reads up to 128
         // bytes past the last record's stored Alh (16-byte pieces + its
         // unguarded block over-read pad), inside the allocation
-        if (len) MH_HIP(c->s_txlog.ensure(len + 256));
-        uint8_t *dbuf = c->s_txlog.as<uint8_t>();
+        if (len && !dlog) MH_HIP(c->s_txlog.ensure(len + 256));
+        uint8_t *dbuf = dlog ? const_cast<uint8_t *>(dlog) : c->s_txlog.as<uint8_t>();
         // A pinned log: 4 chunks from 16 MiB up (txlog_weights: 4 : 2 : 1 : 1;
         // the last chunk's device work is the tail after the copy), all
         // queued from this thread at once.  A
@@ -1173,11 +1175,12 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                 return e ? atoi(e) : 1;
             }();
             // the whole range in one pinned allocation (first and last byte)
-            pinned = inl && len && pinned_same_alloc(buf, buf + len - 1);
+            pinned = inl && len && !dlog && pinned_same_alloc(buf, buf + len - 1);
         }
         tr.mark("attrs");
         const std::vector<double> wts = pinned ? txlog_weights() : std::vector<double>{3, 1};
-        const uint64_t K = len < (16ull << 20) ? 1 : wts.size();
+        // (a resident log: one chunk without a copy, i.e. one group after the hop)
+        const uint64_t K = dlog || len < (16ull << 20) ? 1 : wts.size();
         std::vector<uint64_t> cut(K + 1, 0);
         double wsum = 0, pre = 0;
         for (uint64_t k = 0; k < K; k++) wsum += wts[k];
@@ -1215,7 +1218,7 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
         for (uint64_t k = 0; k < nck; k++)
-            cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], cut[k + 1] - cut[k]}};
+            cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], dlog ? 0 : cut[k + 1] - cut[k]}};
         cc.inline_issue = pinned;
         {  // MH_TXLOG_COPY_LANES=2: chunk k on copy stream k % 2 (A/B, read per call)
             const char *cl = getenv("MH_TXLOG_COPY_LANES");
@@ -1340,9 +1343,11 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                     ho.hdrs = reinterpret_cast<uint64_t *>(hh);
                     g.host_done = true;
                 }
-                // MH_TXLOG_KERNEL=group: the workgroup kernel (read per call: A/B tests)
+                // MH_TXLOG_KERNEL=group | wave | blk (read per call: A/B tests)
                 const char *kn = getenv("MH_TXLOG_KERNEL");
                 const bool wave = !(kn && strcmp(kn, "group") == 0);
+                const bool blk = kn && strcmp(kn, "blk") == 0;
+                const bool lanes = kn && strcmp(kn, "lanes") == 0;
                 // MH_TXLOG_HOST_HDRS=1 (read per call, A/B): the last chunk's
                 // group -- its kernel is the tail of the call -- writes only
                 // the Eh words of the caller's pinned headers; the host fills
@@ -1352,7 +1357,15 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                     ho.eh_only = 1;
                     g.host_hdrs = true;
                 }
-                if (wave)
+                if (lanes)
+                    MH_HIP(launch_txlog_lanes(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
+                                              base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
+                                              len));
+                else if (blk)
+                    MH_HIP(launch_txlog_blk(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
+                                            base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
+                                            g.pro, g.pap));
+                else if (wave)
                     MH_HIP(launch_txlog_wave(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
                                              base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
                                              g.pro, g.pap));
@@ -1595,6 +1608,39 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
         tr.mark("done");
         txlog_probe_report();
         return rc;
+    });
+}
+
+extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                                 uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx_out,
+                                 uint64_t *consumed_out, mh_tx_header *hdrs_out, uint8_t *alh_out,
+                                 int32_t *status_out) {
+    return txlog_validate_impl(c, buf, nullptr, len, max_entries, max_key_len, max_txs, ntx_out,
+                               consumed_out, hdrs_out, alh_out, status_out);
+}
+
+extern "C" int mh_txlog_validate_resident(mh_ctx *c, const uint8_t *buf, const uint8_t *dlog,
+                                          uint64_t len, uint32_t max_entries, uint32_t max_key_len,
+                                          uint64_t max_txs, uint64_t *ntx_out,
+                                          uint64_t *consumed_out, mh_tx_header *hdrs_out,
+                                          uint8_t *alh_out, int32_t *status_out) {
+    return mh_guard([&]() -> int {
+        if (!c || (len && (!buf || !dlog))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (len) {
+            // the kernels stage 16-byte pieces up to 128 bytes past the last
+            // record: the device allocation must extend len + 256 bytes
+            hipSetDevice(c->device);
+            hipDeviceptr_t base = nullptr;
+            size_t size = 0;
+            if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dlog) != hipSuccess) {
+                (void)hipGetLastError();
+                return MH_ERR_ILLEGAL_ARGUMENTS;
+            }
+            const uintptr_t b = (uintptr_t)base, d = (uintptr_t)dlog;
+            if (d < b || d - b + len + 256 > size) return MH_ERR_ILLEGAL_ARGUMENTS;
+        }
+        return txlog_validate_impl(c, buf, dlog, len, max_entries, max_key_len, max_txs, ntx_out,
+                                   consumed_out, hdrs_out, alh_out, status_out);
     });
 }
 

@@ -286,6 +286,18 @@ hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint
                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
                              uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
                              uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off);
+// the same with the phases spread over whole workgroups (k_txlog_blk)
+hipError_t launch_txlog_blk(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                            const uint64_t *rec_off, const uint64_t *alh_off,
+                            const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
+                            uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
+                            uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off);
+// the same with every record on 1, 2 or 4 lanes, each lane's subtree serial (k_txlog_lanes)
+hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                              const uint64_t *rec_off, const uint64_t *alh_off,
+                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
+                              uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
+                              uint64_t wmax, uint64_t log_len);
 // MH_TXLOG_PROBE=1: per-phase wave timings of the last call's k_txlog_wave
 // launches on stderr (call after the call's final sync)
 void txlog_probe_report();

@@ -1460,6 +1460,881 @@ hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- a14, workgroup phases
+// The same a14 check of a group (tx.go:533-630 per record) with the work of
+// every phase spread over the WHOLE workgroup, so that a compression slot
+// never idles lanes of a busy wave (k_txlog_wave: R = 64 / L records per wave,
+// its tree levels and the innerHash + Alh of lane 0 per record leave half of
+// the wave's lanes idle -- VALU active 0.51, profiles/pmc_txlog_wave_r04.txt).
+// A 256-thread workgroup takes RPW = min(128, 512 / P) consecutive records
+// (P = the widest tx rounded up to a power of two >= 2):
+//   0. the records are copied into LDS by LDS-DMA (every wave a quarter of the
+//      16-byte pieces, one round trip); record r's thread parses its header
+//      (tx.go:419-518) and walks its entries (tx.go:578-585) into an offset
+//      table;
+//   1. thread k hashes entry slots 2k and 2k+1 (record 2k / P: the entry
+//      digest tx.go:690-731 in place from the staged record, then the leaf
+//      htree.go:79-83) and their level-1 node (or promotes the lone left leaf),
+//      so every thread is busy and level 1 needs no barrier;
+//   2. levels 2 .. log2 P: node j of record r on thread r * (P >> l) + j, both
+//      children from LDS (htree.go:85-110), a barrier per level -- the idle
+//      threads of a level are whole waves, which issue nothing while the
+//      other workgroups' waves on the SIMD run;
+//   3. thread r hashes record r's innerHash (tx.go:249-302, its message built
+//      from the staged header bytes and Eh) and Alh (tx.go:307-319) and
+//      compares it with the stored one (tx.go:623-627);
+//   4. the results are staged in LDS and stored by the whole workgroup as
+//      contiguous runs (as k_txlog_wave).
+// Every hash goes through the one compression site of one loop over the
+// workgroup-uniform slot sequence (entries | levels 2.. | innerHash + Alh);
+// the phase boundaries are the barriers.
+__host__ __device__ constexpr uint32_t txb_res_bytes(int rpw) { return (uint32_t)rpw * 172; }
+struct TxbLds {
+    uint32_t stage, a, b, eoff, info, red, total;
+};
+__host__ __device__ inline TxbLds txb_lds(uint32_t sbytes, int lgp, int rpw) {
+    TxbLds o{};
+    const uint32_t P = 1u << lgp;
+    o.stage = 0;
+    uint32_t x = sbytes > txb_res_bytes(rpw) ? sbytes : txb_res_bytes(rpw);  // results alias the stage
+    o.a = x;
+    x += (uint32_t)rpw * (P / 2) * 36;
+    o.b = x;
+    x += (uint32_t)rpw * (P / 4 ? P / 4 : 1) * 36;
+    o.eoff = x;
+    x += (uint32_t)rpw * P * 4;
+    o.info = x;
+    x += (uint32_t)rpw * 16;
+    o.red = x;
+    x += 16;
+    o.total = (x + 15) & ~15u;
+    return o;
+}
+
+// workgroup max of a per-thread value (red: 4 LDS words; includes barriers)
+__device__ __forceinline__ uint32_t txb_wg_max(uint32_t v, uint32_t *red) {
+    v = wave_max_u32(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint32_t m = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    return m;
+}
+
+template <bool STAGED>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_txlog_blk(
+    uint64_t ntx, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ rec_off,
+    const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
+    MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ eh_out, uint8_t *__restrict__ alh_out,
+    int32_t *__restrict__ status, TxlogHostOut ho, int lgp, int rpw, uint32_t sbytes, int fence,
+    uint64_t *probe) {
+    extern __shared__ uint4 lds[];
+    uint8_t *sm = reinterpret_cast<uint8_t *>(lds);
+    const TxbLds Lo = txb_lds(sbytes, lgp, rpw);
+    uint32_t(*NA)[9] = reinterpret_cast<uint32_t(*)[9]>(sm + Lo.a);
+    uint32_t(*NB)[9] = reinterpret_cast<uint32_t(*)[9]>(sm + Lo.b);
+    uint32_t *eoff = reinterpret_cast<uint32_t *>(sm + Lo.eoff);
+    uint32_t *info = reinterpret_cast<uint32_t *>(sm + Lo.info);
+    uint32_t *red = reinterpret_cast<uint32_t *>(sm + Lo.red);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int P = 1 << lgp;
+    const uint64_t T0 = (uint64_t)blockIdx.x * rpw;
+    const uint64_t nrec = min((uint64_t)rpw, ntx - T0);  // the grid covers ntx: >= 1
+    const uint64_t lo = STAGED ? rec_off[T0] & ~15ull : 0;
+    // MH_TXLOG_PROBE=1: s_memtime stamps of the workgroup's phases (thread 0)
+#define TXB_PROBE(k_)                                                                             \
+    do {                                                                                          \
+        if (probe && tid == 0) probe[(uint64_t)blockIdx.x * 16 + (k_)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+    TXB_PROBE(0);
+    if (probe && tid == 0) probe[(uint64_t)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+    // record r's bytes (LDS when staged, else the log in HBM)
+    auto rec_ptr = [&](uint64_t r) -> const uint8_t * {
+        return STAGED ? sm + (rec_off[T0 + r] - lo) : buf + rec_off[T0 + r];
+    };
+    if (STAGED) {
+        // 0. the workgroup's records (contiguous in the log, each ending with
+        // its stored Alh) into LDS by LDS-DMA: wave wv moves pieces 64 wv +
+        // 256 k; +96 bytes past the last Alh (rd_le32 reads a dword ahead,
+        // skip12_block a block's 80 bytes unguarded), inside the device buffer
+        const uint64_t hi = alh_off[T0 + nrec - 1] + 32 + 96;
+        const uint8_t *g = buf + lo;
+        const uint32_t n16 = (uint32_t)((hi - lo + 15) >> 4);
+        for (uint32_t k = 64 * wv; k < n16; k += 256) {
+            const uint32_t c = min(k + lane, n16 - 1);  // the last lanes repeat the last piece
+            __builtin_amdgcn_global_load_lds((tx_glb_void_t *)(g + 16 * (uint64_t)c),
+                                             (tx_lds_void_t *)(sm + 16 * k), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    TXB_PROBE(1);
+    // header + entry walk of record tid (tx.go:419-518, 578-585; lengths
+    // validated by the host hop)
+    uint32_t nbi = 0;
+    if ((uint64_t)tid < nrec) {
+        const uint8_t *rp = rec_ptr(tid);
+        const uint32_t ver = rd_be16(rp + 88);
+        uint32_t ml = 0, nent, q = 92;
+        if (ver == 0) {
+            nent = rd_be16(rp + 90);
+        } else {
+            ml = rd_be16(rp + 90);
+            nent = bswap(rd_le32(rp + 92 + ml));
+            q = 96 + ml;
+        }
+        info[tid * 4 + 0] = ver;
+        info[tid * 4 + 1] = ml;
+        info[tid * 4 + 2] = nent;
+        const uint64_t w = leaf_off[T0 + tid + 1] - leaf_off[T0 + tid];
+        info[tid * 4 + 3] = (uint32_t)w;
+        for (uint64_t j = 0; j < w; j++) {
+            eoff[tid * P + j] = q;
+            const uint32_t m = rd_be16(rp + q);
+            const uint32_t k = rd_be16(rp + q + 2 + m);
+            q += 48 + m + k;
+        }
+        const uint32_t mlen = 80 + (ver ? 8 + ml : 4);  // innerHash message bytes
+        nbi = (mlen + 8) / 64 + 1;
+    }
+    __syncthreads();
+    TXB_PROBE(2);
+    // 1. this thread's two entry slots and their level-1 node
+    const uint32_t s0 = 2u * tid;
+    const uint64_t r1 = s0 >> lgp;
+    const bool act1 = r1 < nrec && s0 < (uint32_t)rpw * P;
+    const uint32_t j0 = s0 & (P - 1);
+    uint32_t w1 = 0, ver1 = 0;
+    const uint8_t *rp1 = nullptr;
+    if (act1) {
+        w1 = info[r1 * 4 + 3];
+        ver1 = info[r1 * 4 + 0];
+        rp1 = rec_ptr(r1);
+    }
+    const uint32_t ne = act1 ? (uint32_t)min(2u, w1 > j0 ? w1 - j0 : 0u) : 0u;  // entries of this thread
+    const uint8_t *mp[2] = {rp1, rp1};
+    uint32_t la[2] = {0, 0}, nb[2] = {0, 0};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        if ((uint32_t)e < ne) {
+            const uint8_t *er = rp1 + eoff[r1 * P + j0 + e];
+            const uint32_t m = rd_be16(er), k = rd_be16(er + 2 + m);
+            mp[e] = ver1 == 1 ? er : er + 4 + m;  // tx.go:690-731
+            la[e] = ver1 == 1 ? 4 + m + k : k;
+            nb[e] = (la[e] + 32 + 8) / 64 + 1;
+        }
+    }
+    const uint32_t steps = (ne > 0 ? nb[0] + 1 : 0) + (ne > 1 ? nb[1] + 1 + 2 : 0);
+    const uint32_t nE = txb_wg_max(steps, red);
+    const uint32_t nH = txb_wg_max(nbi ? nbi + 2 : 0, red);
+    const uint32_t nT = 2u * (uint32_t)(lgp - 1);
+    TXB_PROBE(3);
+    // 2./3. the slot loop
+    State s;
+    s.init();
+    // lf0 / lf1: the leaves, then a node's children; lf0 the innerHash in H
+    uint32_t lf0[8], lf1[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) lf0[q] = lf1[q] = 0;
+    uint32_t e = 0, b = 0;
+    bool tnode = false, tprom = false;  // this thread's node at the current level: hash / promote
+    uint32_t tdst = 0;
+    const uint32_t rH = tid;            // record of the H phase
+    const bool actH = (uint64_t)tid < nrec;
+    const uint8_t *rpH = actH ? rec_ptr(rH) : nullptr;
+    uint32_t blenH = 0, mlenH = 0, nbiH = nbi;
+    // record rH's root (Eh) stays in LDS: the final level's buffer, slot rH
+    uint32_t(*fin)[9] = (lgp & 1) ? NA : NB;
+#pragma unroll 1
+    for (uint32_t g = 0; g < nE + nT + nH; g++) {
+        uint32_t wv16[16];
+        bool on = false, tail = false;
+        uint32_t tail_r7 = 0;
+        if (g == nE) TXB_PROBE(4);
+        if (g == nE + nT) TXB_PROBE(5);
+        if (g < nE) {
+            // entry e's digest blocks, its leaf, then (two entries) the node
+            if (e < ne) {
+                on = true;
+                if (b < nb[e]) {
+                    if (b == 0) s.init();
+                    skip12_block<!STAGED>(mp[e], la[e], b, nb[e], wv16);
+                } else {
+                    wv16[0] = s.h[0] >> 8;
+#pragma unroll
+                    for (int j = 1; j < 8; j++) wv16[j] = __builtin_amdgcn_alignbit(s.h[j - 1], s.h[j], 8);
+                    wv16[8] = (s.h[7] << 24) | 0x00800000u;
+#pragma unroll
+                    for (int j = 9; j < 15; j++) wv16[j] = 0;
+                    wv16[15] = 33u * 8u;
+                    s.init();
+                }
+            } else if (ne == 2 && e == 2) {
+                on = true;
+                if (b == 0) {  // SHA256(0x01 || leaf0 || leaf1), first block
+                    s.init();
+                    wv16[0] = 0x01000000u | (lf0[0] >> 8);
+#pragma unroll
+                    for (int j = 1; j < 8; j++) wv16[j] = __builtin_amdgcn_alignbit(lf0[j - 1], lf0[j], 8);
+                    wv16[8] = __builtin_amdgcn_alignbit(lf0[7], lf1[0], 8);
+#pragma unroll
+                    for (int j = 1; j < 8; j++) wv16[8 + j] = __builtin_amdgcn_alignbit(lf1[j - 1], lf1[j], 8);
+                } else {
+                    tail = true;
+                    tail_r7 = lf1[7];
+                }
+            }
+        } else if (g < nE + nT) {
+            const uint32_t k = g - nE, l = 2 + (k >> 1), half = k & 1;
+            if (half == 0) {
+                __syncthreads();  // level l - 1 is written
+                const uint32_t S = (uint32_t)P >> l;  // node slots per record at level l
+                const uint64_t r = tid / S;           // (S >= 1: l <= lgp)
+                const uint32_t j = tid - (uint32_t)r * S;
+                tnode = tprom = false;
+                if (tid < rpw * S && r < nrec) {
+                    const uint32_t w = info[r * 4 + 3];
+                    const uint32_t wp = (w + (1u << (l - 1)) - 1) >> (l - 1);  // width at level l-1
+                    const uint32_t a = (uint32_t)r * 2 * S + 2 * j;
+                    uint32_t(*src)[9] = (l & 1) ? NB : NA;  // level l-1: odd levels in A
+                    if (2 * j + 1 < wp) {
+                        tnode = true;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            lf0[q] = src[a][q];
+                            lf1[q] = src[a + 1][q];
+                        }
+                    } else if (2 * j < wp) {
+                        tprom = true;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) lf0[q] = src[a][q];
+                    }
+                    tdst = tid;
+                }
+                if (tnode) {
+                    on = true;
+                    s.init();
+                    wv16[0] = 0x01000000u | (lf0[0] >> 8);
+#pragma unroll
+                    for (int j2 = 1; j2 < 8; j2++) wv16[j2] = __builtin_amdgcn_alignbit(lf0[j2 - 1], lf0[j2], 8);
+                    wv16[8] = __builtin_amdgcn_alignbit(lf0[7], lf1[0], 8);
+#pragma unroll
+                    for (int j2 = 1; j2 < 8; j2++) wv16[8 + j2] = __builtin_amdgcn_alignbit(lf1[j2 - 1], lf1[j2], 8);
+                }
+            } else if (tnode) {
+                on = true;
+                tail = true;
+                tail_r7 = lf1[7];
+            }
+        } else {
+            const uint32_t k = g - nE - nT;
+            if (k == 0) {
+                __syncthreads();  // every tree is reduced
+                if (actH) {
+                    if (info[rH * 4 + 3] == 0) {  // no entries: SHA256(nil), htree.go:73-77
+                        uint32_t d[8];  // (slot rH of no other record: no reader but this thread)
+                        load_digest(kEmptyRootDev, d);
+#pragma unroll
+                        for (int q = 0; q < 8; q++) fin[rH][q] = d[q];
+                    }
+                    const uint32_t ver = info[rH * 4 + 0];
+                    blenH = ver ? 8 + info[rH * 4 + 1] : 4;
+                    mlenH = 80 + blenH;
+                }
+            }
+            if (actH && k < nbiH + 2) {
+                on = true;
+                if (k < nbiH) {  // innerHash block k: ts || version || md part || Eh || blTxID || blRoot
+                    if (k == 0) s.init();
+#pragma unroll 4
+                    for (int jw = 0; jw < 16; jw++) {
+                        const uint32_t kk0 = 64 * k + 4 * jw;
+                        uint32_t v32 = 0;
+                        if (jw == 15 && k + 1 == nbiH) {  // the bit length (< 2^32)
+                            v32 = mlenH * 8;
+                        } else {
+#pragma unroll
+                            for (int bb = 0; bb < 4; bb++) {
+                                const uint32_t kk = kk0 + bb;
+                                uint32_t v;
+                                if (kk < 8) v = rpH[8 + kk];
+                                else if (kk < 8 + blenH) v = rpH[80 + kk];
+                                else if (kk < 40 + blenH) {
+                                    const uint32_t o = kk - 8 - blenH;
+                                    v = (fin[rH][o >> 2] >> (24 - 8 * (o & 3))) & 0xffu;
+                                } else if (kk < mlenH) v = rpH[kk - 24 - blenH];
+                                else v = kk == mlenH ? 0x80u : 0u;
+                                v32 = v32 << 8 | v;
+                            }
+                        }
+                        wv16[jw] = v32;
+                    }
+                } else if (k == nbiH) {  // BE64 id || prevAlh || innerHash[0:24]
+                    copy8(lf0, s.h);  // the innerHash
+                    s.init();
+                    const uint64_t id = rd_be64(rpH);
+                    wv16[0] = (uint32_t)(id >> 32);
+                    wv16[1] = (uint32_t)id;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) wv16[2 + q] = bswap(rd_le32(rpH + 56 + 4 * q));
+#pragma unroll
+                    for (int q = 0; q < 6; q++) wv16[10 + q] = lf0[q];
+                } else {
+                    wv16[0] = lf0[6];
+                    wv16[1] = lf0[7];
+                    wv16[2] = 0x80000000u;
+#pragma unroll
+                    for (int q = 3; q < 15; q++) wv16[q] = 0;
+                    wv16[15] = 72u * 8u;
+                }
+            }
+        }
+        if (on) {
+            if (tail)
+                compress_node_tail_g(s, tail_r7);
+            else
+                compress(s, wv16);
+        }
+        // bookkeeping after the block
+        if (g < nE) {
+            if (on) {
+                if (e < ne) {
+                    if (b == nb[e]) {  // the leaf is done
+                        if (e == 0) copy8(lf0, s.h);
+                        else copy8(lf1, s.h);
+                        e++;
+                        b = 0;
+                        if (e == ne && ne == 1 && act1) {  // a lone left leaf: promoted to level 1
+#pragma unroll
+                            for (int q = 0; q < 8; q++) NA[tid][q] = lf0[q];
+                        }
+                    } else {
+                        b++;
+                    }
+                } else {  // the level-1 node
+                    if (b == 1) {
+#pragma unroll
+                        for (int q = 0; q < 8; q++) NA[tid][q] = s.h[q];
+                        e++;
+                    }
+                    b++;
+                }
+            }
+        } else if (g < nE + nT) {
+            const uint32_t k = g - nE, l = 2 + (k >> 1), half = k & 1;
+            if (half == 1 && (tnode || tprom)) {
+                uint32_t(*dst)[9] = (l & 1) ? NA : NB;  // level l: odd levels in A
+#pragma unroll
+                for (int q = 0; q < 8; q++) dst[tdst][q] = tnode ? s.h[q] : lf0[q];
+            }
+        }
+    }
+    TXB_PROBE(6);
+    // compare + results (tx.go:623-627)
+    int32_t stv = MH_OK;
+    uint32_t a[8];
+    copy8(a, s.h);
+    const uint64_t t = T0 + tid;
+    uint32_t eh[8];
+    if (actH) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) eh[q] = fin[rH][q];
+        const uint8_t *ap = STAGED ? sm + (alh_off[t] - lo) : buf + alh_off[t];
+        uint32_t xx = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) xx |= bswap(rd_le32(ap + 4 * q)) ^ a[q];
+        stv = xx ? MH_ERR_CORRUPTED_DATA : MH_OK;
+        status[t] = stv;
+        store_digest(eh_out + t * 32, eh);
+        store_digest(alh_out + t * 32, a);
+    }
+    // header words of record tid (before the stage is overwritten)
+    uint64_t hw[17];
+    if (actH) {
+        const uint32_t ver = info[rH * 4 + 0], ml = info[rH * 4 + 1], nent = info[rH * 4 + 2];
+#pragma unroll
+        for (int q = 0; q < 3; q++) hw[q] = rd_be64(rpH + 8 * q);
+#pragma unroll
+        for (int q = 0; q < 8; q++) hw[3 + q] = rd_raw64(rpH + 24 + 8 * q);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            hw[11 + q] = (uint64_t)bswap(eh[2 * q]) | ((uint64_t)bswap(eh[2 * q + 1]) << 32);
+        hw[15] = (uint64_t)ver | ((uint64_t)nent << 32);
+        hw[16] = ver ? (uint64_t)ml | ((uint64_t)(uint32_t)(rec_off[t] + 92) << 32) : 0;
+    }
+    __syncthreads();  // the stage is free: results staged there
+    uint64_t *hst = reinterpret_cast<uint64_t *>(sm);     // rpw x 17 header words
+    uint32_t *ast = reinterpret_cast<uint32_t *>(sm + (uint32_t)rpw * 136);  // rpw x 8 Alh words
+    uint32_t *sst = ast + rpw * 8;                         // rpw statuses
+    if (actH) {
+#pragma unroll
+        for (int q = 0; q < 17; q++) hst[tid * 17 + q] = hw[q];
+#pragma unroll
+        for (int q = 0; q < 8; q++) ast[tid * 8 + q] = bswap(a[q]);
+        sst[tid] = (uint32_t)stv;
+    }
+    __syncthreads();
+    TXB_PROBE(7);
+    uint64_t *hd = ho.hdrs ? ho.hdrs + T0 * 17 : reinterpret_cast<uint64_t *>(hdrs) + T0 * 17;
+    if (ho.hdrs && ho.eh_only) {
+        for (uint32_t k = tid; k < nrec * 4; k += 256) {
+            const uint32_t rec = k >> 2, j = 11 + (k & 3);
+            hd[rec * 17 + j] = hst[rec * 17 + j];
+        }
+    } else {
+        for (uint32_t k = tid; k < nrec * 17; k += 256) hd[k] = hst[k];
+    }
+    if (ho.alh)
+        for (uint32_t k = tid; k < nrec * 8; k += 256) ho.alh[T0 * 8 + k] = ast[k];
+    if (ho.status)
+        for (uint32_t k = tid; k < nrec; k += 256) ho.status[T0 + k] = sst[k];
+    if (fence && (ho.status || ho.alh || ho.hdrs)) __threadfence_system();
+    TXB_PROBE(8);
+    TXB_PROBE(9);
+    if (probe && tid == 0) probe[(uint64_t)blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#undef TXB_PROBE
+}
+
+hipError_t launch_txlog_blk(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                            const uint64_t *rec_off, const uint64_t *alh_off,
+                            const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
+                            uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
+                            uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off) {
+    if (!ntx) return hipSuccess;
+    if (wmax > 64 || ((uintptr_t)ho.hdrs & 7) || ((uintptr_t)ho.alh & 3) || ((uintptr_t)ho.status & 3))
+        return hipErrorInvalidValue;
+    int lgp = 1;
+    while ((1ull << lgp) < wmax) lgp++;
+    const int rpw = std::min(128, 512 >> lgp);
+    // the widest workgroup's records (+ alignment and over-read pad), in the
+    // LDS-DMA's whole passes of 64 pieces
+    uint64_t span = 0;
+    for (uint64_t t0 = 0; t0 < ntx; t0 += rpw) {
+        const uint64_t tl = std::min<uint64_t>(ntx, t0 + rpw) - 1;
+        span = std::max<uint64_t>(span, h_alh_off[tl] + 32 + 96 - (h_rec_off[t0] & ~15ull));
+    }
+    const uint64_t sb = (span + 1023) & ~1023ull;
+    // staged when the workgroup's LDS leaves room for two per CU (MH_TXLOG_STAGE_MAX
+    // bytes, read per call: tests force the HBM path with 0)
+    const char *sm = getenv("MH_TXLOG_STAGE_MAX");
+    const uint64_t smax = sm ? strtoull(sm, nullptr, 10) : (64u << 10);
+    const bool staged = sb <= smax && txb_lds((uint32_t)std::min<uint64_t>(sb, 1u << 20), lgp, rpw).total <= (80u << 10);
+    const uint32_t sbytes = staged ? (uint32_t)sb : 0;
+    const size_t sh = txb_lds(sbytes, lgp, rpw).total;
+    static const int fence = [] {
+        const char *e = getenv("MH_TXLOG_FENCE");
+        return e && atoi(e) ? 1 : 0;
+    }();
+    static const bool attr = [] {
+        const int mx = 160 << 10;
+        hipFuncSetAttribute((const void *)k_txlog_blk<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_blk<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attr;
+    TimerScope ts(tm, "txlog_blk", st);
+    const dim3 grid((unsigned)((ntx + rpw - 1) / rpw)), blk(256);
+    uint64_t *probe = txlog_probe_slot(grid.x);
+    if (staged)
+        hipLaunchKernelGGL(k_txlog_blk<true>, grid, blk, sh, st, ntx, buf, rec_off, alh_off, leaf_off,
+                           hdrs, eh_out, alh_out, status, ho, lgp, rpw, sbytes, fence, probe);
+    else
+        hipLaunchKernelGGL(k_txlog_blk<false>, grid, blk, sh, st, ntx, buf, rec_off, alh_off, leaf_off,
+                           hdrs, eh_out, alh_out, status, ho, lgp, rpw, sbytes, fence, probe);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- a14, lanes per record
+// The same a14 check with every record on L = 1, 2 or 4 lanes (k_txlog_lanes<LGL>):
+// lane i of a record takes its entries [i EP, (i+1) EP) (EP = P / L, P = the
+// widest tx rounded up to a power of two) and builds their subtree itself --
+// entry digest (tx.go:690-731) and leaf (htree.go:79-83) per entry, pushed on
+// a per-lane stack in LDS; after the c-th leaf, tz(c) merges
+// SHA256(0x01 || left || right), and at the end the stack folded from the
+// right, which is htree's pairing with the odd last node promoted
+// (htree.go:85-110): an aligned block of 2^k leaves of a tree is the htree of
+// its leaves (SURVEY.md finding 3).  The L lane roots of a record are then
+// paired log2 L more levels, and the record's first lane hashes innerHash
+// (tx.go:249-302) and Alh (tx.go:307-319) and compares.  No staging, no
+// workgroup barrier before the final stores: a lane is busy on its own record
+// for all but the log2 L combine levels and the four innerHash + Alh
+// compressions, so with L = 1 every lane of a wave works in every compression
+// slot (uniform records).  Against k_txlog_wave (one wave per 64 / L' records,
+// L' = P / 2 lanes per record: its tree levels and the innerHash + Alh leave
+// half of the wave's lanes idle, VALU active 0.51) the lanes stay busy; the
+// price is latency: a record is ~66 dependent compressions on L = 1 lane, so
+// the launch picks L from the record count (few records: more lanes).
+constexpr int kTxlStackPad = 9;  // words per stack slot (8 + 1: bank spread)
+
+__device__ __forceinline__ void txl_node_first(const uint32_t l[8], const uint32_t r[8], uint32_t w[16]) {
+    w[0] = 0x01000000u | (l[0] >> 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[j] = __builtin_amdgcn_alignbit(l[j - 1], l[j], 8);
+    w[8] = __builtin_amdgcn_alignbit(l[7], r[0], 8);
+#pragma unroll
+    for (int j = 1; j < 8; j++) w[8 + j] = __builtin_amdgcn_alignbit(r[j - 1], r[j], 8);
+}
+
+__device__ unsigned g_txl_viol = 0;  // MH_TXLOG_LANES_CHECK: reported violations
+
+template <int LGL, bool CHK>
+__global__ __launch_bounds__(256) void k_txlog_lanes(
+    uint64_t ntx, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ rec_off,
+    const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
+    MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ eh_out, uint8_t *__restrict__ alh_out,
+    int32_t *__restrict__ status, TxlogHostOut ho, int lgp, int dep, int fence, uint64_t blen_) {
+    extern __shared__ uint4 lds[];
+    constexpr int L = 1 << LGL, R = 64 >> LGL;
+    uint32_t *stk = reinterpret_cast<uint32_t *>(lds);  // [dep][256][9]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r = lane >> LGL, i = lane & (L - 1);
+    const int EP = (1 << lgp) >> LGL;  // entries per lane (>= 1)
+    const uint64_t TW = ((uint64_t)blockIdx.x * 4 + wv) * R;  // the wave's first record
+    const uint64_t T0 = (uint64_t)blockIdx.x * 4 * R;        // the workgroup's
+    const uint64_t t = TW + r;
+    const bool act = t < ntx;
+    auto slot = [&](int d) -> uint32_t * { return stk + ((uint32_t)d * 256 + tid) * kTxlStackPad; };
+    // CHK (MH_TXLOG_LANES_CHECK=1, diagnosis): every read range of the log
+    // checked against [buf, buf + len + 256); a range outside is reported and
+    // read from buf instead
+    auto ok_ = [&](const uint8_t *p, uint32_t n, int tag) -> const uint8_t * {
+        if (!CHK) return p;
+        const int64_t o = (int64_t)(p - buf);
+        if (o >= 0 && (uint64_t)o + n <= blen_ + 256) return p;
+        if (atomicAdd(&g_txl_viol, 1u) < 16)
+            printf("txlog_lanes OOB tag=%d blk=%u tid=%d t=%llu off=%lld n=%u len=%llu\n", tag,
+                   blockIdx.x, tid, (unsigned long long)t, (long long)o, n, (unsigned long long)blen_);
+        return buf;
+    };
+    // ---- header (tx.go:419-518) and this lane's first entry (tx.go:578-585)
+    const uint8_t *rp = act ? buf + rec_off[t] : buf;
+    uint32_t ver = 0, ml = 0, nent = 0, w = 0, q = 0;
+    if (act) {
+        ver = rd_be16(ok_(rp + 88, 4, 1));
+        if (ver == 0) {
+            nent = rd_be16(ok_(rp + 90, 2, 2));
+            q = 92;
+        } else {
+            ml = rd_be16(ok_(rp + 90, 2, 2));
+            nent = bswap(rd_le32(ok_(rp + 92 + ml, 8, 3)));
+            q = 96 + ml;
+        }
+        w = (uint32_t)(leaf_off[t + 1] - leaf_off[t]);
+    }
+    const uint32_t j0 = (uint32_t)i * EP;
+    const uint32_t ne = act && w > j0 ? min((uint32_t)EP, w - j0) : 0;  // this lane's entries
+    // skip the j0 entries of the lanes to the left (lengths validated by the
+    // host hop). Only a lane with entries walks: written as `j < j0 && j < w`
+    // for every lane, the compiler dropped the `j < w` bound (q is dead when
+    // ne == 0) and lanes past the record's last entry walked off the log.
+    if (ne) {
+        for (uint32_t j = 0; j < j0; j++) {
+            const uint32_t m = rd_be16(ok_(rp + q, 2, 4));
+            q += 48 + m + rd_be16(ok_(rp + q + 2 + m, 2, 5));
+        }
+    }
+    // ---- 1. this lane's subtree: entries, leaves, merges, the final fold
+    State s;
+    s.init();
+    uint32_t mode = ne ? 0u : 5u;  // 0 digest blocks, 1 leaf, 2 merge / fold (first block), 3 its tail, 5 done
+    uint32_t ej = 0, b = 0, nb = 0, la = 0, c = 0, sp = 0, rt7 = 0;
+    bool fold = false;
+    const uint8_t *mp = rp;
+    auto entry_setup = [&]() {  // entry ej of this lane at offset q
+        const uint8_t *er = rp + q;
+        const uint32_t m = rd_be16(ok_(er, 2, 6)), k = rd_be16(ok_(er + 2 + m, 2, 7));
+        mp = ver == 1 ? er : er + 4 + m;  // tx.go:690-731
+        la = ver == 1 ? 4 + m + k : k;
+        nb = (la + 32 + 8) / 64 + 1;
+        q += 48 + m + k;
+        b = 0;
+    };
+    if (ne) entry_setup();
+#pragma unroll 1
+    while (__builtin_amdgcn_ballot_w64(mode != 5)) {
+        uint32_t wv16[16];
+        bool on = true, tail = false;
+        if (mode == 0) {
+            if (b == 0) s.init();
+            {
+                const uint8_t *p0 = mp - ((uintptr_t)mp & 3) + 64 * b;
+                skip12_block<false>(ok_(p0, 80, 8) == p0 ? mp : buf + 4, la, b, nb, wv16);
+            }
+        } else if (mode == 1) {
+            wv16[0] = s.h[0] >> 8;
+#pragma unroll
+            for (int j = 1; j < 8; j++) wv16[j] = __builtin_amdgcn_alignbit(s.h[j - 1], s.h[j], 8);
+            wv16[8] = (s.h[7] << 24) | 0x00800000u;
+#pragma unroll
+            for (int j = 9; j < 15; j++) wv16[j] = 0;
+            wv16[15] = 33u * 8u;
+            s.init();
+        } else if (mode == 2) {  // pop right and left, SHA256(0x01 || left || right)
+            uint32_t lf[8], rg[8];
+            const uint32_t *pl = slot(sp - 2), *pr = slot(sp - 1);
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) {
+                lf[q2] = pl[q2];
+                rg[q2] = pr[q2];
+            }
+            rt7 = rg[7];
+            s.init();
+            txl_node_first(lf, rg, wv16);
+        } else if (mode == 3) {
+            tail = true;
+        } else {
+            on = false;
+        }
+        if (on) {
+            if (tail)
+                compress_node_tail_g(s, rt7);
+            else
+                compress(s, wv16);
+        }
+        // bookkeeping after the block
+        if (mode == 0) {
+            if (++b == nb) mode = 1;
+        } else if (mode == 1 || mode == 3) {
+            uint32_t *d = slot(mode == 1 ? sp : sp - 2);  // a leaf is pushed; a node replaces its children
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) d[q2] = s.h[q2];
+            if (mode == 1) {
+                sp++;
+                c++;
+                ej++;
+            } else {
+                sp--;
+            }
+            // next: the merges the c-th leaf owes (tz(c): the stack holds one
+            // perfect subtree per set bit of c once they are done), the next
+            // entry, or the fold
+            if (!fold && sp > (uint32_t)__builtin_popcount(c)) {
+                mode = 2;  // two perfect subtrees of one size on top: merge
+            } else if (ej < ne) {
+                entry_setup();
+                mode = 0;
+            } else if (sp >= 2) {
+                fold = true;  // right edge: fold the stack from the right
+                mode = 2;
+            } else {
+                mode = 5;
+            }
+        } else if (mode == 2) {
+            mode = 3;
+        }
+    }
+    // ---- 2. the record's L lane roots paired (htree.go:85-110), via LDS
+    // (slot 0 of each lane; a lane without entries holds nothing)
+#pragma unroll 1
+    for (int l = 0; l < LGL; l++) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t sft = 1u << l;
+        const bool me = act && (i & (2 * sft - 1)) == 0 && (uint32_t)(i + sft) * EP < w;
+        uint32_t wv16[16];
+        if (me) {
+            uint32_t lf[8], rg[8];
+            const uint32_t *pl = slot(0), *pr = stk + (((uint32_t)0 * 256 + tid + sft) * kTxlStackPad);
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) {
+                lf[q2] = pl[q2];
+                rg[q2] = pr[q2];
+            }
+            rt7 = rg[7];
+            s.init();
+            txl_node_first(lf, rg, wv16);
+            compress(s, wv16);
+            compress_node_tail_g(s, rt7);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (me) {
+            uint32_t *d = slot(0);
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) d[q2] = s.h[q2];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- 3. innerHash + Alh on the record's first lane
+    const bool head = act && i == 0;
+    uint32_t eh[8], a[8];
+    if (head) {
+        if (w == 0) {
+            load_digest(kEmptyRootDev, eh);  // SHA256(nil), htree.go:73-77
+        } else {
+            const uint32_t *p0 = slot(0);
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) eh[q2] = p0[q2];
+        }
+    }
+    const uint32_t blen = ver ? 8 + ml : 4, mlen = 80 + blen;
+    const uint32_t nbi = head ? (mlen + 8) / 64 + 1 : 0;
+    const uint32_t nH = wave_max_u32(head ? nbi + 2 : 0);
+#pragma unroll 1
+    for (uint32_t k = 0; k < nH; k++) {
+        uint32_t wv16[16];
+        const bool on = head && k < nbi + 2;
+        if (on) {
+            if (k < nbi) {  // ts || version || md part || Eh || blTxID || blRoot
+                if (k == 0) s.init();
+#pragma unroll 4
+                for (int jw = 0; jw < 16; jw++) {
+                    uint32_t v32 = 0;
+                    if (jw == 15 && k + 1 == nbi) {
+                        v32 = mlen * 8;  // the bit length
+                    } else {
+#pragma unroll
+                        for (int bb = 0; bb < 4; bb++) {
+                            const uint32_t kk = 64 * k + 4 * jw + bb;
+                            uint32_t v;
+                            if (kk < 8) v = *ok_(rp + 8 + kk, 1, 9);
+                            else if (kk < 8 + blen) v = *ok_(rp + 80 + kk, 1, 10);
+                            else if (kk < 40 + blen) {
+                                const uint32_t o = kk - 8 - blen;
+                                v = (eh[o >> 2] >> (24 - 8 * (o & 3))) & 0xffu;
+                            } else if (kk < mlen) v = *ok_(rp + kk - 24 - blen, 1, 11);
+                            else v = kk == mlen ? 0x80u : 0u;
+                            v32 = v32 << 8 | v;
+                        }
+                    }
+                    wv16[jw] = v32;
+                }
+            } else if (k == nbi) {  // BE64 id || prevAlh || innerHash[0:24]
+                copy8(a, s.h);      // (a: the innerHash until the Alh is done)
+                s.init();
+                const uint64_t id = rd_be64(ok_(rp, 16, 12));
+                wv16[0] = (uint32_t)(id >> 32);
+                wv16[1] = (uint32_t)id;
+#pragma unroll
+                for (int q2 = 0; q2 < 8; q2++) wv16[2 + q2] = bswap(rd_le32(ok_(rp + 56 + 4 * q2, 8, 13)));
+#pragma unroll
+                for (int q2 = 0; q2 < 6; q2++) wv16[10 + q2] = a[q2];
+            } else {
+                wv16[0] = a[6];
+                wv16[1] = a[7];
+                wv16[2] = 0x80000000u;
+#pragma unroll
+                for (int q2 = 3; q2 < 15; q2++) wv16[q2] = 0;
+                wv16[15] = 72u * 8u;
+            }
+            compress(s, wv16);
+        }
+    }
+    copy8(a, s.h);
+    int32_t stv = MH_OK;
+    uint64_t hw[17];
+    if (head) {  // tx.go:623-627
+        const uint8_t *ap = ok_(buf + alh_off[t], 40, 14);
+        uint32_t xx = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < 8; q2++) xx |= bswap(rd_le32(ap + 4 * q2)) ^ a[q2];
+        stv = xx ? MH_ERR_CORRUPTED_DATA : MH_OK;
+        status[t] = stv;
+        store_digest(eh_out + t * 32, eh);
+        store_digest(alh_out + t * 32, a);
+#pragma unroll
+        for (int q2 = 0; q2 < 3; q2++) hw[q2] = rd_be64(ok_(rp + 8 * q2, 16, 15));
+#pragma unroll
+        for (int q2 = 0; q2 < 8; q2++) hw[3 + q2] = rd_raw64(ok_(rp + 24 + 8 * q2, 16, 16));
+#pragma unroll
+        for (int q2 = 0; q2 < 4; q2++)
+            hw[11 + q2] = (uint64_t)bswap(eh[2 * q2]) | ((uint64_t)bswap(eh[2 * q2 + 1]) << 32);
+        hw[15] = (uint64_t)ver | ((uint64_t)nent << 32);
+        hw[16] = ver ? (uint64_t)ml | ((uint64_t)(uint32_t)(rec_off[t] + 92) << 32) : 0;
+    }
+    // ---- 4. the workgroup's records out as contiguous runs (the stack is free)
+    __syncthreads();
+    const uint32_t RW = 4 * R;  // records per workgroup
+    uint64_t *hst = reinterpret_cast<uint64_t *>(lds);
+    uint32_t *ast = reinterpret_cast<uint32_t *>(hst + RW * 17);
+    uint32_t *sst = ast + RW * 8;
+    const uint32_t rw = (uint32_t)wv * R + r;  // this record in the workgroup
+    if (head) {
+#pragma unroll
+        for (int q2 = 0; q2 < 17; q2++) hst[rw * 17 + q2] = hw[q2];
+#pragma unroll
+        for (int q2 = 0; q2 < 8; q2++) ast[rw * 8 + q2] = bswap(a[q2]);
+        sst[rw] = (uint32_t)stv;
+    }
+    __syncthreads();
+    const uint64_t nb_ = T0 < ntx ? min((uint64_t)RW, ntx - T0) : 0;
+    uint64_t *hd = ho.hdrs ? ho.hdrs + T0 * 17 : reinterpret_cast<uint64_t *>(hdrs) + T0 * 17;
+    if (ho.hdrs && ho.eh_only) {
+        for (uint32_t k = tid; k < nb_ * 4; k += 256) {
+            const uint32_t rec = k >> 2, j = 11 + (k & 3);
+            hd[rec * 17 + j] = hst[rec * 17 + j];
+        }
+    } else {
+        for (uint32_t k = tid; k < nb_ * 17; k += 256) hd[k] = hst[k];
+    }
+    if (ho.alh)
+        for (uint32_t k = tid; k < nb_ * 8; k += 256) ho.alh[T0 * 8 + k] = ast[k];
+    if (ho.status)
+        for (uint32_t k = tid; k < nb_; k += 256) ho.status[T0 + k] = sst[k];
+    if (fence && (ho.status || ho.alh || ho.hdrs)) __threadfence_system();
+}
+
+hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                              const uint64_t *rec_off, const uint64_t *alh_off,
+                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
+                              uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
+                              uint64_t wmax, uint64_t log_len) {
+    if (!ntx) return hipSuccess;
+    if (wmax > 64 || ((uintptr_t)ho.hdrs & 7) || ((uintptr_t)ho.alh & 3) || ((uintptr_t)ho.status & 3))
+        return hipErrorInvalidValue;
+    int lgp = 0;
+    while ((1ull << lgp) < wmax) lgp++;
+    // lanes per record: L = 1 while the launch still has >= 2 waves per SIMD
+    // (2048 waves of 64 records), more lanes for fewer records (latency);
+    // MH_TXLOG_LANES=1|2|4 forces it (read per call)
+    int lgl = ntx >= 2048ull * 64 ? 0 : ntx >= 2048ull * 32 ? 1 : 2;
+    if (const char *e = getenv("MH_TXLOG_LANES")) lgl = atoi(e) >= 4 ? 2 : atoi(e) >= 2 ? 1 : 0;
+    lgl = std::min(lgl, lgp);  // never more lanes than entries
+    const int R = 64 >> lgl;
+    const int dep = std::max(1, lgp - lgl + 1);  // stack depth: log2(EP) + 1
+    const size_t stack = (size_t)dep * 256 * kTxlStackPad * 4;
+    const size_t res = (size_t)4 * R * (17 * 8 + 8 * 4 + 4);
+    const size_t sh = std::max(stack, res);
+    static const int fence = [] {
+        const char *e = getenv("MH_TXLOG_FENCE");
+        return e && atoi(e) ? 1 : 0;
+    }();
+    static const bool attr = [] {
+        const int mx = 160 << 10;
+        hipFuncSetAttribute((const void *)k_txlog_lanes<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_lanes<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_lanes<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_lanes<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_lanes<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        hipFuncSetAttribute((const void *)k_txlog_lanes<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attr;
+    TimerScope ts(tm, "txlog_lanes", st);
+    const dim3 grid((unsigned)((ntx + 4ull * R - 1) / (4ull * R))), blk(256);
+    static const bool chk = [] {
+        const char *e = getenv("MH_TXLOG_LANES_CHECK");
+        return e && atoi(e) != 0;
+    }();
+#define MH_TXL(l_, c_)                                                                             \
+    hipLaunchKernelGGL((k_txlog_lanes<l_, c_>), grid, blk, sh, st, ntx, buf, rec_off, alh_off,   \
+                       leaf_off, hdrs, eh_out, alh_out, status, ho, lgp, dep, fence, log_len)
+    if (chk) {
+        if (lgl == 0) MH_TXL(0, true);
+        else if (lgl == 1) MH_TXL(1, true);
+        else MH_TXL(2, true);
+    } else {
+        if (lgl == 0) MH_TXL(0, false);
+        else if (lgl == 1) MH_TXL(1, false);
+        else MH_TXL(2, false);
+    }
+#undef MH_TXL
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- many trees
 // Level l of a batch of independent htrees.  Item k describes one tree that
 // still has > 1 node at level l-1: its nodes at level l are written at

@@ -146,3 +146,71 @@ class MultiDevice:
             self.handle, version, n, _addr(kb), _addr(ko), _addr(mb), _addr(mo), _addr(vb),
             _addr(vo), _addr(ov), _addr(use), _addr(hv), _addr(lv), _addr(root)))
         return hv[:n], (lv[:levels_len(n)] if want_levels else None), root.tobytes()
+
+    # ---- the PCIe-bound batch paths split over the devices (mh_multi_*)
+    def htree_verify_inclusion_batch(self, leaf, width, term_off, terms, digests, roots):
+        """Raw arrays as mh_htree_verify_inclusion_batch (leaf / width uint64
+        Go-int patterns, CSR term_off, terms (T, 32), digests / roots (n, 32))
+        -> ok[n] bool; proofs split by index over the devices."""
+        leaf = np.ascontiguousarray(leaf, np.uint64)
+        width = np.ascontiguousarray(width, np.uint64)
+        off = np.ascontiguousarray(term_off, np.uint64)
+        terms = np.ascontiguousarray(terms, np.uint8).reshape(-1, 32)
+        if terms.size == 0:
+            terms = np.zeros((1, 32), np.uint8)
+        d = np.ascontiguousarray(digests, np.uint8)
+        r = np.ascontiguousarray(roots, np.uint8)
+        n = leaf.size
+        ok = np.zeros(max(n, 1), np.uint8)
+        N.check(N.load().mh_multi_htree_verify_inclusion_batch(
+            self.handle, n, _addr(leaf), _addr(width), _addr(off), _addr(terms), _addr(d), _addr(r),
+            _addr(ok)))
+        return ok[:n].astype(bool)
+
+    def verify_dual_proof_v2_batch(self, src_hdrs, tgt_hdrs, md_blob, incl, cons, src, tgt,
+                                   src_alh, tgt_alh):
+        """txlayer.verify_dual_proof_v2_batch's arguments -> status[n]; split
+        by index over the devices."""
+        from .txlayer import _blob, _d32, _hdrs, _terms_csr
+        sh, th = _hdrs(src_hdrs), _hdrs(tgt_hdrs)
+        n = sh.size
+        if n == 0:
+            return np.zeros(0, np.int32)
+        mb, ml = _blob(md_blob)
+        io, it = _terms_csr(incl)
+        co, ct = _terms_csr(cons)
+        s = np.asarray(src, np.uint64)
+        t = np.asarray(tgt, np.uint64)
+        sa, ta = _d32(src_alh, n), _d32(tgt_alh, n)
+        st = np.zeros(n, np.int32)
+        N.check(N.load().mh_multi_verify_dual_proof_v2_batch(
+            self.handle, n, _addr(sh), _addr(th), _addr(mb), ml, _addr(io), _addr(it), _addr(co),
+            _addr(ct), _addr(s), _addr(t), _addr(sa), _addr(ta), _addr(st)))
+        return st
+
+    def txlog_validate(self, buf, max_entries: int = 1024, max_key_len: int = 1024,
+                       max_txs=None, out=None):
+        """txlayer.txlog_validate over the devices (mh_multi_txlog_validate:
+        the log cut at record boundaries, every part over its own link) ->
+        (status, ntx, consumed, hdrs, alh, per_tx)."""
+        from .txlayer import TX_HEADER
+        b = np.frombuffer(bytes(buf), np.uint8) if not isinstance(buf, np.ndarray) else buf
+        cap = max(1, b.size // 122 + 1)
+        if max_txs is not None:
+            cap = max(1, min(cap, max_txs))
+        if out is not None:
+            hd, alh, sts = out
+            cap = max(1, min(cap, len(alh), len(sts), len(hd) if hd is not None else cap))
+        else:
+            hd = np.empty(cap, TX_HEADER)
+            alh = np.empty((cap, 32), np.uint8)
+            sts = np.empty(cap, np.int32)
+        ntx, used = C.c_uint64(0), C.c_uint64(0)
+        rc = N.load().mh_multi_txlog_validate(self.handle, _addr(b) if b.size else None, b.size,
+                                              max_entries, max_key_len, cap, C.byref(ntx),
+                                              C.byref(used), _addr(hd) if hd is not None else None,
+                                              _addr(alh), _addr(sts))
+        if rc < 0:
+            N.check(rc)
+        k = ntx.value
+        return rc, k, used.value, (hd[:k] if hd is not None else None), alh[:k], sts[:k]

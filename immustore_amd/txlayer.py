@@ -335,8 +335,12 @@ def pack_document_batch(docs, pinned=False):
 
 def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
                    max_key_len: int = DEFAULT_MAX_KEY_LEN, max_txs: Optional[int] = None,
-                   ctx: Optional[Context] = None, out=None):
+                   ctx: Optional[Context] = None, out=None, dev: Optional[int] = None):
     """-> (status, ntx, consumed, hdrs[ntx] TX_HEADER (Eh rebuilt), alh[ntx,32], per_tx[ntx])
+
+    dev: the device address of the same bytes already resident on the
+    context's device (mh_txlog_validate_resident: no host->device copy; the
+    allocation must extend 256 bytes past the log)
 
     status is the structural error that stopped parsing (0 at a clean end);
     per_tx[k] is 0 or MH_ERR_CORRUPTED_DATA (ALH mismatch).
@@ -361,11 +365,17 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
         alh = np.empty((cap, 32), np.uint8)
         sts = np.empty(cap, np.int32)
     ntx, used = C.c_uint64(0), C.c_uint64(0)
-    rc = N.load().mh_txlog_validate(_ctx(ctx).handle, _addr(b) if b.size else None, b.size,
-                                    max_entries, max_key_len,
-                                    cap if max_txs is None else min(cap, max_txs), C.byref(ntx),
-                                    C.byref(used), _addr(hd) if hd is not None else None,
-                                    _addr(alh), _addr(sts))
+    lim = cap if max_txs is None else min(cap, max_txs)
+    if dev is None:
+        rc = N.load().mh_txlog_validate(_ctx(ctx).handle, _addr(b) if b.size else None, b.size,
+                                        max_entries, max_key_len, lim, C.byref(ntx),
+                                        C.byref(used), _addr(hd) if hd is not None else None,
+                                        _addr(alh), _addr(sts))
+    else:
+        rc = N.load().mh_txlog_validate_resident(
+            _ctx(ctx).handle, _addr(b) if b.size else None, dev, b.size, max_entries, max_key_len,
+            lim, C.byref(ntx), C.byref(used), _addr(hd) if hd is not None else None, _addr(alh),
+            _addr(sts))
     if rc < 0:
         N.check(rc)
     k = ntx.value

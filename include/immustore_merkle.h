@@ -585,6 +585,18 @@ int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entries, uint32
 int mh_txlog_validate(mh_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t max_entries,
                       uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx, uint64_t *consumed,
                       mh_tx_header *hdrs, uint8_t *alh, int32_t *status);
+/* The same check of a log that is ALREADY in device memory -- the caller
+ * re-validating what it just wrote or keeps resident (a scrub of the tx log,
+ * the indexer's readTx of recent txs, embedded/store/indexer.go:570, tx.go:
+ * 388-630): buf is the host copy the record hop parses, dlog (device, on the
+ * context's device) the same len bytes, read by the kernels in place -- no
+ * host->device copy.  The device allocation holding dlog must extend at least
+ * 256 bytes past dlog + len (checked: MH_ERR_ILLEGAL_ARGUMENTS).  Outputs and
+ * statuses as mh_txlog_validate. */
+int mh_txlog_validate_resident(mh_ctx *ctx, const uint8_t *buf, const uint8_t *dlog, uint64_t len,
+                               uint32_t max_entries, uint32_t max_key_len, uint64_t max_txs,
+                               uint64_t *ntx, uint64_t *consumed, mh_tx_header *hdrs,
+                               uint8_t *alh, int32_t *status);
 
 /* ------------------------------------------------------------ commit path */
 /* the hashing of ImmuStore.precommit / preCommitWith
@@ -753,6 +765,33 @@ int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *shard_bits,
  * payloads, room for its new digests).  peaks (host) on EVERY rank when
  * n0 > 0.  A rank past the plan's ranges (r >= nranges) does nothing but
  * still joins the all-gather.  Asynchronous on the context stream. */
+/* The PCIe-bound batch paths over the K devices: the batch is cut into K
+ * contiguous parts -- by index for proofs, at record boundaries (nearly equal
+ * bytes) for a tx log -- and part d runs the single-context call on device d
+ * from its own thread, over its own PCIe link; outputs land side by side,
+ * byte-equal to one single-context call over the whole batch (K = 1 IS that
+ * call).  Arguments, statuses and outputs as mh_htree_verify_inclusion_batch
+ * (htree.go:166-195), mh_verify_dual_proof_v2_batch (verification.go:303-372)
+ * and mh_txlog_validate (tx.go:388-630; the replay of
+ * immustore.go:1198-1223 and the indexer's readTx, indexer.go:570: every
+ * record carries its prevAlh, so the parts are independent).  For the tx log
+ * the host hop finds the record boundaries once first (mh_txlog_scan's status
+ * is the call's); a header's md_off stays relative to buf. */
+int mh_multi_htree_verify_inclusion_batch(mh_multi *m, uint64_t n, const uint64_t *leaf,
+                                          const uint64_t *width, const uint64_t *term_off,
+                                          const uint8_t *terms, const uint8_t *digests,
+                                          const uint8_t *roots, uint8_t *ok);
+int mh_multi_verify_dual_proof_v2_batch(mh_multi *m, uint64_t n, const mh_tx_header *src_hdr,
+                                        const mh_tx_header *tgt_hdr, const uint8_t *md_blob,
+                                        uint64_t md_blob_len, const uint64_t *incl_off,
+                                        const uint8_t *incl_terms, const uint64_t *cons_off,
+                                        const uint8_t *cons_terms, const uint64_t *src,
+                                        const uint64_t *tgt, const uint8_t *src_alh,
+                                        const uint8_t *tgt_alh, int32_t *status);
+int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                            uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx,
+                            uint64_t *consumed, mh_tx_header *hdrs, uint8_t *alh,
+                            int32_t *status);
 int mh_ahtree_range_sizes(uint64_t n0, uint64_t total, int ndev, uint64_t *send_bytes,
                           uint64_t *work_bytes);
 int mh_dev_ahtree_range_local(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,

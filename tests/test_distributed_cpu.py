@@ -220,3 +220,21 @@ def test_bench_cabi_mode_routing():
     r = subprocess.run([sys.executable, bench, "--api", "cabi", "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=240, env=env2)
     assert r.returncode != 0 and "one process" in r.stderr, r.stderr[-2000:]
+
+
+def test_bench_cabi_txlog_routing():
+    """--api cabi --config txlog (mh_multi_txlog_validate over N devices, VERDICT
+    r04 next #4) refuses with fewer than N devices before touching any, and the
+    torch.distributed mode refuses --config txlog."""
+    import subprocess
+    import sys
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bench = os.path.join(root_dir, "bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, bench, "--api", "cabi", "--config", "txlog", "--gpus", "2",
+                        "--steps", "1"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0 and "device(s) visible" in r.stderr, r.stderr[-2000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    r = subprocess.run([sys.executable, bench, "--config", "txlog", "--steps", "1"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0 and "--api cabi" in r.stderr, r.stderr[-2000:]

@@ -363,3 +363,103 @@ def test_multi_ragged_build_vs_oracle(m, orc, devices):
         assert root == orc.sha256(b"")
     finally:
         md.close()
+
+
+# ------------------------------------------------- PCIe-bound batch paths, split
+_SPLIT_DEVICES = [[0], [0, 0], [0, 0, 0, 0], [0] * 8]
+
+
+@pytest.mark.parametrize("devices", _SPLIT_DEVICES)
+def test_multi_txlog_validate_vs_single_and_oracle(m, orc, fixtures, devices):
+    """mh_multi_txlog_validate (the log cut at record boundaries, part d on
+    device d): status, count, consumed bytes, every header (md_off relative to
+    the whole log), Alh and per-tx status byte-equal to one mh_txlog_validate
+    call and to the oracle -- synthetic logs with metadata and mixed versions,
+    corrupted records, a log cut inside a record (structural error), the
+    Go-written fixture log (tx.go:388-630)."""
+    from immustore_amd.multi import MultiDevice
+    from tx_util import _synthetic_txlog
+    rng = np.random.default_rng(len(devices))
+    logs = [_synthetic_txlog(rng, 700, orc, max_entries=16),
+            _synthetic_txlog(rng, 500, orc, max_entries=64)]
+    bad = bytearray(logs[0])
+    for p in rng.integers(0, len(bad), 30):
+        bad[int(p)] ^= 0x20
+    logs += [bytes(bad), logs[1][:len(logs[1]) * 2 // 3],
+             bytes.fromhex(fixtures["long_linear_proof"]["txlog"]), b""]
+    ctx = m.Context(0)
+    md = MultiDevice(devices)
+    try:
+        for k, raw in enumerate(logs):
+            single = m.txlog_validate(raw, ctx=ctx)
+            got = md.txlog_validate(raw)
+            assert got[:3] == single[:3], (devices, k)
+            assert np.array_equal(got[3], single[3]) and np.array_equal(got[4], single[4])
+            assert np.array_equal(got[5], single[5]), (devices, k)
+            o = orc.txlog_validate(raw)
+            assert got[:3] == (o[0], o[1], o[2]) and np.array_equal(got[4], o[3][:got[1]])
+            assert list(got[5]) == list(o[4][:got[1]])
+    finally:
+        md.close()
+        ctx.close()
+
+
+@pytest.mark.parametrize("devices", _SPLIT_DEVICES)
+def test_multi_verify_batches_vs_single_and_oracle(m, orc, fixtures, devices):
+    """mh_multi_htree_verify_inclusion_batch and
+    mh_multi_verify_dual_proof_v2_batch, split by index: the same verdicts as
+    one single-context call and the oracle -- 3001 htree proofs over a 5000-leaf
+    tree (10 % tampered) and every fixture DualProofV2 case with tampered
+    variants (htree.go:166-195, verification.go:303-372)."""
+    from immustore_amd import txlayer
+    from immustore_amd.multi import MultiDevice
+    from tx_util import headers_from_fixture
+    rng = np.random.default_rng(3)
+    W, n = 5000, 3001
+    dig = orc.fill_random(W * 32, 41).reshape(W, 32)
+    lv, root = orc.htree_build(dig)
+    leaf = rng.integers(0, W, n)
+    proofs = [orc.htree_inclusion_proof(lv, W, int(i))[1] for i in leaf]
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(p) for p in proofs])
+    terms = np.concatenate(proofs)
+    tamper = rng.random(n) < 0.1
+    digs = dig[np.where(tamper, (leaf + 1) % W, leaf)]
+    roots = np.tile(np.frombuffer(root, np.uint8), (n, 1))
+    want = np.array([orc.htree_verify_inclusion(int(leaf[p]), W, proofs[p], digs[p], root)
+                     for p in range(n)])
+    assert (want == ~tamper).all()
+    ctx = m.Context(0)
+    md = MultiDevice(devices)
+    try:
+        ok = md.htree_verify_inclusion_batch(leaf.astype(np.uint64), np.full(n, W, np.uint64), off,
+                                             terms, digs, roots)
+        assert np.array_equal(ok, want), devices
+        for name, fx in fixtures.items():
+            recs, blob, alhs = headers_from_fixture(fx["txs"])
+            S, T, I, Cn, SA, TA = [], [], [], [], [], []
+            for c in fx["dual_v2"]:
+                for variant in range(3):
+                    ii = [bytes.fromhex(x) for x in c["incl"]]
+                    cc = [bytes.fromhex(x) for x in c["cons"]]
+                    if variant == 1 and ii:
+                        ii[0] = bytes([ii[0][0] ^ 1]) + ii[0][1:]
+                    if variant == 2 and cc:
+                        cc[-1] = bytes([cc[-1][0] ^ 1]) + cc[-1][1:]
+                    S.append(c["src"])
+                    T.append(c["tgt"])
+                    I.append(ii)
+                    Cn.append(cc)
+                    SA.append(alhs[c["src"] - 1])
+                    TA.append(alhs[c["tgt"] - 1])
+            SH = np.array([recs[s - 1] for s in S])
+            TH = np.array([recs[t - 1] for t in T])
+            single = txlayer.verify_dual_proof_v2_batch(SH, TH, blob, I, Cn, S, T, SA, TA, ctx)
+            got = md.verify_dual_proof_v2_batch(SH, TH, blob, I, Cn, S, T, SA, TA)
+            assert np.array_equal(got, single), (devices, name)
+            exp = [orc.verify_dual_proof_v2(SH[p], TH[p], blob, I[p], Cn[p], S[p], T[p], SA[p], TA[p])
+                   for p in range(len(S))]
+            assert list(got) == exp, (devices, name)
+    finally:
+        md.close()
+        ctx.close()

@@ -642,8 +642,11 @@ def _record_heads(raw, n):
 @pytest.mark.parametrize("max_entries", [1, 2, 3, 5, 8, 16, 17, 40, 64])
 def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries):
     """k_txlog_wave (one wave per 64 / L records, L lanes per record: every
-    lane-count the widest tx can pick) with the records staged in LDS and
-    read from HBM, against the workgroup kernel (MH_TXLOG_KERNEL=group), the
+    lane-count the widest tx can pick), k_txlog_blk (every phase spread over
+    the workgroup: every records-per-workgroup shape) and k_txlog_lanes (1, 2
+    and 4 lanes per record, each lane's subtree serial) with the records
+    staged in LDS and read from HBM, against the round-3 workgroup kernel
+    (MH_TXLOG_KERNEL=group), the
     oracle and the record heads parsed in Python: headers (every field, Eh
     included), Alh and per-tx statuses, clean and with corrupted records,
     with pageable and pinned outputs."""
@@ -661,11 +664,14 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
     for buf in (raw, bytes(bad)):
         o = orc.txlog_validate(buf)
         res = {}
-        for kern, smax in (("group", None), ("wave", None), ("wave", "0")):
+        for kern, smax in (("group", None), ("wave", None), ("wave", "0"), ("blk", None),
+                           ("blk", "0"), ("lanes", "L1"), ("lanes", "L2"), ("lanes", "L4")):
             monkeypatch.setenv("MH_TXLOG_KERNEL", kern)
-            if smax is None:
-                monkeypatch.delenv("MH_TXLOG_STAGE_MAX", raising=False)
-            else:
+            monkeypatch.delenv("MH_TXLOG_STAGE_MAX", raising=False)
+            monkeypatch.delenv("MH_TXLOG_LANES", raising=False)
+            if smax is not None and smax.startswith("L"):
+                monkeypatch.setenv("MH_TXLOG_LANES", smax[1:])
+            elif smax is not None:
                 monkeypatch.setenv("MH_TXLOG_STAGE_MAX", smax)
             for out in (None, pin):
                 a = m.txlog_validate(buf, ctx=ctx, out=out)
@@ -683,3 +689,56 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
                        int(h["md_len"]), int(h["md_off"]))
                 assert got == x
     monkeypatch.delenv("MH_TXLOG_KERNEL", raising=False)
+    monkeypatch.delenv("MH_TXLOG_LANES", raising=False)
+
+
+@pytest.mark.parametrize("kern", ["wave", "blk", "lanes"])
+def test_txlog_validate_resident_vs_host_path(m, ctx, orc, monkeypatch, kern):
+    """mh_txlog_validate_resident (the log already in HBM: scrub / re-validate
+    of what was just written, one group, no copy) equals the copying call and
+    the oracle -- clean and corrupted logs, the Go-written fixture log, pinned
+    and pageable outputs; a device allocation ending less than 256 bytes past
+    the log, or a host pointer, is refused."""
+    import ctypes as C
+    import torch
+    from immustore_amd import _native as N
+    from immustore_amd.txlayer import TX_HEADER
+    monkeypatch.setenv("MH_TXLOG_KERNEL", kern)
+    rng = np.random.default_rng(7)
+    logs = [_synthetic_txlog(rng, 900, orc, max_entries=16),
+            _synthetic_txlog(rng, 300, orc, max_entries=64)]
+    bad = bytearray(logs[0])
+    for p in rng.integers(0, len(bad), 20):
+        bad[int(p)] ^= 0x08
+    logs.append(bytes(bad))
+    cap = 1000
+    pin = (torch.empty(cap * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy().view(TX_HEADER),
+           torch.empty(cap * 32, dtype=torch.uint8).pin_memory().numpy().reshape(cap, 32),
+           torch.empty(cap, dtype=torch.int32).pin_memory().numpy())
+    for raw in logs:
+        d = torch.zeros(len(raw) + 256, dtype=torch.uint8, device="cuda")
+        d[:len(raw)] = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        o = orc.txlog_validate(raw)
+        want = m.txlog_validate(raw, ctx=ctx)
+        for out in (None, pin):
+            got = m.txlog_validate(raw, ctx=ctx, out=out, dev=d.data_ptr())
+            assert (got[0], got[1], got[2]) == (o[0], o[1], o[2])
+            assert np.array_equal(got[4], o[3]) and list(got[5]) == list(o[4])
+            assert np.array_equal(got[3], want[3][:want[1]])
+    L = N.load()
+    raw = logs[0]
+    p = C.c_void_p()
+    size = (len(raw) + 65535) & ~65535
+    N.check(L.mh_dev_alloc(ctx.handle, size, C.byref(p)))
+    try:
+        hb = np.frombuffer(raw, np.uint8)
+        ntx, used = C.c_uint64(), C.c_uint64()
+        alh = np.zeros((cap, 32), np.uint8)
+        sts = np.zeros(cap, np.int32)
+        args = lambda dp: (ctx.handle, hb.ctypes.data, dp, len(raw), 1024, 1024, cap, C.byref(ntx),  # noqa: E731
+                           C.byref(used), None, alh.ctypes.data, sts.ctypes.data)
+        assert L.mh_txlog_validate_resident(*args(p.value + size - len(raw))) == N.MH_ERR_ILLEGAL_ARGUMENTS
+        assert L.mh_txlog_validate_resident(*args(hb.ctypes.data)) == N.MH_ERR_ILLEGAL_ARGUMENTS
+    finally:
+        L.mh_dev_free(ctx.handle, p.value)

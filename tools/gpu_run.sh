@@ -12,6 +12,7 @@
 #   corrupt          bench.py with MH_BENCH_CORRUPT=0: must exit 1 (root check)
 #   corrupt_cabi     the same through --api cabi
 #   c3cabi           bench.py --api cabi --config c3 (replay append onto n0)
+#   txcabi           bench.py --api cabi --config txlog (mh_multi_txlog_validate); txcabi_corrupt: must exit 1
 #   dist2            2 gloo ranks sharing GPU 0 (bench.py --gpus 2 rehearsal)
 #   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
@@ -29,6 +30,7 @@
 #   txtl:<VARIANTS>  a14 kernel + copy timeline of the last call per variant -> txtl.txt
 #   txprobe:<VARS>   MH_TXLOG_PROBE=1 per-phase wave cycles of the a14 launches -> txprobe.txt
 #   workload:<name>  bench_workloads.py --workload <name>
+#   txres:<VARS>     a14 kernel over a resident log (tools/txlog_resident.py) per env variant
 #   fuzz             host-ASan tx-log fuzzer with the device path (FUZZ_ITERS, FUZZ_SEED)
 #   queue            tools/queue_bench: group commit, 30 committers (QWAIT us, QMAXTXS)
 #   traffic          tools/gpu_pmc.sh: the counter passes behind traffic_r*.json (PMC_CMD overrides)
@@ -62,6 +64,10 @@ for s in "$@"; do
     corrupt_cabi)
       MH_BENCH_CORRUPT=0 step corrupt_cabi 300 python bench.py --api cabi --gpus 1 --steps 20 --warmup 3
       rc=$?; echo "corrupt_cabi exit $rc (want 1)"; [ $rc -eq 1 ] || exit 1 ;;
+    txcabi) step txcabi 400 python bench.py --api cabi --gpus 1 --config txlog --steps 100 --warmup 5 --prewarm 1 || exit 1 ;;
+    txcabi_corrupt)
+      MH_BENCH_CORRUPT=0 step txcabi_corrupt 400 python bench.py --api cabi --gpus 1 --config txlog --steps 5 --warmup 1 --prewarm 0
+      rc=$?; echo "txcabi_corrupt exit $rc (want 1)"; [ $rc -eq 1 ] || exit 1 ;;
     c3cabi) step c3cabi 400 python bench.py --api cabi --gpus 1 --config c3 --steps 10 --warmup 2 || exit 1 ;;
     dist2)
       MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist2 400 python -m torch.distributed.run \
@@ -134,6 +140,13 @@ for s in "$@"; do
         envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
         env MH_TXLOG_PROBE=1 $envs timeout -k 10 200 python3 tools/txlog_timeline.py > "$O/txprobe.out" 2> "$O/txprobe.err" || { tail -5 "$O/txprobe.err"; exit 1; }
         { echo "# variant $v"; grep txlog_probe "$O/txprobe.err" | tail -4; tail -1 "$O/txprobe.out"; } | tee -a "$O/txprobe.txt"
+      done ;;
+    txres:*)  # a14 kernel over a resident log per env variant (tools/txlog_resident.py) -> txres.txt
+      vs="$(echo "${s#txres:}" | tr ';' ' ')"
+      for v in $vs; do
+        envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
+        env $envs timeout -k 10 200 python3 tools/txlog_resident.py ${TXRES_ARGS:-} > "$O/txres.out" 2> "$O/txres.err" || { tail -5 "$O/txres.err"; exit 1; }
+        { echo "# variant $v: $(tail -1 "$O/txres.out")"; grep txlog_probe "$O/txres.err" | tail -2; } | tee -a "$O/txres.txt"
       done ;;
     workload:*) w="${s#workload:}"; step "wl_$w" 600 python bench_workloads.py --workload "$w" || exit 1 ;;
     pmctx) step pmctx 900 bash tools/gpu_pmc_txlog.sh || exit 1; cat "gpurun_out/pmctx${PMC_TAG:-}/table.txt" ;;
