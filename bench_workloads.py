@@ -1067,7 +1067,7 @@ def run_single(a):
         sync()
         resident = {}
         kvar = os.environ.get("MH_TXLOG_KERNEL")
-        for kern, tname in (("wave", "txlog_wave"), ("blk", "txlog_blk")):
+        for kern, tname in (("lanes", "txlog_lanes"), ("wave", "txlog_wave"), ("blk", "txlog_blk")):
             os.environ["MH_TXLOG_KERNEL"] = kern
 
             def step_res():

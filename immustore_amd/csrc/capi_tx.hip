@@ -1343,11 +1343,19 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                     ho.hdrs = reinterpret_cast<uint64_t *>(hh);
                     g.host_done = true;
                 }
-                // MH_TXLOG_KERNEL=group | wave | blk (read per call: A/B tests)
+                // MH_TXLOG_KERNEL=group | wave | blk | lanes (read per call: A/B
+                // tests); by default a group of >= MH_TXLOG_LANES_MIN records
+                // (16384) takes the lane-per-record kernel (throughput), a
+                // smaller one the wave kernel (its chain per record is shorter:
+                // the latency-shaped tail after the last chunk lands)
                 const char *kn = getenv("MH_TXLOG_KERNEL");
+                static const uint64_t lanes_min = [] {
+                    const char *e = getenv("MH_TXLOG_LANES_MIN");
+                    return e ? strtoull(e, nullptr, 10) : 16384ull;
+                }();
                 const bool wave = !(kn && strcmp(kn, "group") == 0);
                 const bool blk = kn && strcmp(kn, "blk") == 0;
-                const bool lanes = kn && strcmp(kn, "lanes") == 0;
+                const bool lanes = kn ? strcmp(kn, "lanes") == 0 : nt >= lanes_min;
                 // MH_TXLOG_HOST_HDRS=1 (read per call, A/B): the last chunk's
                 // group -- its kernel is the tail of the call -- writes only
                 // the Eh words of the caller's pinned headers; the host fills

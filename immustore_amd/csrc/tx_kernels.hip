@@ -914,6 +914,32 @@ __device__ __forceinline__ uint32_t head_mask(int n) {
 // block b of nb of SHA256(p[0:la] || p[la+12 : la+44]) (sha256_skip12's
 // words), padding included.  GUARD: loads confined to [p, p + la + 44) (the
 // log in HBM); staged records have >= 96 readable bytes past every message
+// the 20 dwords block b of skip12_block reads (unguarded)
+__device__ __forceinline__ void skip12_load(const uint8_t *p, uint32_t b, uint32_t d[20]) {
+    const uint32_t *qq = reinterpret_cast<const uint32_t *>(p - ((uintptr_t)p & 3)) + b * 16;
+#pragma unroll
+    for (int j = 0; j < 20; j++) d[j] = qq[j];
+}
+// the block's message words from those dwords (al = p & 3)
+__device__ __forceinline__ void skip12_words(const uint32_t d[20], uint32_t al, uint32_t la,
+                                             uint32_t b, uint32_t nb, uint32_t w[16]) {
+    const uint32_t L = la + 32;
+    const int hv0 = (int)la - (int)(b * 64), v0 = (int)L - (int)(b * 64);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t w1 = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        const uint32_t w2 = bswap(__builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], al));
+        const int v = v0 - 4 * j;
+        const uint32_t pad = (uint32_t)(0x80000000ull >> (8 * (v < 0 ? 5 : min(v, 4))));
+        const uint32_t x = __builtin_amdgcn_bitop3_b32(head_mask(hv0 - 4 * j), w1, w2, 0xCA);
+        w[j] = __builtin_amdgcn_bitop3_b32(x, head_mask(v), pad, 0xEA);
+    }
+    if (b + 1 == nb) {
+        w[14] = 0;
+        w[15] = L * 8;
+    }
+}
+
 template <bool GUARD>
 __device__ __forceinline__ void skip12_block(const uint8_t *p, uint32_t la, uint32_t b,
                                              uint32_t nb, uint32_t w[16]) {
@@ -2051,16 +2077,32 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         b = 0;
     };
     if (ne) entry_setup();
+    // the next entry prefetched while this one hashes (a lane's loads are
+    // otherwise ~3 dependent round trips per entry with no other wave on the
+    // SIMD to cover them at L = 1): its first 24 bytes (mdLen, kLen) issued
+    // before one compression, its first message block before the next, each
+    // consumed after the compression it was issued before
+    uint32_t pst = ne > 1 ? 0u : 3u;  // 0 issue head, 1 parse head + issue block, 2 block loaded, 3 none
+    uint32_t nq = q, n_la = 0, n_nb = 0, n_adv = 0;
+    const uint8_t *n_mp = rp;
+    uint32_t nx[6], pf[20];
+    bool pfok = false;
 #pragma unroll 1
     while (__builtin_amdgcn_ballot_w64(mode != 5)) {
         uint32_t wv16[16];
         bool on = true, tail = false;
         if (mode == 0) {
             if (b == 0) s.init();
-            {
+            uint32_t d[20];
+            if (b == 0 && pfok) {
+#pragma unroll
+                for (int j = 0; j < 20; j++) d[j] = pf[j];
+                pfok = false;
+            } else {
                 const uint8_t *p0 = mp - ((uintptr_t)mp & 3) + 64 * b;
-                skip12_block<false>(ok_(p0, 80, 8) == p0 ? mp : buf + 4, la, b, nb, wv16);
+                skip12_load(ok_(p0, 80, 8) == p0 ? mp : buf + 4, b, d);
             }
+            skip12_words(d, (uint32_t)((uintptr_t)mp & 3), la, b, nb, wv16);
         } else if (mode == 1) {
             wv16[0] = s.h[0] >> 8;
 #pragma unroll
@@ -2085,6 +2127,37 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
             tail = true;
         } else {
             on = false;
+        }
+        // the prefetch stage of this iteration (loads land during the compression)
+        if (pst == 0) {
+            const uint8_t *e = rp + nq;
+            const uint32_t *ea = reinterpret_cast<const uint32_t *>(ok_(e - ((uintptr_t)e & 3), 24, 17));
+#pragma unroll
+            for (int j = 0; j < 6; j++) nx[j] = ea[j];
+            pst = 1;
+        } else if (pst == 1) {
+            const uint32_t o = (uint32_t)((uintptr_t)(rp + nq) & 3);
+            auto be16_at = [&](uint32_t x) -> uint32_t {  // bytes x, x+1 of nx (x <= 22)
+                uint32_t lo = nx[0], hi = nx[1];
+#pragma unroll
+                for (int j = 1; j < 5; j++)
+                    if ((x >> 2) == (uint32_t)j) {
+                        lo = nx[j];
+                        hi = nx[j + 1];
+                    }
+                const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, x & 3);
+                return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
+            };
+            const uint32_t m = be16_at(o);
+            const uint32_t k = o + 4 + m <= 24 ? be16_at(o + 2 + m) : rd_be16(ok_(rp + nq + 2 + m, 2, 18));
+            const uint8_t *er = rp + nq;
+            n_mp = ver == 1 ? er : er + 4 + m;  // as entry_setup
+            n_la = ver == 1 ? 4 + m + k : k;
+            n_nb = (n_la + 32 + 8) / 64 + 1;
+            n_adv = 48 + m + k;
+            const uint8_t *p0 = n_mp - ((uintptr_t)n_mp & 3);
+            skip12_load(ok_(p0, 80, 19) == p0 ? n_mp : buf + 4, 0, pf);
+            pst = 2;
         }
         if (on) {
             if (tail)
@@ -2112,7 +2185,18 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
             if (!fold && sp > (uint32_t)__builtin_popcount(c)) {
                 mode = 2;  // two perfect subtrees of one size on top: merge
             } else if (ej < ne) {
-                entry_setup();
+                if (pst == 2) {  // the prefetched entry (q is at its start)
+                    mp = n_mp;
+                    la = n_la;
+                    nb = n_nb;
+                    q += n_adv;
+                    b = 0;
+                    pfok = true;
+                } else {
+                    entry_setup();
+                }
+                nq = q;
+                pst = ej + 1 < ne ? 0u : 3u;
                 mode = 0;
             } else if (sp >= 2) {
                 fold = true;  // right edge: fold the stack from the right
@@ -2160,6 +2244,29 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     // ---- 3. innerHash + Alh on the record's first lane
     const bool head = act && i == 0;
     uint32_t eh[8], a[8];
+    const uint32_t blen = ver ? 8 + ml : 4, mlen = 80 + blen;
+    // fast path (every v0 record, v1 with mdLen <= 16): the record head
+    // [rp, rp + 116) and the stored Alh in ONE batch of aligned dword loads,
+    // the innerHash message assembled in this record's LDS row (33 words: no
+    // bank conflicts between the wave's rows) with two aligned runs -- ts ||
+    // (version ...nentries) and Eh || blTxID || blRoot shifted by blen & 3 --
+    // and read back word by word; otherwise message bytes straight from the log
+    const bool fast = !ver || ml <= 16;
+    const uint32_t al = (uint32_t)((uintptr_t)rp & 3);
+    uint32_t hrw[30], av[9];
+    if (head && fast) {  // (a record is >= 124 bytes: header + Alh)
+        const uint32_t *hb = reinterpret_cast<const uint32_t *>(ok_(rp - al, 120, 20));
+#pragma unroll
+        for (int j = 0; j < 30; j++) hrw[j] = hb[j];
+        const uint8_t *ap = buf + alh_off[t];
+        const uint32_t *ab = reinterpret_cast<const uint32_t *>(ok_(ap - ((uintptr_t)ap & 3), 36, 21));
+#pragma unroll
+        for (int j = 0; j < 9; j++) av[j] = ab[j];
+    }
+    auto le = [&](int o) -> uint32_t {  // the LE dword at rp + o (o: a constant multiple of 4, <= 112)
+        return __builtin_amdgcn_alignbyte(hrw[o / 4 + 1], hrw[o / 4], al);
+    };
+    uint32_t *msg = stk + (uint32_t)dep * 256 * kTxlStackPad + ((uint32_t)wv * R + r) * 33;
     if (head) {
         if (w == 0) {
             load_digest(kEmptyRootDev, eh);  // SHA256(nil), htree.go:73-77
@@ -2168,8 +2275,27 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
 #pragma unroll
             for (int q2 = 0; q2 < 8; q2++) eh[q2] = p0[q2];
         }
+        if (fast) {  // message bytes in order: [0,8) ts, [8, 8 + blen) rp[88..), then Eh, rp[16..56)
+            msg[0] = le(8);
+            msg[1] = le(12);
+            const uint32_t nY = blen >> 2, sh = blen & 3;
+#pragma unroll
+            for (int u = 0; u < 7; u++)
+                if ((uint32_t)u <= nY) msg[2 + u] = le(88 + 4 * u);  // u == nY: the partial word
+            uint32_t S[18];
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) S[q2] = bswap(eh[q2]);
+#pragma unroll
+            for (int u = 0; u < 10; u++) S[8 + u] = le(16 + 4 * u);
+            uint32_t *dst = msg + 2 + nY;
+            const uint32_t prev = sh ? dst[0] << (8 * (4 - sh)) : 0u;  // Y's last sh bytes, on top
+#pragma unroll
+            for (int t2 = 0; t2 < 19; t2++) {
+                const uint32_t lo = t2 ? S[t2 - 1] : prev, hi = t2 < 18 ? S[t2] : 0u;
+                dst[t2] = sh ? __builtin_amdgcn_alignbyte(hi, lo, 4 - sh) : hi;
+            }
+        }
     }
-    const uint32_t blen = ver ? 8 + ml : 4, mlen = 80 + blen;
     const uint32_t nbi = head ? (mlen + 8) / 64 + 1 : 0;
     const uint32_t nH = wave_max_u32(head ? nbi + 2 : 0);
 #pragma unroll 1
@@ -2179,36 +2305,56 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         if (on) {
             if (k < nbi) {  // ts || version || md part || Eh || blTxID || blRoot
                 if (k == 0) s.init();
-#pragma unroll 4
-                for (int jw = 0; jw < 16; jw++) {
-                    uint32_t v32 = 0;
-                    if (jw == 15 && k + 1 == nbi) {
-                        v32 = mlen * 8;  // the bit length
-                    } else {
+                if (fast) {
 #pragma unroll
-                        for (int bb = 0; bb < 4; bb++) {
-                            const uint32_t kk = 64 * k + 4 * jw + bb;
-                            uint32_t v;
-                            if (kk < 8) v = *ok_(rp + 8 + kk, 1, 9);
-                            else if (kk < 8 + blen) v = *ok_(rp + 80 + kk, 1, 10);
-                            else if (kk < 40 + blen) {
-                                const uint32_t o = kk - 8 - blen;
-                                v = (eh[o >> 2] >> (24 - 8 * (o & 3))) & 0xffu;
-                            } else if (kk < mlen) v = *ok_(rp + kk - 24 - blen, 1, 11);
-                            else v = kk == mlen ? 0x80u : 0u;
-                            v32 = v32 << 8 | v;
-                        }
+                    for (int jw = 0; jw < 16; jw++) {
+                        const int v = (int)mlen - (int)(64 * k + 4 * jw);  // message bytes left at this word
+                        const uint32_t pad = (uint32_t)(0x80000000ull >> (8 * (v < 0 ? 5 : min(v, 4))));
+                        wv16[jw] = __builtin_amdgcn_bitop3_b32(bswap(msg[16 * k + jw]), head_mask(v), pad, 0xEA);
                     }
-                    wv16[jw] = v32;
+                    if (k + 1 == nbi) {
+                        wv16[14] = 0;
+                        wv16[15] = mlen * 8;  // the bit length
+                    }
+                } else {
+#pragma unroll 4
+                    for (int jw = 0; jw < 16; jw++) {
+                        uint32_t v32 = 0;
+                        if (jw == 15 && k + 1 == nbi) {
+                            v32 = mlen * 8;  // the bit length
+                        } else {
+#pragma unroll
+                            for (int bb = 0; bb < 4; bb++) {
+                                const uint32_t kk = 64 * k + 4 * jw + bb;
+                                uint32_t v;
+                                if (kk < 8) v = *ok_(rp + 8 + kk, 1, 9);
+                                else if (kk < 8 + blen) v = *ok_(rp + 80 + kk, 1, 10);
+                                else if (kk < 40 + blen) {
+                                    const uint32_t o = kk - 8 - blen;
+                                    v = (eh[o >> 2] >> (24 - 8 * (o & 3))) & 0xffu;
+                                } else if (kk < mlen) v = *ok_(rp + kk - 24 - blen, 1, 11);
+                                else v = kk == mlen ? 0x80u : 0u;
+                                v32 = v32 << 8 | v;
+                            }
+                        }
+                        wv16[jw] = v32;
+                    }
                 }
             } else if (k == nbi) {  // BE64 id || prevAlh || innerHash[0:24]
                 copy8(a, s.h);      // (a: the innerHash until the Alh is done)
                 s.init();
-                const uint64_t id = rd_be64(ok_(rp, 16, 12));
-                wv16[0] = (uint32_t)(id >> 32);
-                wv16[1] = (uint32_t)id;
+                if (fast) {
+                    wv16[0] = bswap(le(0));
+                    wv16[1] = bswap(le(4));
 #pragma unroll
-                for (int q2 = 0; q2 < 8; q2++) wv16[2 + q2] = bswap(rd_le32(ok_(rp + 56 + 4 * q2, 8, 13)));
+                    for (int q2 = 0; q2 < 8; q2++) wv16[2 + q2] = bswap(le(56 + 4 * q2));
+                } else {
+                    const uint64_t id = rd_be64(ok_(rp, 16, 12));
+                    wv16[0] = (uint32_t)(id >> 32);
+                    wv16[1] = (uint32_t)id;
+#pragma unroll
+                    for (int q2 = 0; q2 < 8; q2++) wv16[2 + q2] = bswap(rd_le32(ok_(rp + 56 + 4 * q2, 8, 13)));
+                }
 #pragma unroll
                 for (int q2 = 0; q2 < 6; q2++) wv16[10 + q2] = a[q2];
             } else {
@@ -2226,18 +2372,34 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     int32_t stv = MH_OK;
     uint64_t hw[17];
     if (head) {  // tx.go:623-627
-        const uint8_t *ap = ok_(buf + alh_off[t], 40, 14);
         uint32_t xx = 0;
+        if (fast) {
+            const uint32_t aal = (uint32_t)((uintptr_t)(buf + alh_off[t]) & 3);
 #pragma unroll
-        for (int q2 = 0; q2 < 8; q2++) xx |= bswap(rd_le32(ap + 4 * q2)) ^ a[q2];
+            for (int q2 = 0; q2 < 8; q2++)
+                xx |= bswap(__builtin_amdgcn_alignbyte(av[q2 + 1], av[q2], aal)) ^ a[q2];
+        } else {
+            const uint8_t *ap = ok_(buf + alh_off[t], 40, 14);
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) xx |= bswap(rd_le32(ap + 4 * q2)) ^ a[q2];
+        }
         stv = xx ? MH_ERR_CORRUPTED_DATA : MH_OK;
         status[t] = stv;
         store_digest(eh_out + t * 32, eh);
         store_digest(alh_out + t * 32, a);
+        if (fast) {
 #pragma unroll
-        for (int q2 = 0; q2 < 3; q2++) hw[q2] = rd_be64(ok_(rp + 8 * q2, 16, 15));
+            for (int q2 = 0; q2 < 3; q2++)
+                hw[q2] = ((uint64_t)bswap(le(8 * q2)) << 32) | bswap(le(8 * q2 + 4));
 #pragma unroll
-        for (int q2 = 0; q2 < 8; q2++) hw[3 + q2] = rd_raw64(ok_(rp + 24 + 8 * q2, 16, 16));
+            for (int q2 = 0; q2 < 8; q2++)
+                hw[3 + q2] = (uint64_t)le(24 + 8 * q2) | ((uint64_t)le(28 + 8 * q2) << 32);
+        } else {
+#pragma unroll
+            for (int q2 = 0; q2 < 3; q2++) hw[q2] = rd_be64(ok_(rp + 8 * q2, 16, 15));
+#pragma unroll
+            for (int q2 = 0; q2 < 8; q2++) hw[3 + q2] = rd_raw64(ok_(rp + 24 + 8 * q2, 16, 16));
+        }
 #pragma unroll
         for (int q2 = 0; q2 < 4; q2++)
             hw[11 + q2] = (uint64_t)bswap(eh[2 * q2]) | ((uint64_t)bswap(eh[2 * q2 + 1]) << 32);
@@ -2286,15 +2448,16 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
         return hipErrorInvalidValue;
     int lgp = 0;
     while ((1ull << lgp) < wmax) lgp++;
-    // lanes per record: L = 1 while the launch still has >= 2 waves per SIMD
-    // (2048 waves of 64 records), more lanes for fewer records (latency);
+    // lanes per record: the fewest that still give every SIMD a wave (1024
+    // waves; one wave per SIMD runs at VALU active 0.75 once its loads are
+    // prefetched), more lanes for fewer records (latency);
     // MH_TXLOG_LANES=1|2|4 forces it (read per call)
-    int lgl = ntx >= 2048ull * 64 ? 0 : ntx >= 2048ull * 32 ? 1 : 2;
+    int lgl = ntx >= 1024ull * 64 ? 0 : ntx >= 1024ull * 32 ? 1 : 2;
     if (const char *e = getenv("MH_TXLOG_LANES")) lgl = atoi(e) >= 4 ? 2 : atoi(e) >= 2 ? 1 : 0;
     lgl = std::min(lgl, lgp);  // never more lanes than entries
     const int R = 64 >> lgl;
     const int dep = std::max(1, lgp - lgl + 1);  // stack depth: log2(EP) + 1
-    const size_t stack = (size_t)dep * 256 * kTxlStackPad * 4;
+    const size_t stack = (size_t)dep * 256 * kTxlStackPad * 4 + (size_t)4 * R * 33 * 4;  // + innerHash rows
     const size_t res = (size_t)4 * R * (17 * 8 + 8 * 4 + 4);
     const size_t sh = std::max(stack, res);
     static const int fence = [] {

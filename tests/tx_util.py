@@ -39,8 +39,9 @@ def _txmd(rng, kind):
     trunc = b"\x00" + rb(8)
     if kind == 2:
         return trunc
-    if kind == 3:
-        return b"\x01" + struct.pack(">H", 5) + rb(5)
+    if kind == 3:  # 8..11 bytes: every alignment of what follows it in the header
+        n = int(rng.integers(5, 9))
+        return b"\x01" + struct.pack(">H", n) + rb(n)
     if kind == 4:
         return trunc + b"\x01" + struct.pack(">H", 256) + rb(256)
     return b""

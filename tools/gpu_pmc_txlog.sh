@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes over the fused a14 group kernel (bench_workloads --workload txlog):
 # stall split, instruction mix, HBM bytes; each counter set its own run.
+# PMC_PY overrides the profiled script + args (e.g. "tools/txlog_resident.py 65536 5").
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out/pmctx${PMC_TAG:-}"
@@ -14,6 +15,6 @@ i=0
 P5="${PMC_EXTRA:-}"
 for ctrs in "$P1" "$P2" "$P3" "$P4" ${P5:+"$P5"}; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs --output-format csv -d "$OUT/b$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench_workloads.py" --workload txlog --steps 3 --warmup 1 --prewarm 0 > "$OUT/b$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/b$i.log"; exit 1; }
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs --output-format csv -d "$OUT/b$i" -o run -- python3 "$GRAFT_REPO_ROOT/"${PMC_PY:-bench_workloads.py --workload txlog --steps 3 --warmup 1 --prewarm 0} > "$OUT/b$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/b$i.log"; exit 1; }
 done
 python3 "$GRAFT_REPO_ROOT/tools/pmc_table.py" "${PMC_MATCH:-k_txlog_wave}" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/table.txt"

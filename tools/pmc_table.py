@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel PMC table from rocprofv3 counter_collection CSVs: mean counter
+"""Per-kernel PMC table from rocprofv3 counter_collection CSVs: median counter
 values per dispatch of the kernels matching a substring, plus the effective
 clock (GRBM_GUI_ACTIVE / 8 XCDs / duration) and the stall split."""
 import collections
@@ -28,7 +28,7 @@ def main():
         d = sorted(dur[k].values())
         dmed = d[len(d) // 2]
         print("kernel:", k[:90], "dispatches", len(d), "median ns", dmed)
-        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        m = {c: sorted(v)[len(v) // 2] for c, v in cs.items()}  # median dispatch
         for c in sorted(m):
             print("  %-24s %.4g" % (c, m[c]))
         if "GRBM_GUI_ACTIVE" in m:
