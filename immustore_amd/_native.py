@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("MH_LIB_PATH") or os.path.join(_HERE, "libimmustore_me
 MH_OK = 0
 # test-only fault sites of mh_debug_fail_at
 MH_FAULT_RCCL_GROUP = 1
+MH_FAULT_RCCL_GROUP_LATE = 3
 MH_FAULT_TXLOG_AFTER_GROUP = 2
 MH_ERR_MAX_WIDTH_EXCEEDED = 1
 MH_ERR_ILLEGAL_ARGUMENTS = 2

@@ -29,16 +29,16 @@ hipError_t launch_copy_nodes(hipStream_t st, const uint8_t *src, uint64_t n, uin
 extern "C" int mh_abi_version(void) { return MH_ABI_VERSION; }
 
 namespace {
-std::atomic<int> g_fault[3];
+std::atomic<int> g_fault[4];
 }
 
 bool mh_fault(int site) {
-    if (site <= 0 || site >= 3 || g_fault[site].load(std::memory_order_relaxed) <= 0) return false;
+    if (site <= 0 || site >= 4 || g_fault[site].load(std::memory_order_relaxed) <= 0) return false;
     return g_fault[site].fetch_sub(1) == 1;
 }
 
 extern "C" int mh_debug_fail_at(int site, int countdown) {
-    if (site <= 0 || site >= 3 || countdown < 0) return MH_ERR_ILLEGAL_ARGUMENTS;
+    if (site <= 0 || site >= 4 || countdown < 0) return MH_ERR_ILLEGAL_ARGUMENTS;
     g_fault[site].store(countdown);
     return MH_OK;
 }

@@ -278,6 +278,7 @@ int gather_bytes(mh_multi *m, const std::vector<const uint8_t *> &send,
         else
             queued++;
     }
+    if (st == MH_OK && mh_fault(MH_FAULT_RCCL_GROUP_LATE)) st = MH_ERR_COLLECTIVE;
     const ncclResult_t ge = group.end();
     if (st == MH_OK && ge == ncclSuccess) return MH_OK;
     if (queued > 0) {

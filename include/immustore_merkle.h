@@ -126,10 +126,14 @@ int mh_ctx_timing_reset(mh_ctx *ctx);
  * there as if the HIP / RCCL call at that point had failed.  countdown 0
  * disarms the site.  Sites: MH_FAULT_RCCL_GROUP (inside the RCCL group of a
  * multi-device all-gather, after ncclGroupStart), MH_FAULT_TXLOG_AFTER_GROUP
- * (mh_txlog_validate, after the first chunk group's kernels were queued).
- * No reference counterpart: production callers never arm it. */
+ * (mh_txlog_validate, after the first chunk group's kernels were queued),
+ * MH_FAULT_RCCL_GROUP_LATE (the same all-gather after every device's
+ * collective was queued: the clique is aborted and the handle refuses every
+ * later collective).  No reference counterpart: production callers never arm
+ * it. */
 #define MH_FAULT_RCCL_GROUP 1
 #define MH_FAULT_TXLOG_AFTER_GROUP 2
+#define MH_FAULT_RCCL_GROUP_LATE 3
 int mh_debug_fail_at(int site, int countdown);
 
 /* device memory helpers, so that a cgo caller needs no HIP headers */
@@ -765,6 +769,14 @@ int mh_ahtree_range_plan(uint64_t n0, uint64_t total, int ndev, int *shard_bits,
  * payloads, room for its new digests).  peaks (host) on EVERY rank when
  * n0 > 0.  A rank past the plan's ranges (r >= nranges) does nothing but
  * still joins the all-gather.  Asynchronous on the context stream. */
+int mh_ahtree_range_sizes(uint64_t n0, uint64_t total, int ndev, uint64_t *send_bytes,
+                          uint64_t *work_bytes);
+int mh_dev_ahtree_range_local(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
+                              int world, int rank, const uint8_t *payloads, uint32_t plen,
+                              uint8_t *dlog_range, uint8_t *work, uint8_t *send);
+int mh_dev_ahtree_range_finish(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
+                               int world, int rank, const uint8_t *recv, uint8_t *dlog_range,
+                               uint8_t *work, uint8_t *roots_out);
 /* The PCIe-bound batch paths over the K devices: the batch is cut into K
  * contiguous parts -- by index for proofs, at record boundaries (nearly equal
  * bytes) for a tx log -- and part d runs the single-context call on device d
@@ -792,14 +804,6 @@ int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t len, uint3
                             uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx,
                             uint64_t *consumed, mh_tx_header *hdrs, uint8_t *alh,
                             int32_t *status);
-int mh_ahtree_range_sizes(uint64_t n0, uint64_t total, int ndev, uint64_t *send_bytes,
-                          uint64_t *work_bytes);
-int mh_dev_ahtree_range_local(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
-                              int world, int rank, const uint8_t *payloads, uint32_t plen,
-                              uint8_t *dlog_range, uint8_t *work, uint8_t *send);
-int mh_dev_ahtree_range_finish(mh_ctx *ctx, uint64_t n0, const uint8_t *peaks, uint64_t total,
-                               int world, int rank, const uint8_t *recv, uint8_t *dlog_range,
-                               uint8_t *work, uint8_t *roots_out);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

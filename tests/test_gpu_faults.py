@@ -67,6 +67,54 @@ def test_rccl_group_closed_after_injected_failure(m, orc):
         md.close()
 
 
+def test_rccl_clique_aborted_after_late_failure(m, orc):
+    """A failure after the group's collectives were queued (on
+    K > 1 devices those would wait for peers that never join) aborts the
+    clique: the call returns MH_ERR_COLLECTIVE, every later collective on the
+    handle returns it too (no hang), the handle still closes, and a new
+    clique on the same device builds the oracle's root."""
+    import torch
+    from immustore_amd import _native as N
+    from immustore_amd.multi import MultiDevice
+    L = N.load()
+    n, vl, kl = 1 << 12, 256, 8
+    vals = orc.fill_random(n * vl, 22).reshape(n, vl)
+    keys = np.frombuffer(np.arange(n, dtype=">u8").tobytes(), np.uint8).reshape(n, kl)
+    _, _, want = orc.build_entries_fixed(1, keys, vals)
+    dk = torch.from_numpy(keys.reshape(-1).copy()).cuda()
+    dv = torch.from_numpy(vals.reshape(-1).copy()).cuda()
+    lv = torch.empty(m.levels_len(n) * 32, dtype=torch.uint8, device="cuda")
+    top = torch.empty(32 * 2, dtype=torch.uint8, device="cuda")
+    rt = torch.empty(32, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    args = (1, n, [dk.data_ptr()], kl, [dv.data_ptr()], vl, [lv.data_ptr()],
+            [top.data_ptr()], [rt.data_ptr()])
+    md = MultiDevice([0])
+    assert md.uses_rccl()
+    try:
+        N.check(L.mh_debug_fail_at(N.MH_FAULT_RCCL_GROUP_LATE, 1))
+        try:
+            with pytest.raises(N.MerkleError) as e:
+                md.dev_build_entries_fixed(*args)
+            assert e.value.status == N.MH_ERR_COLLECTIVE
+        finally:
+            N.check(L.mh_debug_fail_at(N.MH_FAULT_RCCL_GROUP_LATE, 0))
+        with pytest.raises(N.MerkleError) as e:
+            md.dev_build_entries_fixed(*args)
+        assert e.value.status == N.MH_ERR_COLLECTIVE
+    finally:
+        md.close()
+    md = MultiDevice([0])
+    try:
+        rt.zero_()
+        torch.cuda.synchronize()
+        md.dev_build_entries_fixed(*args)
+        md.synchronize()
+        assert rt.cpu().numpy().tobytes() == want
+    finally:
+        md.close()
+
+
 def test_debug_fail_at_arguments(m):
     from immustore_amd import _native as N
     L = N.load()
