@@ -1415,6 +1415,15 @@ void txlog_probe_report() {
         }
         std::sort(ghz.begin(), ghz.end());
         std::sort(life.begin(), life.end());
+        for (int k = 12; k < 16; k++) {  // k_txlog_lanes: loop cycles by iteration kind (+1)
+            std::vector<uint64_t> d;
+            for (unsigned w = 0; w < nw; w++)
+                if (h[(size_t)w * 16 + k]) d.push_back(h[(size_t)w * 16 + k] - 1);
+            if (d.empty()) continue;
+            std::sort(d.begin(), d.end());
+            fprintf(stderr, " it%d=%llu/%llu", k - 12, (unsigned long long)d[d.size() / 2],
+                    (unsigned long long)d.back());
+        }
         fprintf(stderr, " clock_ghz med %.2f wave_life_us med/max %.1f/%.1f launch_span_us %.1f\n",
                 ghz.empty() ? 0.0 : ghz[ghz.size() / 2], life.empty() ? 0.0 : life[life.size() / 2],
                 life.empty() ? 0.0 : life.back(), r1 > r0 ? (double)(r1 - r0) / 100.0 : 0.0);
@@ -1972,7 +1981,7 @@ hipError_t launch_txlog_blk(hipStream_t st, Timer *tm, uint64_t ntx, const uint8
 }
 
 // ---------------------------------------------------------------- a14, lanes per record
-// The same a14 check with every record on L = 1, 2 or 4 lanes (k_txlog_lanes<LGL>):
+// The same a14 check with every record on L = 1, 2, 4, 8 or 16 lanes (k_txlog_lanes<LGL>):
 // lane i of a record takes its entries [i EP, (i+1) EP) (EP = P / L, P = the
 // widest tx rounded up to a power of two) and builds their subtree itself --
 // entry digest (tx.go:690-731) and leaf (htree.go:79-83) per entry, pushed on
@@ -2009,7 +2018,8 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     uint64_t ntx, const uint8_t *__restrict__ buf, const uint64_t *__restrict__ rec_off,
     const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
     MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ eh_out, uint8_t *__restrict__ alh_out,
-    int32_t *__restrict__ status, TxlogHostOut ho, int lgp, int dep, int fence, uint64_t blen_) {
+    int32_t *__restrict__ status, TxlogHostOut ho, int lgp, int dep, int fence, uint64_t blen_,
+    uint64_t *__restrict__ probe) {
     extern __shared__ uint4 lds[];
     constexpr int L = 1 << LGL, R = 64 >> LGL;
     uint32_t *stk = reinterpret_cast<uint32_t *>(lds);  // [dep][256][9]
@@ -2021,6 +2031,18 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     const uint64_t t = TW + r;
     const bool act = t < ntx;
     auto slot = [&](int d) -> uint32_t * { return stk + ((uint32_t)d * 256 + tid) * kTxlStackPad; };
+    // MH_TXLOG_PROBE=1: s_memtime stamps of the wave's phases (lane 0; 0 start,
+    // 1 loop start, 2 loop end, 3 lanes combined, 4 innerHash message built, 5
+    // Alh done, 6 results staged, 9 end; 10 / 11 s_memrealtime) and the cycles
+    // of the loop's iterations by kind (12 digest blocks, 13 leaves, 14 node
+    // first blocks, 15 node tails)
+    const uint64_t pw = (uint64_t)blockIdx.x * 4 + wv;
+    auto stamp = [&](int k) {
+        if (probe && lane == 0) probe[pw * 16 + k] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
+    if (probe && lane == 0) probe[pw * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+    uint64_t acc[4] = {0, 0, 0, 0};
     // CHK (MH_TXLOG_LANES_CHECK=1, diagnosis): every read range of the log
     // checked against [buf, buf + len + 256); a range outside is reported and
     // read from buf instead
@@ -2054,10 +2076,30 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     // host hop). Only a lane with entries walks: written as `j < j0 && j < w`
     // for every lane, the compiler dropped the `j < w` bound (q is dead when
     // ne == 0) and lanes past the record's last entry walked off the log.
+    // Each step reads the entry's first 24 bytes at once (mdLen and, for
+    // mdLen <= 16, kLen in them): one load round trip per entry, not two.
     if (ne) {
         for (uint32_t j = 0; j < j0; j++) {
-            const uint32_t m = rd_be16(ok_(rp + q, 2, 4));
-            q += 48 + m + rd_be16(ok_(rp + q + 2 + m, 2, 5));
+            const uint8_t *e = rp + q;
+            const uint32_t o = (uint32_t)((uintptr_t)e & 3);
+            const uint32_t *ea = reinterpret_cast<const uint32_t *>(ok_(e - o, 24, 4));
+            uint32_t x[6];
+#pragma unroll
+            for (int u = 0; u < 6; u++) x[u] = ea[u];
+            auto be16x = [&](uint32_t y) -> uint32_t {  // bytes y, y+1 of x (y <= 22)
+                uint32_t lo = x[0], hi = x[1];
+#pragma unroll
+                for (int u = 1; u < 5; u++)
+                    if ((y >> 2) == (uint32_t)u) {
+                        lo = x[u];
+                        hi = x[u + 1];
+                    }
+                const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, y & 3);
+                return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
+            };
+            const uint32_t m = be16x(o);
+            const uint32_t k = o + 4 + m <= 24 ? be16x(o + 2 + m) : rd_be16(ok_(e + 2 + m, 2, 5));
+            q += 48 + m + k;
         }
     }
     // ---- 1. this lane's subtree: entries, leaves, merges, the final fold
@@ -2087,10 +2129,13 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     const uint8_t *n_mp = rp;
     uint32_t nx[6], pf[20];
     bool pfok = false;
+    stamp(1);
 #pragma unroll 1
     while (__builtin_amdgcn_ballot_w64(mode != 5)) {
         uint32_t wv16[16];
         bool on = true, tail = false;
+        const uint64_t it0 = probe ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t mode0 = mode;
         if (mode == 0) {
             if (b == 0) s.init();
             uint32_t d[20];
@@ -2207,7 +2252,11 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         } else if (mode == 2) {
             mode = 3;
         }
+        if (probe && mode0 < 4) acc[mode0] += __builtin_amdgcn_s_memtime() - it0;
     }
+    stamp(2);
+    if (probe && lane == 0)
+        for (int k = 0; k < 4; k++) probe[pw * 16 + 12 + k] = acc[k] + 1;
     // ---- 2. the record's L lane roots paired (htree.go:85-110), via LDS
     // (slot 0 of each lane; a lane without entries holds nothing)
 #pragma unroll 1
@@ -2241,6 +2290,7 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(3);
     // ---- 3. innerHash + Alh on the record's first lane
     const bool head = act && i == 0;
     uint32_t eh[8], a[8];
@@ -2298,6 +2348,7 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     }
     const uint32_t nbi = head ? (mlen + 8) / 64 + 1 : 0;
     const uint32_t nH = wave_max_u32(head ? nbi + 2 : 0);
+    stamp(4);
 #pragma unroll 1
     for (uint32_t k = 0; k < nH; k++) {
         uint32_t wv16[16];
@@ -2369,6 +2420,7 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         }
     }
     copy8(a, s.h);
+    stamp(5);
     int32_t stv = MH_OK;
     uint64_t hw[17];
     if (head) {  // tx.go:623-627
@@ -2421,6 +2473,7 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         sst[rw] = (uint32_t)stv;
     }
     __syncthreads();
+    stamp(6);
     const uint64_t nb_ = T0 < ntx ? min((uint64_t)RW, ntx - T0) : 0;
     uint64_t *hd = ho.hdrs ? ho.hdrs + T0 * 17 : reinterpret_cast<uint64_t *>(hdrs) + T0 * 17;
     if (ho.hdrs && ho.eh_only) {
@@ -2436,6 +2489,10 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     if (ho.status)
         for (uint32_t k = tid; k < nb_; k += 256) ho.status[T0 + k] = sst[k];
     if (fence && (ho.status || ho.alh || ho.hdrs)) __threadfence_system();
+    stamp(7);
+    stamp(8);
+    stamp(9);
+    if (probe && lane == 0) probe[pw * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
@@ -2448,12 +2505,18 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
         return hipErrorInvalidValue;
     int lgp = 0;
     while ((1ull << lgp) < wmax) lgp++;
-    // lanes per record: the fewest that still give every SIMD a wave (1024
-    // waves; one wave per SIMD runs at VALU active 0.75 once its loads are
-    // prefetched), more lanes for fewer records (latency);
-    // MH_TXLOG_LANES=1|2|4 forces it (read per call)
-    int lgl = ntx >= 1024ull * 64 ? 0 : ntx >= 1024ull * 32 ? 1 : 2;
-    if (const char *e = getenv("MH_TXLOG_LANES")) lgl = atoi(e) >= 4 ? 2 : atoi(e) >= 2 ? 1 : 0;
+    // lanes per record: the fewest that give every SIMD two waves (2048 waves
+    // of 64 lanes: one wave per SIMD issues VALU 0.76 of its cycles, two 0.9,
+    // for ~10 % more instructions at L = 2, profiles/txlog_lanes_r05.txt; a
+    // record's chain is 2 EP + 2 (EP - 1) + 2 log2 L + 4 compressions, EP = P /
+    // L, so fewer records take more lanes: latency), at most 16;
+    // MH_TXLOG_LANES=1|2|4|8|16 forces it (read per call)
+    int lgl = 0;
+    while (lgl < 4 && (ntx << lgl) < 2048ull * 64) lgl++;  // two waves per SIMD (176 VGPRs: at most 2)
+    if (const char *e = getenv("MH_TXLOG_LANES")) {
+        const int v = atoi(e);
+        lgl = v >= 16 ? 4 : v >= 8 ? 3 : v >= 4 ? 2 : v >= 2 ? 1 : 0;
+    }
     lgl = std::min(lgl, lgp);  // never more lanes than entries
     const int R = 64 >> lgl;
     const int dep = std::max(1, lgp - lgl + 1);  // stack depth: log2(EP) + 1
@@ -2466,12 +2529,12 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
     }();
     static const bool attr = [] {
         const int mx = 160 << 10;
-        hipFuncSetAttribute((const void *)k_txlog_lanes<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        hipFuncSetAttribute((const void *)k_txlog_lanes<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        hipFuncSetAttribute((const void *)k_txlog_lanes<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        hipFuncSetAttribute((const void *)k_txlog_lanes<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        hipFuncSetAttribute((const void *)k_txlog_lanes<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        hipFuncSetAttribute((const void *)k_txlog_lanes<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        const void *fs[] = {(const void *)k_txlog_lanes<0, false>, (const void *)k_txlog_lanes<1, false>,
+                            (const void *)k_txlog_lanes<2, false>, (const void *)k_txlog_lanes<3, false>,
+                            (const void *)k_txlog_lanes<4, false>, (const void *)k_txlog_lanes<0, true>,
+                            (const void *)k_txlog_lanes<1, true>,  (const void *)k_txlog_lanes<2, true>,
+                            (const void *)k_txlog_lanes<3, true>,  (const void *)k_txlog_lanes<4, true>};
+        for (const void *f : fs) hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
         (void)hipGetLastError();
         return true;
     }();
@@ -2482,17 +2545,22 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
         const char *e = getenv("MH_TXLOG_LANES_CHECK");
         return e && atoi(e) != 0;
     }();
+    uint64_t *probe = txlog_probe_slot(grid.x * 4);
 #define MH_TXL(l_, c_)                                                                             \
     hipLaunchKernelGGL((k_txlog_lanes<l_, c_>), grid, blk, sh, st, ntx, buf, rec_off, alh_off,   \
-                       leaf_off, hdrs, eh_out, alh_out, status, ho, lgp, dep, fence, log_len)
+                       leaf_off, hdrs, eh_out, alh_out, status, ho, lgp, dep, fence, log_len, probe)
     if (chk) {
         if (lgl == 0) MH_TXL(0, true);
         else if (lgl == 1) MH_TXL(1, true);
-        else MH_TXL(2, true);
+        else if (lgl == 2) MH_TXL(2, true);
+        else if (lgl == 3) MH_TXL(3, true);
+        else MH_TXL(4, true);
     } else {
         if (lgl == 0) MH_TXL(0, false);
         else if (lgl == 1) MH_TXL(1, false);
-        else MH_TXL(2, false);
+        else if (lgl == 2) MH_TXL(2, false);
+        else if (lgl == 3) MH_TXL(3, false);
+        else MH_TXL(4, false);
     }
 #undef MH_TXL
     return hipGetLastError();

@@ -643,8 +643,8 @@ def _record_heads(raw, n):
 def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries):
     """k_txlog_wave (one wave per 64 / L records, L lanes per record: every
     lane-count the widest tx can pick), k_txlog_blk (every phase spread over
-    the workgroup: every records-per-workgroup shape) and k_txlog_lanes (1, 2
-    and 4 lanes per record, each lane's subtree serial) with the records
+    the workgroup: every records-per-workgroup shape) and k_txlog_lanes (1, 2,
+    4, 8 and 16 lanes per record, each lane's subtree serial) with the records
     staged in LDS and read from HBM, against the round-3 workgroup kernel
     (MH_TXLOG_KERNEL=group), the
     oracle and the record heads parsed in Python: headers (every field, Eh
@@ -665,7 +665,8 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
         o = orc.txlog_validate(buf)
         res = {}
         for kern, smax in (("group", None), ("wave", None), ("wave", "0"), ("blk", None),
-                           ("blk", "0"), ("lanes", "L1"), ("lanes", "L2"), ("lanes", "L4")):
+                           ("blk", "0"), ("lanes", "L1"), ("lanes", "L2"), ("lanes", "L4"),
+                           ("lanes", "L8"), ("lanes", "L16")):
             monkeypatch.setenv("MH_TXLOG_KERNEL", kern)
             monkeypatch.delenv("MH_TXLOG_STAGE_MAX", raising=False)
             monkeypatch.delenv("MH_TXLOG_LANES", raising=False)
