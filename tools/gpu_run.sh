@@ -103,7 +103,9 @@ for s in "$@"; do
     c4) step c4 600 python bench.py --config c4 --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline || exit 1 ;;
     prof)
       rm -rf "$O/prof"
-      step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1 ;;
+      step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+      python3 tools/prof_summary.py "$O/prof/run_kernel_trace.csv" --steps 20 --warmup 5 > "$O/prof_summary.json" || exit 1
+      gzip -f "$O/prof/run_kernel_trace.csv" ;;
     txlog) step txlog 300 ./tools/txlog_bench || exit 1 ;;
     copyprobe) step copyprobe 200 ./tools/copy_probe || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;
