@@ -29,7 +29,7 @@ def main():
             if not isinstance(d, dict) or "metric" not in d:
                 continue
             d = dict({"step": step}, **d)
-            if step.startswith(("wcorrupt", "corrupt")):
+            if step.startswith(("wcorrupt", "corrupt")) or step.endswith("_corrupt"):
                 d["expected_exit"] = 1
             out.append(json.dumps(d))
     with open(dst, "w") as fh:
