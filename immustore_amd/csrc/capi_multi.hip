@@ -98,6 +98,7 @@ struct mh_multi {
     };
     std::vector<std::unique_ptr<Dev>> buf;
     std::vector<hipEvent_t> ev;  // duplicate-device gathers (one per context)
+    std::vector<mh_commit_pipe *> pipe;  // mh_multi_precommit_batch: one per context, made on first use
     std::mutex mu;  // one build at a time per mh_multi
 };
 
@@ -168,6 +169,8 @@ extern "C" int mh_multi_destroy(mh_multi *m) {
             m->buf[d].reset();  // frees on the owning device
             if (d < (int)m->ev.size()) hipEventDestroy(m->ev[d]);
         }
+        for (mh_commit_pipe *p : m->pipe)
+            if (p) mh_commit_pipe_free(p);
         for (mh_ctx *c : m->ctx)
             if (c) mh_ctx_destroy(c);
         delete m;
@@ -930,6 +933,26 @@ inline void split_part(uint64_t n, int K, int d, uint64_t &lo, uint64_t &hi) {
     hi = (uint64_t)((unsigned __int128)n * (unsigned)(d + 1) / (unsigned)K);
 }
 
+// K + 1 item bounds splitting n items into K parts of nearly equal bytes,
+// bytes(i) = the byte offset where item i starts (non-decreasing, i <= n)
+template <class B>
+std::vector<uint64_t> split_by_bytes(uint64_t n, int K, B bytes) {
+    std::vector<uint64_t> t(K + 1, 0);
+    t[K] = n;
+    const uint64_t b0 = bytes(0), tot = bytes(n) - b0;
+    for (int d = 1; d < K; d++) {
+        const uint64_t want = b0 + (uint64_t)((unsigned __int128)tot * (unsigned)d / (unsigned)K);
+        uint64_t lo = t[d - 1], hi = n;  // the first item starting at or after want
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if (bytes(mid) < want) lo = mid + 1;
+            else hi = mid;
+        }
+        t[d] = lo;
+    }
+    return t;
+}
+
 }  // namespace
 
 // htree.VerifyInclusion over n proofs (htree.go:166-195), split by index.
@@ -1042,5 +1065,107 @@ extern "C" int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t
             return MH_OK;
         });
         return st ? st : rc;
+    });
+}
+
+// readValueAt's hVal check (immustore.go:3183-3240, the compare at :3235)
+// over a batch of values, split into K parts of nearly equal value bytes.
+// *ncorrupted (may be NULL) is the sum over the parts.
+extern "C" int mh_multi_verify_values_batch(mh_multi *m, uint64_t n, const uint8_t *vals,
+                                            const uint64_t *off, const uint64_t *vlen,
+                                            const uint8_t *hvals, int32_t *status,
+                                            uint64_t *ncorrupted) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (m->K == 1 || n < (uint64_t)m->K)
+            return mh_verify_values_batch(m->ctx[0], n, vals, off, vlen, hvals, status, ncorrupted);
+        if (!off || !vlen || !hvals || !status) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const std::vector<uint64_t> t = split_by_bytes(n, m->K, [&](uint64_t i) { return off[i]; });
+        std::vector<uint64_t> bad(m->K, 0);
+        std::lock_guard<std::mutex> lk(m->mu);
+        const int st = per_device(m->K, [&](int d) -> int {
+            const uint64_t lo = t[d], hi = t[d + 1];
+            if (hi == lo) return MH_OK;
+            return mh_verify_values_batch(m->ctx[d], hi - lo, vals, off + lo, vlen + lo,
+                                          hvals + 32 * lo, status + lo, &bad[d]);
+        });
+        if (st) return st;
+        if (ncorrupted) {
+            uint64_t c = 0;
+            for (uint64_t b : bad) c += b;
+            *ncorrupted = c;
+        }
+        return MH_OK;
+    });
+}
+
+// The fused DualProofV2 wire verify (DualProofV2FromProto,
+// database_protoconv.go:226-262, + VerifyDualProofV2, verification.go:303-372)
+// over n messages, split into K parts of nearly equal message bytes.
+extern "C" int mh_multi_verify_dual_proof_v2_pb_batch(mh_multi *m, uint64_t n, const uint8_t *msgs,
+                                                      const uint64_t *msg_off, const uint64_t *src,
+                                                      const uint64_t *tgt, const uint8_t *src_alh,
+                                                      const uint8_t *tgt_alh, int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (m->K == 1 || n < (uint64_t)m->K)
+            return mh_verify_dual_proof_v2_pb_batch(m->ctx[0], n, msgs, msg_off, src, tgt, src_alh,
+                                                    tgt_alh, status);
+        if (!msg_off || !src || !tgt || !src_alh || !tgt_alh || !status) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(msg_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const std::vector<uint64_t> t =
+            split_by_bytes(n, m->K, [&](uint64_t i) { return msg_off[i]; });
+        std::lock_guard<std::mutex> lk(m->mu);
+        return per_device(m->K, [&](int d) -> int {
+            const uint64_t lo = t[d], hi = t[d + 1];
+            if (hi == lo) return MH_OK;
+            return mh_verify_dual_proof_v2_pb_batch(m->ctx[d], hi - lo, msgs, msg_off + lo, src + lo,
+                                                    tgt + lo, src_alh + 32 * lo,
+                                                    tgt_alh + 32 * lo, status + lo);
+        });
+    });
+}
+
+// precommit's hashing (immustore.go:1620-1632, 2301-2313 -> tx.go:332-355) for
+// a batch of transactions, split into K parts of whole transactions with
+// nearly equal value bytes; part d runs on device d's own commit pipe (made
+// on first use with the default chunk size).  Arguments and outputs as
+// mh_precommit_batch; entry-indexed inputs keep their absolute indexing.
+extern "C" int mh_multi_precommit_batch(mh_multi *m, int version, uint64_t max_width, uint64_t ntx,
+                                        const uint64_t *tx_off, const uint8_t *keys,
+                                        const uint64_t *key_off, const uint8_t *md,
+                                        const uint64_t *md_off, const uint8_t *vals,
+                                        const uint64_t *val_off, const uint8_t *hval_override,
+                                        const uint8_t *use_override, const uint8_t *expect_eh,
+                                        uint8_t *hvals_out, uint8_t *eh_out, int32_t *status) {
+    return mh_guard([&]() -> int {
+        if (!m) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(m->mu);
+        if (m->pipe.empty()) m->pipe.assign(m->K, nullptr);
+        auto pipe = [&](int d) -> int {
+            return m->pipe[d] ? MH_OK : mh_commit_pipe_new(m->ctx[d], 0, &m->pipe[d]);
+        };
+        if (m->K == 1 || ntx < (uint64_t)m->K) {
+            if (int e = pipe(0)) return e;
+            return mh_precommit_batch(m->pipe[0], version, max_width, ntx, tx_off, keys, key_off, md,
+                                      md_off, vals, val_off, hval_override, use_override, expect_eh,
+                                      hvals_out, eh_out, status);
+        }
+        if (!tx_off || !val_off || !status) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(tx_off, ntx)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(val_off + tx_off[0], tx_off[ntx] - tx_off[0])) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const std::vector<uint64_t> t =
+            split_by_bytes(ntx, m->K, [&](uint64_t i) { return val_off[tx_off[i]]; });
+        return per_device(m->K, [&](int d) -> int {
+            const uint64_t lo = t[d], hi = t[d + 1];
+            if (hi == lo) return MH_OK;
+            if (int e = pipe(d)) return e;
+            return mh_precommit_batch(m->pipe[d], version, max_width, hi - lo, tx_off + lo, keys,
+                                      key_off, md, md_off, vals, val_off, hval_override, use_override,
+                                      expect_eh ? expect_eh + 32 * lo : nullptr,
+                                      hvals_out ? hvals_out + 32 * (tx_off[lo] - tx_off[0]) : nullptr,
+                                      eh_out ? eh_out + 32 * lo : nullptr, status + lo);
+        });
     });
 }

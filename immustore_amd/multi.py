@@ -188,6 +188,57 @@ class MultiDevice:
             _addr(ct), _addr(s), _addr(t), _addr(sa), _addr(ta), _addr(st)))
         return st
 
+    def verify_values(self, vals, off, hvals, vlen=None):
+        """merkle.verify_values over the devices (mh_multi_verify_values_batch:
+        parts of nearly equal value bytes) -> (corrupted count, status[n])."""
+        off = np.ascontiguousarray(off, np.uint64)
+        n = len(off) - 1
+        v = np.ascontiguousarray(vals, np.uint8)
+        hv = np.ascontiguousarray(hvals, np.uint8)
+        vl = None if vlen is None else np.ascontiguousarray(vlen, np.uint64)
+        st = np.zeros(max(n, 1), np.int32)
+        bad = C.c_uint64()
+        N.check(N.load().mh_multi_verify_values_batch(
+            self.handle, n, _addr(v) if v.size else None, _addr(off), _addr(vl), _addr(hv),
+            _addr(st), C.byref(bad)))
+        return bad.value, st[:n]
+
+    def verify_dual_proof_v2_pb_batch(self, msgs, src, tgt, src_alh, tgt_alh):
+        """txlayer.verify_dual_proof_v2_pb_batch over the devices (parts of
+        nearly equal message bytes) -> status[n]."""
+        from .txlayer import _d32
+        n = len(msgs)
+        if n == 0:
+            return np.zeros(0, np.int32)
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in msgs], dtype=np.uint64)
+        buf = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+        s_, t_ = np.asarray(src, np.uint64), np.asarray(tgt, np.uint64)
+        sa, ta = _d32(src_alh, n), _d32(tgt_alh, n)
+        st = np.zeros(n, np.int32)
+        N.check(N.load().mh_multi_verify_dual_proof_v2_pb_batch(
+            self.handle, n, _addr(buf), _addr(off), _addr(s_), _addr(t_), _addr(sa), _addr(ta),
+            _addr(st)))
+        return st
+
+    def precommit_csr(self, version: int, tx_off, keys, key_off, vals, val_off, md=None,
+                      md_off=None, hval_override=None, use_override=None, expect_eh=None,
+                      max_width: int = 0):
+        """commit.CommitPipe.precommit_csr over the devices
+        (mh_multi_precommit_batch: whole transactions, parts of nearly equal
+        value bytes, a commit pipe per device) -> (hvals, eh, status)."""
+        tx_off = np.ascontiguousarray(tx_off, np.uint64)
+        ntx = len(tx_off) - 1
+        ne = int(tx_off[-1] - tx_off[0]) if ntx > 0 else 0
+        hv = np.zeros((max(ne, 1), 32), np.uint8)
+        eh = np.zeros((max(ntx, 1), 32), np.uint8)
+        st = np.zeros(max(ntx, 1), np.int32)
+        N.check(N.load().mh_multi_precommit_batch(
+            self.handle, version, max_width, ntx, _addr(tx_off), _addr(keys), _addr(key_off),
+            _addr(md), _addr(md_off), _addr(vals), _addr(val_off), _addr(hval_override),
+            _addr(use_override), _addr(expect_eh), _addr(hv), _addr(eh), _addr(st)))
+        return hv[:ne], eh[:ntx], st[:ntx]
+
     def txlog_validate(self, buf, max_entries: int = 1024, max_key_len: int = 1024,
                        max_txs=None, out=None):
         """txlayer.txlog_validate over the devices (mh_multi_txlog_validate:

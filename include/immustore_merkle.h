@@ -804,6 +804,27 @@ int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t len, uint3
                             uint32_t max_key_len, uint64_t max_txs, uint64_t *ntx,
                             uint64_t *consumed, mh_tx_header *hdrs, uint8_t *alh,
                             int32_t *status);
+/* More PCIe-bound batches over the K devices, each part on its own link, cut
+ * into parts of nearly equal input bytes: readValueAt's hVal check
+ * (immustore.go:3183-3240; *ncorrupted summed over the parts), the fused
+ * DualProofV2 wire verify (database_protoconv.go:226-262 +
+ * verification.go:303-372), and precommit's hashing (immustore.go:1620-1632;
+ * whole transactions per part, each device with its own commit pipe made on
+ * first use).  Arguments and outputs as mh_verify_values_batch,
+ * mh_verify_dual_proof_v2_pb_batch and mh_precommit_batch. */
+int mh_multi_verify_values_batch(mh_multi *m, uint64_t n, const uint8_t *vals, const uint64_t *off,
+                                 const uint64_t *vlen, const uint8_t *hvals, int32_t *status,
+                                 uint64_t *ncorrupted);
+int mh_multi_verify_dual_proof_v2_pb_batch(mh_multi *m, uint64_t n, const uint8_t *msgs,
+                                           const uint64_t *msg_off, const uint64_t *src,
+                                           const uint64_t *tgt, const uint8_t *src_alh,
+                                           const uint8_t *tgt_alh, int32_t *status);
+int mh_multi_precommit_batch(mh_multi *m, int version, uint64_t max_width, uint64_t ntx,
+                             const uint64_t *tx_off, const uint8_t *keys, const uint64_t *key_off,
+                             const uint8_t *md, const uint64_t *md_off, const uint8_t *vals,
+                             const uint64_t *val_off, const uint8_t *hval_override,
+                             const uint8_t *use_override, const uint8_t *expect_eh,
+                             uint8_t *hvals_out, uint8_t *eh_out, int32_t *status);
 
 /* ------------------------------------------------------------ wire formats
  * proofs as the protobuf messages the gRPC server sends

@@ -463,3 +463,72 @@ def test_multi_verify_batches_vs_single_and_oracle(m, orc, fixtures, devices):
     finally:
         md.close()
         ctx.close()
+
+
+@pytest.mark.parametrize("devices", _SPLIT_DEVICES)
+def test_multi_values_wire_precommit_vs_single_and_oracle(m, orc, fixtures, devices):
+    """mh_multi_verify_values_batch, mh_multi_verify_dual_proof_v2_pb_batch
+    and mh_multi_precommit_batch (parts of nearly equal input bytes, one per
+    listed device): the same statuses / hashes as one single-context call and
+    the oracle -- ragged values with 10 % corrupted and offsets not starting
+    at 0 (immustore.go:3235), the fixture stores' device-written DualProofV2
+    messages with flipped bytes (verification.go:303-372), and 300 random
+    transactions with KV metadata, truncated values and two expected-Eh
+    mismatches (immustore.go:1620-1654)."""
+    from immustore_amd import txlayer
+    from immustore_amd.multi import MultiDevice
+    from commit_util import random_batch
+    from test_oracle import _values_case
+    from tx_util import headers_from_fixture
+    ctx = m.Context(0)
+    md = MultiDevice(devices)
+    try:
+        # values
+        vb, off, hv, vlen, bad = _values_case(11, 2000)
+        pad = np.concatenate([np.zeros(5, np.uint8), vb])
+        c, st = md.verify_values(pad, off + np.uint64(5), hv, vlen)
+        oc, ost = orc.verify_values(vb, off, hv, vlen)
+        assert c == oc == int(bad.sum()) and np.array_equal(st, ost), devices
+        c1, st1 = m.verify_values(pad, off + np.uint64(5), hv, vlen, ctx=ctx)
+        assert c1 == c and np.array_equal(st1, st)
+        # DualProofV2 messages over the wire form
+        rng = np.random.default_rng(5)
+        for name, fx in fixtures.items():
+            pay = np.stack([np.frombuffer(bytes.fromhex(p), np.uint8) for p in fx["aht_payloads"]])
+            t = m.AHtree(ctx)
+            try:
+                t.append_batch(pay)
+                recs, blob, alhs = headers_from_fixture(fx["txs"])
+                cases = [(c_["src"], c_["tgt"]) for c_ in fx["dual_v2"] if c_["src"] <= c_["tgt"]]
+                S = np.array([a for a, _ in cases], np.uint64)
+                T = np.array([b for _, b in cases], np.uint64)
+                msgs, _ = t.dual_proof_v2_pb_batch(recs[S.astype(int) - 1], recs[T.astype(int) - 1],
+                                                   blob)
+            finally:
+                t.close()
+            msgs = list(msgs)
+            for k in range(0, len(msgs), 3):  # every third message with a flipped byte
+                b = bytearray(msgs[k])
+                b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+                msgs[k] = bytes(b)
+            SA = [alhs[int(x) - 1] for x in S]
+            TA = [alhs[int(x) - 1] for x in T]
+            single = txlayer.verify_dual_proof_v2_pb_batch(msgs, S, T, SA, TA, ctx=ctx)
+            got = md.verify_dual_proof_v2_pb_batch(msgs, S, T, SA, TA)
+            assert np.array_equal(got, single), (devices, name)
+            assert (got[1::3] == 0).all() or len(got) < 2
+        # precommit
+        for version in (0, 1):
+            b = random_batch(np.random.default_rng(40 + version), 300, version=version,
+                             md_prob=0.2 if version else 0.0)
+            hv_o, eh_o, st_o = orc.precommit_batch(version, **b)
+            hv2, eh2, st2 = md.precommit_csr(version, **b)
+            assert np.array_equal(st2, st_o) and np.array_equal(eh2, eh_o), (devices, version)
+            assert np.array_equal(hv2, hv_o), (devices, version)
+            exp = eh_o.copy()
+            exp[[7, 250], 1] ^= 0x40
+            _, eh3, st3 = md.precommit_csr(version, expect_eh=exp, **b)
+            assert sorted(np.nonzero(st3)[0].tolist()) == [7, 250] and np.array_equal(eh3, eh_o)
+    finally:
+        md.close()
+        ctx.close()
