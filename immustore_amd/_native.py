@@ -305,6 +305,7 @@ SIGNATURES = {
     "mh_multi_txlog_validate": (i32, [vp, u8p, u64, u32, u32, u64, C.POINTER(u64),
                                       C.POINTER(u64), vp, u8p, vp]),
     "mh_multi_verify_values_batch": (i32, [vp, u64, u8p, vp, vp, u8p, vp, C.POINTER(u64)]),
+    "mh_multi_verify_document_batch": (i32, [vp, vp, vp, u8p]),
     "mh_multi_verify_dual_proof_v2_pb_batch": (i32, [vp, u64, u8p, vp, vp, vp, u8p, u8p, vp]),
     "mh_multi_precommit_batch": (i32, [vp, i32, u64, u64, vp, u8p, vp, u8p, vp, u8p, vp, u8p,
                                        u8p, u8p, u8p, u8p, vp]),

@@ -1169,3 +1169,45 @@ extern "C" int mh_multi_precommit_batch(mh_multi *m, int version, uint64_t max_w
         });
     });
 }
+
+// pkg/verification.VerifyDocument's hashing part (verification.go:37-196)
+// for n documents, split into K parts of nearly equal work (entries + document
+// bytes): part d is the same batch with its per-document arrays advanced to
+// its first document; entry, term and byte arrays are indexed through the
+// offsets, which index them directly, so they are shared.
+extern "C" int mh_multi_verify_document_batch(mh_multi *m, const mh_document_batch *batch,
+                                              int32_t *status, uint8_t *target_alh_out) {
+    return mh_guard([&]() -> int {
+        if (!m || !batch) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const uint64_t n = batch->n;
+        if (m->K == 1 || n < (uint64_t)m->K)
+            return mh_verify_document_batch(m->ctx[0], batch, status, target_alh_out);
+        const mh_document_batch &B = *batch;
+        if (!B.doc_off || !B.doc_key_off || !B.tx_hdr || !B.ent_off || !B.src_hdr || !B.tgt_hdr ||
+            !B.incl_off || !B.cons_off || !B.known_tx_id || !B.known_alh || !status)
+            return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (!monotonic(B.ent_off, n) || !monotonic(B.doc_off, n)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        const std::vector<uint64_t> t = split_by_bytes(n, m->K, [&](uint64_t i) {
+            return (B.ent_off[i] - B.ent_off[0]) * 64 + (B.doc_off[i] - B.doc_off[0]);
+        });
+        std::lock_guard<std::mutex> lk(m->mu);
+        return per_device(m->K, [&](int d) -> int {
+            const uint64_t lo = t[d], hi = t[d + 1];
+            if (hi == lo) return MH_OK;
+            mh_document_batch P = B;
+            P.n = hi - lo;
+            P.doc_off = B.doc_off + lo;
+            P.doc_key_off = B.doc_key_off + lo;
+            P.tx_hdr = B.tx_hdr + lo;
+            P.ent_off = B.ent_off + lo;
+            P.src_hdr = B.src_hdr + lo;
+            P.tgt_hdr = B.tgt_hdr + lo;
+            P.incl_off = B.incl_off + lo;
+            P.cons_off = B.cons_off + lo;
+            P.known_tx_id = B.known_tx_id + lo;
+            P.known_alh = B.known_alh + 32 * lo;
+            return mh_verify_document_batch(m->ctx[d], &P, status + lo,
+                                            target_alh_out ? target_alh_out + 32 * lo : nullptr);
+        });
+    });
+}

@@ -221,6 +221,21 @@ class MultiDevice:
             _addr(st)))
         return st
 
+    def verify_document_batch(self, docs):
+        """txlayer.verify_document_batch over the devices
+        (mh_multi_verify_document_batch) -> (status[n], target_alh[n, 32])."""
+        from .txlayer import pack_document_batch
+        n = len(docs)
+        if n == 0:
+            return np.zeros(0, np.int32), np.zeros((0, 32), np.uint8)
+        b, keep = pack_document_batch(docs)
+        st = np.zeros(n, np.int32)
+        alh = np.zeros((n, 32), np.uint8)
+        N.check(N.load().mh_multi_verify_document_batch(self.handle, C.byref(b), _addr(st),
+                                                        _addr(alh)))
+        del keep
+        return st, alh
+
     def precommit_csr(self, version: int, tx_off, keys, key_off, vals, val_off, md=None,
                       md_off=None, hval_override=None, use_override=None, expect_eh=None,
                       max_width: int = 0):

@@ -819,6 +819,10 @@ int mh_multi_verify_dual_proof_v2_pb_batch(mh_multi *m, uint64_t n, const uint8_
                                            const uint64_t *msg_off, const uint64_t *src,
                                            const uint64_t *tgt, const uint8_t *src_alh,
                                            const uint8_t *tgt_alh, int32_t *status);
+/* VerifyDocument's hashing part (verification.go:37-196) over the devices:
+ * parts of nearly equal entries + document bytes, as mh_verify_document_batch. */
+int mh_multi_verify_document_batch(mh_multi *m, const mh_document_batch *batch, int32_t *status,
+                                   uint8_t *target_alh_out);
 int mh_multi_precommit_batch(mh_multi *m, int version, uint64_t max_width, uint64_t ntx,
                              const uint64_t *tx_off, const uint8_t *keys, const uint64_t *key_off,
                              const uint8_t *md, const uint64_t *md_off, const uint8_t *vals,

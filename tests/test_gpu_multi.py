@@ -532,3 +532,56 @@ def test_multi_values_wire_precommit_vs_single_and_oracle(m, orc, fixtures, devi
     finally:
         md.close()
         ctx.close()
+
+
+@pytest.mark.parametrize("devices", _SPLIT_DEVICES)
+def test_multi_verify_document_batch_vs_single_and_oracle(m, orc, devices):
+    """mh_multi_verify_document_batch (parts of nearly equal entries +
+    document bytes; each part's per-document arrays start past 0, the shared
+    entry / byte arrays are indexed through them): the statuses and new-state
+    Alh values of one single-context call and of the oracle's VerifyDocument
+    (verification.go:37-196) -- 60 documents of 1-700 entries, every third
+    with a tampered entry."""
+    import struct
+    from immustore_amd import txlayer
+    from immustore_amd.multi import MultiDevice
+    from tx_util import TX_HEADER
+    rng = np.random.default_rng(23)
+    docs = []
+    for k in range(60):
+        ne = int(rng.integers(1, 700)) if k % 4 else int(rng.integers(1, 5))
+        ents = []
+        for e in range(ne):
+            key = b"doc/%d/%d" % (k, e)
+            md_ = [b"", b"\x00", b"\x02", b"\x01" + struct.pack(">Q", e)][e % 4]
+            ents.append((key, md_, bytes(rng.integers(0, 256, 32, dtype=np.uint8))))
+        j = int(rng.integers(0, ne))
+        doc = bytes(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8))
+        ents[j] = (ents[j][0], ents[j][1], orc.sha256(doc))
+        digs = np.frombuffer(b"".join(orc.entry_digest(1, a, b_, c)[1] for a, b_, c in ents),
+                             np.uint8).reshape(-1, 32)
+        eh = orc.htree_build(digs)[1]
+        h = np.zeros(1, TX_HEADER)
+        h["id"], h["bl_tx_id"], h["version"], h["nentries"] = 100 + k, 99 + k, 1, ne
+        h["eh"] = np.frombuffer(eh, np.uint8)
+        h["ts"] = 1_700_000_000 + k
+        alh = orc.tx_header_alh(h[0])[2]
+        if k % 3 == 2:
+            i = (j + 1) % ne
+            ents[i] = (ents[i][0], ents[i][1], bytes([ents[i][2][0] ^ 0x80]) + ents[i][2][1:])
+        docs.append({"encoded_document": doc, "doc_key": ents[j][0], "tx_hdr": h[0],
+                     "entries": ents, "src_hdr": h[0], "tgt_hdr": h[0], "incl": [], "cons": [],
+                     "known_tx_id": 100 + k, "known_alh": alh})
+    ctx = m.Context(0)
+    md = MultiDevice(devices)
+    try:
+        st1, alh1 = txlayer.verify_document_batch(docs, ctx=ctx)
+        st, alh = md.verify_document_batch(docs)
+        assert np.array_equal(st, st1) and np.array_equal(alh, alh1), devices
+        for k, d in enumerate(docs):
+            ost, oalh = orc.verify_document(d)
+            assert int(st[k]) == ost, (devices, k)
+            assert alh[k].tobytes() == (oalh if ost == 0 else bytes(32))
+    finally:
+        md.close()
+        ctx.close()
