@@ -1035,7 +1035,7 @@ def run_single(a):
         prewarm(step, sync, a.prewarm)
         # (the call's ~25 launches would carry ~0.15 ms of timing events)
         t = timed_k(ctx, step, a.steps, a.warmup, sync)
-        names = ("txlog_wave", "txlog_blk", "txlog_group", "tx_hdr_from_raw", "txe_index", "txe_leaf",
+        names = ("txlog_lanes", "txlog_wave", "txlog_blk", "txlog_group", "tx_hdr_from_raw", "txe_index", "txe_leaf",
                  "small_roots", "seg_level", "tx_alh")
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
         # breakdown: the host hop alone (mh_txlog_scan, no headers out) and a

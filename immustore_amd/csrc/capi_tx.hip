@@ -1064,13 +1064,17 @@ static uint64_t txlog_chunks() {
     return k;
 }
 
-// relative sizes of a pinned log's copy chunks, first to last: 4 : 2 : 1 : 1 --
-// with uniform records the groups' k_txlog_wave launches are then whole rounds
-// of resident waves (two per SIMD: 4096, 2048, 1024, 1024 waves for 2^16
-// records), 0.59 instead of 0.70 ms of kernels per call at the same end-to-end
-// time as 4 : 3 : 2 : 1 (profiles/txlog_weights_r04.txt); MH_TXLOG_CHUNKS=K
-// gives K : K-1 : ... : 1, MH_TXLOG_WEIGHTS="w0:w1:..." any sizes (read per
-// call, A/B; up to 16 positive numbers separated by ':' or ',')
+// relative sizes of a pinned log's copy chunks, first to last: 5 : 2 : 1.
+// The first two groups take the lane-per-record kernel (k_txlog_lanes, >=
+// 16384 records of 2^16), whose launch over 5/8 of the log finishes under the
+// next chunk's copy; the last group (1/8) takes the wave kernel, the shorter
+// chain per record after the last byte lands.  One chunk boundary fewer than
+// round 4's 4 : 2 : 1 : 1: 1.529-1.535 vs 1.555-1.568 ms per call, 3
+// interleaved rounds (profiles/txlog_lanes_r05.txt; 6 : 1 : 1 ties, 7 : 1
+// and 13 : 2 : 1 overrun the last copy, 11 : 4 : 1 and 9 : 4 : 2 : 1 lose).
+// MH_TXLOG_CHUNKS=K gives K : K-1 : ... : 1, MH_TXLOG_WEIGHTS="w0:w1:..."
+// any sizes (read per call, A/B; up to 16 positive numbers separated by ':'
+// or ',')
 static std::vector<double> txlog_weights() {
     std::vector<double> w;
     if (const char *e = getenv("MH_TXLOG_WEIGHTS")) {
@@ -1083,7 +1087,7 @@ static std::vector<double> txlog_weights() {
             p = q + 1;
         }
     }
-    if (w.empty() && !getenv("MH_TXLOG_CHUNKS")) w = {4, 2, 1, 1};
+    if (w.empty() && !getenv("MH_TXLOG_CHUNKS")) w = {5, 2, 1};
     if (w.empty())
         for (uint64_t k = txlog_chunks(); k >= 1; k--) w.push_back((double)k);
     return w;
@@ -1158,7 +1162,7 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         // unguarded block over-read pad), inside the allocation
         if (len && !dlog) MH_HIP(c->s_txlog.ensure(len + 256));
         uint8_t *dbuf = dlog ? const_cast<uint8_t *>(dlog) : c->s_txlog.as<uint8_t>();
-        // A pinned log: 4 chunks from 16 MiB up (txlog_weights: 4 : 2 : 1 : 1;
+        // A pinned log: 3 chunks from 16 MiB up (txlog_weights: 5 : 2 : 1;
         // the last chunk's device work is the tail after the copy), all
         // queued from this thread at once.  A
         // pageable one is staged by the runtime inside each copy call, so a

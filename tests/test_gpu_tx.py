@@ -204,9 +204,9 @@ def test_txlog_validate_parallel_hop(m, ctx, orc):
     same(raw, max_txs=4321)
 
 
-def _chunk_cuts(n, weights=(4, 2, 1, 1)):
+def _chunk_cuts(n, weights=(5, 2, 1)):
     """mh_txlog_validate's copy chunks of a pinned n-byte log (from 16 MiB,
-    sizes 4 : 2 : 1 : 1 by default, cut at 4 KiB multiples)."""
+    sizes 5 : 2 : 1 by default, cut at 4 KiB multiples)."""
     tot, pre, cuts = float(sum(weights)), 0.0, []
     for w in weights[:-1]:
         pre += w
@@ -214,14 +214,19 @@ def _chunk_cuts(n, weights=(4, 2, 1, 1)):
     return cuts
 
 
-def test_txlog_validate_chunk_phases(m, ctx, orc):
-    """From 16 MiB the log goes up in 4 copy chunks and the hop runs in one
+@pytest.mark.parametrize("weights", [None, "4:2:1:1"])
+def test_txlog_validate_chunk_phases(m, ctx, orc, monkeypatch, weights):
+    """From 16 MiB the log goes up in copy chunks (5 : 2 : 1 by default, and
+    round 4's 4 : 2 : 1 : 1 through MH_TXLOG_WEIGHTS) and the hop runs in one
     phase per chunk (the records ending inside a chunk are validated while the
     rest is copied and parsed): errors on either side of every cut and in the
     records that straddle them, max_txs at a cut, a cut short of a record,
     non-canonical metadata (patched records) and wide txs (tree plan) in the
     first or the last chunk -- all equal to the one-pass oracle."""
     from tx_util import metadata_logs
+    if weights:
+        monkeypatch.setenv("MH_TXLOG_WEIGHTS", weights)
+    wts = tuple(int(x) for x in weights.split(":")) if weights else (5, 2, 1)
     rng = np.random.default_rng(5)
     raw, starts = _bulk_txlog(rng, 9000)
     assert len(raw) >= (16 << 20)
@@ -233,7 +238,7 @@ def test_txlog_validate_chunk_phases(m, ctx, orc):
         assert list(a[5]) == list(b[4]) and np.array_equal(a[4], b[3]), kw
         return a
 
-    for cut in _chunk_cuts(len(raw)):
+    for cut in _chunk_cuts(len(raw), wts):
         j = max(k for k in range(len(starts)) if starts[k] < cut)  # straddles the cut
         for k in (j - 1, j, j + 1):
             bad = bytearray(raw)
@@ -246,7 +251,7 @@ def test_txlog_validate_chunk_phases(m, ctx, orc):
         for mt in (j - 1, j, j + 1):
             a = same(raw, max_txs=mt)
             assert a[1] == mt
-    cut = _chunk_cuts(len(raw))[0]
+    cut = _chunk_cuts(len(raw), wts)[0]
     j = max(k for k in range(len(starts)) if starts[k] < cut)
     same(raw[:starts[j + 1]] + bytes(len(raw) - starts[j + 1]))  # zero tail from the first cut
     same(raw[:len(raw) - 5])
