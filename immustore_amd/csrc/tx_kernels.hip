@@ -2549,12 +2549,25 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
 #define MH_TXL(l_, c_)                                                                             \
     hipLaunchKernelGGL((k_txlog_lanes<l_, c_>), grid, blk, sh, st, ntx, buf, rec_off, alh_off,   \
                        leaf_off, hdrs, eh_out, alh_out, status, ho, lgp, dep, fence, log_len, probe)
-    if (chk) {
+    if (chk) {  // diagnosis: the launch is synchronous and fails on any out-of-range read
+        unsigned zero = 0, viol = 0;
+        hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_txl_viol), &zero, sizeof zero, 0,
+                                              hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
         if (lgl == 0) MH_TXL(0, true);
         else if (lgl == 1) MH_TXL(1, true);
         else if (lgl == 2) MH_TXL(2, true);
         else if (lgl == 3) MH_TXL(3, true);
         else MH_TXL(4, true);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        e = hipMemcpyFromSymbolAsync(&viol, HIP_SYMBOL(g_txl_viol), sizeof viol, 0,
+                                     hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        if (viol) {
+            fprintf(stderr, "txlog_lanes: %u out-of-range reads\n", viol);
+            return hipErrorIllegalAddress;
+        }
     } else {
         if (lgl == 0) MH_TXL(0, false);
         else if (lgl == 1) MH_TXL(1, false);
