@@ -1360,12 +1360,16 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                 const bool wave = !(kn && strcmp(kn, "group") == 0);
                 const bool blk = kn && strcmp(kn, "blk") == 0;
                 const bool lanes = kn ? strcmp(kn, "lanes") == 0 : nt >= lanes_min;
-                // MH_TXLOG_HOST_HDRS=1 (read per call, A/B): the last chunk's
-                // group -- its kernel is the tail of the call -- writes only
-                // the Eh words of the caller's pinned headers; the host fills
-                // the other fields from the log while that kernel runs
+                // The last chunk's group -- its kernel is the tail of the call
+                // -- writes only the Eh words of the caller's pinned headers;
+                // the host fills the other fields from the log while that
+                // kernel runs (32 instead of 136 B per record over PCIe at the
+                // end: -4..-10 us per call in 9 of 10 interleaved rounds with
+                // the 5 : 2 : 1 chunks, profiles/txlog_lanes_r05.txt).
+                // MH_TXLOG_HOST_HDRS=0 (read per call, A/B) turns it off.
                 const char *hh_env = getenv("MH_TXLOG_HOST_HDRS");
-                if (wave && ho.hdrs && hh_env && atoi(hh_env) == 1 && g.early && g.k + 1 == nck) {
+                const bool host_hdrs = !(hh_env && atoi(hh_env) == 0);
+                if (wave && ho.hdrs && host_hdrs && g.early && g.k + 1 == nck) {
                     ho.eh_only = 1;
                     g.host_hdrs = true;
                 }
