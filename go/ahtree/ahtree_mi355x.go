@@ -28,30 +28,11 @@ import (
 	"github.com/codenotary/immudb/embedded/internal/mi355x"
 )
 
-var (
-	multiOnce sync.Once
-	multi     *C.mh_multi
-	multiErr  error
-)
-
-// devices returns the clique over every visible GPU (mh_multi_create: one
-// context per device and an RCCL clique inside the library).
+// devices returns the process-wide clique over every visible GPU
+// (mi355x.Multi).
 func devices() (*C.mh_multi, error) {
-	multiOnce.Do(func() {
-		var n C.int
-		if st := C.mh_device_count(&n); st != C.MH_OK || n < 1 {
-			multiErr = mi355x.ErrNoDevice
-			return
-		}
-		devs := make([]C.int, int(n))
-		for i := range devs {
-			devs[i] = C.int(i)
-		}
-		if st := C.mh_multi_create(n, &devs[0], &multi); st != C.MH_OK {
-			multiErr = mapErr(st)
-		}
-	})
-	return multi, multiErr
+	m, err := mi355x.Multi()
+	return (*C.mh_multi)(m), err
 }
 
 func mapErr(st C.int) error {

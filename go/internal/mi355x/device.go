@@ -39,6 +39,35 @@ func Context() (unsafe.Pointer, error) {
 	return unsafe.Pointer(ctx), ctxErr
 }
 
+var (
+	multiOnce sync.Once
+	multi     *C.mh_multi
+	multiErr  error
+)
+
+// Multi returns the process-wide clique over every visible GPU
+// (mh_multi_create: one context per device, an RCCL clique inside the
+// library), created on first use: the batch paths bound by one device's PCIe
+// link (tx-log validation, value checks, precommit batches, proof batches)
+// split their input over it, each part over its own link.
+func Multi() (unsafe.Pointer, error) {
+	multiOnce.Do(func() {
+		var n C.int
+		if st := C.mh_device_count(&n); st != C.MH_OK || n < 1 {
+			multiErr = ErrNoDevice
+			return
+		}
+		devs := make([]C.int, int(n))
+		for i := range devs {
+			devs[i] = C.int(i)
+		}
+		if st := C.mh_multi_create(n, &devs[0], &multi); st != C.MH_OK {
+			multiErr = Status(int(st))
+		}
+	})
+	return unsafe.Pointer(multi), multiErr
+}
+
 // StatusError is a C ABI status with no Go sentinel of its own.
 type StatusError struct {
 	Code int

@@ -4,7 +4,9 @@
 // precommit / preCommitWith for many transactions at once
 // (immustore.go:1620-1632, 2301-2313, with ReplicateTx's Eh check
 // :1649-1654), readValueAt's integrity check over many values (:3235) and
-// the read-path re-hash of a run of tx-log records (tx.go:388-630).  Single
+// the read-path re-hash of a run of tx-log records (tx.go:388-630), each
+// split over every GPU of the process (mi355x.Multi, the mh_multi_* forms:
+// one part per device over its own PCIe link).  Single
 // small transactions keep the reference's CPU path (a 16 KiB transaction is
 // 10 us on one SHA-NI core against ~300 us through the device queue,
 // DESIGN.md section 5).  Uncompiled in the build image (no Go toolchain); see
@@ -108,25 +110,23 @@ func (p *packed) pack(txs [][]*EntrySpec) error {
 // truncated), the entry digests of the header version and one htree per
 // transaction -> Eh.  expectEh (nil, or one per tx) is ReplicateTx's check
 // (immustore.go:1649-1654): a mismatch is ErrIllegalArguments for that tx.
+// The batch runs over every GPU of the process-wide clique
+// (mh_multi_precommit_batch: whole transactions, parts of nearly equal value
+// bytes, each device with its own commit pipe); the clique serialises calls.
 type PrecommitBatch struct {
-	pipe *C.mh_commit_pipe
-	p    packed
+	multi *C.mh_multi
+	p     packed
 }
 
 func NewPrecommitBatch() (*PrecommitBatch, error) {
-	c, err := mi355x.Context()
+	m, err := mi355x.Multi()
 	if err != nil {
 		return nil, err
 	}
-	b := &PrecommitBatch{}
-	if st := C.mh_commit_pipe_new((*C.mh_ctx)(c), 0 /* 64 MiB chunks */, &b.pipe); st != C.MH_OK {
-		return nil, mapErr(st)
-	}
-	return b, nil
+	return &PrecommitBatch{multi: (*C.mh_multi)(m)}, nil
 }
 
 func (b *PrecommitBatch) Close() {
-	C.mh_commit_pipe_free(b.pipe)
 	b.p.arena.Free()
 }
 
@@ -147,7 +147,7 @@ func (b *PrecommitBatch) Run(version int, maxTxEntries int, txs [][]*EntrySpec,
 	hv := make([][sha256.Size]byte, ne+1)
 	copy(hv, b.p.hvOverride)
 	use := append(b.p.useOverride, 0)
-	st := C.mh_precommit_batch(b.pipe, C.int(version), C.uint64_t(maxTxEntries), C.uint64_t(ntx),
+	st := C.mh_multi_precommit_batch(b.multi, C.int(version), C.uint64_t(maxTxEntries), C.uint64_t(ntx),
 		(*C.uint64_t)(unsafe.Pointer(&b.p.txOff[0])),
 		(*C.uint8_t)(unsafe.Add(base, b.p.keys)), (*C.uint64_t)(unsafe.Pointer(&b.p.keyOff[0])),
 		(*C.uint8_t)(unsafe.Add(base, b.p.md)), (*C.uint64_t)(unsafe.Pointer(&b.p.mdOff[0])),
@@ -184,7 +184,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 	if n == 0 {
 		return nil, nil
 	}
-	c, err := mi355x.Context()
+	m, err := mi355x.Multi()
 	if err != nil {
 		return nil, err
 	}
@@ -206,7 +206,8 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 	}
 	status := make([]int32, n)
 	var bad C.uint64_t
-	st := C.mh_verify_values_batch((*C.mh_ctx)(c), C.uint64_t(n), (*C.uint8_t)(arena.Ptr()),
+	// parts of nearly equal value bytes, one per GPU (mh_multi_verify_values_batch)
+	st := C.mh_multi_verify_values_batch((*C.mh_multi)(m), C.uint64_t(n), (*C.uint8_t)(arena.Ptr()),
 		(*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint64_t)(unsafe.Pointer(&lens[0])),
 		(*C.uint8_t)(unsafe.Pointer(&hVal[0][0])), (*C.int32_t)(unsafe.Pointer(&status[0])), &bad)
 	if st != C.MH_OK {
@@ -232,7 +233,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 // record at consumed.
 func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha256.Size]byte,
 	errs []error, consumed uint64, err error) {
-	c, e := mi355x.Context()
+	m, e := mi355x.Multi()
 	if e != nil {
 		return nil, nil, 0, e
 	}
@@ -243,7 +244,9 @@ func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha25
 	if len(buf) > 0 {
 		p = (*C.uint8_t)(unsafe.Pointer(&buf[0]))
 	}
-	st := C.mh_txlog_validate((*C.mh_ctx)(c), p, C.uint64_t(len(buf)), C.uint32_t(maxEntries),
+	// the records cut at record boundaries into one part per GPU, each copied
+	// and validated over its own link (mh_multi_txlog_validate)
+	st := C.mh_multi_txlog_validate((*C.mh_multi)(m), p, C.uint64_t(len(buf)), C.uint32_t(maxEntries),
 		C.uint32_t(maxKeyLen), C.uint64_t(maxTxs), &ntx, &used, nil,
 		(*C.uint8_t)(unsafe.Pointer(&alhs[0][0])), (*C.int32_t)(unsafe.Pointer(&status[0])))
 	errs = make([]error, int(ntx))
