@@ -244,6 +244,19 @@ int main(int argc, char **argv) {
         good = 0;
         for (uint64_t q = 0; q + 1 < np; q++) good += vst[q] == MH_OK;
         printf("wire_verify_tampered %d %llu\n", vst[np - 1], (unsigned long long)good);
+        {
+            /* the same batch over a clique listing device 0 three times
+             * (mh_multi_verify_dual_proof_v2_pb_batch: parts of nearly equal
+             * message bytes, one per context): the single call's statuses */
+            int devs3[3] = {0, 0, 0};
+            mh_multi *m3;
+            int32_t *mst = malloc(np * 4);
+            CHECK(mh_multi_create(3, devs3, &m3));
+            CHECK(mh_multi_verify_dual_proof_v2_pb_batch(m3, np, msgs, off, si, ti, sa, ta, mst));
+            printf("multi3_wire_verify_equal %d\n", memcmp(mst, vst, np * 4) == 0);
+            CHECK(mh_multi_destroy(m3));
+            free(mst);
+        }
         CHECK(mh_ahtree_free(st));
         free(h); free(alh); free(sh); free(th); free(si); free(ti); free(off); free(sa); free(ta);
         free(pst); free(vst); free(msgs);

@@ -101,6 +101,7 @@ def test_c_client_matches_oracle(w, m):
     assert out["wire_verify_ok"] == "40/40"
     code, rest = out["wire_verify_tampered"].split()
     assert int(code) != 0 and rest == "39"
+    assert out["multi3_wire_verify_equal"] == "1"  # the mh_multi_* split, from plain C
 
     t = O.AHtree(cap=m)
     t.append_batch(p)
