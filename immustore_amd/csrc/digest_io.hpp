@@ -39,12 +39,16 @@ __device__ __forceinline__ uint32_t ld_guard(const uint32_t *p, const uint8_t *l
     return (b + 4 > lo && b < hi) ? *p : 0u;
 }
 
+// bswap(alignbyte(hi, lo, al)) -- the big-endian message word at byte al of
+// the 8 bytes lo || hi -- as ONE v_perm: output byte k is byte 3 - k + al
+__device__ __forceinline__ uint32_t be_sel(uint32_t al) { return 0x00010203u + al * 0x01010101u; }
+
 __device__ inline void sha256_bytes(const uint8_t *p, uint64_t len, int pre, uint32_t out[8]) {
     State s;
     s.init();
     const uint64_t L = len + (pre >= 0 ? 1 : 0);   // virtual message length
     const uint8_t *q = p - (pre >= 0 ? 1 : 0);       // virtual byte 0 address
-    const uint32_t al = (uint32_t)((uintptr_t)q & 3);
+    const uint32_t al = (uint32_t)((uintptr_t)q & 3), sel = be_sel(al);
     const uint32_t *base = reinterpret_cast<const uint32_t *>(q - al);
     const uint8_t *end = p + len;
     const uint64_t nfull = L >> 6;
@@ -60,7 +64,7 @@ __device__ inline void sha256_bytes(const uint8_t *p, uint64_t len, int pre, uin
             d[16] = al ? ld_guard(qq + 16, p, end) : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        for (int j = 0; j < 16; j++) w[j] = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
         if (b == 0 && pre >= 0) w[0] = (w[0] & 0x00ffffffu) | ((uint32_t)pre << 24);
         compress(s, w);
     }
@@ -71,7 +75,7 @@ __device__ inline void sha256_bytes(const uint8_t *p, uint64_t len, int pre, uin
     for (int j = 0; j < 17; j++) d[j] = ld_guard(qq + j, p, end);
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        uint32_t x = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
+        uint32_t x = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
         const int v = (int)rem - 4 * j;  // valid bytes in this word
         const uint32_t m = v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu << (32 - 8 * v)));
         x &= m;
@@ -110,13 +114,13 @@ __device__ inline void sha256_skip12(const uint8_t *p, uint32_t la, uint32_t out
     State s;
     s.init();
     const uint32_t L = la + 32;
-    const uint32_t al = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t al = (uint32_t)((uintptr_t)p & 3), sel = be_sel(al);
     const uint32_t *base = reinterpret_cast<const uint32_t *>(p - al);
     const uint8_t *end = p + la + 44;
     const uint32_t nfull = L >> 6;
     auto word = [&](const uint32_t d[20], int j, uint32_t x0) {
-        const uint32_t w1 = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
-        const uint32_t w2 = bswap(__builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], al));
+        const uint32_t w1 = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
+        const uint32_t w2 = __builtin_amdgcn_perm(d[j + 4], d[j + 3], sel);
         const int v = (int)la - (int)(x0 + 4 * j);  // head bytes in this word
         const uint32_t m = v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : (0xffffffffu << (32 - 8 * v)));
         return (w1 & m) | (w2 & ~m);

@@ -920,20 +920,35 @@ __device__ __forceinline__ void skip12_load(const uint8_t *p, uint32_t b, uint32
 #pragma unroll
     for (int j = 0; j < 20; j++) d[j] = qq[j];
 }
+// Message words j = 0..15 of block b from the 20 dwords d[] read at the
+// block's aligned start (al = p & 3, hv0 = la - 64 b): the head bytes, then
+// the hVal 12 bytes further on, cut at the message end (la + 32 - 64 b) with
+// the 0x80 marker after it.  Each word's bytes come out of one v_perm (the
+// byte-aligned window and the big-endian swap in one selector); the end mask
+// of word j is the head mask of word j - 8 (the message ends 32 bytes after
+// the head), and the marker is the one byte by which the end mask of a
+// message one byte longer, (em_j >> 8) | (em_{j-1} << 24), exceeds em_j --
+// 25 masks for the 48 masks and markers of the direct form.
+__device__ __forceinline__ void skip12_assemble(const uint32_t d[20], uint32_t al, int hv0,
+                                                uint32_t w[16]) {
+    const uint32_t sel = be_sel(al);
+    uint32_t hm[25];  // hm[k] = head_mask(hv0 - 4 (k - 9)): words -9..15
+#pragma unroll
+    for (int k = 0; k < 25; k++) hm[k] = head_mask(hv0 - 4 * (k - 9));
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t w1 = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
+        const uint32_t w2 = __builtin_amdgcn_perm(d[j + 4], d[j + 3], sel);
+        const uint32_t x = __builtin_amdgcn_bitop3_b32(hm[j + 9], w1, w2, 0xCA);  // head ? w1 : w2
+        const uint32_t em = hm[j + 1], nm = __builtin_amdgcn_alignbit(hm[j], em, 8);
+        w[j] = __builtin_amdgcn_bitop3_b32(em, x, nm & 0x80808080u, 0xCA);  // message ? x : marker
+    }
+}
 // the block's message words from those dwords (al = p & 3)
 __device__ __forceinline__ void skip12_words(const uint32_t d[20], uint32_t al, uint32_t la,
                                              uint32_t b, uint32_t nb, uint32_t w[16]) {
     const uint32_t L = la + 32;
-    const int hv0 = (int)la - (int)(b * 64), v0 = (int)L - (int)(b * 64);
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t w1 = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
-        const uint32_t w2 = bswap(__builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], al));
-        const int v = v0 - 4 * j;
-        const uint32_t pad = (uint32_t)(0x80000000ull >> (8 * (v < 0 ? 5 : min(v, 4))));
-        const uint32_t x = __builtin_amdgcn_bitop3_b32(head_mask(hv0 - 4 * j), w1, w2, 0xCA);
-        w[j] = __builtin_amdgcn_bitop3_b32(x, head_mask(v), pad, 0xEA);
-    }
+    skip12_assemble(d, al, (int)la - (int)(b * 64), w);
     if (b + 1 == nb) {
         w[14] = 0;
         w[15] = L * 8;
@@ -955,18 +970,7 @@ __device__ __forceinline__ void skip12_block(const uint8_t *p, uint32_t la, uint
 #pragma unroll
         for (int j = 0; j < 20; j++) d[j] = qq[j];
     }
-    const int hv0 = (int)la - (int)(b * 64), v0 = (int)L - (int)(b * 64);
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t w1 = bswap(__builtin_amdgcn_alignbyte(d[j + 1], d[j], al));
-        const uint32_t w2 = bswap(__builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], al));
-        const int v = v0 - 4 * j;  // message bytes left at this word
-        const uint32_t pad = (uint32_t)(0x80000000ull >> (8 * (v < 0 ? 5 : min(v, 4))));
-        // head bytes from w1, hVal bytes from w2, then cut at the message end
-        // and the 0x80 marker (two bitop3)
-        const uint32_t x = __builtin_amdgcn_bitop3_b32(head_mask(hv0 - 4 * j), w1, w2, 0xCA);
-        w[j] = __builtin_amdgcn_bitop3_b32(x, head_mask(v), pad, 0xEA);
-    }
+    skip12_assemble(d, al, (int)la - (int)(b * 64), w);
     if (b + 1 == nb) {
         w[14] = 0;
         w[15] = L * 8;
