@@ -1035,7 +1035,7 @@ def run_single(a):
         prewarm(step, sync, a.prewarm)
         # (the call's ~25 launches would carry ~0.15 ms of timing events)
         t = timed_k(ctx, step, a.steps, a.warmup, sync)
-        names = ("txlog_lanes", "txlog_wave", "txlog_blk", "txlog_group", "tx_hdr_from_raw", "txe_index", "txe_leaf",
+        names = ("txlog_lanes", "txlog_wave", "tx_hdr_from_raw", "txe_index", "txe_leaf",
                  "small_roots", "seg_level", "tx_alh")
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in names}
         # breakdown: the host hop alone (mh_txlog_scan, no headers out) and a
@@ -1071,8 +1071,7 @@ def run_single(a):
         # kernel_ms is the kernel's own time) and into the caller's pinned
         # arrays (the kernel stores 172 B per record over PCIe itself)
         for kern, tname, o in (("lanes", "txlog_lanes", None), ("wave", "txlog_wave", None),
-                               ("blk", "txlog_blk", None), ("lanes", "txlog_lanes", outs),
-                               ("wave", "txlog_wave", outs)):
+                               ("lanes", "txlog_lanes", outs), ("wave", "txlog_wave", outs)):
             os.environ["MH_TXLOG_KERNEL"] = kern
 
             def step_res():
@@ -1090,6 +1089,45 @@ def run_single(a):
             os.environ.pop("MH_TXLOG_KERNEL", None)
         else:
             os.environ["MH_TXLOG_KERNEL"] = kvar
+        # the same resident log indexed by its commit log (mh_txlog_validate_clog:
+        # no host copy, no host hop -- the structure pass, the lane kernel and
+        # a status summary on the device; results into device arrays)
+        from immustore_amd.txlayer import txlog_validate_clog
+        import struct as _st
+        clog = b"".join(_st.pack(">QI", k * rec, rec) for k in range(ntx))
+        dcl = torch.frombuffer(bytearray(clog), dtype=torch.uint8).to(dev)
+        d_alh = torch.empty(ntx * 32, dtype=torch.uint8, device=dev)
+        d_sts = torch.empty(ntx, dtype=torch.int32, device=dev)
+        d_out = (None, d_alh.data_ptr(), d_sts.data_ptr())
+
+        def step_clog():
+            r = txlog_validate_clog(dres.data_ptr(), raw.size, None, ntx=ntx, clog_dev=dcl.data_ptr(),
+                                    ctx=ctx, out=d_out)
+            assert r[0] == 0 and r[1] == 0 and r[2] == ntx
+
+        prewarm(step_clog, sync, a.prewarm)
+        tcl = timed_k(ctx, step_clog, a.steps, a.warmup, sync)
+        k_struct = ctx.timing("txlog_struct")[0] / (a.steps + a.warmup)
+        k_lanes = ctx.timing("txlog_lanes")[0] / (a.steps + a.warmup)
+        got_alh = d_alh.view(ntx, 32).cpu().numpy()
+        samp = np.unique(np.random.default_rng(3).integers(0, ntx, 256))
+        orc = _oracle()  # (after the timed region: the checker, not the measured path)
+        o_alh, o_sts = orc.txlog_validate_clog(raw_pageable, b"".join(clog[12 * k:12 * k + 12] for k in samp))
+        clog_ok = bool(np.array_equal(got_alh, alh) and np.array_equal(got_alh[samp], o_alh)
+                       and not o_sts.any() and not d_sts.cpu().numpy().any())
+        dbad = dres.clone()
+        dbad[(ntx // 2) * rec + hdr + 4 + kl + 12] ^= 1  # one hVal of the middle record
+        rb = txlog_validate_clog(dbad.data_ptr(), raw.size, clog, ctx=ctx)
+        clog_bad_ok = rb[1] == 1 and rb[2] == ntx // 2 and rb[5][ntx // 2] == 14
+        del dbad
+        resident["clog"] = {"ms_per_call": round(tcl * 1e3, 3),
+                            "kernel_ms": {"txlog_struct": round(k_struct, 4),
+                                          "txlog_lanes": round(k_lanes, 4)},
+                            "root_check": {"vs": "oracle (256 sampled records) + the sealed Alh",
+                                           "ok": clog_ok and clog_bad_ok}}
+        if not (clog_ok and clog_bad_ok):
+            print(json.dumps({"clog_check_failed": True}), file=sys.stderr)
+            sys.exit(1)
         del dres
         _, _, _, _, _, sts = m.txlog_validate(raw, ctx=ctx)
         bad = raw_pageable.copy()

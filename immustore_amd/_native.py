@@ -317,6 +317,8 @@ SIGNATURES = {
                                 u8p, vp]),
     "mh_txlog_validate_resident": (i32, [vp, u8p, u8p, u64, u32, u32, u64, C.POINTER(u64),
                                          C.POINTER(u64), vp, u8p, vp]),
+    "mh_txlog_validate_clog": (i32, [vp, vp, u64, vp, u64, u32, u32, u32, vp, vp, vp,
+                                     C.POINTER(u64), C.POINTER(u64)]),
     "mh_commit_pipe_new": (i32, [vp, u64, C.POINTER(vp)]),
     "mh_commit_pipe_free": (i32, [vp]),
     "mh_precommit_batch": (i32, [vp, i32, u64, u64, vp, u8p, vp, u8p, vp, u8p, vp, u8p, u8p, u8p,

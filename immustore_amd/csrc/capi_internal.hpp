@@ -188,6 +188,7 @@ struct mh_ctx {
     DevBuf s_tx, s_tree;  // tx layer (capi_tx.hip)
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
+    DevBuf s_clog;        // mh_txlog_validate_clog's per-record arrays
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
     // mh_txlog_validate's groups (one per copy chunk): device arrays and
     // pinned index staging of each, kept across calls
@@ -291,12 +292,9 @@ struct ChunkCopier {
         // the copies overwrite device buffers that work queued earlier on the
         // context's stream may still read: the copy streams wait for it, unless
         // that stream is idle already (a cross-queue wait ahead of the first
-        // copy delays its start; MH_COPY_WAIT0=1 always waits, A/B)
-        static const bool always = [] {
-            const char *e = getenv("MH_COPY_WAIT0");
-            return e && atoi(e) != 0;
-        }();
-        if (always || !idle) {
+        // copy delays its start: -20..-50 us per a14 call,
+        // profiles/ab_txlog_wait0_flags_r04.txt)
+        if (!idle) {
             if (hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_done[0], 0)) return e;
             if (hipError_t e = hipStreamWaitEvent(c->copy_stream2, c->ev_done[0], 0)) return e;
         }
@@ -390,13 +388,9 @@ inline bool pinned_same_alloc(const void *a, const void *b) {
 // Without the system-scope fence: every waiter on these events is a device
 // stream (the host waits on streams), and the fence held each chunk's
 // consumer ~4 us longer (-12..-19 us per a14 call in three interleaved
-// rounds, profiles/ab_txlog_evfence_r04.txt).  MH_EV_NOFENCE=0 (read once)
-// restores it.
+// rounds, profiles/ab_txlog_evfence_r04.txt).
 inline hipError_t ensure_chunk_events(mh_ctx *c, size_t n) {
-    static const unsigned flags = [] {
-        const char *e = getenv("MH_EV_NOFENCE");
-        return e && !atoi(e) ? hipEventDisableTiming : hipEventDisableTiming | hipEventDisableSystemFence;
-    }();
+    const unsigned flags = hipEventDisableTiming | hipEventDisableSystemFence;
     while (c->ev_chunks.size() < n) {
         hipEvent_t e;
         if (hipError_t r = hipEventCreateWithFlags(&e, flags)) return r;

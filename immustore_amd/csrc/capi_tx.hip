@@ -1035,13 +1035,9 @@ extern "C" int mh_txlog_scan(const uint8_t *buf, uint64_t len, uint32_t max_entr
 
 // The device address of [p, p + bytes) when the whole range is pinned host
 // memory the kernels can store to (one registration or allocation, word
-// aligned), else null.  MH_TXLOG_KERNEL_STORES=0 turns the path off.
+// aligned), else null.
 static uint32_t *host_words(void *p, uint64_t bytes) {
-    static const bool on = [] {
-        const char *e = getenv("MH_TXLOG_KERNEL_STORES");
-        return !(e && e[0] == '0');
-    }();
-    if (!on || !p || !bytes || ((uintptr_t)p & 3) || (bytes & 3)) return nullptr;
+    if (!p || !bytes || ((uintptr_t)p & 3) || (bytes & 3)) return nullptr;
     hipPointerAttribute_t a, b;
     if (hipPointerGetAttributes(&a, p) != hipSuccess ||
         hipPointerGetAttributes(&b, (uint8_t *)p + bytes - 1) != hipSuccess) {
@@ -1054,16 +1050,6 @@ static uint32_t *host_words(void *p, uint64_t bytes) {
     return (uint32_t *)a.devicePointer;
 }
 
-// copy chunks of a long tx log: MH_TXLOG_CHUNKS (1..16, read once), default 4
-static uint64_t txlog_chunks() {
-    static const uint64_t k = [] {
-        const char *e = getenv("MH_TXLOG_CHUNKS");
-        const long v = e ? strtol(e, nullptr, 10) : 4;
-        return (uint64_t)std::min(16l, std::max(1l, v));
-    }();
-    return k;
-}
-
 // relative sizes of a pinned log's copy chunks, first to last: 5 : 2 : 1.
 // The first two groups take the lane-per-record kernel (k_txlog_lanes, >=
 // 16384 records of 2^16), whose launch over 5/8 of the log finishes under the
@@ -1072,9 +1058,8 @@ static uint64_t txlog_chunks() {
 // round 4's 4 : 2 : 1 : 1: 1.529-1.535 vs 1.555-1.568 ms per call, 3
 // interleaved rounds (profiles/txlog_lanes_r05.txt; 6 : 1 : 1 ties, 7 : 1
 // and 13 : 2 : 1 overrun the last copy, 11 : 4 : 1 and 9 : 4 : 2 : 1 lose).
-// MH_TXLOG_CHUNKS=K gives K : K-1 : ... : 1, MH_TXLOG_WEIGHTS="w0:w1:..."
-// any sizes (read per call, A/B; up to 16 positive numbers separated by ':'
-// or ',')
+// MH_TXLOG_WEIGHTS="w0:w1:..." gives any sizes (read per call, tests: up to
+// 16 positive numbers separated by ':' or ',')
 static std::vector<double> txlog_weights() {
     std::vector<double> w;
     if (const char *e = getenv("MH_TXLOG_WEIGHTS")) {
@@ -1087,9 +1072,7 @@ static std::vector<double> txlog_weights() {
             p = q + 1;
         }
     }
-    if (w.empty() && !getenv("MH_TXLOG_CHUNKS")) w = {5, 2, 1};
-    if (w.empty())
-        for (uint64_t k = txlog_chunks(); k >= 1; k--) w.push_back((double)k);
+    if (w.empty()) w = {5, 2, 1};
     return w;
 }
 
@@ -1120,40 +1103,20 @@ static void fill_header_host(const uint8_t *buf, uint64_t rec, uint64_t *h) {
     h[16] = ver ? (uint64_t)ml | ((uint64_t)(uint32_t)(rec + 92) << 32) : 0;
 }
 
-// MH_TXLOG_TRACE=1: host timestamps of the call's phases on stderr (A/B
-// measurements of the copy / hop / device overlap)
-namespace {
-struct PhaseTrace {
-    bool on;
-    std::chrono::steady_clock::time_point t0;
-    char buf[512];
-    int n = 0;
-    PhaseTrace() : on(getenv("MH_TXLOG_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
-    void mark(const char *what) {
-        if (!on || n > 400) return;
-        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-        n += snprintf(buf + n, sizeof buf - n, " %s=%.0f", what, us);
-    }
-    ~PhaseTrace() {
-        if (on) fprintf(stderr, "txlog_trace%s\n", buf);
-    }
-};
-}  // namespace
-
 // buf: the log in host memory (the hop parses it); dlog: the same bytes
 // already resident on the device (no copy; nullptr: copied from buf in chunks)
 static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlog, uint64_t len,
                                uint32_t max_entries, uint32_t max_key_len, uint64_t max_txs,
                                uint64_t *ntx_out, uint64_t *consumed_out, mh_tx_header *hdrs_out,
-                               uint8_t *alh_out, int32_t *status_out) {
+                               uint8_t *alh_out, int32_t *status_out, bool take_lock = true) {
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        PhaseTrace tr;
         // The raw records go to the device first, in chunks with an event
         // after each: the copy (DMA when buf is pinned) runs under the host
         // hop, and the device work on the records of a chunk starts as soon as
         // it has landed, under the copy of the rest.
-        std::lock_guard<std::mutex> lk(c->mu);
+        std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+        if (take_lock) lk.lock();  // (mh_txlog_validate_clog holds it already)
         hipSetDevice(c->device);
         MH_HIP(c->copy_lane());
         hipStream_t st = c->stream;
@@ -1172,16 +1135,8 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         // waiters are device streams), ev_results[0, K) the end of each
         // group's kernels (with the fence: c->d2h_stream's copies of a
         // group's results may run on a DMA engine).
-        bool pinned = false;
-        {
-            static const int inl = [] {
-                const char *e = getenv("MH_TXLOG_INLINE_COPY");
-                return e ? atoi(e) : 1;
-            }();
-            // the whole range in one pinned allocation (first and last byte)
-            pinned = inl && len && !dlog && pinned_same_alloc(buf, buf + len - 1);
-        }
-        tr.mark("attrs");
+        // the whole range in one pinned allocation (first and last byte)
+        const bool pinned = len && !dlog && pinned_same_alloc(buf, buf + len - 1);
         const std::vector<double> wts = pinned ? txlog_weights() : std::vector<double>{3, 1};
         // (a resident log: one chunk without a copy, i.e. one group after the hop)
         const uint64_t K = dlog || len < (16ull << 20) ? 1 : wts.size();
@@ -1196,47 +1151,30 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         const uint64_t nck = len ? K : 0;
         MH_HIP(ensure_chunk_events(c, nck));
         MH_HIP(ensure_result_events(c, nck));
-        tr.mark("events");
         // once a group's kernels are queued they may store into the caller's
         // pinned status / alh / header arrays: every exit (errors included)
         // waits for both streams, so nothing writes caller memory after return
+        // (every group on the context's stream: a second compute stream for
+        // alternate groups slowed the last one, profiles/ab_txlog_streams_r04.txt)
         struct StreamGuard {
-            hipStream_t a, b, c2;
+            hipStream_t a, b;
             bool armed = true;  // cleared once the call's own final waits ran
             ~StreamGuard() {
                 if (!armed) return;
                 hipStreamSynchronize(a);
                 hipStreamSynchronize(b);
-                hipStreamSynchronize(c2);
             }
-        } stream_guard{st, c->d2h_stream, c->stream2};
-        // MH_TXLOG_STREAMS=2 (A/B, read per call): early groups alternate
-        // between the context's stream and a second compute stream, so a
-        // group's kernel never waits behind the previous group's.  Off by
-        // default: with k_txlog_wave a group's kernel ends before the next
-        // chunk lands, and two groups sharing the CUs slowed the last one
-        // (profiles/ab_txlog_streams_r04.txt)
-        const char *nse = getenv("MH_TXLOG_STREAMS");
-        const bool two_streams = nse && atoi(nse) == 2;
-        auto gstream = [&](uint64_t k) { return two_streams && (k & 1) ? c->stream2 : st; };
+        } stream_guard{st, c->d2h_stream};
         ChunkCopier cc(c);
         cc.chunks.resize(nck);
         for (uint64_t k = 0; k < nck; k++)
             cc.chunks[k] = {{dbuf + cut[k], buf + cut[k], dlog ? 0 : cut[k + 1] - cut[k]}};
         cc.inline_issue = pinned;
-        {  // MH_TXLOG_COPY_LANES=2: chunk k on copy stream k % 2 (A/B, read per call)
-            const char *cl = getenv("MH_TXLOG_COPY_LANES");
-            if (cl && atoi(cl) == 2 && pinned) cc.lanes = 2;
-        }
         MH_HIP(cc.start());
-        // the second compute stream starts after everything queued on the
-        // context's stream before this call too (cc.start() recorded ev_done[0])
-        if (two_streams) MH_HIP(hipStreamWaitEvent(c->stream2, c->ev_done[0], 0));
         auto join_copies = [&]() -> int {
             hipError_t e = cc.join();
             return e == hipSuccess ? MH_OK : -(int)e;
         };
-        tr.mark("copies_started");
         const HopLimits lim{max_entries, max_key_len};
 
         // ---- one group of records: its own device arrays (per entry record
@@ -1248,7 +1186,8 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             bool small = true, fetched = false, host_done = false, early = false, host_hdrs = false;
             uint8_t *base = nullptr;
             uint64_t *pro = nullptr, *pap = nullptr, *plo = nullptr;
-            uint64_t b_rec, b_ver, b_lv, b_h, b_es, b_ro, b_ap, b_lo, b_eh, b_s, b_a, b_st, idx_bytes;
+            uint64_t b_rec, b_ver, b_lv, b_h, b_es, b_ro, b_ap, b_lo, b_eh, b_s, b_a, b_st, b_pre, b_stats,
+                idx_bytes;
             TreePlan P;
         };
         HopOut hop;
@@ -1280,6 +1219,8 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             g.b_s = L.add(nt * kTxInnerStride);
             g.b_a = L.add(nt * 32);
             g.b_st = L.add(nt * 4);
+            g.b_pre = L.add(nt * 4);
+            g.b_stats = L.add(4 * 8);
             MH_HIP(c->s_txg[gi].ensure(L.total));
             g.base = c->s_txg[gi].as<uint8_t>();
             g.idx_bytes = 3 * (nt + 1) * 8;
@@ -1314,8 +1255,12 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         // trees one lane / wave per tree, a group with a wide tx through the
         // host tree plan), Alh with the rebuilt Eh vs the stored one
         // (tx.go:623-627).  pl: the group's metadata patch lists (below).
+        // pre (resident logs): the per-record statuses of the device bytes'
+        // structure (txlog_struct.hip) -- filled here for the fused kernels,
+        // by the caller for the chain -- so no kernel walks a length of the
+        // resident log that differs from the host copy's.
         auto run = [&](Grp &g, const uint8_t *db, const uint64_t *pl, uint64_t npe,
-                       uint64_t nph, hipStream_t st) -> int {
+                       uint64_t nph, hipStream_t st, int32_t *pre) -> int {
             const uint64_t nt = g.t1 - g.t0;
             uint8_t *base = g.base;
             uint64_t *ro = (uint64_t *)(base + g.b_ro), *ap = (uint64_t *)(base + g.b_ap),
@@ -1324,17 +1269,11 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             MhTxHeader *hd = (MhTxHeader *)(base + g.b_h);
             if (!g.fetched)
                 MH_HIP(launch_fetch_host(st, HostRuns{{g.pro, g.pap, g.plo}, {ro, ap, lo}, {nt, nt, nt + 1}}));
-            static const bool fused = [] {
-                const char *e = getenv("MH_TXLOG_FUSED");
-                return !e || atoi(e) != 0;
-            }();
-            // MH_TXLOG_BULK=chain (read per call, A/B): groups whose chunk is
-            // not the last one -- their kernels run under a later chunk's copy,
-            // so only throughput counts -- take the six-launch chain (every
-            // phase lane-parallel), the last group the fused kernel (latency)
-            const char *bk = getenv("MH_TXLOG_BULK");
-            const bool bulk_chain = bk && strcmp(bk, "chain") == 0 && g.early && g.k + 1 < nck;
-            if (fused && !bulk_chain && g.small && npe + nph == 0) {  // the whole chain in one launch
+            if (g.small && npe + nph == 0) {  // the whole chain in one launch
+                if (pre)  // the resident bytes' structure against the host's
+                    MH_HIP(launch_txlog_struct(st, c->tm(), nt, db, len, nullptr, 0, ro, ap, lo,
+                                               max_entries, max_key_len, pre,
+                                               (uint64_t *)(base + g.b_stats)));
                 // pinned outputs: the kernel writes the results there itself
                 TxlogHostOut ho;
                 uint32_t *hs = status_out ? host_words(status_out + g.t0, nt * 4) : nullptr;
@@ -1347,48 +1286,31 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                     ho.hdrs = reinterpret_cast<uint64_t *>(hh);
                     g.host_done = true;
                 }
-                // MH_TXLOG_KERNEL=group | wave | blk | lanes (read per call: A/B
-                // tests); by default a group of >= MH_TXLOG_LANES_MIN records
-                // (16384) takes the lane-per-record kernel (throughput), a
-                // smaller one the wave kernel (its chain per record is shorter:
-                // the latency-shaped tail after the last chunk lands)
+                // a group of >= 16384 records takes the lane-per-record kernel
+                // (throughput), a smaller one the wave kernel (its chain per
+                // record is shorter: the latency-shaped tail after the last
+                // chunk lands).  MH_TXLOG_KERNEL=wave | lanes (read per call)
+                // forces one of them: the tests run both on the same logs.
                 const char *kn = getenv("MH_TXLOG_KERNEL");
-                static const uint64_t lanes_min = [] {
-                    const char *e = getenv("MH_TXLOG_LANES_MIN");
-                    return e ? strtoull(e, nullptr, 10) : 16384ull;
-                }();
-                const bool wave = !(kn && strcmp(kn, "group") == 0);
-                const bool blk = kn && strcmp(kn, "blk") == 0;
-                const bool lanes = kn ? strcmp(kn, "lanes") == 0 : nt >= lanes_min;
+                const bool lanes = kn ? strcmp(kn, "lanes") == 0 : nt >= 16384;
                 // The last chunk's group -- its kernel is the tail of the call
                 // -- writes only the Eh words of the caller's pinned headers;
                 // the host fills the other fields from the log while that
                 // kernel runs (32 instead of 136 B per record over PCIe at the
                 // end: -4..-10 us per call in 9 of 10 interleaved rounds with
                 // the 5 : 2 : 1 chunks, profiles/txlog_lanes_r05.txt).
-                // MH_TXLOG_HOST_HDRS=0 (read per call, A/B) turns it off.
-                const char *hh_env = getenv("MH_TXLOG_HOST_HDRS");
-                const bool host_hdrs = !(hh_env && atoi(hh_env) == 0);
-                if (wave && ho.hdrs && host_hdrs && g.early && g.k + 1 == nck) {
+                if (!lanes && ho.hdrs && g.early && g.k + 1 == nck) {
                     ho.eh_only = 1;
                     g.host_hdrs = true;
                 }
                 if (lanes)
-                    MH_HIP(launch_txlog_lanes(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
+                    MH_HIP(launch_txlog_lanes(st, c->tm(), nt, db, ro, ap, lo, pre, hd, base + g.b_eh,
                                               base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
                                               len));
-                else if (blk)
-                    MH_HIP(launch_txlog_blk(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
-                                            base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
-                                            g.pro, g.pap));
-                else if (wave)
-                    MH_HIP(launch_txlog_wave(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_eh,
+                else
+                    MH_HIP(launch_txlog_wave(st, c->tm(), nt, db, ro, ap, lo, pre, hd, base + g.b_eh,
                                              base + g.b_a, (int32_t *)(base + g.b_st), ho, g.wmax,
                                              g.pro, g.pap));
-                else
-                    MH_HIP(launch_txlog_group(st, c->tm(), nt, db, ro, ap, lo, hd, base + g.b_s,
-                                              base + g.b_eh, base + g.b_a,
-                                              (int32_t *)(base + g.b_st), ho, g.wmax));
                 return MH_OK;
             }
             MH_HIP(launch_tx_hdr_from_raw(st, c->tm(), nt, db, ro, hd, es));
@@ -1406,6 +1328,8 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             }
             MH_HIP(launch_tx_alh(st, c->tm(), nt, hd, db, base + g.b_eh, base + g.b_s, db, ap, nullptr,
                                  base + g.b_a, (int32_t *)(base + g.b_st)));
+            if (pre)  // records whose resident bytes differ from the host copy
+                MH_HIP(launch_txlog_apply_pre(st, nt, pre, (int32_t *)(base + g.b_st), base + g.b_a));
             if (hdrs_out)  // the device headers with the rebuilt Eh
                 MH_HIP(launch_put_eh(st, nt, base + g.b_eh, hd));
             return MH_OK;
@@ -1473,7 +1397,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         auto launch = [&](Grp &g) -> int {
             // the index arrays do not need the chunk: fetched before its event
             const uint64_t nt = g.t1 - g.t0;
-            hipStream_t st = gstream(g.k);
             MH_HIP(launch_fetch_host(
                 st, HostRuns{{g.pro, g.pap, g.plo},
                              {(uint64_t *)(g.base + g.b_ro), (uint64_t *)(g.base + g.b_ap),
@@ -1483,7 +1406,7 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             g.early = true;
             if (hipError_t e = cc.wait(g.k)) return -(int)e;
             MH_HIP(cc.stream_wait(st, g.k));
-            if (int e = run(g, dbuf, nullptr, 0, 0, st)) return e;
+            if (int e = run(g, dbuf, nullptr, 0, 0, st, nullptr)) return e;
             MH_HIP(hipEventRecord(c->ev_results[g.k], st));
             return results(g, c->ev_results[g.k]);
         };
@@ -1505,7 +1428,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             }
             hop.rc = h.rc;
             hop.end = pos + h.end;
-            tr.mark("hop");
             const bool more = k + 1 < nphase && hop.R.size() < max_txs &&
                               (h.rc == MH_ERR_TRUNCATED || (h.rc == MH_OK && hop.end + 8 > end));
             if (early && h.P.empty() && hop.R.size() > r0) {
@@ -1524,7 +1446,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                     if (deferred == gs.size() - 1 && cc.issued(k)) {
                         if (int e = launch(g)) return e;
                         deferred++;
-                        tr.mark("group");
                     }
                 }
             } else if (!h.P.empty()) {
@@ -1536,7 +1457,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         if (!nck) hop_all(buf, len, max_txs, lim, hop, false);  // empty log
         for (; deferred < gs.size(); deferred++) {
             if (int e = launch(gs[deferred])) return e;
-            tr.mark("group");
         }
         // header fields other than Eh of a host_hdrs group (readHeader,
         // tx.go:419-518, as k_txlog_wave lays them out: 17 words per record)
@@ -1544,7 +1464,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             if (g.host_hdrs)
                 for (uint64_t t = g.t0; t < g.t1; t++)
                     fill_header_host(buf, hop.R[t].rec, reinterpret_cast<uint64_t *>(hdrs_out + t));
-        tr.mark("host_hdrs");
         if (!gs.empty() && mh_fault(MH_FAULT_TXLOG_AFTER_GROUP)) return -(int)hipErrorOutOfMemory;
         const uint64_t ntx = hop.R.size();
         const int rc = hop.rc;
@@ -1552,7 +1471,6 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         if (ntx_out) *ntx_out = ntx;
         if (consumed_out) *consumed_out = hop.end;
         if (int e = join_copies()) return e;
-        tr.mark("joined");
         const uint64_t t_rest = gs.empty() ? 0 : gs.back().t1;
         if (t_rest < ntx) {
             // ---- the rest as one group once the whole log is in
@@ -1568,6 +1486,22 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             const uint8_t *db = dbuf;
             const uint64_t *pl = nullptr;
             uint64_t npe = 0, nph = 0;
+            int32_t *pre = dlog ? (int32_t *)(g.base + g.b_pre) : nullptr;
+            if (dlog && !(g.small && hop.P.empty())) {
+                // a resident log whose group the fused kernels do not take
+                // (re-encoded metadata, a wide tx): the chain runs over the
+                // host copy uploaded beside it, and a record whose resident
+                // bytes differ from that copy is corrupted (one byte compare)
+                const uint64_t nt = ntx - t_rest;
+                uint64_t *ro = (uint64_t *)(g.base + g.b_ro), *ap = (uint64_t *)(g.base + g.b_ap),
+                         *lo = (uint64_t *)(g.base + g.b_lo);
+                MH_HIP(c->s_txlog.ensure(len + 256));
+                MH_HIP(hipMemcpyAsync(c->s_txlog.as<uint8_t>(), buf, len, hipMemcpyHostToDevice, st));
+                MH_HIP(launch_fetch_host(st, HostRuns{{g.pro, g.pap, g.plo}, {ro, ap, lo}, {nt, nt, nt + 1}}));
+                g.fetched = true;
+                MH_HIP(launch_txlog_bytes_cmp(st, nt, dlog, c->s_txlog.as<uint8_t>(), ro, ap, pre));
+                db = dbuf = c->s_txlog.as<uint8_t>();
+            }
             if (!hop.P.empty()) {
                 std::vector<uint64_t> first_leaf(ntx - t_rest);  // group-local entry index
                 for (uint64_t t = t_rest, acc = 0; t < ntx; t++) {
@@ -1606,23 +1540,19 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                 db = nb;
                 pl = reinterpret_cast<const uint64_t *>(nb + po);
             }
-            if (int e = run(g, db, pl, npe, nph, st)) return e;
+            if (int e = run(g, db, pl, npe, nph, st, pre)) return e;
             MH_HIP(hipEventRecord(c->ev_done[1], st));
             if (int e = results(g, c->ev_done[1])) return e;
         }
         for (const auto &r : late)
             if (int e = results_dma(*r.first, r.second)) return e;
-        tr.mark("enqueued");
         // only the streams this call queued work on (every wait is an API
         // round trip on the critical path of the call)
         MH_HIP(hipStreamSynchronize(st));
         if (d2h_used) MH_HIP(hipStreamSynchronize(c->d2h_stream));
-        if (two_streams) MH_HIP(hipStreamSynchronize(c->stream2));
         stream_guard.armed = false;
         // buf stays the caller's once we return
         if (nck) MH_HIP(cc.sync());
-        tr.mark("done");
-        txlog_probe_report();
         return rc;
     });
 }
@@ -1660,3 +1590,186 @@ extern "C" int mh_txlog_validate_resident(mh_ctx *c, const uint8_t *buf, const u
     });
 }
 
+
+// The device range [p, p + bytes) lies in one allocation of the context's
+// device (hipMemGetAddressRange), or the address is not device memory at all.
+static bool dev_range(const void *p, uint64_t bytes) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t b = (uintptr_t)base, d = (uintptr_t)p;
+    return d >= b && d - b <= size && bytes <= size - (d - b);
+}
+
+// Where a kernel can store the caller's output array p of `bytes`: p itself
+// when it is device memory (its whole range in one allocation; *bad when it
+// is not), the device alias of pinned host memory, else null (staged on the
+// device and copied down).
+static void *kernel_dst(void *p, uint64_t bytes, bool *bad, bool *is_dev) {
+    *is_dev = false;
+    if (!p || !bytes) return nullptr;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;  // pageable host memory
+    }
+    if (a.type == hipMemoryTypeDevice) {
+        if (!dev_range(p, bytes)) *bad = true;
+        *is_dev = true;
+        return p;
+    }
+    if (a.type == hipMemoryTypeHost) return host_words(p, bytes);
+    return nullptr;
+}
+
+// a14 over a tx log that is already in HBM, indexed by its commit log
+// (txOffsetAndSize, immustore.go:2569-2597): no host copy and no host hop.
+// The structure pass (txlog_struct.hip) parses every record where its cLog
+// entry points, with every check of the host hop; the lane kernel hashes
+// the accepted ones (entry digests, htree, innerHash, Alh vs the stored Alh);
+// a record whose metadata is valid but not canonical (Go hashes the
+// re-serialised form) or that is wider than the lane kernel takes is
+// re-validated by mh_txlog_validate on a host copy of that record alone.
+extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t len,
+                                      const uint8_t *clog, uint64_t ntx, uint32_t clog_entry_size,
+                                      uint32_t max_entries, uint32_t max_key_len,
+                                      mh_tx_header *hdrs_out, uint8_t *alh_out,
+                                      int32_t *status_out, uint64_t *nbad_out,
+                                      uint64_t *first_bad_out) {
+    return mh_guard([&]() -> int {
+        const uint32_t es = clog_entry_size;
+        if (!c || (es != 12 && es != 44) || (ntx && (!dlog || !clog))) return MH_ERR_ILLEGAL_ARGUMENTS;
+        if (nbad_out) *nbad_out = 0;
+        if (first_bad_out) *first_bad_out = ntx;
+        if (!ntx) return MH_OK;
+        if (ntx > (1ull << 40)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStream_t st = c->stream;
+        // the kernels' unguarded block reads run up to 256 bytes past a record
+        if (!dev_range(dlog, len + 256)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        hipPointerAttribute_t ca;
+        const bool clog_dev = hipPointerGetAttributes(&ca, clog) == hipSuccess &&
+                              ca.type == hipMemoryTypeDevice;
+        (void)hipGetLastError();
+        if (clog_dev && !dev_range(clog, ntx * es)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        bool bad = false, st_dev, alh_dev, hd_dev;
+        uint32_t *k_st = (uint32_t *)kernel_dst(status_out, ntx * 4, &bad, &st_dev);
+        uint32_t *k_alh = (uint32_t *)kernel_dst(alh_out, ntx * 32, &bad, &alh_dev);
+        uint64_t *k_hd = (uint64_t *)kernel_dst(hdrs_out, ntx * sizeof(mh_tx_header), &bad, &hd_dev);
+        if (bad || ((uintptr_t)k_hd & 7)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        Layout L;
+        const uint64_t b_ro = L.add(ntx * 8), b_ao = L.add(ntx * 8), b_pre = L.add(ntx * 4),
+                       b_st = L.add(ntx * 4), b_eh = L.add(ntx * 32), b_a = L.add(ntx * 32),
+                       b_hd = L.add(hdrs_out && !k_hd ? ntx * sizeof(mh_tx_header) : 0),
+                       b_cl = L.add(clog_dev ? 0 : ntx * es), b_stats = L.add(4 * 8);
+        MH_HIP(c->s_clog.ensure(L.total));
+        uint8_t *base = c->s_clog.as<uint8_t>();
+        uint64_t *ro = (uint64_t *)(base + b_ro), *ao = (uint64_t *)(base + b_ao),
+                 *stats = (uint64_t *)(base + b_stats);
+        int32_t *pre = (int32_t *)(base + b_pre), *sts = (int32_t *)(base + b_st);
+        MhTxHeader *hd = hdrs_out && !k_hd ? (MhTxHeader *)(base + b_hd) : nullptr;
+        const uint8_t *dcl = clog_dev ? clog : base + b_cl;
+        MH_HIP(hipMemsetAsync(stats, 0, 3 * 8, st));
+        MH_HIP(hipMemsetAsync(stats + 3, 0xff, 8, st));
+        if (!clog_dev) MH_HIP(hipMemcpyAsync(base + b_cl, clog, ntx * es, hipMemcpyHostToDevice, st));
+        // 1. every record's structure where its cLog entry points
+        MH_HIP(launch_txlog_struct(st, c->tm(), ntx, dlog, len, dcl, es, ro, ao, nullptr, max_entries,
+                                   max_key_len, pre, stats));
+        MH_HIP(c->p_small.ensure(64));
+        volatile uint64_t *hs = c->p_small.as<volatile uint64_t>();
+        MH_HIP(hipMemcpyAsync((void *)hs, stats, 2 * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));  // the widest record sizes the lane kernel's launch
+        const uint64_t wmax = hs[0], nhost = hs[1];
+        // 2. the accepted records hashed and checked
+        TxlogHostOut ho;
+        ho.status = k_st;
+        ho.alh = k_alh;
+        ho.hdrs = k_hd;
+        MH_HIP(launch_txlog_lanes(st, c->tm(), ntx, dlog, ro, ao, nullptr, pre, hd, base + b_eh,
+                                  base + b_a, sts, ho, std::max<uint64_t>(wmax, 1), len));
+        // 3. records for the host hop (rare: a log not written by immudb)
+        struct Fix {
+            uint64_t t;
+            int32_t st;
+            mh_tx_header h;
+            uint8_t alh[32];
+        };
+        std::vector<Fix> fix;
+        if (nhost) {
+            std::vector<int32_t> hpre(ntx);
+            std::vector<uint64_t> hro(ntx);
+            std::vector<uint8_t> hcl(clog_dev ? ntx * es : 0);
+            MH_HIP(hipMemcpyAsync(hpre.data(), pre, ntx * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(hro.data(), ro, ntx * 8, hipMemcpyDeviceToHost, st));
+            if (clog_dev) MH_HIP(hipMemcpyAsync(hcl.data(), clog, ntx * es, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipStreamSynchronize(st));
+            const uint8_t *cl = clog_dev ? hcl.data() : clog;
+            for (uint64_t t = 0; t < ntx; t++) {
+                if (hpre[t] != kTxlNeedsHost) continue;
+                const uint64_t off = hro[t], size = be_at(cl + t * es + 8, 4);  // parsed: inside the log
+                std::vector<uint8_t> rb(size);
+                MH_HIP(hipMemcpyAsync(rb.data(), dlog + off, size, hipMemcpyDeviceToHost, st));
+                MH_HIP(hipStreamSynchronize(st));
+                Fix f{};
+                f.t = t;
+                uint64_t n = 0, used = 0;
+                int32_t one = 0;
+                const int rc = txlog_validate_impl(c, rb.data(), nullptr, size, max_entries, max_key_len,
+                                                   1, &n, &used, &f.h, f.alh, &one, false);
+                if (rc < 0) return rc;
+                // the structure pass's verdicts first (as the kernel's: then
+                // header and Alh 0), then the Alh compare
+                int s1 = rc != MH_OK ? rc : n != 1 ? MH_ERR_TRUNCATED : used != size ? MH_ERR_CORRUPTED_DATA : MH_OK;
+                if (s1 == MH_OK && es == 44 && memcmp(cl + t * es + 12, rb.data() + size - 32, 32))
+                    s1 = MH_ERR_CORRUPTED_DATA;
+                if (s1 != MH_OK) {
+                    memset(&f.h, 0, sizeof f.h);
+                    memset(f.alh, 0, 32);
+                }
+                f.st = s1 != MH_OK ? s1 : one;
+                if (f.h.version) f.h.md_off += (uint32_t)off;  // relative to the log, as the kernel's
+                fix.push_back(f);
+            }
+            MH_HIP(c->p_stage.ensure(fix.size() * sizeof(Fix)));
+            Fix *pf = c->p_stage.as<Fix>();
+            for (size_t k = 0; k < fix.size(); k++) pf[k] = fix[k];
+            for (size_t k = 0; k < fix.size(); k++) {  // into the device arrays the summary reads
+                const uint64_t t = pf[k].t;
+                MH_HIP(hipMemcpyAsync(sts + t, &pf[k].st, 4, hipMemcpyHostToDevice, st));
+                MH_HIP(hipMemcpyAsync(base + b_a + t * 32, pf[k].alh, 32, hipMemcpyHostToDevice, st));
+                if (hd) MH_HIP(hipMemcpyAsync(hd + t, &pf[k].h, sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
+                // device outputs get theirs here, host outputs after the sync
+                if (st_dev)
+                    MH_HIP(hipMemcpyAsync(status_out + t, &pf[k].st, 4, hipMemcpyHostToDevice, st));
+                if (alh_dev)
+                    MH_HIP(hipMemcpyAsync(alh_out + t * 32, pf[k].alh, 32, hipMemcpyHostToDevice, st));
+                if (hd_dev)
+                    MH_HIP(hipMemcpyAsync(hdrs_out + t, &pf[k].h, sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
+            }
+        }
+        // 4. how many records failed, and the first
+        MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
+        MH_HIP(hipMemcpyAsync((void *)(hs + 2), stats + 2, 2 * 8, hipMemcpyDeviceToHost, st));
+        if (status_out && !k_st) MH_HIP(hipMemcpyAsync(status_out, sts, ntx * 4, hipMemcpyDeviceToHost, st));
+        if (alh_out && !k_alh) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
+        if (hdrs_out && !k_hd)
+            MH_HIP(hipMemcpyAsync(hdrs_out, hd, ntx * sizeof(mh_tx_header), hipMemcpyDeviceToHost, st));
+        MH_HIP(hipStreamSynchronize(st));
+        if (!fix.empty()) {
+            const Fix *pf = c->p_stage.as<Fix>();
+            for (size_t k = 0; k < fix.size(); k++) {  // host outputs (pinned: the kernel wrote zeros)
+                const uint64_t t = pf[k].t;
+                if (status_out && !st_dev) status_out[t] = pf[k].st;
+                if (alh_out && !alh_dev) memcpy(alh_out + t * 32, pf[k].alh, 32);
+                if (hdrs_out && !hd_dev) hdrs_out[t] = pf[k].h;
+            }
+        }
+        if (nbad_out) *nbad_out = hs[2];
+        if (first_bad_out) *first_bad_out = hs[2] ? hs[3] : ntx;
+        return MH_OK;
+    });
+}

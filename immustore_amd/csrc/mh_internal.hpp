@@ -260,47 +260,71 @@ hipError_t launch_txlog_patch(hipStream_t st, uint64_t ne, const uint64_t *e_idx
                               const uint64_t *e_off, uint64_t *rec_off, uint64_t nh,
                               const uint64_t *h_idx, const uint64_t *h_val, MhTxHeader *hdrs);
 hipError_t launch_put_eh(hipStream_t st, uint64_t n, const uint8_t *eh, MhTxHeader *hdrs);
-// a14 for a group of records whose trees have <= 64 leaves, one launch:
-// headers, entry walk, entry digests + leaves, tx trees, Eh into hdrs and
-// eh_out, Alh vs the stored one (statuses).  Arrays are indexed from the
-// group's first record; leaf_off has ntx + 1 entries.
-// ho (device addresses of pinned host arrays, each member nullable, indexed
-// from the group's first record like the device arrays): results written
-// there by the kernel too.  hdrs 8-byte aligned, alh / status 4-byte.
+// The fused a14 kernels (tx.go:533-630 per record, one launch for a group of
+// records): headers, entry walk, entry digests + leaves, each tx's htree, Eh,
+// innerHash + Alh against the stored Alh (statuses).  Arrays are indexed from
+// the group's first record; leaf_off has ntx + 1 entries (nullable for
+// k_txlog_lanes: the entry count is then the header's, checked by the
+// structure pre-pass).  pre (nullable): the pre-pass statuses -- a record with
+// pre[t] != 0 is not walked, its status is pre[t] and its Alh / Eh / header 0.
+// ho (device addresses of pinned host arrays, or device arrays, each member
+// nullable, indexed like the device arrays): results written there by the
+// kernel too.  hdrs 8-byte aligned, alh / status 4-byte.
 struct TxlogHostOut {
     uint32_t *status = nullptr;
     uint32_t *alh = nullptr;
     uint64_t *hdrs = nullptr;
-    int eh_only = 0;  // k_txlog_wave: of hdrs, only the Eh words (the host writes the rest)
+    int eh_only = 0;  // of hdrs, only the Eh words (the host writes the rest)
 };
-hipError_t launch_txlog_group(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
-                              const uint64_t *rec_off, const uint64_t *alh_off,
-                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *scratch,
-                              uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
-                              const TxlogHostOut &ho, uint64_t wmax);
-// the same with one wave per 64 / L records (k_txlog_wave); h_rec_off /
-// h_alh_off: host-readable copies of rec_off / alh_off (the wave's LDS
-// staging is sized from them)
+// one wave per 64 / L records (k_txlog_wave, txlog_wave.hip), wmax <= 64;
+// h_rec_off / h_alh_off: host-readable copies of rec_off / alh_off (the
+// wave's LDS staging is sized from them)
 hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                              const uint64_t *rec_off, const uint64_t *alh_off,
-                             const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
-                             uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
-                             uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off);
-// the same with the phases spread over whole workgroups (k_txlog_blk)
-hipError_t launch_txlog_blk(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
-                            const uint64_t *rec_off, const uint64_t *alh_off,
-                            const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
-                            uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
-                            uint64_t wmax, const uint64_t *h_rec_off, const uint64_t *h_alh_off);
-// the same with every record on 1, 2 or 4 lanes, each lane's subtree serial (k_txlog_lanes)
+                             const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
+                             uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
+                             const TxlogHostOut &ho, uint64_t wmax, const uint64_t *h_rec_off,
+                             const uint64_t *h_alh_off);
+// every record on 1-16 lanes, each lane's subtree serial (k_txlog_lanes,
+// txlog_lanes.hip), wmax <= kTxlLanesMaxEntries; log_len: the log's length
+// (the checking build's range)
+constexpr uint64_t kTxlLanesMaxEntries = 1024;
 hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                               const uint64_t *rec_off, const uint64_t *alh_off,
-                              const uint64_t *leaf_off, MhTxHeader *hdrs, uint8_t *eh_out,
-                              uint8_t *alh_out, int32_t *status, const TxlogHostOut &ho,
-                              uint64_t wmax, uint64_t log_len);
-// MH_TXLOG_PROBE=1: per-phase wave timings of the last call's k_txlog_wave
-// launches on stderr (call after the call's final sync)
-void txlog_probe_report();
+                              const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
+                              uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
+                              const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len);
+// The device structure pass over tx-log records (txlog_struct.hip), one lane
+// per record, every check of the host hop (tx.go:419-588) on the device bytes:
+//  * clog != null (mh_txlog_validate_clog): record t at the offset of cLog
+//    entry t (BE64 offset || BE32 size [|| Alh], clog_es = 12 or 44 bytes,
+//    immustore.go:122-123, 2569-2597); writes rec_off / alh_off / leaf_off
+//    (leaf_off[t] = t's entry count, not a prefix);
+//  * clog == null (mh_txlog_validate_resident): rec_off / alh_off / leaf_off
+//    (prefix) from the host hop; the device bytes must parse to the same
+//    structure, else the record is MH_ERR_CORRUPTED_DATA.
+// pre[t]: the record's status (0, or the reader's error), kTxlNeedsHost for a
+// record whose metadata is valid but not canonical or that is wider than the
+// lanes kernel takes (the host re-validates those).  stats (device, zeroed by
+// the caller): [0] widest accepted record, [1] records needing the host.
+// Check mode: a record the device bytes give otherwise is MH_ERR_CORRUPTED_DATA.
+constexpr int32_t kTxlNeedsHost = 0x40000000;
+hipError_t launch_txlog_struct(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
+                               uint64_t len, const uint8_t *clog, uint32_t clog_es,
+                               uint64_t *rec_off, uint64_t *alh_off, uint64_t *leaf_off,
+                               uint32_t max_entries, uint32_t max_key_len, int32_t *pre,
+                               uint64_t *stats);
+// pre[t] = MH_ERR_CORRUPTED_DATA where a and b differ over record t's bytes
+// [rec_off[t], alh_off[t] + 32), else MH_OK
+hipError_t launch_txlog_bytes_cmp(hipStream_t st, uint64_t ntx, const uint8_t *a, const uint8_t *b,
+                                  const uint64_t *rec_off, const uint64_t *alh_off, int32_t *pre);
+// status[t] = pre[t] and the Alh zeroed where pre[t] != 0
+hipError_t launch_txlog_apply_pre(hipStream_t st, uint64_t ntx, const int32_t *pre, int32_t *status,
+                                  uint8_t *alh);
+// stats[2] += the number of non-OK statuses, stats[3] = min(stats[3], the
+// first non-OK record)
+hipError_t launch_txlog_status_summary(hipStream_t st, uint64_t ntx, const int32_t *status,
+                                       uint64_t *stats);
 // up to three runs of words pinned host memory -> HBM by a kernel (k_fetch_host)
 struct HostRuns {
     const uint64_t *src[3];

@@ -382,6 +382,48 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
     return rc, k, used.value, (hd[:k] if hd is not None else None), alh[:k], sts[:k]
 
 
+def txlog_validate_clog(dev: int, length: int, clog, ntx: Optional[int] = None,
+                        clog_entry_size: int = 12, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
+                        max_key_len: int = DEFAULT_MAX_KEY_LEN, ctx: Optional[Context] = None,
+                        out=None, clog_dev: Optional[int] = None):
+    """mh_txlog_validate_clog: readTx (immustore.go:3048-3060) of txs 1..ntx of
+    a tx log already on the device (dev: its address, length bytes, the
+    allocation 256 bytes longer), located by the commit-log entries clog
+    (bytes, 12 or 44 per tx; or clog_dev: their device address with ntx)
+    -> (status, nbad, first_bad, hdrs[ntx] TX_HEADER, alh[ntx,32], per_tx[ntx]).
+
+    out: optional (hdrs, alh, per_tx) arrays (host numpy, pinned or not), or
+    (hdrs_addr, alh_addr, per_tx_addr) device addresses (ints; any may be None)
+    -- then the arrays returned are None."""
+    if clog_dev is None:
+        cb = _u8(clog)
+        n = len(cb) // clog_entry_size if ntx is None else ntx
+        assert len(cb) >= n * clog_entry_size
+        caddr = _addr(cb) if cb.size else None
+    else:
+        assert ntx is not None
+        n, caddr = ntx, clog_dev
+    nbad, first = C.c_uint64(0), C.c_uint64(0)
+    if out is not None and all(x is None or isinstance(x, int) for x in out):
+        ptrs, arrs = list(out), (None, None, None)
+    else:
+        if out is not None:
+            hd, alh, sts = out
+            assert len(alh) >= n and len(sts) >= n and (hd is None or len(hd) >= n)
+        else:
+            hd = np.empty(max(n, 1), TX_HEADER)
+            alh = np.empty((max(n, 1), 32), np.uint8)
+            sts = np.empty(max(n, 1), np.int32)
+        ptrs = [_addr(hd) if hd is not None else None, _addr(alh), _addr(sts)]
+        arrs = (hd[:n] if hd is not None else None, alh[:n], sts[:n])
+    rc = N.load().mh_txlog_validate_clog(_ctx(ctx).handle, dev, length, caddr, n, clog_entry_size,
+                                         max_entries, max_key_len, ptrs[0], ptrs[1], ptrs[2],
+                                         C.byref(nbad), C.byref(first))
+    if rc < 0:
+        N.check(rc)
+    return (rc, nbad.value, first.value) + arrs
+
+
 def txlog_scan(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
                max_key_len: int = DEFAULT_MAX_KEY_LEN, max_txs: Optional[int] = None):
     """Record structure only (host, no device) -> (status, ntx, consumed,

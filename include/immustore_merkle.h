@@ -596,11 +596,46 @@ int mh_txlog_validate(mh_ctx *ctx, const uint8_t *buf, uint64_t len, uint32_t ma
  * context's device) the same len bytes, read by the kernels in place -- no
  * host->device copy.  The device allocation holding dlog must extend at least
  * 256 bytes past dlog + len (checked: MH_ERR_ILLEGAL_ARGUMENTS).  Outputs and
- * statuses as mh_txlog_validate. */
+ * statuses as mh_txlog_validate.  The kernels never walk a length of dlog:
+ * every record's structure in dlog is checked on the device against the host
+ * copy's first, and a record whose resident bytes give another structure (or
+ * differ from buf, for records the fused kernels do not take) is
+ * MH_ERR_CORRUPTED_DATA with its Alh zeroed -- a drifted resident log is
+ * reported per record, never a fault. */
 int mh_txlog_validate_resident(mh_ctx *ctx, const uint8_t *buf, const uint8_t *dlog, uint64_t len,
                                uint32_t max_entries, uint32_t max_key_len, uint64_t max_txs,
                                uint64_t *ntx, uint64_t *consumed, mh_tx_header *hdrs,
                                uint8_t *alh, int32_t *status);
+/* The same check of a log already in device memory, indexed by the store's
+ * commit log instead of a host copy (no host hop, no host->device copy of the
+ * log): ImmuStore.readTx for txs 1..ntx of the cLog (immustore.go:3048-3060 ->
+ * txOffsetAndSize :2569-2597 -> Tx.readFrom tx.go:388-630).  clog holds ntx
+ * commit-log entries of clog_entry_size bytes (12: BE64 tx offset || BE32 tx
+ * size, cLogEntrySizeV1; 44: + the tx's Alh, cLogEntrySizeV2,
+ * immustore.go:122-123) -- the entries after the appendable header, in device
+ * or host memory.  dlog: the tx-log data (after its appendable header), len
+ * bytes, on the context's device, its allocation extending 256 bytes past it.
+ * Record t is parsed where entry t points, on to the end of the log as Go's
+ * reader does; status[t] (each output nullable; device, pinned or pageable
+ * memory, capacity ntx):
+ *   MH_ERR_TRUNCATED        the record runs past len / reads as an id-0 tail
+ *                           (readTx's "unexpected EOF", ErrCorruptedTxData);
+ *   MH_ERR_CORRUPTED_*, MH_ERR_METADATA_UNSUPPORTED  the reader's structural
+ *                           errors, as mh_txlog_validate reports them;
+ *   MH_ERR_CORRUPTED_DATA   ALH mismatch (tx.go:625); or the record does not
+ *                           end exactly at offset + size, or a 44-byte entry's
+ *                           Alh differs (the open path's cLog checks,
+ *                           immustore.go:458-528);
+ * with hdrs (md_off relative to dlog, eh rebuilt) and alh as mh_txlog_validate
+ * for valid records, zeros for records with a structural error.  *nbad: the
+ * number of non-OK records, *first_bad: the first (ntx when none).  Returns
+ * MH_OK when the call ran.  Records with metadata not in Go's canonical form
+ * or with more than 1024 entries are re-validated from a host copy of that
+ * record alone (mh_txlog_validate). */
+int mh_txlog_validate_clog(mh_ctx *ctx, const uint8_t *dlog, uint64_t len, const uint8_t *clog,
+                           uint64_t ntx, uint32_t clog_entry_size, uint32_t max_entries,
+                           uint32_t max_key_len, mh_tx_header *hdrs, uint8_t *alh,
+                           int32_t *status, uint64_t *nbad, uint64_t *first_bad);
 
 /* ------------------------------------------------------------ commit path */
 /* the hashing of ImmuStore.precommit / preCommitWith

@@ -525,6 +525,53 @@ def txlog_validate(buf, max_entries=1024, max_key_len=1024, max_txs=1 << 40):
     return st, n, used.value, alh[:n].copy(), sts[:n].copy()
 
 
+ERR_CORRUPTED_DATA = 14
+ERR_TRUNCATED = 18
+
+
+def txlog_validate_clog(buf, clog, es=12, max_entries=1024, max_key_len=1024):
+    """ImmuStore.readTx (embedded/store/immustore.go:3048-3060) of txs 1..n
+    located by the commit-log entries clog (txOffsetAndSize, :2569-2597: BE64
+    offset || BE32 size [|| Alh], es = 12 or 44 bytes, :122-123), each read from
+    its offset on to the end of the log (the reader is not bounded by the
+    size), plus the open path's cLog checks (:458-528: the record ends at
+    offset + size; a 44-byte entry's Alh is the tx's).
+    -> (alh[n,32], status[n]); alh is zero where the record's structure or the
+    cLog checks fail (status: the reader's error, MH_ERR_TRUNCATED for its
+    unexpected EOF, MH_ERR_CORRUPTED_DATA for a cLog mismatch)."""
+    import struct
+    b = _u8(buf) if len(buf) else np.zeros(1, np.uint8)
+    blen = len(buf)
+    n = len(clog) // es
+    alh = np.zeros((n, 32), np.uint8)
+    sts = np.zeros(n, np.int32)
+    one_a = np.zeros((1, 32), np.uint8)
+    one_s = np.zeros(1, np.int32)
+    base = b.ctypes.data
+    for t in range(n):
+        off, size = struct.unpack_from(">QI", clog, t * es)
+        if off + 8 > blen:
+            sts[t] = ERR_TRUNCATED
+            continue
+        ntx, used = C.c_uint64(0), C.c_uint64(0)
+        st = lib().orc_txlog_validate(C.cast(base + off, u8p), blen - off, max_entries, max_key_len,
+                                      1, C.byref(ntx), C.byref(used), _p(one_a),
+                                      one_s.ctypes.data_as(C.POINTER(C.c_int32)))
+        if st == 0 and ntx.value == 0:
+            st = ERR_TRUNCATED  # an id-0 record: the reader's EOF
+        if st == 0 and used.value != size:
+            st = ERR_CORRUPTED_DATA
+        if st == 0 and es == 44 and bytes(clog[t * es + 12:t * es + 44]) != \
+                b[off + size - 32:off + size].tobytes():
+            st = ERR_CORRUPTED_DATA
+        if st == 0:
+            sts[t] = one_s[0]
+            alh[t] = one_a[0]
+        else:
+            sts[t] = st
+    return alh, sts
+
+
 def verify_dual_proof(sh, th, md_blob, incl, cons, tbl_alh, last, lin, lap, src, tgt, src_alh,
                       tgt_alh):
     """VerifyDualProof (v1).  lin: None or (lin_src, lin_tgt, terms); lap: None or

@@ -410,10 +410,23 @@ def fixture_store(root):
                        for k in range(a0 + 1, a1)]
                 c["lap"] = {"terms": lt, "incl": ips}
             dual1.append(c)
+    # the store's commit log (commit/00000000.txi): one entry per tx, BE64
+    # offset || BE32 size of its record in the tx log (cLogEntrySizeV1,
+    # immustore.go:122, 2569-2597) -- pinned against the records parsed above
+    txi = read_appendable(os.path.join(root, "commit/00000000.txi"))
+    assert len(txi) == 12 * len(txs), "cLog size"
+    q = 0
+    for k, tx in enumerate(txs):
+        off, size = struct.unpack(">QI", txi[12 * k:12 * k + 12])
+        n = 90 + (2 if tx["header"]["version"] == 0 else 2 + len(tx["header"]["md"]) // 2 + 4)
+        n += sum(4 + len(e["md"]) // 2 + len(e["key"]) // 2 + 12 + 32 for e in tx["entries"]) + 32
+        assert off == q and size == n, "cLog entry %d" % k
+        q += n
     headers = {rel: appendable_header(os.path.join(root, rel)).hex()
                for rel in ("aht/data/00000000.dat", "aht/tree/00000000.sha",
                            "aht/commit/00000000.di")}
-    return {"txs": txs, "aht_payloads": payloads, "aht_dlog": dlog.hex(), "app_headers": headers,
+    return {"txs": txs, "txi": txi.hex(),
+        "txi_header": appendable_header(os.path.join(root, "commit/00000000.txi")).hex(), "aht_payloads": payloads, "aht_dlog": dlog.hex(), "app_headers": headers,
         "aht_plog": pl.hex(), "aht_clog": clog.hex(), "n_values": sum(
         1 for t in txs for e in t["entries"] if "value" in e), "txlog": raw.hex(),
         "dual_v2": dual, "linear": linear, "dual_v1": dual1}

@@ -329,19 +329,15 @@ def test_txlog_validate_pinned_buffers(m, ctx, orc, hdrs):
             assert np.array_equal(a[3], c[3])
 
 
-@pytest.mark.parametrize("bulk,host_hdrs", [("", "0"), ("chain", "0"), ("", "1")])
-def test_txlog_validate_pinned_last_chunk(m, ctx, orc, monkeypatch, bulk, host_hdrs):
+def test_txlog_validate_pinned_last_chunk(m, ctx, orc):
     """The last copy chunk of a pinned log (its group's kernel runs right
-    after it lands and stores the results into the pinned outputs itself):
-    ends that are not 16-byte multiples, errors / max_txs / a corrupted hVal
-    inside the last chunk, and a wide tx or re-encoded metadata at the end (the
+    after it lands and stores the results into the pinned outputs itself; the
+    header fields other than Eh are filled by the host meanwhile): ends that
+    are not 16-byte multiples, errors / max_txs / a corrupted hVal inside the
+    last chunk, and a wide tx or re-encoded metadata at the end (the
     rest-group path) -- equal to the oracle and to the pageable call, headers
-    included.  bulk=chain: the early groups through the six-launch chain
-    (MH_TXLOG_BULK), the last through the fused kernel; host_hdrs=1: the last
-    group's header fields other than Eh filled by the host (MH_TXLOG_HOST_HDRS)."""
+    included."""
     import torch
-    monkeypatch.setenv("MH_TXLOG_BULK", bulk)
-    monkeypatch.setenv("MH_TXLOG_HOST_HDRS", host_hdrs)
     from tx_util import metadata_logs
     from immustore_amd.txlayer import TX_HEADER
     rng = np.random.default_rng(31)
@@ -645,16 +641,14 @@ def _record_heads(raw, n):
 
 
 @pytest.mark.parametrize("max_entries", [1, 2, 3, 5, 8, 16, 17, 40, 64])
-def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries):
+def test_txlog_fused_kernels_vs_oracle(m, ctx, orc, monkeypatch, max_entries):
     """k_txlog_wave (one wave per 64 / L records, L lanes per record: every
-    lane-count the widest tx can pick), k_txlog_blk (every phase spread over
-    the workgroup: every records-per-workgroup shape) and k_txlog_lanes (1, 2,
-    4, 8 and 16 lanes per record, each lane's subtree serial) with the records
-    staged in LDS and read from HBM, against the round-3 workgroup kernel
-    (MH_TXLOG_KERNEL=group), the
-    oracle and the record heads parsed in Python: headers (every field, Eh
-    included), Alh and per-tx statuses, clean and with corrupted records,
-    with pageable and pinned outputs."""
+    lane-count the widest tx can pick; the records staged in LDS and read from
+    HBM) and k_txlog_lanes (1, 2, 4, 8 and 16 lanes per record, each lane's
+    subtree serial) against the oracle and the record heads parsed in Python:
+    Alh and per-tx statuses equal to the oracle's, headers (every field, Eh
+    included) equal across kernels and to the Python parse, clean and with
+    corrupted records, with pageable and pinned outputs."""
     import torch
     from immustore_amd.txlayer import TX_HEADER
     rng = np.random.default_rng(100 + max_entries)
@@ -669,9 +663,8 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
     for buf in (raw, bytes(bad)):
         o = orc.txlog_validate(buf)
         res = {}
-        for kern, smax in (("group", None), ("wave", None), ("wave", "0"), ("blk", None),
-                           ("blk", "0"), ("lanes", "L1"), ("lanes", "L2"), ("lanes", "L4"),
-                           ("lanes", "L8"), ("lanes", "L16")):
+        for kern, smax in (("wave", None), ("wave", "0"), ("lanes", "L1"), ("lanes", "L2"),
+                           ("lanes", "L4"), ("lanes", "L8"), ("lanes", "L16")):
             monkeypatch.setenv("MH_TXLOG_KERNEL", kern)
             monkeypatch.delenv("MH_TXLOG_STAGE_MAX", raising=False)
             monkeypatch.delenv("MH_TXLOG_LANES", raising=False)
@@ -684,7 +677,7 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
                 assert (a[0], a[1], a[2]) == (o[0], o[1], o[2]), (kern, smax)
                 assert np.array_equal(a[4], o[3]) and list(a[5]) == list(o[4]), (kern, smax)
                 res[(kern, smax, out is None)] = a[3][:a[1]].copy()
-        ref = res[("group", None, True)]
+        ref = res[("wave", None, True)]
         for key, h in res.items():
             assert np.array_equal(h, ref), key
         if buf is raw:
@@ -698,7 +691,7 @@ def test_txlog_wave_kernel_vs_group_kernel(m, ctx, orc, monkeypatch, max_entries
     monkeypatch.delenv("MH_TXLOG_LANES", raising=False)
 
 
-@pytest.mark.parametrize("kern", ["wave", "blk", "lanes"])
+@pytest.mark.parametrize("kern", ["wave", "lanes"])
 def test_txlog_validate_resident_vs_host_path(m, ctx, orc, monkeypatch, kern):
     """mh_txlog_validate_resident (the log already in HBM: scrub / re-validate
     of what was just written, one group, no copy) equals the copying call and

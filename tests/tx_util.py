@@ -250,3 +250,40 @@ def metadata_logs(orc):
     for k, md in enumerate(bad_tx):
         logs.append(("bad_tx_%d" % k, chain([good, (md, md, [], True), good])))
     return logs
+
+
+def record_spans(raw, n=None):
+    """(start, end) of the first n records of a structurally valid tx log
+    (immustore.go:1812-1924 layout, parsed in Python), stopping at an id-0
+    tail or the end of the buffer."""
+    spans, p = [], 0
+    while p + 8 <= len(raw) and (n is None or len(spans) < n):
+        if struct.unpack_from(">Q", raw, p)[0] == 0:
+            break
+        ver, = struct.unpack_from(">H", raw, p + 88)
+        if ver == 0:
+            ne, = struct.unpack_from(">H", raw, p + 90)
+            q = p + 92
+        else:
+            ml, = struct.unpack_from(">H", raw, p + 90)
+            ne, = struct.unpack_from(">I", raw, p + 92 + ml)
+            q = p + 96 + ml
+        for _ in range(ne):
+            m_, = struct.unpack_from(">H", raw, q)
+            k_, = struct.unpack_from(">H", raw, q + 2 + m_)
+            q += 4 + m_ + k_ + 44
+        spans.append((p, q + 32))
+        p = q + 32
+    return spans
+
+
+def clog_for(raw, spans, es=12):
+    """The commit-log entries of those records (txOffsetAndSize,
+    immustore.go:2569-2597: BE64 offset || BE32 size, + the stored Alh for the
+    44-byte cLogEntrySizeV2, :122-123)."""
+    out = bytearray()
+    for s, e in spans:
+        out += struct.pack(">QI", s, e - s)
+        if es == 44:
+            out += raw[e - 32:e]
+    return bytes(out)
