@@ -13,7 +13,12 @@ all by the HIP kernels of libimmustore_merkle.so through its C ABI.
 builds the subtree over its own 2^20 entries (power-of-two aligned shard of a
 global N x 2^20-leaf tree), the N subtree roots are all-gathered over RCCL and
 the top log2(N) levels are reduced on every rank (exact by
-finding 3).  Weak scaling: per-GPU work is fixed.
+finding 3).  Weak scaling by default: per-GPU work is fixed (the metric's
+"1M x 1KiB leaves @1/2/4/8 GPU" read as 1M leaves per GPU, an N x 2^20-leaf
+tree).  --scaling strong reads it as ONE 2^20 x 1 KiB tree at every N: each
+rank builds 2^20 / N leaves (power-of-two N: shards stay aligned subtrees),
+the values being exactly the N = 1 tree's (the splitmix64 stream at the
+rank's entry offset), so the root is the same at every N.
 
 --config c4 runs BASELINE configs[3] instead: 2^23 x 4 KiB entries per GPU
 (values generated in HBM), i.e. the 2^26-entry tree at 8 GPUs.
@@ -98,6 +103,9 @@ def parse():
                    help="torch: one process per GPU over torch.distributed (driver default); "
                         "cabi: one process, mh_multi_* over N devices with the in-library "
                         "RCCL clique (the cgo caller's path)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                   help="weak: 2^20 entries per GPU (default); strong: one 2^20-entry tree "
+                        "split over the N GPUs (c2 only, N a power of two)")
     p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r03.json"),
                    help="PMC-derived HBM bytes per launch of the dominant kernel (or missing)")
     return p.parse_args()
@@ -129,6 +137,15 @@ def host_threads(share=1):
     except (AttributeError, OSError):
         avail = os.cpu_count() or 1
     return max(1, avail // max(share, 1))
+
+
+def shard_seed(rank, n, val, strong):
+    """The mh_dev_fill_random seed of rank's values: weak, an independent
+    stream per rank (2 + rank); strong, the N = 1 tree's stream (seed 2) from
+    the rank's first entry on, so the N shards are that one tree's values."""
+    if not strong:
+        return 2 + rank
+    return (2 + (rank * n * val // 8) * SPLITMIX_G) & 0xFFFFFFFFFFFFFFFF
 
 
 def shard_block(orc, seed, key0, e0, cnt, val):
@@ -557,7 +574,7 @@ def cabi_main(a):
 
 
 def root_check_ranks(a, n, val, rank, world, dist, backend, dev, levels_dev, sub_root_dev,
-                     glob_root_dev, corrupted):
+                     glob_root_dev, corrupted, seed=None):
     """Every rank rebuilds its own shard with the oracle on its share of the
     host cores; the 128-byte records (device subtree root, device global
     root, oracle shard root, block verdict) are all-gathered and rank 0
@@ -567,8 +584,8 @@ def root_check_ranks(a, n, val, rank, world, dist, backend, dev, levels_dev, sub
     t0 = time.perf_counter()
     orc = _oracle()
     threads = host_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
-    o_sub, blocks_ok, mode = oracle_shard_root(orc, n, val, 2 + rank, rank * n, levels_dev,
-                                               threads)
+    o_sub, blocks_ok, mode = oracle_shard_root(orc, n, val, 2 + rank if seed is None else seed,
+                                               rank * n, levels_dev, threads)
     rec = np.zeros(128, np.uint8)
     rec[0:32] = sub_root_dev.cpu().numpy()
     rec[32:64] = glob_root_dev.cpu().numpy()
@@ -876,6 +893,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    strong = a.scaling == "strong"
+    if strong and (a.config != "c2" or world & (world - 1)):
+        raise SystemExit("--scaling strong: --config c2 and a power-of-two --gpus")
     dist = None
     # one process per GPU; MH_DIST_BACKEND=gloo rehearses several ranks on
     # fewer GPUs (device = local rank modulo the visible devices)
@@ -916,11 +936,16 @@ def main():
     L = N.load()
     VAL = 4096 if a.config == "c4" else VAL_LEN
     n = a.entries or ((1 << 23) if a.config == "c4" else N_ENTRIES)
+    if strong:  # one tree of n entries: this rank's aligned 1 / world of it
+        if n % world:
+            raise SystemExit("--scaling strong: %d entries do not split over %d GPUs" % (n, world))
+        n //= world
+    seed = shard_seed(rank, n, VAL, strong)
     # inputs resident in HBM before the timed region (synthetic, deterministic)
     vals = torch.empty(n * VAL, dtype=torch.uint8, device=dev)
     keys = torch.empty(n * KEY_LEN, dtype=torch.uint8, device=dev)
     with torch.cuda.stream(streams[0]):
-        N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), 2 + rank))
+        N.check(L.mh_dev_fill_random(ctx.handle, vals.data_ptr(), vals.numel(), seed))
         N.check(L.mh_dev_fill_keys_be64(ctx.handle, keys.data_ptr(), n, rank * n))
         corrupted = corrupt_hook(vals, rank)
     torch.cuda.synchronize(dev)
@@ -1053,7 +1078,7 @@ def main():
     r0 = root[0].cpu()
     assert all(torch.equal(r0, r.cpu()) for r in root), "in-flight builds disagree"
     rcheck = root_check_ranks(a, n, VAL, rank, world, dist, backend, dev, levels[0], root[0],
-                              groot[0] if dist else root[0], corrupted)
+                              groot[0] if dist else root[0], corrupted, seed)
 
     k_ms = sum(c.timing("entries_fixed")[0] for c in ctxs[1:]) + k_ms0
     k_cnt = sum(c.timing("entries_fixed")[1] for c in ctxs[1:]) + k_cnt0
@@ -1110,13 +1135,16 @@ def main():
                           "note": "untimed full builds before the warmup steps (GPU clock ramp)"},
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (splitmix64 values generated in HBM, keys BE64(i))",
         "config": {"workload": "htree build (value SHA-256 + TxEntryDigest_v1_2 + leaf + all "
-                               "levels), %d x %d B entries per GPU, %d B keys" % (n, VAL, KEY_LEN),
-                   "entries_per_gpu": n, "value_len": VAL, "key_len": KEY_LEN,
+                               "levels), %d x %d B entries per GPU, %d B keys" % (n, VAL, KEY_LEN)
+                   + ("; strong scaling: one %d-entry tree over %d GPUs" % (n * world, world)
+                      if strong else ""),
+                   "entries_per_gpu": n, "entries_total": n * world, "value_len": VAL,
+                   "key_len": KEY_LEN,
                    "parallelism": "subtree shard per GPU + %s all-gather of roots"
                    % ("RCCL" if backend != "gloo" else "gloo") if dist else "single GPU", "lanes_per_leaf_group": lpl,
                    "builds_in_flight": D, "wg_subtree_levels": wgl, "stream_priority": prio},

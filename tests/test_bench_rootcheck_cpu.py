@@ -134,3 +134,54 @@ def test_root_check_ranks_gloo(orc, world, bad_rank):
         assert ok == (bad_rank < 0), (rank, ok)   # every rank shares the verdict
         assert root == whole.hex() and ntot == world * n
         assert bad == ([] if bad_rank < 0 else [bad_rank])
+
+
+def _rank_strong(rank, world, port, total, val, bad_rank, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+    import bench
+    import oracle as orc
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = total // world
+        seed = bench.shard_seed(rank, n, val, True)
+        lv, sub = _shard_levels(orc, bench, n, val, seed, rank * n, corrupt=rank == bad_rank)
+        g = torch.empty(world * 32, dtype=torch.uint8)
+        dist.all_gather_into_tensor(g, torch.from_numpy(np.frombuffer(sub, np.uint8).copy()))
+        glob = bench.reduce_nodes(orc, [bytes(x) for x in g.numpy().reshape(-1, 32)])
+        t = lambda b: torch.from_numpy(np.frombuffer(b, np.uint8).copy())  # noqa: E731
+        rc = bench.root_check_ranks(None, n, val, rank, world, dist, "gloo", torch.device("cpu"),
+                                    lv, t(sub), t(glob), rank == bad_rank, seed)
+        q.put((rank, rc["ok"], rc["root"], glob.hex(), rc["n"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad_rank", [(2, -1), (8, -1), (8, 3)])
+def test_strong_scaling_root_check_gloo(orc, world, bad_rank):
+    """bench.py --scaling strong: ONE tree of `total` entries split over the
+    ranks (each rank's values the N = 1 tree's stream at its entry offset,
+    bench.shard_seed): the global root every rank assembles, and the root
+    check's, equal the oracle's rebuild of the whole tree -- the same root at
+    every world size; a corrupted rank fails the check on every rank."""
+    total, val = 1 << 10, 64
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_strong, args=(r, world, port, total, val, bad_rank, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    b = _bench()
+    keys, vals = b.shard_block(orc, 2, 0, 0, total, val)  # the N = 1 tree
+    whole = orc.build_entries_fixed(1, keys, vals)[2].hex()
+    assert b.shard_seed(0, total, val, True) == 2
+    for rank, ok, root, glob, ntot in res:
+        assert ok == (bad_rank < 0), (rank, ok)
+        assert root == whole and ntot == total
+        assert (glob == whole) == (bad_rank < 0)

@@ -223,9 +223,15 @@ def test_clog_arguments(m, ctx, orc):
     L = N.load()
     nb, fb = C.c_uint64(), C.c_uint64()
     cb = np.frombuffer(cl, np.uint8)
-    short = _dev(raw, pad=100)
-    assert L.mh_txlog_validate_clog(ctx.handle, short.data_ptr(), len(raw), cb.ctypes.data, 20, 12,
-                                    1024, 1024, None, None, None, C.byref(nb), C.byref(fb)) == ILLEGAL
+    p = C.c_void_p()
+    size = (len(raw) + 65535) & ~65535  # an allocation of its own (not torch's cache)
+    N.check(L.mh_dev_alloc(ctx.handle, size, C.byref(p)))
+    try:
+        assert L.mh_txlog_validate_clog(ctx.handle, p.value + size - len(raw) - 100, len(raw),
+                                        cb.ctypes.data, 20, 12, 1024, 1024, None, None, None,
+                                        C.byref(nb), C.byref(fb)) == ILLEGAL
+    finally:
+        L.mh_dev_free(ctx.handle, p.value)
     hb = np.frombuffer(raw, np.uint8)
     assert L.mh_txlog_validate_clog(ctx.handle, hb.ctypes.data, len(raw), cb.ctypes.data, 20, 12,
                                     1024, 1024, None, None, None, C.byref(nb), C.byref(fb)) == ILLEGAL
@@ -249,7 +255,7 @@ def test_resident_log_drifted_from_host_copy(m, ctx, orc, monkeypatch, kern):
     import struct
     rng = np.random.default_rng(77)
     if kern == "chain":
-        raw = _synthetic_txlog(rng, 150, orc, max_entries=16) + \
+        raw = _synthetic_txlog(rng, 300, orc, max_entries=16) + \
             b"".join(r for n, r in metadata_logs(orc) if n == "noncanonical_sealed_canonical")
     else:
         monkeypatch.setenv("MH_TXLOG_KERNEL", kern)

@@ -15,6 +15,8 @@
 #   txcabi           bench.py --api cabi --config txlog (mh_multi_txlog_validate); txcabi_corrupt: must exit 1
 #   dist2            2 gloo ranks sharing GPU 0 (bench.py --gpus 2 rehearsal)
 #   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
+#   dist2s / dist8s  the same with --scaling strong (one 2^20 tree split over the ranks);
+#                    dist8s_corrupt: rank 5 corrupted, must exit 1; strong1: N = 1 strong
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   wdist:<w>:<N>    bench_workloads.py --workload <w> (c3 / c5) as N gloo ranks sharing GPU 0
 #   wcorrupt:<w>:<N> the same with MH_BENCH_CORRUPT=1 (N >= 2): must exit 1 (result check)
@@ -77,6 +79,17 @@ for s in "$@"; do
       MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist8 500 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 \
         bench.py --gpus 8 --steps 20 --warmup 3 --prewarm 1 --no-cpu-baseline || exit 1 ;;
+    dist2s|dist8s)  # --scaling strong: ONE 2^20-entry tree over N gloo ranks sharing GPU 0 (root vs the oracle)
+      n=${s:4:1}
+      MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step "$s" 500 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 2953$n \
+        bench.py --gpus "$n" --scaling strong --steps 20 --warmup 3 --prewarm 1 --no-cpu-baseline || exit 1 ;;
+    dist8s_corrupt)  # the same with rank 5's shard corrupted: must exit 1
+      MH_BENCH_CORRUPT=5 MH_DIST_BACKEND=gloo HIP_VISIBLE_DEVICES=0 step dist8s_corrupt 500 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 \
+        bench.py --gpus 8 --scaling strong --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline
+      rc=$?; echo "dist8s_corrupt exit $rc (want 1)"; [ $rc -eq 1 ] || exit 1 ;;
+    strong1) step strong1 300 python bench.py --scaling strong --steps 200 --warmup 5 --no-cpu-baseline || exit 1 ;;
     wdist:*|wcorrupt:*)  # bench_workloads.py multi-rank lines, N gloo ranks sharing GPU 0
       w=$(echo "$s" | cut -d: -f2); n=$(echo "$s" | cut -d: -f3); kind=${s%%:*}
       corrupt=""; [ "$kind" = wcorrupt ] && corrupt="MH_BENCH_CORRUPT=1"
