@@ -28,10 +28,10 @@ import (
 	"github.com/codenotary/immudb/embedded/internal/mi355x"
 )
 
-// devices returns the process-wide clique over every visible GPU
-// (mi355x.Multi).
+// devices checks a clique over every visible GPU out of the process's pool
+// (mi355x.AcquireClique); the caller returns it with mi355x.ReleaseClique.
 func devices() (*C.mh_multi, error) {
-	m, err := mi355x.Multi()
+	m, err := mi355x.AcquireClique()
 	return (*C.mh_multi)(m), err
 }
 
@@ -124,6 +124,12 @@ func (t *AHtree) appendRun(ds [][]byte) (n uint64, root [sha256.Size]byte, err e
 	if err != nil {
 		return 0, root, err
 	}
+	released := false
+	defer func() { // on the early returns; the call's own status releases it below
+		if !released {
+			mi355x.ReleaseClique(unsafe.Pointer(mm), 0)
+		}
+	}()
 	// what earlier single Appends buffered goes to disk first, so the cLog
 	// entries of the batch follow synced pLog / dLog bytes (ahtree.go:788-836)
 	if err = t.sync(); err != nil {
@@ -161,6 +167,8 @@ func (t *AHtree) appendRun(ds [][]byte) (n uint64, root [sha256.Size]byte, err e
 	st := C.mh_multi_ahtree_append_batch(mm, C.uint64_t(n0), pkp,
 		pp, C.uint64_t(m), C.uint32_t(plen),
 		(*C.uint8_t)(unsafe.Pointer(&dlog[0])), (*C.uint8_t)(unsafe.Pointer(&root[0])))
+	mi355x.ReleaseClique(unsafe.Pointer(mm), int(st))
+	released = true
 	if st != C.MH_OK {
 		return 0, root, mapErr(st)
 	}

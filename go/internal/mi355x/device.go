@@ -39,33 +39,96 @@ func Context() (unsafe.Pointer, error) {
 	return unsafe.Pointer(ctx), ctxErr
 }
 
+// Cliques for the batch paths bound by one device's PCIe link (tx-log
+// validation, value checks, precommit batches, ahtree batch appends): each is
+// an mh_multi over every visible GPU (one context per device and an RCCL
+// clique inside the library) that splits its input over the devices, each
+// part over its own link.  A clique serialises its calls, so concurrent
+// committers (immudb runs up to MaxConcurrency precommits at once,
+// immustore.go:1620-1632, options.go:35) each check one out of a small pool
+// instead of sharing one: two handles per device by default (two builds in
+// flight measured 1247 GiB/s against 1094 with one, profiles/
+// cabi_inflight_r05.txt; the pool's aggregate from plain C threads,
+// tests/c_client/mh_committers.c, profiles/committers_r06.txt).
 var (
-	multiOnce sync.Once
-	multi     *C.mh_multi
-	multiErr  error
+	poolMu   sync.Mutex
+	poolCond = sync.NewCond(&poolMu)
+	poolFree []*C.mh_multi
+	poolMade int
+	poolMax  int // 0 until first use or SetCliquePool
+	poolDevs []C.int
 )
 
-// Multi returns the process-wide clique over every visible GPU
-// (mh_multi_create: one context per device, an RCCL clique inside the
-// library), created on first use: the batch paths bound by one device's PCIe
-// link (tx-log validation, value checks, precommit batches, proof batches)
-// split their input over it, each part over its own link.
-func Multi() (unsafe.Pointer, error) {
-	multiOnce.Do(func() {
-		var n C.int
-		if st := C.mh_device_count(&n); st != C.MH_OK || n < 1 {
-			multiErr = ErrNoDevice
-			return
+// SetCliquePool sets how many cliques the batch paths may hold at once (the
+// number of callers that run in parallel; the store sets it from its
+// options).  Takes effect for cliques created after the call; n < 1 means
+// the default of two per device.
+func SetCliquePool(n int) {
+	poolMu.Lock()
+	defer poolMu.Unlock()
+	poolMax = n
+	poolCond.Broadcast()
+}
+
+func poolInit() error {
+	if poolDevs != nil {
+		return nil
+	}
+	var n C.int
+	if st := C.mh_device_count(&n); st != C.MH_OK || n < 1 {
+		return ErrNoDevice
+	}
+	poolDevs = make([]C.int, int(n))
+	for i := range poolDevs {
+		poolDevs[i] = C.int(i)
+	}
+	if poolMax < 1 {
+		poolMax = 2 * int(n)
+	}
+	return nil
+}
+
+// AcquireClique checks out a clique over every visible GPU: a free one, a
+// new one while fewer than the pool size exist, else it waits for one to be
+// returned.  Every AcquireClique is paired with a ReleaseClique.
+func AcquireClique() (unsafe.Pointer, error) {
+	poolMu.Lock()
+	defer poolMu.Unlock()
+	if err := poolInit(); err != nil {
+		return nil, err
+	}
+	for {
+		if k := len(poolFree); k > 0 {
+			m := poolFree[k-1]
+			poolFree = poolFree[:k-1]
+			return unsafe.Pointer(m), nil
 		}
-		devs := make([]C.int, int(n))
-		for i := range devs {
-			devs[i] = C.int(i)
+		if poolMade < poolMax {
+			var m *C.mh_multi
+			if st := C.mh_multi_create(C.int(len(poolDevs)), &poolDevs[0], &m); st != C.MH_OK {
+				return nil, Status(int(st))
+			}
+			poolMade++
+			return unsafe.Pointer(m), nil
 		}
-		if st := C.mh_multi_create(n, &devs[0], &multi); st != C.MH_OK {
-			multiErr = Status(int(st))
-		}
-	})
-	return unsafe.Pointer(multi), multiErr
+		poolCond.Wait()
+	}
+}
+
+// ReleaseClique returns a clique after a call that ended with status st.  A
+// clique whose call failed with MH_ERR_COLLECTIVE has aborted its
+// communicators (capi_multi.hip gather_bytes) and fails every later call, so
+// it is destroyed instead and the next AcquireClique creates a new one.
+func ReleaseClique(m unsafe.Pointer, st int) {
+	poolMu.Lock()
+	defer poolMu.Unlock()
+	if st == int(C.MH_ERR_COLLECTIVE) || poolMade > poolMax && poolMax > 0 {
+		C.mh_multi_destroy((*C.mh_multi)(m))
+		poolMade--
+	} else {
+		poolFree = append(poolFree, (*C.mh_multi)(m))
+	}
+	poolCond.Signal()
 }
 
 // StatusError is a C ABI status with no Go sentinel of its own.

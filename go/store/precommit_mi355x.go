@@ -5,8 +5,10 @@
 // (immustore.go:1620-1632, 2301-2313, with ReplicateTx's Eh check
 // :1649-1654), readValueAt's integrity check over many values (:3235) and
 // the read-path re-hash of a run of tx-log records (tx.go:388-630), each
-// split over every GPU of the process (mi355x.Multi, the mh_multi_* forms:
-// one part per device over its own PCIe link).  Single
+// split over every GPU of the process (the mh_multi_* forms: one part per
+// device over its own PCIe link), each call on a clique checked out of the
+// process's pool (mi355x.AcquireClique), so concurrent committers run in
+// parallel.  Single
 // small transactions keep the reference's CPU path (a 16 KiB transaction is
 // 10 us on one SHA-NI core against ~300 us through the device queue,
 // DESIGN.md section 5).  Uncompiled in the build image (no Go toolchain); see
@@ -110,20 +112,16 @@ func (p *packed) pack(txs [][]*EntrySpec) error {
 // truncated), the entry digests of the header version and one htree per
 // transaction -> Eh.  expectEh (nil, or one per tx) is ReplicateTx's check
 // (immustore.go:1649-1654): a mismatch is ErrIllegalArguments for that tx.
-// The batch runs over every GPU of the process-wide clique
-// (mh_multi_precommit_batch: whole transactions, parts of nearly equal value
-// bytes, each device with its own commit pipe); the clique serialises calls.
+// The batch runs over every GPU (mh_multi_precommit_batch: whole
+// transactions, parts of nearly equal value bytes, each device with its own
+// commit pipe) on a clique checked out for the call: each concurrent
+// committer holds its own (INTEGRATION.md, "concurrent committers").
 type PrecommitBatch struct {
-	multi *C.mh_multi
-	p     packed
+	p packed
 }
 
 func NewPrecommitBatch() (*PrecommitBatch, error) {
-	m, err := mi355x.Multi()
-	if err != nil {
-		return nil, err
-	}
-	return &PrecommitBatch{multi: (*C.mh_multi)(m)}, nil
+	return &PrecommitBatch{}, nil
 }
 
 func (b *PrecommitBatch) Close() {
@@ -147,7 +145,11 @@ func (b *PrecommitBatch) Run(version int, maxTxEntries int, txs [][]*EntrySpec,
 	hv := make([][sha256.Size]byte, ne+1)
 	copy(hv, b.p.hvOverride)
 	use := append(b.p.useOverride, 0)
-	st := C.mh_multi_precommit_batch(b.multi, C.int(version), C.uint64_t(maxTxEntries), C.uint64_t(ntx),
+	mm, err := mi355x.AcquireClique()
+	if err != nil {
+		return nil, nil, nil, err
+	}
+	st := C.mh_multi_precommit_batch((*C.mh_multi)(mm), C.int(version), C.uint64_t(maxTxEntries), C.uint64_t(ntx),
 		(*C.uint64_t)(unsafe.Pointer(&b.p.txOff[0])),
 		(*C.uint8_t)(unsafe.Add(base, b.p.keys)), (*C.uint64_t)(unsafe.Pointer(&b.p.keyOff[0])),
 		(*C.uint8_t)(unsafe.Add(base, b.p.md)), (*C.uint64_t)(unsafe.Pointer(&b.p.mdOff[0])),
@@ -155,6 +157,7 @@ func (b *PrecommitBatch) Run(version int, maxTxEntries int, txs [][]*EntrySpec,
 		(*C.uint8_t)(unsafe.Pointer(&hv[0][0])), (*C.uint8_t)(unsafe.Pointer(&use[0])), exp,
 		(*C.uint8_t)(unsafe.Pointer(&hvals[0][0])), (*C.uint8_t)(unsafe.Pointer(&eh[0][0])),
 		(*C.int32_t)(unsafe.Pointer(&status[0])))
+	mi355x.ReleaseClique(mm, int(st))
 	if st != C.MH_OK {
 		return nil, nil, nil, mapErr(st)
 	}
@@ -184,7 +187,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 	if n == 0 {
 		return nil, nil
 	}
-	m, err := mi355x.Multi()
+	m, err := mi355x.AcquireClique()
 	if err != nil {
 		return nil, err
 	}
@@ -195,6 +198,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 		total += len(v)
 	}
 	if err := arena.Ensure(total + 16); err != nil {
+		mi355x.ReleaseClique(m, 0)
 		return nil, err
 	}
 	buf := arena.Bytes()
@@ -210,6 +214,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 	st := C.mh_multi_verify_values_batch((*C.mh_multi)(m), C.uint64_t(n), (*C.uint8_t)(arena.Ptr()),
 		(*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint64_t)(unsafe.Pointer(&lens[0])),
 		(*C.uint8_t)(unsafe.Pointer(&hVal[0][0])), (*C.int32_t)(unsafe.Pointer(&status[0])), &bad)
+	mi355x.ReleaseClique(m, int(st))
 	if st != C.MH_OK {
 		return nil, mapErr(st)
 	}
@@ -233,7 +238,7 @@ func VerifyValues(vals [][]byte, vLen []int, hVal [][sha256.Size]byte) ([]error,
 // record at consumed.
 func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha256.Size]byte,
 	errs []error, consumed uint64, err error) {
-	m, e := mi355x.Multi()
+	m, e := mi355x.AcquireClique()
 	if e != nil {
 		return nil, nil, 0, e
 	}
@@ -249,6 +254,7 @@ func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha25
 	st := C.mh_multi_txlog_validate((*C.mh_multi)(m), p, C.uint64_t(len(buf)), C.uint32_t(maxEntries),
 		C.uint32_t(maxKeyLen), C.uint64_t(maxTxs), &ntx, &used, nil,
 		(*C.uint8_t)(unsafe.Pointer(&alhs[0][0])), (*C.int32_t)(unsafe.Pointer(&status[0])))
+	mi355x.ReleaseClique(m, int(st))
 	errs = make([]error, int(ntx))
 	for k := range errs {
 		if status[k] != 0 {

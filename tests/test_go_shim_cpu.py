@@ -169,3 +169,38 @@ def test_verify_values_length_guards():
     b = _func_body("store/precommit_mi355x.go", "VerifyValues")
     assert re.search(r"len\(vLen\) != n \|\| len\(hVal\) != n", b)
     assert b.index("len(vLen) != n") < b.index("C.mh_multi_verify_values_batch")
+
+
+def test_batch_paths_check_cliques_out_of_the_pool():
+    """each batch call of the store / ahtree shims checks a
+    clique out of the process's pool (mi355x.AcquireClique) and returns it
+    (ReleaseClique, with the call's status so a clique whose collectives
+    aborted is replaced) -- no process-wide shared handle is
+    left, and no return between the checkout and the C call leaks it."""
+    dev = open(os.path.join(GO, "internal/mi355x/device.go")).read()
+    assert "func Multi(" not in dev
+    acq = _func_body("internal/mi355x/device.go", "AcquireClique")
+    assert "C.mh_multi_create" in acq and "poolCond.Wait()" in acq
+    rel = _func_body("internal/mi355x/device.go", "ReleaseClique")
+    assert "C.MH_ERR_COLLECTIVE" in rel and "C.mh_multi_destroy" in rel
+    for path, fn, call in (("store/precommit_mi355x.go", "Run", "C.mh_multi_precommit_batch"),
+                           ("store/precommit_mi355x.go", "VerifyValues",
+                            "C.mh_multi_verify_values_batch"),
+                           ("store/precommit_mi355x.go", "ValidateTxLog",
+                            "C.mh_multi_txlog_validate"),
+                           ("ahtree/ahtree_mi355x.go", "appendRun",
+                            "C.mh_multi_ahtree_append_batch")):
+        b = _func_body(path, fn)
+        a = b.index("AcquireClique()" if "AcquireClique()" in b else "devices()")
+        c = b.index(call)
+        r = b.index("ReleaseClique(", c)
+        assert a < c < r, (path, fn)
+        # every return between the checkout and the call releases the clique
+        # first (or a deferred release covers it)
+        between = b[b.index("\n\t}", a) + 3:c]  # after the checkout's own error return
+        if "defer func()" not in between:
+            for m_ in re.finditer(r"\n\s*return ", between):
+                seg = between[:m_.start()]
+                assert seg.rfind("ReleaseClique(") > seg.rfind("if err"), (path, fn)
+    src = open(os.path.join(GO, "store/precommit_mi355x.go")).read()
+    assert "mi355x.Multi" not in src and "b.multi" not in src

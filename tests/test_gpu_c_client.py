@@ -134,3 +134,49 @@ def test_c_client_links_and_reports_no_device():
     r = subprocess.run([CLIENT, "8", "8"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "abi 1" in r.stdout, (r.stdout, r.stderr)
     assert "mh_ctx_create" in r.stderr
+
+
+COMMITTERS = os.path.join(HERE, "c_client", "mh_committers")
+
+
+def _committer_batch(t, ntx, ne, vlen):
+    """Thread t's batch in tests/c_client/mh_committers.c (see its comment)."""
+    n = ntx * ne
+    e = np.arange(n, dtype=np.int64)
+    keys = np.frombuffer(((np.int64(t) << 32) | e).astype(">u8").tobytes(), np.uint8).copy()
+    j = np.arange(vlen, dtype=np.int64)
+    vals = ((7 * t + 13 * e[:, None] + 11 * j[None, :] + 1) & 0xFF).astype(np.uint8).reshape(-1)
+    return dict(tx_off=np.arange(0, n + 1, ne, dtype=np.uint64), keys=keys,
+                key_off=np.arange(0, 8 * n + 1, 8, dtype=np.uint64), vals=vals,
+                val_off=np.arange(0, vlen * n + 1, vlen, dtype=np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,cliques", [(4, 4), (4, 2), (3, 1)])
+def test_concurrent_committers_clique_pool(threads, cliques):
+    """Concurrent committers from plain C (one handle per
+    concurrent committer): `threads` threads share a pool of `cliques`
+    mh_multi handles over device 0 (checkout / return, as the cgo shim's
+    AcquireClique / ReleaseClique) and run mh_multi_precommit_batch at once;
+    every thread's Eh and sampled hVals equal the oracle's precommit
+    (immustore.go:1620-1632)."""
+    if not os.path.exists(COMMITTERS):
+        pytest.fail("tests/c_client/mh_committers not built (run __graft_entry__.build())")
+    ntx, ne, vlen, rounds = 48, 8, 300, 3
+    r = subprocess.run([COMMITTERS, str(threads), str(cliques), str(rounds), str(ntx), str(ne),
+                        str(vlen)], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    eh, hv = {}, {}
+    for line in r.stdout.splitlines():
+        k, *rest = line.split()
+        if k == "eh":
+            eh[int(rest[0])] = rest[1]
+        elif k == "hv":
+            hv[int(rest[0])] = rest[1]
+    assert sorted(eh) == list(range(threads))
+    n = ntx * ne
+    for t in range(threads):
+        h_o, e_o, st_o = O.precommit_batch(1, **_committer_batch(t, ntx, ne, vlen))
+        assert not st_o.any()
+        assert eh[t] == e_o.tobytes().hex(), t
+        assert hv[t] == (h_o[0].tobytes() + h_o[n // 2].tobytes() + h_o[n - 1].tobytes()).hex(), t
