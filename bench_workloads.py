@@ -1118,13 +1118,13 @@ def run_single(a):
         dbad = dres.clone()
         dbad[(ntx // 2) * rec + hdr + 4 + kl + 12] ^= 1  # one hVal of the middle record
         rb = txlog_validate_clog(dbad.data_ptr(), raw.size, clog, ctx=ctx)
-        clog_bad_ok = rb[1] == 1 and rb[2] == ntx // 2 and rb[5][ntx // 2] == 14
+        clog_bad_ok = bool(rb[1] == 1 and rb[2] == ntx // 2 and rb[5][ntx // 2] == 14)
         del dbad
         resident["clog"] = {"ms_per_call": round(tcl * 1e3, 3),
                             "kernel_ms": {"txlog_struct": round(k_struct, 4),
                                           "txlog_lanes": round(k_lanes, 4)},
                             "root_check": {"vs": "oracle (256 sampled records) + the sealed Alh",
-                                           "ok": clog_ok and clog_bad_ok}}
+                                           "ok": bool(clog_ok and clog_bad_ok)}}
         if not (clog_ok and clog_bad_ok):
             print(json.dumps({"clog_check_failed": True}), file=sys.stderr)
             sys.exit(1)
