@@ -887,35 +887,40 @@ def run_single(a):
         kt = {k: ctx.timing(k)[0] / (a.steps + a.warmup) for k in ("aht_leaves", "aht_perfect",
                                                                    "aht_spine")}
         comps = M + 2 * (nd - M)
-        # spot check against the reference recurrence (ahtree.go:296-322) on
-        # the device dLog: 200 random appends re-derived with hashlib
-        import hashlib
-        dl = dlog.view(-1, 32)
+        # ---- check vs the oracle, after the timed region (as the multi-rank
+        # line): the batch once more with its RootAt values kept, then every
+        # dLog digest and RootAt of 64 first, 64 last and 256 random appends
+        # against the oracle's streamed append of the same payload stream
+        # (orc.ahtree_stream, ahtree.go:287-322)
+        tc = time.perf_counter()
+        rts = torch.empty(M * 32, dtype=torch.uint8, device=dev)
+        if a.logs:
+            N.check(L.mh_dev_ahtree_append_batch_logs(ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(),
+                                                      M, 32, 0, plog.data_ptr(), clog.data_ptr(),
+                                                      rts.data_ptr()))
+        else:
+            N.check(L.mh_dev_ahtree_append_batch(ctx.handle, dlog.data_ptr(), 0, pay.data_ptr(), M,
+                                                 32, rts.data_ptr()))
+        sync()
+        orc = _oracle()
+        samples = aht_samples(0, M, np.random.default_rng(7))
+        dl, rr = dlog.view(-1, 32), rts.view(-1, 32)
+        rows = lambda t_, i: t_[torch.from_numpy(i).to(dev)].cpu().numpy()  # noqa: E731
+        ok, root_o = c3_rank_check(orc, 3, 32, 0, M, lambda i: rows(dl, i), lambda i: rows(rr, i),
+                                   samples, host_threads())
         pay_h = pay.view(-1, 32)
-        rng = np.random.default_rng(1)
-        ok = True
-        for n in [int(x) for x in rng.integers(1, M + 1, 200)] + [M]:
-            def node(k, l):
-                return bytes(dl[m.nodes_upto(k - 1) + l if k > 1 else l].cpu().numpy())
-            base = m.nodes_upto(n - 1) if n > 1 else 0
-            h = hashlib.sha256(b"\x00" + bytes(pay_h[n - 1].cpu().numpy())).digest()
-            ok &= bytes(dl[base].cpu().numpy()) == h
-            w, k, l, c = n - 1, n - 1, 0, 1
-            while w > 0:
-                if w & 1:
-                    h = hashlib.sha256(b"\x01" + node(k, l) + h).digest()
-                    ok &= bytes(dl[base + c].cpu().numpy()) == h
-                    c += 1
-                k &= ~(1 << l)
-                w >>= 1
-                l += 1
         out = {"metric": "ahtree batch append, 10^7 x 32 B payloads (configs[2])",
                "value": round(M / t / 1e6, 3), "unit": "M appends/s",
                "ms_per_step": round(t * 1e3, 3), "dlog_digests": nd,
                "dlog_GBps": round(nd * 32 / t / 1e9, 2),
                "gcomp_per_s": round(comps / t / 1e9, 2),
                "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
-               "spot_check_vs_reference_recurrence": bool(ok)}
+               "root_check": {"vs": "oracle", "ok": bool(ok), "root": root_o.hex(),
+                              "samples": int(len(samples)),
+                              "seconds": round(time.perf_counter() - tc, 2),
+                              "what": "every dLog digest and RootAt of 64 first, 64 last and "
+                                      "256 random appends vs the oracle's streamed append of "
+                                      "the same payload stream (orc.ahtree_stream)"}}
         if a.logs:
             # records of the first / last appends vs the format (ahtree.go:266-282, 341-351)
             import struct
@@ -927,7 +932,8 @@ def run_single(a):
                 ok &= bytes(cl[n].cpu().numpy()) == struct.pack(">QI", 36 * n, 32)
             out["metric"] += " + pLog/cLog appendable records"
             out["records_bytes"] = M * 48
-            out["spot_check_vs_reference_recurrence"] = bool(ok)
+            out["root_check"]["ok"] = bool(ok)
+            out["root_check"]["what"] += "; pLog / cLog records of appends 1, 2, M vs the format"
 
     elif a.workload == "c5":
         D = a.depth
@@ -960,9 +966,15 @@ def run_single(a):
         tgen = timed_k(ctx, gen, a.steps, a.warmup, sync)
         assert int(pst.abs().sum().item()) == 0 and int((nterms != D).sum().item()) == 0
         gen_ms = ctx.timing("htree_proof")[0] / (a.steps + a.warmup)
+        # 10 % tampered as SURVEY 8(d) states it: one bit of one term flipped
         tamper = rng.random(P) < 0.10
-        src = np.where(tamper, (leaf + 1) % W, leaf)  # wrong digest for 10 %
-        digests = dig.view(-1, 32)[torch.from_numpy(src).to(dev)].contiguous()
+        tp = np.nonzero(tamper)[0]
+        tbyte = tp * (D * 32) + rng.integers(0, D * 32, len(tp))
+        tbit = (1 << rng.integers(0, 8, len(tp))).astype(np.uint8)
+        tv = terms.view(-1)
+        ti = torch.from_numpy(tbyte).to(dev)
+        tv[ti] ^= torch.from_numpy(tbit).to(dev)
+        digests = dig.view(-1, 32)[leaf_t].contiguous()
         roots = root.view(1, 32).expand(P, 32).contiguous()
         width_t = torch.full((P,), W, dtype=torch.int64, device=dev)
         toff = torch.arange(0, (P + 1) * D, D, dtype=torch.int64, device=dev)
@@ -979,6 +991,17 @@ def run_single(a):
         nok = int(ok.sum().item())
         exp = int((~tamper).sum())
         comps = P * (1 + 2 * D)
+        # ---- check vs the oracle, after the timed region (as the multi-rank line)
+        tc = time.perf_counter()
+        orc = _oracle()
+        okh = ok.cpu().numpy()
+        srng = np.random.default_rng(11)
+        sample = np.unique(np.concatenate([np.arange(min(P, 1 << 13)), srng.integers(0, P, 1 << 13),
+                                           tp[:256]]))
+        st_ = torch.from_numpy(sample).to(dev)
+        rk_ok, ns = c5_rank_check(orc, leaf, W, terms.view(P, D, 32)[st_].cpu().numpy(),
+                                  digests[st_].cpu().numpy(), root.cpu().numpy().tobytes(), okh,
+                                  tamper, sample)
         out = {"metric": "htree inclusion-proof re-hash, 10^6 proofs x depth 24 (configs[4])",
                "value": round(P / t / 1e6, 3), "unit": "M proofs/s",
                "ms_per_step": round(t * 1e3, 3), "kernel_ms": round(kms, 3),
@@ -994,7 +1017,14 @@ def run_single(a):
                                     "kernel_ms": round(gen_ms, 3),
                                     "terms_GBps": round(P * D * 32 / (gen_ms * 1e-3) / 1e9, 1)},
                "verified": nok, "expected_verified": exp, "bitmap_exact": nok == exp and bool(
-                   (ok.cpu().numpy().astype(bool) == ~tamper).all())}
+                   (okh.astype(bool) == ~tamper).all()),
+               "root_check": {"vs": "oracle", "ok": bool(rk_ok), "sampled": ns,
+                              "seconds": round(time.perf_counter() - tc, 2),
+                              "what": "every verdict equals the expected bitmap (10 % of the "
+                                      "proofs with one bit of one term flipped: false, the rest "
+                                      "true), and the oracle's VerifyInclusion (htree.go:166-195) "
+                                      "over the same terms / digests / root of >= 2^13 proofs "
+                                      "gives the device's verdicts"}}
         if not a.no_ahtree:
             out["ahtree"] = c5_ahtree(a, m, N, L, ctx, dev, sync)
 
@@ -1488,7 +1518,14 @@ def main():
         raise SystemExit(relaunch_one_rank())
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 or force:
         return distributed_main(a)
-    print(json.dumps(run_single(a)), flush=True)
+    out = run_single(a)
+    print(json.dumps(out), flush=True)
+    # a line whose own result check failed exits non-zero (as the multi-rank lines)
+    bad = [k for k, v in list(out.items()) + list(out.get("resident_log", {}).items())
+           if isinstance(v, dict) and v.get("root_check", v if k == "root_check" else {}).get("ok") is False]
+    if bad:
+        print("result check FAILED: %s" % bad, file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

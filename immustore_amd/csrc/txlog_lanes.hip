@@ -115,7 +115,13 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
         w = leaf_off ? (uint32_t)(leaf_off[t + 1] - leaf_off[t]) : nent;
     }
     const uint32_t j0 = (uint32_t)i * EP;
-    const uint32_t ne = act && w > j0 ? min((uint32_t)EP, w - j0) : 0;  // this lane's entries
+    // this lane's entries.  No subtraction under a condition: written as
+    // `w > j0 ? min(EP, w - j0) : 0`, LLVM hoisted `sub nuw w, j0` out of its
+    // guard and later turned the guard's select into a plain `or`, so for w <
+    // j0 the test of ne branched on poison, and IndVarSimplify then dropped
+    // the `j < w` bound of round 5's walk -- lanes past a record's last entry
+    // walked off the log (profiles/lanes_walk_isa_r06.txt: ISA and IR trace).
+    const uint32_t ne = act ? min((uint32_t)EP, w - min(w, j0)) : 0u;
     // skip the j0 entries of the lanes to the left; only a lane with entries
     // walks (a lane past the record's last entry has nothing to find).  Each
     // step reads the entry's first 24 bytes at once (mdLen and, for mdLen <=

@@ -17,6 +17,7 @@
 #   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
 #   dist2s / dist8s  the same with --scaling strong (one 2^20 tree split over the ranks);
 #                    dist8s_corrupt: rank 5 corrupted, must exit 1; strong1: N = 1 strong
+#   lanes_check      rebuild with LANES_CHECK=1 (range-checked lanes kernel), then the tx-log tests
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   wdist:<w>:<N>    bench_workloads.py --workload <w> (c3 / c5) as N gloo ranks sharing GPU 0
 #   wcorrupt:<w>:<N> the same with MH_BENCH_CORRUPT=1 (N >= 2): must exit 1 (result check)
@@ -89,6 +90,11 @@ for s in "$@"; do
         --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29539 \
         bench.py --gpus 8 --scaling strong --steps 5 --warmup 1 --prewarm 0 --no-cpu-baseline
       rc=$?; echo "dist8s_corrupt exit $rc (want 1)"; [ $rc -eq 1 ] || exit 1 ;;
+    lanes_check)  # the range-checking k_txlog_lanes (make LANES_CHECK=1, built here over the snapshot's
+      # library) under every tx-log test: any read outside the log fails the call
+      step lanes_build 600 make -s -j16 -C immustore_amd/csrc LANES_CHECK=1 || exit 1
+      step lanes_check 900 python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread tests/ \
+        -k "txlog or clog or resident or fused or c_client" || exit 1 ;;
     strong1) step strong1 300 python bench.py --scaling strong --steps 200 --warmup 5 --no-cpu-baseline || exit 1 ;;
     wdist:*|wcorrupt:*)  # bench_workloads.py multi-rank lines, N gloo ranks sharing GPU 0
       w=$(echo "$s" | cut -d: -f2); n=$(echo "$s" | cut -d: -f3); kind=${s%%:*}
