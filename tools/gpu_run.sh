@@ -17,6 +17,7 @@
 #   dist8            8 gloo ranks sharing GPU 0 (the driver's N = 8 path rehearsed)
 #   dist2s / dist8s  the same with --scaling strong (one 2^20 tree split over the ranks);
 #                    dist8s_corrupt: rank 5 corrupted, must exit 1; strong1: N = 1 strong
+#   committers       tests/c_client/mh_committers: threads x clique-pool sizes -> committers.txt
 #   lanes_check      rebuild with LANES_CHECK=1 (range-checked lanes kernel), then the tx-log tests
 #   c4               bench.py --config c4 (2^23 x 4 KiB, sampled root check)
 #   wdist:<w>:<N>    bench_workloads.py --workload <w> (c3 / c5) as N gloo ranks sharing GPU 0
@@ -95,6 +96,15 @@ for s in "$@"; do
       step lanes_build 600 make -s -j16 -C immustore_amd/csrc LANES_CHECK=1 || exit 1
       step lanes_check 900 python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread tests/ \
         -k "txlog or clog or resident or fused or c_client" || exit 1 ;;
+    committers)  # concurrent committers over a clique pool (tests/c_client/mh_committers): aggregate
+      # GiB/s of values per (threads, cliques), 3 interleaved rounds
+      for r in 1 2 3; do
+        for tc in "2 1" "2 2" "4 1" "4 2" "4 4"; do
+          set -- $tc
+          line=$(timeout -k 10 120 tests/c_client/mh_committers $1 $2 ${CM_ROUNDS:-10} ${CM_NTX:-4096} 16 1024 | grep '^rate') || exit 1
+          echo "round $r threads $1 cliques $2 $line" | tee -a "$O/committers.txt"
+        done
+      done ;;
     strong1) step strong1 300 python bench.py --scaling strong --steps 200 --warmup 5 --no-cpu-baseline || exit 1 ;;
     wdist:*|wcorrupt:*)  # bench_workloads.py multi-rank lines, N gloo ranks sharing GPU 0
       w=$(echo "$s" | cut -d: -f2); n=$(echo "$s" | cut -d: -f3); kind=${s%%:*}
