@@ -269,7 +269,7 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
         // the caller's arrays: one copy each, or -- when they all lie in one
         // pinned allocation (the shim's packing arena) with little between
         // them -- ONE copy of the whole span, each array then addressed inside
-        // it (MH_DOC_ARENA=0: per-array copies, A/B)
+        // it
         struct Up {
             uint64_t off;
             const uint8_t *src;
@@ -309,12 +309,8 @@ extern "C" int mh_verify_document_batch(mh_ctx *c, const mh_document_batch *B, i
                 hi = hi ? std::max(hi, u.src + u.bytes) : u.src + u.bytes;
                 sum += u.bytes;
             }
-        static const bool arena_on = [] {
-            const char *e = getenv("MH_DOC_ARENA");
-            return !(e && e[0] == '0');
-        }();
         const uint8_t *alo = lo ? reinterpret_cast<const uint8_t *>((uintptr_t)lo & ~(uintptr_t)255) : nullptr;
-        const bool arena = arena_on && lo && (uint64_t)(hi - alo) <= sum + sum / 4 + (1u << 20) &&
+        const bool arena = lo && (uint64_t)(hi - alo) <= sum + sum / 4 + (1u << 20) &&
                            pinned_same_alloc(alo, hi - 1);
         const uint64_t b_span = L.add(arena ? (uint64_t)(hi - alo) : 0);
         MH_HIP(c->s_msgs.ensure(L.total));

@@ -234,6 +234,54 @@ struct mh_ctx {
     }
 };
 
+// ---- the tx-log record hop (capi_tx.hip), shared with the multi-device call
+// Records of one stretch of a tx log (the structure readHeader / readEntry
+// read, tx.go:419-603; no hashing).
+// Per record: where it starts, where its stored Alh is, its entry count and
+// the bytes of its entry-digest messages.  The headers themselves are only
+// kept when asked (mh_txlog_scan); the validation path rebuilds them on the
+// device from the raw record bytes (k_tx_hdr_from_raw).
+struct HopRec {
+    uint64_t rec, alh;
+    uint32_t nent, pad;
+};
+
+// A record whose metadata is valid but not in the canonical form Go hashes
+// (the reader re-serialises parsed metadata: KVMetadata.Bytes() in the entry
+// digest, TxMetadata.Bytes() in the inner hash): the canonical bytes the
+// device hashes instead.  kind 0: entry `entry` of the record, bytes = the
+// whole entry record with canonical KV metadata; kind 1: the tx metadata.
+struct HopPatch {
+    uint64_t rec;  // index into HopOut::R
+    uint32_t kind, entry;
+    std::vector<uint8_t> bytes;
+};
+
+struct HopOut {
+    std::vector<HopRec> R;
+    std::vector<HopPatch> P;
+    std::vector<mh_tx_header> H;  // want_headers only
+    bool want_headers = false;
+    uint64_t start = 0, end = 0;  // first record parsed / where parsing stopped
+    int rc = MH_OK;
+    bool stopped = false;  // EOF (id 0 / end of buffer) or a structural error
+};
+
+struct HopLimits {
+    uint32_t max_entries, max_key_len;
+};
+
+// The whole hop of a run of records (no headers kept), as mh_txlog_validate
+// runs it: out.R, out.P, out.rc (the structural status), out.end (consumed).
+void txlog_hop(const uint8_t *buf, uint64_t len, uint32_t max_entries, uint32_t max_key_len,
+               uint64_t max_txs, HopOut &out);
+// mh_txlog_validate with the record structure parsed already (pre: every
+// record of [buf, buf + len) with offsets relative to buf, patches indexed by
+// record, rc MH_OK, end == len): no host hop in the call.
+int txlog_validate_parsed(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                          uint32_t max_key_len, const HopOut &pre, mh_tx_header *hdrs_out,
+                          uint8_t *alh_out, int32_t *status_out);
+
 // Host-to-device copies of a call cut into chunks, issued from one helper
 // thread (or two, chunk k on lane k % 2) onto the context's copy stream(s)
 // with an event after each chunk.  A copy call from pinned memory holds its

@@ -1009,11 +1009,12 @@ extern "C" int mh_multi_verify_dual_proof_v2_batch(
 
 // The read path's re-hash of a tx log (tx.go:388-630: replay,
 // immustore.go:1198-1223; the indexer's readTx, indexer.go:570) over the
-// devices: the host hop finds the record boundaries once (mh_txlog_scan, the
-// call's structural status), the records are cut into K parts of nearly equal
-// bytes at record boundaries -- every record carries its prevAlh, so the parts
-// are independent -- and part d is validated by device d (mh_txlog_validate
-// on its bytes: its own copy over its own link).  A v1 header's md_off is
+// devices: the host hop parses the record structure ONCE (txlog_hop: the
+// call's structural status, the records, any re-encoded metadata), the
+// records are cut into K parts of nearly equal bytes at record boundaries --
+// every record carries its prevAlh, so the parts are independent -- and part
+// d is validated by device d from that parse (txlog_validate_parsed: its own
+// copy over its own link, no second hop).  A v1 header's md_off is
 // relative to buf, as in the single call.
 extern "C" int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t len,
                                        uint32_t max_entries, uint32_t max_key_len,
@@ -1026,39 +1027,55 @@ extern "C" int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t
             return mh_txlog_validate(m->ctx[0], buf, len, max_entries, max_key_len, max_txs,
                                      ntx_out, consumed_out, hdrs_out, alh_out, status_out);
         if (len && !buf) return MH_ERR_ILLEGAL_ARGUMENTS;
-        // a record is >= 122 bytes (90-byte head + 32-byte Alh)
-        const uint64_t cap = std::min<uint64_t>(max_txs, len / 122 + 1);
-        std::vector<uint64_t> aoff(cap ? cap : 1);
-        uint64_t cnt = 0, used = 0;
-        const int rc = mh_txlog_scan(buf, len, max_entries, max_key_len, cap, &cnt, &used, nullptr,
-                                     aoff.data());
-        if (rc < 0) return rc;
+        HopOut all;
+        txlog_hop(buf, len, max_entries, max_key_len, max_txs, all);
+        const uint64_t cnt = all.R.size(), used = all.end;
+        const int rc = all.rc;
         if (ntx_out) *ntx_out = cnt;
         if (consumed_out) *consumed_out = used;
         if (!cnt) return rc;
         // part d: records [t[d], t[d+1]), bytes [start(t[d]), start(t[d+1]))
         const int K = m->K;
-        auto start = [&](uint64_t t) -> uint64_t { return t ? aoff[t - 1] + 32 : 0; };
+        auto start = [&](uint64_t t) -> uint64_t { return t ? all.R[t - 1].alh + 32 : 0; };
         std::vector<uint64_t> t(K + 1, 0);
         t[K] = cnt;
         for (int d = 1; d < K; d++) {
             const uint64_t want = (uint64_t)((unsigned __int128)used * (unsigned)d / (unsigned)K);
-            uint64_t x = (uint64_t)(std::lower_bound(aoff.begin(), aoff.begin() + cnt, want) - aoff.begin());
-            t[d] = std::max(t[d - 1], std::min(x, cnt));  // the first record ending at or after want
+            uint64_t lo = 0, hi = cnt;  // the first record ending at or after want
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                if (all.R[mid].alh < want) lo = mid + 1; else hi = mid;
+            }
+            t[d] = std::max(t[d - 1], std::min(lo, cnt));
+        }
+        // each part's records and patches, rebased to the part
+        std::vector<HopOut> part(K);
+        size_t p = 0;
+        for (int d = 0; d < K; d++) {
+            const uint64_t t0 = t[d], t1 = t[d + 1], b0 = start(t0);
+            HopOut &o = part[d];
+            o.R.reserve(t1 - t0);
+            for (uint64_t k = t0; k < t1; k++)
+                o.R.push_back(HopRec{all.R[k].rec - b0, all.R[k].alh - b0, all.R[k].nent, 0});
+            for (; p < all.P.size() && all.P[p].rec < t1; p++) {
+                HopPatch pt = all.P[p];
+                pt.rec -= t0;
+                o.P.push_back(std::move(pt));
+            }
+            o.rc = MH_OK;
+            o.end = start(t1) - b0;
         }
         std::lock_guard<std::mutex> lk(m->mu);
         const int st = per_device(K, [&](int d) -> int {
             const uint64_t t0 = t[d], t1 = t[d + 1];
             if (t1 == t0) return MH_OK;
             const uint64_t b0 = start(t0), b1 = start(t1);
-            uint64_t n = 0, u = 0;
-            int r = mh_txlog_validate(m->ctx[d], buf + b0, b1 - b0, max_entries, max_key_len,
-                                      t1 - t0, &n, &u, hdrs_out ? hdrs_out + t0 : nullptr,
-                                      alh_out ? alh_out + 32 * t0 : nullptr,
-                                      status_out ? status_out + t0 : nullptr);
-            if (r < 0) return r;
-            // the part's records parsed as in the whole-log scan
-            if (r != MH_OK || n != t1 - t0 || u != b1 - b0) return MH_ERR_ILLEGAL_STATE;
+            const int r = txlog_validate_parsed(m->ctx[d], buf + b0, b1 - b0, max_entries,
+                                                max_key_len, part[d],
+                                                hdrs_out ? hdrs_out + t0 : nullptr,
+                                                alh_out ? alh_out + 32 * t0 : nullptr,
+                                                status_out ? status_out + t0 : nullptr);
+            if (r != MH_OK) return r < 0 ? r : MH_ERR_ILLEGAL_STATE;
             if (hdrs_out)
                 for (uint64_t k = t0; k < t1; k++)
                     if (hdrs_out[k].version == 1) hdrs_out[k].md_off += (uint32_t)b0;

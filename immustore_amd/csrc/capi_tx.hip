@@ -599,42 +599,6 @@ extern "C" int mh_verify_dual_proof_batch(mh_ctx *c, const mh_dual_proof_batch *
 // ------------------------------------------------------------------ a14
 namespace {
 
-// Records of one stretch of a tx log (the structure readHeader / readEntry
-// read, tx.go:419-603; no hashing).
-// Per record: where it starts, where its stored Alh is, its entry count and
-// the bytes of its entry-digest messages.  The headers themselves are only
-// kept when asked (mh_txlog_scan); the validation path rebuilds them on the
-// device from the raw record bytes (k_tx_hdr_from_raw).
-struct HopRec {
-    uint64_t rec, alh;
-    uint32_t nent, pad;
-};
-
-// A record whose metadata is valid but not in the canonical form Go hashes
-// (the reader re-serialises parsed metadata: KVMetadata.Bytes() in the entry
-// digest, TxMetadata.Bytes() in the inner hash): the canonical bytes the
-// device hashes instead.  kind 0: entry `entry` of the record, bytes = the
-// whole entry record with canonical KV metadata; kind 1: the tx metadata.
-struct HopPatch {
-    uint64_t rec;  // index into HopOut::R
-    uint32_t kind, entry;
-    std::vector<uint8_t> bytes;
-};
-
-struct HopOut {
-    std::vector<HopRec> R;
-    std::vector<HopPatch> P;
-    std::vector<mh_tx_header> H;  // want_headers only
-    bool want_headers = false;
-    uint64_t start = 0, end = 0;  // first record parsed / where parsing stopped
-    int rc = MH_OK;
-    bool stopped = false;  // EOF (id 0 / end of buffer) or a structural error
-};
-
-struct HopLimits {
-    uint32_t max_entries, max_key_len;
-};
-
 inline uint64_t be16p(const uint8_t *q) { return (uint64_t)((uint32_t)q[0] << 8 | q[1]); }
 
 // KVMetadata.unsafeReadFrom + Bytes() (kv_metadata.go:207-256): deleted(0),
@@ -1108,7 +1072,8 @@ static void fill_header_host(const uint8_t *buf, uint64_t rec, uint64_t *h) {
 static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlog, uint64_t len,
                                uint32_t max_entries, uint32_t max_key_len, uint64_t max_txs,
                                uint64_t *ntx_out, uint64_t *consumed_out, mh_tx_header *hdrs_out,
-                               uint8_t *alh_out, int32_t *status_out, bool take_lock = true) {
+                               uint8_t *alh_out, int32_t *status_out, bool take_lock = true,
+                               const HopOut *parsed = nullptr) {
     return mh_guard([&]() -> int {
         if (!c || (len && !buf)) return MH_ERR_ILLEGAL_ARGUMENTS;
         // The raw records go to the device first, in chunks with an event
@@ -1412,6 +1377,7 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
         };
         size_t deferred = 0;  // gs[0, deferred) are queued
         uint64_t pos = 0, e_done = 0;
+        size_t pre_r = 0, pre_p = 0;  // the next pre-parsed record / patch
         // (a log past 4 GiB is parsed in one phase: hop_record's 32-bit
         // metadata-offset check depends on where the parse starts)
         const uint64_t nphase = len <= 0xffffffffull ? nck : 1;
@@ -1420,7 +1386,27 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             const uint64_t end = k + 1 < nphase ? cut[k + 1] : len;
             const uint64_t r0 = hop.R.size();
             HopOut h;
-            hop_all(buf + pos, end - pos, max_txs - r0, lim, h, false);
+            if (parsed) {
+                // parsed already (the multi-device call): the phase's records
+                // are those ending inside it, and the phase reads as truncated
+                // while more records follow, as the hop of a cut log does
+                for (; pre_r < parsed->R.size() && r0 + h.R.size() < max_txs &&
+                       parsed->R[pre_r].alh + 32 <= end;
+                     pre_r++) {
+                    const HopRec &r = parsed->R[pre_r];
+                    for (; pre_p < parsed->P.size() && parsed->P[pre_p].rec == pre_r; pre_p++) {
+                        HopPatch pt = parsed->P[pre_p];
+                        pt.rec = h.R.size();
+                        h.P.push_back(std::move(pt));
+                    }
+                    h.R.push_back(HopRec{r.rec - pos, r.alh - pos, r.nent, 0});
+                }
+                h.end = h.R.empty() ? 0 : h.R.back().alh + 32;
+                h.rc = pre_r < parsed->R.size() ? MH_ERR_TRUNCATED : MH_OK;
+                if (h.rc == MH_OK) h.end = end - pos;  // (the pre-parsed run ends at len)
+            } else {
+                hop_all(buf + pos, end - pos, max_txs - r0, lim, h, false);
+            }
             for (const HopRec &r : h.R) hop.R.push_back(HopRec{r.rec + pos, r.alh + pos, r.nent, 0});
             for (HopPatch &pt : h.P) {
                 pt.rec += r0;
@@ -1454,7 +1440,7 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
             if (!more) break;
             pos = hop.end;
         }
-        if (!nck) hop_all(buf, len, max_txs, lim, hop, false);  // empty log
+        if (!nck && !parsed) hop_all(buf, len, max_txs, lim, hop, false);  // empty log
         for (; deferred < gs.size(); deferred++) {
             if (int e = launch(gs[deferred])) return e;
         }
@@ -1563,6 +1549,23 @@ extern "C" int mh_txlog_validate(mh_ctx *c, const uint8_t *buf, uint64_t len, ui
                                  int32_t *status_out) {
     return txlog_validate_impl(c, buf, nullptr, len, max_entries, max_key_len, max_txs, ntx_out,
                                consumed_out, hdrs_out, alh_out, status_out);
+}
+
+void txlog_hop(const uint8_t *buf, uint64_t len, uint32_t max_entries, uint32_t max_key_len,
+               uint64_t max_txs, HopOut &out) {
+    hop_all(buf, len, max_txs, HopLimits{max_entries, max_key_len}, out, false);
+}
+
+int txlog_validate_parsed(mh_ctx *c, const uint8_t *buf, uint64_t len, uint32_t max_entries,
+                          uint32_t max_key_len, const HopOut &pre, mh_tx_header *hdrs_out,
+                          uint8_t *alh_out, int32_t *status_out) {
+    if (pre.rc != MH_OK || pre.end != len) return MH_ERR_ILLEGAL_STATE;
+    uint64_t n = 0, used = 0;
+    const int rc = txlog_validate_impl(c, buf, nullptr, len, max_entries, max_key_len,
+                                       pre.R.size(), &n, &used, hdrs_out, alh_out, status_out,
+                                       true, &pre);
+    if (rc == MH_OK && (n != pre.R.size() || used != len)) return MH_ERR_ILLEGAL_STATE;
+    return rc;
 }
 
 extern "C" int mh_txlog_validate_resident(mh_ctx *c, const uint8_t *buf, const uint8_t *dlog,

@@ -273,7 +273,7 @@ template <int LPL>
 __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
     const uint8_t *__restrict__ vals, uint32_t val_len, const uint8_t *__restrict__ keys,
     uint32_t key_len, int version, uint64_t n, uint8_t *__restrict__ hvals_out,
-    uint8_t *__restrict__ levels, LaneLevels la, int wg_levels, int prio) {
+    uint8_t *__restrict__ levels, LaneLevels la, int wg_levels) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -329,20 +329,6 @@ __global__ __launch_bounds__(kFixedThreads) void k_entries_fixed(
             // no state-machine dispatch per block
 #pragma unroll 1
             for (; b < nfull; b++) {
-                if (prio && (b & 3) == 0) {
-                    // issue priority falls as the wave progresses (3 at the start, 0
-                    // in its last quarter): priority outranks age in the SIMD's
-                    // arbitration, so a workgroup dispatched later catches up with
-                    // the older ones on its CU instead of running alone, at one
-                    // wave per SIMD, after they are done (the launch's tail)
-                    const uint32_t q = ((uint32_t)i * nfull + b) * 4u / ((uint32_t)LPL * nfull);
-                    switch (q) {
-                        case 0: __builtin_amdgcn_s_setprio(3); break;
-                        case 1: __builtin_amdgcn_s_setprio(2); break;
-                        case 2: __builtin_amdgcn_s_setprio(1); break;
-                        default: __builtin_amdgcn_s_setprio(0); break;
-                    }
-                }
                 const uint32_t u = b >> 1;
                 const bool two = u < nsteps2;
                 const int h = two ? (int)(b & 1) : 0;
@@ -810,20 +796,17 @@ hipError_t launch_entries_fixed(hipStream_t st, Timer *tm, int version, uint64_t
     // the end of the leaf kernel.
     int wgl = 1;
     if (const char *e = getenv("MH_WG_LEVELS")) wgl = std::max(0, std::min(8, atoi(e)));
-    // falling wave priority over each wave's work (k_entries_fixed, A/B knob)
-    int prio = 0;
-    if (const char *e = getenv("MH_SETPRIO")) prio = atoi(e) != 0;
     {
         TimerScope ts(tm, "entries_fixed", st);
         if (lpl == 4)
             hipLaunchKernelGGL(k_entries_fixed<4>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl, prio);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
         else if (lpl == 2)
             hipLaunchKernelGGL(k_entries_fixed<2>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl, prio);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
         else
             hipLaunchKernelGGL(k_entries_fixed<1>, dim3(grid), dim3(kFixedThreads), lds, st, vals,
-                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl, prio);
+                               val_len, keys, key_len, version, n, hvals_out, levels, la, wgl);
     }
     *levels_done = std::min((lpl == 4 ? 2 : lpl == 2 ? 1 : 0) + wgl, g.nlevels - 1);
     return hipGetLastError();

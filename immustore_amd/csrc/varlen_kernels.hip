@@ -483,13 +483,13 @@ size_t sha_varlen_scratch_bytes(uint64_t n) {
 }
 
 // Length-class order of n messages (perm in scratch), or null when the batch
-// is too small to profit or MH_VARLEN_NOSORT is set (A/B switch).
+// is too small to profit (unsorted: 438 vs 1170 GiB/s of ragged values,
+// DESIGN.md history, round 2).
 static const uint32_t *nb_sort(hipStream_t st, Timer *tm, const uint64_t *off, const uint8_t *use,
                                uint64_t n, uint8_t *scratch, hipError_t *err) {
-    static const bool nosort = getenv("MH_VARLEN_NOSORT") != nullptr;
     *err = hipSuccess;
     // below ~16K messages the four sort launches cost more than the divergence
-    if (!scratch || nosort || n < 16384 || n >= 0xffffffffull) return nullptr;
+    if (!scratch || n < 16384 || n >= 0xffffffffull) return nullptr;
     TimerScope ts(tm, "varlen_sort", st);
     uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *cursor = hist + kNbBuckets;
