@@ -387,6 +387,12 @@ def test_multi_txlog_validate_vs_single_and_oracle(m, orc, fixtures, devices):
         bad[int(p)] ^= 0x20
     logs += [bytes(bad), logs[1][:len(logs[1]) * 2 // 3],
              bytes.fromhex(fixtures["long_linear_proof"]["txlog"]), b""]
+    # round 6: the parts are validated from the one host parse (no second hop)
+    # -- re-encoded metadata in several parts, and a > 16 MiB log whose parts
+    # are copied in chunks
+    from tx_util import _bulk_txlog, metadata_logs
+    nc = b"".join(r for n, r in metadata_logs(orc) if n == "noncanonical_sealed_canonical")
+    logs += [nc * 40 + logs[0] + nc * 40, _bulk_txlog(rng, 9000)[0]]
     ctx = m.Context(0)
     md = MultiDevice(devices)
     try:
