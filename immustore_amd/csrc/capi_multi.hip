@@ -1081,7 +1081,18 @@ extern "C" int mh_multi_txlog_validate(mh_multi *m, const uint8_t *buf, uint64_t
                     if (hdrs_out[k].version == 1) hdrs_out[k].md_off += (uint32_t)b0;
             return MH_OK;
         });
-        return st ? st : rc;
+        if (st) return st;
+        // a header whose tx metadata was re-encoded points at the canonical
+        // copy placed after the log (md_off >= len): where the one-device call
+        // places it, i.e. after the whole log, the patches in log order
+        if (hdrs_out) {
+            uint64_t side = 0;
+            for (const HopPatch &pt : all.P) {
+                if (pt.kind == 1 && pt.rec < cnt) hdrs_out[pt.rec].md_off = (uint32_t)(len + side);
+                side += pt.bytes.size();
+            }
+        }
+        return rc;
     });
 }
 
