@@ -1158,6 +1158,27 @@ def run_single(a):
         if not (clog_ok and clog_bad_ok):
             print(json.dumps({"clog_check_failed": True}), file=sys.stderr)
             sys.exit(1)
+        # the log in host memory (the pinned arena of the headline call, and a
+        # pageable copy) indexed by its cLog: copied up in chunks, each chunk's
+        # records checked as it lands -- the headline's PCIe-inclusive work
+        # without the host hop; results into the pinned arena
+        for key, src in (("clog_host_pinned", raw), ("clog_host_pageable", raw_pageable)):
+            def step_hcl(src=src):
+                r = txlog_validate_clog(src, src.size, None, ntx=ntx, clog_dev=dcl.data_ptr(), ctx=ctx,
+                                        out=outs)
+                assert r[0] == 0 and r[1] == 0 and r[2] == ntx
+
+            prewarm(step_hcl, sync, a.prewarm)
+            th = timed_k(ctx, step_hcl, a.steps, a.warmup, sync)
+            ok = bool(np.array_equal(outs[1], alh) and not outs[2].any()
+                      and np.array_equal(outs[1][samp], o_alh))
+            resident[key] = {"ms_per_call": round(th * 1e3, 3),
+                             "M_tx_per_s": round(ntx / th / 1e6, 3),
+                             "root_check": {"vs": "oracle (256 sampled records) + the sealed Alh",
+                                            "ok": ok}}
+            if not ok:
+                print(json.dumps({key + "_check_failed": True}), file=sys.stderr)
+                sys.exit(1)
         del dres
         _, _, _, _, _, sts = m.txlog_validate(raw, ctx=ctx)
         bad = raw_pageable.copy()

@@ -1236,7 +1236,7 @@ static int txlog_validate_impl(mh_ctx *c, const uint8_t *buf, const uint8_t *dlo
                 MH_HIP(launch_fetch_host(st, HostRuns{{g.pro, g.pap, g.plo}, {ro, ap, lo}, {nt, nt, nt + 1}}));
             if (g.small && npe + nph == 0) {  // the whole chain in one launch
                 if (pre)  // the resident bytes' structure against the host's
-                    MH_HIP(launch_txlog_struct(st, c->tm(), nt, db, len, nullptr, 0, ro, ap, lo,
+                    MH_HIP(launch_txlog_struct(st, c->tm(), nt, db, len, len, nullptr, 0, ro, ap, lo,
                                                max_entries, max_key_len, pre,
                                                (uint64_t *)(base + g.b_stats)));
                 // pinned outputs: the kernel writes the results there itself
@@ -1628,14 +1628,23 @@ static void *kernel_dst(void *p, uint64_t bytes, bool *bad, bool *is_dev) {
     return nullptr;
 }
 
-// a14 over a tx log that is already in HBM, indexed by its commit log
-// (txOffsetAndSize, immustore.go:2569-2597): no host copy and no host hop.
-// The structure pass (txlog_struct.hip) parses every record where its cLog
-// entry points, with every check of the host hop; the lane kernel hashes
-// the accepted ones (entry digests, htree, innerHash, Alh vs the stored Alh);
-// a record whose metadata is valid but not canonical (Go hashes the
-// re-serialised form) or that is wider than the lane kernel takes is
-// re-validated by mh_txlog_validate on a host copy of that record alone.
+// a14 over a tx log indexed by its commit log (txOffsetAndSize,
+// immustore.go:2569-2597): no host hop.  The structure pass
+// (txlog_struct.hip) parses every record where its cLog entry points, with
+// every check of the host hop; the lane kernel hashes the accepted ones (entry
+// digests, htree, innerHash, Alh vs the stored Alh); a record whose metadata
+// is valid but not canonical (Go hashes the re-serialised form), that is wider
+// than the lane kernel takes, or whose read runs past the bytes landed when
+// its group ran is re-validated by mh_txlog_validate on a host copy of that
+// record alone.
+//  * log in device memory: one group, no copy;
+//  * log in host memory (pinned: the cgo shim's arena): copied up in chunks
+//    (5 : 2 : 1 from 16 MiB, as mh_txlog_validate), each chunk's records --
+//    those whose cLog entry ends inside it, when the entries are in log order
+//    -- checked as soon as it lands, under the copy of the rest; the lane
+//    kernel takes its entries per lane from the structure pass's widest
+//    record on the device (launch shape from the cLog sizes), so nothing
+//    waits on the host between the chunks.
 extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t len,
                                       const uint8_t *clog, uint64_t ntx, uint32_t clog_entry_size,
                                       uint32_t max_entries, uint32_t max_key_len,
@@ -1651,84 +1660,244 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         if (ntx > (1ull << 40)) return MH_ERR_ILLEGAL_ARGUMENTS;
         std::lock_guard<std::mutex> lk(c->mu);
         hipSetDevice(c->device);
+        MH_HIP(c->copy_lane());
         hipStream_t st = c->stream;
-        // the kernels' unguarded block reads run up to 256 bytes past a record
-        if (!dev_range(dlog, len + 256)) return MH_ERR_ILLEGAL_ARGUMENTS;
-        hipPointerAttribute_t ca;
-        const bool clog_dev = hipPointerGetAttributes(&ca, clog) == hipSuccess &&
-                              ca.type == hipMemoryTypeDevice;
-        (void)hipGetLastError();
+        auto is_dev = [](const void *q) {
+            hipPointerAttribute_t a;
+            const bool d = hipPointerGetAttributes(&a, q) == hipSuccess && a.type == hipMemoryTypeDevice;
+            (void)hipGetLastError();
+            return d;
+        };
+        const bool log_dev = is_dev(dlog), clog_dev = is_dev(clog);
+        // a resident log: the kernels' unguarded block reads run up to 256
+        // bytes past a record, inside the allocation
+        if (log_dev && !dev_range(dlog, len + 256)) return MH_ERR_ILLEGAL_ARGUMENTS;
         if (clog_dev && !dev_range(clog, ntx * es)) return MH_ERR_ILLEGAL_ARGUMENTS;
         bool bad = false, st_dev, alh_dev, hd_dev;
         uint32_t *k_st = (uint32_t *)kernel_dst(status_out, ntx * 4, &bad, &st_dev);
         uint32_t *k_alh = (uint32_t *)kernel_dst(alh_out, ntx * 32, &bad, &alh_dev);
         uint64_t *k_hd = (uint64_t *)kernel_dst(hdrs_out, ntx * sizeof(mh_tx_header), &bad, &hd_dev);
         if (bad || ((uintptr_t)k_hd & 7)) return MH_ERR_ILLEGAL_ARGUMENTS;
+        // ---- copy chunks and record groups of a host log
+        const bool pinned = !log_dev && len && pinned_same_alloc(dlog, dlog + len - 1);
+        std::vector<uint64_t> cut{0, len};
+        if (!log_dev && len >= (16ull << 20)) {
+            const std::vector<double> wts = pinned ? txlog_weights() : std::vector<double>{3, 1};
+            const uint64_t K = wts.size();
+            cut.assign(K + 1, 0);
+            double wsum = 0, acc = 0;
+            for (double w : wts) wsum += w;
+            for (uint64_t k = 1; k < K; k++) {
+                acc += wts[k - 1];
+                cut[k] = std::max<uint64_t>(cut[k - 1], (uint64_t)((double)len * acc / wsum) & ~4095ull);
+            }
+            cut[K] = len;
+        }
+        const uint64_t nck = cut.size() - 1;
+        // the host's view of the cLog entries (for the groups and the launch
+        // shapes of a host log, and for the host fallback)
+        std::vector<uint8_t> hcl_copy;
+        const uint8_t *hcl = clog_dev ? nullptr : clog;
+        if (clog_dev && !log_dev) {
+            hcl_copy.resize(ntx * es);
+            MH_HIP(hipMemcpy(hcl_copy.data(), clog, ntx * es, hipMemcpyDeviceToHost));
+            hcl = hcl_copy.data();
+        }
+        // group g: records [tg[g], tg[g+1]), read within the first lim[g] bytes
+        std::vector<uint64_t> tg{0, ntx}, lim{len}, bound{kTxlLanesMaxEntries};
+        if (!log_dev) {
+            // the widest record a cLog size allows: header + Alh >= 124 bytes,
+            // an entry >= 48 (2 + 2 + 4 + 8 + 32)
+            auto wbound = [&](uint64_t t) -> uint64_t {
+                const uint64_t sz = be_at(hcl + t * es + 8, 4);
+                return std::min<uint64_t>(kTxlLanesMaxEntries, sz >= 124 ? (sz - 124) / 48 : 0);
+            };
+            bool ordered = true;
+            uint64_t prev_end = 0;
+            std::vector<uint64_t> end(ntx);
+            for (uint64_t t = 0; t < ntx; t++) {
+                const uint64_t off = be_at(hcl + t * es, 8), sz = be_at(hcl + t * es + 8, 4);
+                end[t] = off + sz < off ? ~0ull : off + sz;
+                ordered &= end[t] >= prev_end;
+                prev_end = end[t];
+            }
+            if (ordered && nck > 1) {
+                tg.assign(nck + 1, 0);
+                lim.assign(nck, len);
+                for (uint64_t k = 1; k < nck; k++) {
+                    tg[k] = (uint64_t)(std::upper_bound(end.begin(), end.end(), cut[k]) - end.begin());
+                    lim[k - 1] = cut[k];
+                }
+                tg[nck] = ntx;
+            } else {
+                tg = {0, ntx};
+                lim = {len};
+            }
+            bound.assign(tg.size() - 1, 1);
+            for (size_t g = 0; g + 1 < tg.size(); g++)
+                for (uint64_t t = tg[g]; t < tg[g + 1]; t++) bound[g] = std::max(bound[g], wbound(t));
+        }
+        const size_t ng = tg.size() - 1;
         Layout L;
         const uint64_t b_ro = L.add(ntx * 8), b_ao = L.add(ntx * 8), b_pre = L.add(ntx * 4),
                        b_st = L.add(ntx * 4), b_eh = L.add(ntx * 32), b_a = L.add(ntx * 32),
                        b_hd = L.add(hdrs_out && !k_hd ? ntx * sizeof(mh_tx_header) : 0),
-                       b_cl = L.add(clog_dev ? 0 : ntx * es), b_stats = L.add(4 * 8);
+                       b_cl = L.add(clog_dev ? 0 : ntx * es), b_stats = L.add((4 + 2 * ng) * 8);
         MH_HIP(c->s_clog.ensure(L.total));
         uint8_t *base = c->s_clog.as<uint8_t>();
         uint64_t *ro = (uint64_t *)(base + b_ro), *ao = (uint64_t *)(base + b_ao),
-                 *stats = (uint64_t *)(base + b_stats);
+                 *stats = (uint64_t *)(base + b_stats), *gstats = stats + 4;
         int32_t *pre = (int32_t *)(base + b_pre), *sts = (int32_t *)(base + b_st);
         MhTxHeader *hd = hdrs_out && !k_hd ? (MhTxHeader *)(base + b_hd) : nullptr;
         const uint8_t *dcl = clog_dev ? clog : base + b_cl;
-        MH_HIP(hipMemsetAsync(stats, 0, 3 * 8, st));
+        if (!log_dev) MH_HIP(c->s_txlog.ensure(len + 256));
+        const uint8_t *db = log_dev ? dlog : c->s_txlog.as<uint8_t>();
+        MH_HIP(hipMemsetAsync(stats, 0, (4 + 2 * ng) * 8, st));
         MH_HIP(hipMemsetAsync(stats + 3, 0xff, 8, st));
         if (!clog_dev) MH_HIP(hipMemcpyAsync(base + b_cl, clog, ntx * es, hipMemcpyHostToDevice, st));
-        // 1. every record's structure where its cLog entry points
-        MH_HIP(launch_txlog_struct(st, c->tm(), ntx, dlog, len, dcl, es, ro, ao, nullptr, max_entries,
-                                   max_key_len, pre, stats));
-        MH_HIP(c->p_small.ensure(64));
+        MH_HIP(c->p_small.ensure(64 + 16 * ng));
         volatile uint64_t *hs = c->p_small.as<volatile uint64_t>();
-        MH_HIP(hipMemcpyAsync((void *)hs, stats, 2 * 8, hipMemcpyDeviceToHost, st));
-        MH_HIP(hipStreamSynchronize(st));  // the widest record sizes the lane kernel's launch
-        const uint64_t wmax = hs[0], nhost = hs[1];
-        // 2. the accepted records hashed and checked
-        TxlogHostOut ho;
-        ho.status = k_st;
-        ho.alh = k_alh;
-        ho.hdrs = k_hd;
-        MH_HIP(launch_txlog_lanes(st, c->tm(), ntx, dlog, ro, ao, nullptr, pre, hd, base + b_eh,
-                                  base + b_a, sts, ho, std::max<uint64_t>(wmax, 1), len));
-        // 3. records for the host hop (rare: a log not written by immudb)
-        struct Fix {
-            uint64_t t;
-            int32_t st;
-            mh_tx_header h;
-            uint8_t alh[32];
+        // every exit waits for the streams (kernels may store into the caller's
+        // pinned / device arrays; copies read the caller's log)
+        struct StreamGuard {
+            hipStream_t a;
+            bool armed = true;
+            ~StreamGuard() {
+                if (armed) hipStreamSynchronize(a);
+            }
+        } guard{st};
+        ChunkCopier cc(c);
+        if (!log_dev) {
+            MH_HIP(ensure_chunk_events(c, nck));
+            cc.chunks.resize(nck);
+            for (uint64_t k = 0; k < nck; k++)
+                cc.chunks[k] = {{const_cast<uint8_t *>(db) + cut[k], dlog + cut[k], cut[k + 1] - cut[k]}};
+            cc.inline_issue = pinned;
+            MH_HIP(cc.start());
+        }
+        TxlogHostOut ho0;
+        ho0.status = k_st;
+        ho0.alh = k_alh;
+        ho0.hdrs = k_hd;
+        // group g's arrays start at its first record
+        auto run_group = [&](size_t g, uint64_t wmax, const uint64_t *wmax_dev) -> int {
+            const uint64_t t0 = tg[g], n = tg[g + 1] - t0;
+            if (!n) return MH_OK;
+            TxlogHostOut ho = ho0;
+            if (ho.status) ho.status += t0;
+            if (ho.alh) ho.alh += t0 * 8;
+            if (ho.hdrs) ho.hdrs += t0 * 17;
+            MH_HIP(launch_txlog_lanes(st, c->tm(), n, db, ro + t0, ao + t0, nullptr, pre + t0,
+                                      hd ? hd + t0 : nullptr, base + b_eh + t0 * 32,
+                                      base + b_a + t0 * 32, sts + t0, ho, std::max<uint64_t>(wmax, 1),
+                                      len, wmax_dev));
+            return MH_OK;
         };
-        std::vector<Fix> fix;
+        uint64_t nhost = 0;
+        if (log_dev) {
+            // 1. every record's structure where its cLog entry points
+            MH_HIP(launch_txlog_struct(st, c->tm(), ntx, db, len, len, dcl, es, ro, ao, nullptr,
+                                       max_entries, max_key_len, pre, gstats));
+            MH_HIP(hipMemcpyAsync((void *)hs, gstats, 2 * 8, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipStreamSynchronize(st));  // the widest record sizes the lane kernel's launch
+            nhost = hs[1];
+            // 2. the accepted records hashed and checked
+            if (int e = run_group(0, hs[0], nullptr)) return e;
+        } else {
+            for (size_t g = 0; g < ng; g++) {
+                const uint64_t t0 = tg[g], n = tg[g + 1] - t0;
+                // the group's bytes have landed: chunk g (or every chunk for the
+                // one group of a cLog out of log order)
+                const size_t ck = ng == nck ? g : nck - 1;
+                if (ng == nck || g == 0) {
+                    for (size_t k = ng == nck ? ck : 0; k <= ck; k++) {
+                        if (hipError_t e = cc.wait(k)) return -(int)e;
+                        MH_HIP(cc.stream_wait(st, k));
+                    }
+                }
+                if (!n) continue;
+                MH_HIP(launch_txlog_struct(st, c->tm(), n, db, len, lim[g], dcl + t0 * es, es, ro + t0,
+                                           ao + t0, nullptr, max_entries, max_key_len, pre + t0,
+                                           gstats + 2 * g));
+                if (int e = run_group(g, bound[g], gstats + 2 * g)) return e;
+            }
+        }
+        // 3. how many records failed, and the first (and, for a host log, how
+        // many records the host must re-validate); results down
+        MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
+        MH_HIP(hipMemcpyAsync((void *)(hs + 2), stats + 2, 2 * 8, hipMemcpyDeviceToHost, st));
+        if (!log_dev)
+            MH_HIP(hipMemcpyAsync((void *)(hs + 8), gstats, 2 * ng * 8, hipMemcpyDeviceToHost, st));
+        auto results_down = [&]() -> int {
+            if (status_out && !k_st) MH_HIP(hipMemcpyAsync(status_out, sts, ntx * 4, hipMemcpyDeviceToHost, st));
+            if (alh_out && !k_alh) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
+            if (hdrs_out && !k_hd)
+                MH_HIP(hipMemcpyAsync(hdrs_out, hd, ntx * sizeof(mh_tx_header), hipMemcpyDeviceToHost, st));
+            return MH_OK;
+        };
+        if (int e = results_down()) return e;
+        MH_HIP(hipStreamSynchronize(st));
+        if (!log_dev) {
+            if (hipError_t e = cc.sync()) return -(int)e;  // the caller's log is no longer read
+            for (size_t g = 0; g < ng; g++) nhost += hs[8 + 2 * g + 1];
+        }
+        // 4. records for the host hop (rare: a log not written by immudb, or a
+        // record that disagrees with its cLog entry)
         if (nhost) {
+            struct Fix {
+                uint64_t t;
+                int32_t st;
+                mh_tx_header h;
+                uint8_t alh[32];
+            };
+            std::vector<Fix> fix;
             std::vector<int32_t> hpre(ntx);
             std::vector<uint64_t> hro(ntx);
-            std::vector<uint8_t> hcl(clog_dev ? ntx * es : 0);
+            if (clog_dev && hcl_copy.empty()) {
+                hcl_copy.resize(ntx * es);
+                MH_HIP(hipMemcpyAsync(hcl_copy.data(), clog, ntx * es, hipMemcpyDeviceToHost, st));
+                hcl = hcl_copy.data();
+            }
             MH_HIP(hipMemcpyAsync(hpre.data(), pre, ntx * 4, hipMemcpyDeviceToHost, st));
             MH_HIP(hipMemcpyAsync(hro.data(), ro, ntx * 8, hipMemcpyDeviceToHost, st));
-            if (clog_dev) MH_HIP(hipMemcpyAsync(hcl.data(), clog, ntx * es, hipMemcpyDeviceToHost, st));
             MH_HIP(hipStreamSynchronize(st));
-            const uint8_t *cl = clog_dev ? hcl.data() : clog;
+            std::vector<uint8_t> rb;
             for (uint64_t t = 0; t < ntx; t++) {
                 if (hpre[t] != kTxlNeedsHost) continue;
-                const uint64_t off = hro[t], size = be_at(cl + t * es + 8, 4);  // parsed: inside the log
-                std::vector<uint8_t> rb(size);
-                MH_HIP(hipMemcpyAsync(rb.data(), dlog + off, size, hipMemcpyDeviceToHost, st));
-                MH_HIP(hipStreamSynchronize(st));
+                const uint64_t off = hro[t], size = be_at(hcl + t * es + 8, 4);
                 Fix f{};
                 f.t = t;
-                uint64_t n = 0, used = 0;
                 int32_t one = 0;
-                const int rc = txlog_validate_impl(c, rb.data(), nullptr, size, max_entries, max_key_len,
-                                                   1, &n, &used, &f.h, f.alh, &one, false);
-                if (rc < 0) return rc;
-                // the structure pass's verdicts first (as the kernel's: then
-                // header and Alh 0), then the Alh compare
+                // the record within its cLog size first (valid records end
+                // there); a read past it needs the rest of the log (readTx reads
+                // on), for the reader's own verdict
+                uint64_t n = 0, used = 0, span = off < len ? std::min(size, len - off) : 0;
+                int rc = off >= len || len - off < 8 ? MH_ERR_TRUNCATED : MH_OK;  // the reader's EOF
+                for (int pass = 0; pass < 2 && rc == MH_OK; pass++) {
+                    const uint8_t *src = dlog + off;
+                    if (log_dev) {
+                        rb.resize(span);
+                        MH_HIP(hipMemcpy(rb.data(), dlog + off, span, hipMemcpyDeviceToHost));
+                        src = rb.data();
+                    }
+                    n = used = 0;
+                    memset(&f.h, 0, sizeof f.h);
+                    rc = txlog_validate_impl(c, src, nullptr, span, max_entries, max_key_len, 1, &n,
+                                             &used, &f.h, f.alh, &one, false);
+                    if (rc < 0) return rc;
+                    if ((rc != MH_ERR_TRUNCATED && (rc != MH_OK || n == 1)) || span == len - off) break;
+                    span = len - off;
+                    rc = MH_OK;
+                }
                 int s1 = rc != MH_OK ? rc : n != 1 ? MH_ERR_TRUNCATED : used != size ? MH_ERR_CORRUPTED_DATA : MH_OK;
-                if (s1 == MH_OK && es == 44 && memcmp(cl + t * es + 12, rb.data() + size - 32, 32))
-                    s1 = MH_ERR_CORRUPTED_DATA;
+                if (s1 == MH_OK && es == 44) {
+                    uint8_t a[32];
+                    if (log_dev)
+                        MH_HIP(hipMemcpy(a, dlog + off + size - 32, 32, hipMemcpyDeviceToHost));
+                    else
+                        memcpy(a, dlog + off + size - 32, 32);
+                    if (memcmp(hcl + t * es + 12, a, 32)) s1 = MH_ERR_CORRUPTED_DATA;
+                }
                 if (s1 != MH_OK) {
                     memset(&f.h, 0, sizeof f.h);
                     memset(f.alh, 0, 32);
@@ -1753,17 +1922,12 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
                 if (hd_dev)
                     MH_HIP(hipMemcpyAsync(hdrs_out + t, &pf[k].h, sizeof(mh_tx_header), hipMemcpyHostToDevice, st));
             }
-        }
-        // 4. how many records failed, and the first
-        MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
-        MH_HIP(hipMemcpyAsync((void *)(hs + 2), stats + 2, 2 * 8, hipMemcpyDeviceToHost, st));
-        if (status_out && !k_st) MH_HIP(hipMemcpyAsync(status_out, sts, ntx * 4, hipMemcpyDeviceToHost, st));
-        if (alh_out && !k_alh) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
-        if (hdrs_out && !k_hd)
-            MH_HIP(hipMemcpyAsync(hdrs_out, hd, ntx * sizeof(mh_tx_header), hipMemcpyDeviceToHost, st));
-        MH_HIP(hipStreamSynchronize(st));
-        if (!fix.empty()) {
-            const Fix *pf = c->p_stage.as<Fix>();
+            MH_HIP(hipMemsetAsync(stats + 2, 0, 8, st));
+            MH_HIP(hipMemsetAsync(stats + 3, 0xff, 8, st));
+            MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
+            MH_HIP(hipMemcpyAsync((void *)(hs + 2), stats + 2, 2 * 8, hipMemcpyDeviceToHost, st));
+            if (int e = results_down()) return e;
+            MH_HIP(hipStreamSynchronize(st));
             for (size_t k = 0; k < fix.size(); k++) {  // host outputs (pinned: the kernel wrote zeros)
                 const uint64_t t = pf[k].t;
                 if (status_out && !st_dev) status_out[t] = pf[k].st;
@@ -1771,6 +1935,7 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
                 if (hdrs_out && !hd_dev) hdrs_out[t] = pf[k].h;
             }
         }
+        guard.armed = false;
         if (nbad_out) *nbad_out = hs[2];
         if (first_bad_out) *first_bad_out = hs[2] ? hs[3] : ntx;
         return MH_OK;

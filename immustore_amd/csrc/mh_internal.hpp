@@ -287,13 +287,16 @@ hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint
                              const uint64_t *h_alh_off);
 // every record on 1-16 lanes, each lane's subtree serial (k_txlog_lanes,
 // txlog_lanes.hip), wmax <= kTxlLanesMaxEntries; log_len: the log's length
-// (the checking build's range)
+// (the checking build's range).  wmax_dev (nullable): the widest record as the
+// structure pass found it on the device; wmax is then an upper bound of it
+// (the launch shape), the kernel takes the entries per lane from wmax_dev.
 constexpr uint64_t kTxlLanesMaxEntries = 1024;
 hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                               const uint64_t *rec_off, const uint64_t *alh_off,
                               const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
                               uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
-                              const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len);
+                              const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len,
+                              const uint64_t *wmax_dev = nullptr);
 // The device structure pass over tx-log records (txlog_struct.hip), one lane
 // per record, every check of the host hop (tx.go:419-588) on the device bytes:
 //  * clog != null (mh_txlog_validate_clog): record t at the offset of cLog
@@ -307,10 +310,13 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
 // record whose metadata is valid but not canonical or that is wider than the
 // lanes kernel takes (the host re-validates those).  stats (device, zeroed by
 // the caller): [0] widest accepted record, [1] records needing the host.
+// lim (cLog mode, <= len): the bytes landed so far -- a record whose read runs
+// past lim while lim < len needs the whole log and is left to the host
+// (kTxlNeedsHost).
 // Check mode: a record the device bytes give otherwise is MH_ERR_CORRUPTED_DATA.
 constexpr int32_t kTxlNeedsHost = 0x40000000;
 hipError_t launch_txlog_struct(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
-                               uint64_t len, const uint8_t *clog, uint32_t clog_es,
+                               uint64_t len, uint64_t lim, const uint8_t *clog, uint32_t clog_es,
                                uint64_t *rec_off, uint64_t *alh_off, uint64_t *leaf_off,
                                uint32_t max_entries, uint32_t max_key_len, int32_t *pre,
                                uint64_t *stats);

@@ -74,13 +74,22 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
     const int32_t *__restrict__ pre, MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ eh_out,
     uint8_t *__restrict__ alh_out, int32_t *__restrict__ status, TxlogHostOut ho, int lgp,
-    int dep, uint64_t blen_) {
+    int dep, uint64_t blen_, const unsigned long long *__restrict__ wmax_dev) {
     extern __shared__ uint4 lds[];
     constexpr int L = 1 << LGL, R = 64 >> LGL;
     uint32_t *stk = reinterpret_cast<uint32_t *>(lds);  // [dep][256][9]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r = lane >> LGL, i = lane & (L - 1);
-    const int EP = (1 << lgp) >> LGL;  // entries per lane (>= 1)
+    // entries per lane (>= 1): from the widest record, known on the host, or
+    // (wmax_dev) found by the structure pass on the device -- the launch's
+    // lane count and stack depth were then sized from an upper bound of it
+    int lgpk = lgp;
+    if (wmax_dev) {
+        const uint32_t wm = (uint32_t)*wmax_dev;
+        lgpk = 0;
+        while (lgpk < lgp && (1u << lgpk) < wm) lgpk++;  // (never past the launch's shape)
+    }
+    const int EP = max(1, (1 << lgpk) >> LGL);
     const uint64_t TW = ((uint64_t)blockIdx.x * 4 + wv) * R;  // the wave's first record
     const uint64_t T0 = (uint64_t)blockIdx.x * 4 * R;        // the workgroup's
     const uint64_t t = TW + r;
@@ -549,7 +558,8 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
                               const uint64_t *rec_off, const uint64_t *alh_off,
                               const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
                               uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
-                              const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len) {
+                              const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len,
+                              const uint64_t *wmax_dev) {
     if (!ntx) return hipSuccess;
     if (wmax > kTxlLanesMaxEntries || ((uintptr_t)ho.hdrs & 7) || ((uintptr_t)ho.alh & 3) ||
         ((uintptr_t)ho.status & 3))
@@ -576,7 +586,8 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
     }
 #define MH_TXL(l_)                                                                                 \
     hipLaunchKernelGGL((k_txlog_lanes<l_>), grid, blk, sh.lds, st, ntx, buf, rec_off, alh_off,   \
-                       leaf_off, pre, hdrs, eh_out, alh_out, status, ho, sh.lgp, sh.dep, log_len)
+                       leaf_off, pre, hdrs, eh_out, alh_out, status, ho, sh.lgp, sh.dep, log_len,   \
+                       reinterpret_cast<const unsigned long long *>(wmax_dev))
     if (sh.lgl == 0) MH_TXL(0);
     else if (sh.lgl == 1) MH_TXL(1);
     else if (sh.lgl == 2) MH_TXL(2);

@@ -148,7 +148,8 @@ __device__ int struct_record(const uint8_t *buf, uint64_t p, uint64_t lim, uint3
 }
 
 __global__ __launch_bounds__(256) void k_txlog_struct(
-    uint64_t ntx, const uint8_t *__restrict__ buf, uint64_t len, const uint8_t *__restrict__ clog,
+    uint64_t ntx, const uint8_t *__restrict__ buf, uint64_t len, uint64_t lim,
+    const uint8_t *__restrict__ clog,
     uint32_t es, uint64_t *__restrict__ rec_off, uint64_t *__restrict__ alh_off,
     uint64_t *__restrict__ leaf_off, uint32_t max_entries, uint32_t max_key_len,
     int32_t *__restrict__ pre, unsigned long long *__restrict__ stats) {
@@ -161,8 +162,10 @@ __global__ __launch_bounds__(256) void k_txlog_struct(
     if (clog) {
         const uint8_t *ce = clog + t * es;
         const uint64_t p = ld_be(ce, 8), size = ld_be(ce + 8, 4);
-        st = struct_record(buf, p, len, max_entries, max_key_len, nent, alh, eof, canon);
+        st = struct_record(buf, p, lim, max_entries, max_key_len, nent, alh, eof, canon);
         if (st == MH_OK && eof) st = MH_ERR_TRUNCATED;  // readTx: unexpected EOF (immustore.go:3054-3056)
+        // a read past the bytes landed (not past the log's end)
+        const bool cut_short = st == MH_ERR_TRUNCATED && lim < len && p < len && len - p >= 8;
         if (st == MH_OK && alh + 32 - p != size) st = MH_ERR_CORRUPTED_DATA;  // the cLog disagrees
         if (st == MH_OK && es == 44) {  // the cLog's Alh (immustore.go:519-527)
             uint32_t x = 0;
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void k_txlog_struct(
         }
         rec_off[t] = p;
         alh_off[t] = st == MH_OK ? alh : p;
-        if (st == MH_OK && (!canon || nent > kTxlLanesMaxEntries)) st = kTxlNeedsHost;
+        if (cut_short || (st == MH_OK && (!canon || nent > kTxlLanesMaxEntries))) st = kTxlNeedsHost;
     } else {
         const uint64_t p = rec_off[t], a = alh_off[t];
         st = struct_record(buf, p, a + 32, max_entries, max_key_len, nent, alh, eof, canon);
@@ -188,14 +191,14 @@ __global__ __launch_bounds__(256) void k_txlog_struct(
 }
 
 hipError_t launch_txlog_struct(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
-                               uint64_t len, const uint8_t *clog, uint32_t clog_es,
+                               uint64_t len, uint64_t lim, const uint8_t *clog, uint32_t clog_es,
                                uint64_t *rec_off, uint64_t *alh_off, uint64_t *leaf_off,
                                uint32_t max_entries, uint32_t max_key_len, int32_t *pre,
                                uint64_t *stats) {
     if (!ntx) return hipSuccess;
     TimerScope ts(tm, "txlog_struct", st);
     hipLaunchKernelGGL(k_txlog_struct, dim3(grid_for(ntx, 256)), dim3(256), 0, st, ntx, buf, len,
-                       clog, clog_es, rec_off, alh_off, leaf_off, max_entries, max_key_len, pre,
+                       std::min(lim, len), clog, clog_es, rec_off, alh_off, leaf_off, max_entries, max_key_len, pre,
                        reinterpret_cast<unsigned long long *>(stats));
     return hipGetLastError();
 }

@@ -382,19 +382,26 @@ def txlog_validate(buf, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
     return rc, k, used.value, (hd[:k] if hd is not None else None), alh[:k], sts[:k]
 
 
-def txlog_validate_clog(dev: int, length: int, clog, ntx: Optional[int] = None,
+def txlog_validate_clog(dev, length: Optional[int], clog, ntx: Optional[int] = None,
                         clog_entry_size: int = 12, max_entries: int = DEFAULT_MAX_TX_ENTRIES,
                         max_key_len: int = DEFAULT_MAX_KEY_LEN, ctx: Optional[Context] = None,
                         out=None, clog_dev: Optional[int] = None):
     """mh_txlog_validate_clog: readTx (immustore.go:3048-3060) of txs 1..ntx of
     a tx log already on the device (dev: its address, length bytes, the
-    allocation 256 bytes longer), located by the commit-log entries clog
+    allocation 256 bytes longer) or in host memory (dev: a bytes-like / numpy
+    buffer, pinned or not; length None or at most its size), located by the
+    commit-log entries clog
     (bytes, 12 or 44 per tx; or clog_dev: their device address with ntx)
     -> (status, nbad, first_bad, hdrs[ntx] TX_HEADER, alh[ntx,32], per_tx[ntx]).
 
     out: optional (hdrs, alh, per_tx) arrays (host numpy, pinned or not), or
     (hdrs_addr, alh_addr, per_tx_addr) device addresses (ints; any may be None)
     -- then the arrays returned are None."""
+    if not isinstance(dev, int):
+        hb = _u8(dev)
+        length = hb.size if length is None else length
+        assert length <= hb.size
+        dev = _addr(hb) if hb.size else None
     if clog_dev is None:
         cb = _u8(clog)
         n = len(cb) // clog_entry_size if ntx is None else ntx

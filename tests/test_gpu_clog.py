@@ -3,7 +3,8 @@ row 2), through the C ABI:
 
 * mh_txlog_validate_clog -- the log located by its commit log (readTx,
   immustore.go:3048-3060 -> txOffsetAndSize :2569-2597 -> Tx.readFrom
-  tx.go:388-630), no host copy: against the reference's Go-written stores with
+  tx.go:388-630), no host hop, the log resident in HBM or in host memory
+  (pageable or pinned; copied up in chunks, each checked as it lands): against the reference's Go-written stores with
   their Go-written commit logs (tests/golden: tx/00000000.tx +
   commit/00000000.txi), against mh_txlog_validate and against the oracle's
   restatement (oracle.txlog_validate_clog) on synthetic logs, corrupted
@@ -46,10 +47,23 @@ def _dev(raw, pad=256):
     return d
 
 
-def _clog(ctx, raw, d, clog, es=12, out=None, **kw):
+MODES = ("dev", "host", "pinned")
+
+
+def _pinned(raw):
+    import torch
+    t = torch.empty(max(len(raw), 1), dtype=torch.uint8).pin_memory()
+    a = t.numpy()
+    a[:len(raw)] = np.frombuffer(raw, np.uint8)
+    return a[:len(raw)]
+
+
+def _clog(ctx, raw, d, clog, es=12, out=None, mode="dev", **kw):
+    """mode: the log resident (d), pageable host bytes, or a pinned host copy."""
     from immustore_amd.txlayer import txlog_validate_clog
-    return txlog_validate_clog(d.data_ptr(), len(raw), clog, clog_entry_size=es, ctx=ctx, out=out,
-                               **kw)
+    src = d.data_ptr() if mode == "dev" else np.frombuffer(raw, np.uint8) if mode == "host" \
+        else _pinned(raw)
+    return txlog_validate_clog(src, len(raw), clog, clog_entry_size=es, ctx=ctx, out=out, **kw)
 
 
 def _same_as_oracle(orc, raw, clog, es, r, **kw):
@@ -73,8 +87,9 @@ def test_clog_fixture_stores(m, ctx, orc, fixtures):
         txi = bytes.fromhex(fx["txi"])
         want = m.txlog_validate(raw, ctx=ctx)
         d = _dev(raw)
-        for es, cl in ((12, txi), (44, clog_for(raw, record_spans(raw), 44))):
-            r = _clog(ctx, raw, d, cl, es)
+        for es, cl, mode in ((12, txi, "dev"), (44, clog_for(raw, record_spans(raw), 44), "dev"),
+                             (12, txi, "host"), (12, txi, "pinned")):
+            r = _clog(ctx, raw, d, cl, es, mode=mode)
             _same_as_oracle(orc, raw, cl, es, r)
             assert r[1] == 0 and r[2] == len(fx["txs"])
             for k, tx in enumerate(fx["txs"]):
@@ -119,11 +134,14 @@ def test_clog_synthetic_vs_validate_and_oracle(m, ctx, orc, max_entries):
                                  ds.cpu().numpy())
                 else:
                     r = _clog(ctx, buf, d, cl, es, out=out)
-                _same_as_oracle(orc, buf, cl, es, r)
-                if buf is raw:
-                    assert r[1] == 0
-                    assert np.array_equal(r[3], want[3]) and np.array_equal(r[4], want[4])
-                    assert list(r[5]) == list(want[5])
+                rs = [r] + [_clog(ctx, buf, d, cl, es, out=out, mode=md)
+                            for md in ("host", "pinned") if out is None or es == 12]
+                for r in rs:
+                    _same_as_oracle(orc, buf, cl, es, r)
+                    if buf is raw:
+                        assert r[1] == 0
+                        assert np.array_equal(r[3], want[3]) and np.array_equal(r[4], want[4])
+                        assert list(r[5]) == list(want[5])
 
 
 def test_clog_entry_mutations(m, ctx, orc):
@@ -142,8 +160,9 @@ def test_clog_entry_mutations(m, ctx, orc):
 
     def run(entries, es):
         cl = b"".join(bytes(x[:es]) for x in entries)
-        r = _clog(ctx, raw, d, cl, es)
-        return _same_as_oracle(orc, raw, cl, es, r)
+        for mode in MODES:
+            sts = _same_as_oracle(orc, raw, cl, es, _clog(ctx, raw, d, cl, es, mode=mode))
+        return sts
 
     e = [bytearray(x) for x in ent]
     e[3][8:12] = struct.pack(">I", spans[3][1] - spans[3][0] - 1)
@@ -176,7 +195,8 @@ def test_clog_metadata_and_wide_records(m, ctx, orc):
         d = _dev(raw)
         for es in (12, 44):
             cl = clog_for(raw, spans, es)
-            _same_as_oracle(orc, raw, cl, es, _clog(ctx, raw, d, cl, es))
+            for mode in MODES:
+                _same_as_oracle(orc, raw, cl, es, _clog(ctx, raw, d, cl, es, mode=mode))
     mixed = b"".join(r for _, r in metadata_logs(orc))
     wide = _synthetic_txlog(rng, 12, orc, max_entries=1500)
     for raw, kw in ((mixed, {}), (wide, {"max_entries": 1500}),
@@ -184,7 +204,8 @@ def test_clog_metadata_and_wide_records(m, ctx, orc):
         spans = record_spans(raw)
         d = _dev(raw)
         cl = clog_for(raw, spans, 12)
-        _same_as_oracle(orc, raw, cl, 12, _clog(ctx, raw, d, cl, 12, **kw), **kw)
+        for mode in MODES:
+            _same_as_oracle(orc, raw, cl, 12, _clog(ctx, raw, d, cl, 12, mode=mode, **kw), **kw)
     # the wide log with the default limit: MAX_ENTRIES per record, as the reader
     spans = record_spans(wide)
     cl = clog_for(wide, spans, 12)
@@ -209,12 +230,54 @@ def test_clog_bulk_log(m, ctx, orc):
     _same_as_oracle(orc, raw, cl, 12, r)
     want = m.txlog_validate(raw, ctx=ctx)
     assert np.array_equal(r[4], want[4]) and np.array_equal(r[3], want[3])
+    for mode in ("host", "pinned"):  # > 16 MiB: copied up in 3 (pageable: 2) chunks
+        r = _clog(ctx, raw, d, cl, 12, mode=mode)
+        _same_as_oracle(orc, raw, cl, 12, r)
+        assert np.array_equal(r[4], want[4]) and np.array_equal(r[3], want[3])
+
+
+def test_clog_host_log_chunk_edges(m, ctx, orc):
+    """A host log > 16 MiB copied up in chunks, its records grouped by the
+    chunk their cLog entry ends in: entries whose size reaches past the chunk
+    boundary (a read past the bytes landed: the host takes the record, as the
+    reader would see the whole log), past the log's end, entries out of log
+    order (one group after every chunk), a 44-byte entry's Alh flipped, and
+    non-canonical metadata records in the middle -- equal to the oracle and to
+    the resident log's results, pageable and pinned."""
+    import struct
+    rng = np.random.default_rng(19)
+    raw, _ = _bulk_txlog(rng, 8000)
+    raw += b"".join(r for n, r in metadata_logs(orc) if n == "noncanonical_sealed_canonical")
+    raw += _synthetic_txlog(rng, 200, orc, max_entries=40)
+    spans = record_spans(raw)
+    assert len(raw) > (16 << 20)
+    d = _dev(raw)
+    ent = [bytearray(struct.pack(">QI", s, e - s) + raw[e - 32:e]) for s, e in spans]
+    # a record near each 5:2:1 / 3:1 cut (4 KiB aligned)
+    cuts = [(int(len(raw) * f) & ~4095) for f in (5 / 8, 7 / 8, 3 / 4)]
+    e = [bytearray(x) for x in ent]
+    for c in cuts:
+        t = next(k for k, (s, en) in enumerate(spans) if en > c)
+        e[t - 1][8:12] = struct.pack(">I", spans[t - 1][1] - spans[t - 1][0] + 5000)  # past the cut
+        e[t + 2][8:12] = struct.pack(">I", spans[t + 2][1] - spans[t + 2][0] - 1)
+    e[len(e) - 3][8:12] = struct.pack(">I", 1 << 30)  # past the log's end
+    e[100][12] ^= 1
+    for es in (12, 44):
+        cl = b"".join(bytes(x[:es]) for x in e)
+        want = _same_as_oracle(orc, raw, cl, es, _clog(ctx, raw, d, cl, es))
+        assert want.any()
+        for mode in ("host", "pinned"):
+            _same_as_oracle(orc, raw, cl, es, _clog(ctx, raw, d, cl, es, mode=mode))
+    perm = np.concatenate([np.arange(1, 50), [0], np.arange(50, len(ent))])
+    cl = b"".join(bytes(ent[k][:12]) for k in perm)
+    for mode in MODES:
+        _same_as_oracle(orc, raw, cl, 12, _clog(ctx, raw, d, cl, 12, mode=mode))
 
 
 def test_clog_arguments(m, ctx, orc):
-    """A device allocation ending less than 256 bytes past the log, a host
-    pointer as the log, an entry size other than 12 / 44: illegal arguments;
-    no records: MH_OK with nothing bad."""
+    """A device allocation ending less than 256 bytes past the log, an entry
+    size other than 12 / 44: illegal arguments; a host pointer as the log: the
+    host-log mode; no records: MH_OK with nothing bad."""
     import ctypes as C
     from immustore_amd import _native as N
     rng = np.random.default_rng(2)
@@ -234,7 +297,8 @@ def test_clog_arguments(m, ctx, orc):
         L.mh_dev_free(ctx.handle, p.value)
     hb = np.frombuffer(raw, np.uint8)
     assert L.mh_txlog_validate_clog(ctx.handle, hb.ctypes.data, len(raw), cb.ctypes.data, 20, 12,
-                                    1024, 1024, None, None, None, C.byref(nb), C.byref(fb)) == ILLEGAL
+                                    1024, 1024, None, None, None, C.byref(nb), C.byref(fb)) == OK
+    assert nb.value == 0 and fb.value == 20
     d = _dev(raw)
     assert L.mh_txlog_validate_clog(ctx.handle, d.data_ptr(), len(raw), cb.ctypes.data, 20, 13,
                                     1024, 1024, None, None, None, C.byref(nb), C.byref(fb)) == ILLEGAL
