@@ -1754,7 +1754,6 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         const uint8_t *db = log_dev ? dlog : c->s_txlog.as<uint8_t>();
         MH_HIP(hipMemsetAsync(stats, 0, (4 + 2 * ng) * 8, st));
         MH_HIP(hipMemsetAsync(stats + 3, 0xff, 8, st));
-        if (!clog_dev) MH_HIP(hipMemcpyAsync(base + b_cl, clog, ntx * es, hipMemcpyHostToDevice, st));
         MH_HIP(c->p_small.ensure(64 + 16 * ng));
         volatile uint64_t *hs = c->p_small.as<volatile uint64_t>();
         // every exit waits for the streams (kernels may store into the caller's
@@ -1775,6 +1774,9 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
             cc.inline_issue = pinned;
             MH_HIP(cc.start());
         }
+        // (after the chunk copies are issued: they wait for this stream's
+        // earlier work, the previous call's readers of the staging buffer)
+        if (!clog_dev) MH_HIP(hipMemcpyAsync(base + b_cl, clog, ntx * es, hipMemcpyHostToDevice, st));
         TxlogHostOut ho0;
         ho0.status = k_st;
         ho0.alh = k_alh;

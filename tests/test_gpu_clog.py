@@ -134,9 +134,11 @@ def test_clog_synthetic_vs_validate_and_oracle(m, ctx, orc, max_entries):
                                  ds.cpu().numpy())
                 else:
                     r = _clog(ctx, buf, d, cl, es, out=out)
-                rs = [r] + [_clog(ctx, buf, d, cl, es, out=out, mode=md)
-                            for md in ("host", "pinned") if out is None or es == 12]
-                for r in rs:
+                for md in ("dev", "host", "pinned"):
+                    if md != "dev":
+                        if out == "dev" or (out is not None and es == 44):
+                            continue
+                        r = _clog(ctx, buf, d, cl, es, out=out, mode=md)
                     _same_as_oracle(orc, buf, cl, es, r)
                     if buf is raw:
                         assert r[1] == 0

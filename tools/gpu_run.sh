@@ -27,6 +27,7 @@
 #                    bench.py (C2), bench.py --config c4, bench_workloads.py c3 and c5
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
 #   txlog            tools/txlog_bench (a14 through the C ABI)
+#   txclog           tools/txlog_bench with TXB_CLOG=1 (mh_txlog_validate_clog, pinned log + cLog)
 #   txwl             bench_workloads.py --workload txlog (a14 + resident / cLog lines) -> txwl.out
 #   copyprobe        tools/copy_probe: chunked pinned H2D pipeline costs (host wall time)
 #   workloads        bench_workloads.py: every secondary workload line
@@ -137,6 +138,7 @@ for s in "$@"; do
       python3 tools/prof_summary.py "$O/prof/run_kernel_trace.csv" --steps 20 --warmup 5 > "$O/prof_summary.json" || exit 1
       gzip -f "$O/prof/run_kernel_trace.csv" ;;
     txlog) step txlog 300 ./tools/txlog_bench || exit 1 ;;
+    txclog) TXB_CLOG=1 step txclog 300 ./tools/txlog_bench ${TXB_ARGS:-200} || exit 1 ;;
     txwl) step txwl 400 python bench_workloads.py --workload txlog --steps ${TXWL_STEPS:-50} --warmup 3 || exit 1 ;;
     copyprobe) step copyprobe 200 ./tools/copy_probe || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;

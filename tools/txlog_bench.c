@@ -4,7 +4,8 @@
  * keys, no metadata, 75.5 MB), the log and the outputs in pinned arenas
  * (mh_host_alloc_pinned).  The stored Alh of every record is sealed from a
  * first validation; after 2 s of untimed calls (GPU clock pre-warm) K calls
- * are timed one by one.
+ * are timed one by one.  TXB_CLOG=1: mh_txlog_validate_clog over the same
+ * pinned log with its commit log (12-byte entries, pinned) -- no host hop.
  *
  * usage: txlog_bench [K=50] [records=65536] [entries=16]
  * prints one JSON line. */
@@ -50,6 +51,7 @@ static int cmp(const void *a, const void *b) {
 int main(int argc, char **argv) {
     /* TXB_NO_HDRS=1: no header output (validation only: Alh + statuses) */
     const int nohdr = getenv("TXB_NO_HDRS") && atoi(getenv("TXB_NO_HDRS"));
+    const int use_clog = getenv("TXB_CLOG") && atoi(getenv("TXB_CLOG"));
     const int K = argc > 1 ? atoi(argv[1]) : 50;
     const uint64_t ntx = argc > 2 ? strtoull(argv[2], 0, 10) : 65536;
     const uint64_t ne = argc > 3 ? strtoull(argv[3], 0, 10) : 16;
@@ -57,13 +59,18 @@ int main(int argc, char **argv) {
     const uint64_t len = ntx * rec;
     mh_ctx *c = NULL;
     CHECK(mh_ctx_create(0, NULL, &c));
-    uint8_t *log = NULL, *alh = NULL;
+    uint8_t *log = NULL, *alh = NULL, *clog = NULL;
     mh_tx_header *hd = NULL;
     int32_t *st = NULL;
     CHECK(mh_host_alloc_pinned(len, (void **)&log));
     CHECK(mh_host_alloc_pinned(ntx * 32, (void **)&alh));
     CHECK(mh_host_alloc_pinned(ntx * sizeof(mh_tx_header), (void **)&hd));
     CHECK(mh_host_alloc_pinned(ntx * 4, (void **)&st));
+    CHECK(mh_host_alloc_pinned(ntx * 12, (void **)&clog));
+    for (uint64_t t = 0; t < ntx; t++) { /* txOffsetAndSize (immustore.go:2569-2597) */
+        be(clog + t * 12, t * rec, 8);
+        be(clog + t * 12 + 8, rec, 4);
+    }
     uint64_t s = 14;
     for (uint64_t t = 0; t < ntx; t++) {
         uint8_t *r = log + t * rec;
@@ -88,31 +95,42 @@ int main(int argc, char **argv) {
     mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, NULL, alh, st);
     for (uint64_t t = 0; t < ntx; t++) memcpy(log + t * rec + rec - 32, alh + t * 32, 32);
     double *ms = malloc(sizeof(double) * (size_t)K);
+    uint64_t nbad = 0, first = 0;
+#define CALL()                                                                                    \
+    (use_clog ? mh_txlog_validate_clog(c, log, len, clog, ntx, 12, 1024, 1024, nohdr ? NULL : hd, \
+                                       alh, st, &nbad, &first)                                    \
+              : mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, nohdr ? NULL : hd, alh, st))
     /* clock pre-warm: calls for 2 s first (as bench_workloads.py --prewarm) */
-    for (const double tw = now(); now() - tw < 2.0;)
-        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, nohdr ? NULL : hd, alh, st));
+    for (const double tw = now(); now() - tw < 2.0;) CHECK(CALL());
     for (int k = 0; k < K; k++) {
         const double t0 = now();
-        CHECK(mh_txlog_validate(c, log, len, 1024, 1024, ntx, &n, &used, nohdr ? NULL : hd, alh, st));
+        CHECK(CALL());
         ms[k] = (now() - t0) * 1e3;
     }
     int bad = 0;
     for (uint64_t t = 0; t < ntx; t++) bad += st[t] != MH_OK;
+    if (use_clog) { /* the cLog call reports no count / consumed bytes */
+        bad += (int)nbad + (first != ntx);
+        n = ntx;
+        used = len;
+    }
     qsort(ms, (size_t)K, sizeof(double), cmp);
     double sum = 0;
     for (int k = 0; k < K; k++) sum += ms[k];
     printf("{\"metric\": \"tx-log read-path validation (a14) through the C ABI\", \"records\": %llu, "
            "\"entries_per_record\": %llu, \"log_bytes\": %llu, \"calls\": %d, \"ms_median\": %.4f, "
            "\"ms_min\": %.4f, \"ms_mean\": %.4f, \"M_tx_per_s_median\": %.3f, \"ntx\": %llu, "
-           "\"consumed\": %llu, \"invalid\": %d, \"pinned\": true, \"headers_out\": %s}\n",
+           "\"consumed\": %llu, \"invalid\": %d, \"pinned\": true, \"headers_out\": %s, \"api\": \"%s\"}\n",
            (unsigned long long)ntx, (unsigned long long)ne, (unsigned long long)len, K, ms[K / 2],
            ms[0], sum / K, ntx / (ms[K / 2] * 1e-3) / 1e6, (unsigned long long)n,
-           (unsigned long long)used, bad, nohdr ? "false" : "true");
+           (unsigned long long)used, bad, nohdr ? "false" : "true",
+           use_clog ? "mh_txlog_validate_clog" : "mh_txlog_validate");
     free(ms);
     mh_host_free_pinned(log);
     mh_host_free_pinned(alh);
     mh_host_free_pinned(hd);
     mh_host_free_pinned(st);
+    mh_host_free_pinned(clog);
     mh_ctx_destroy(c);
     return bad != 0 || n != ntx || used != len;
 }

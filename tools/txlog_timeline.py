@@ -37,10 +37,19 @@ pin.numpy()[:] = buf.reshape(-1)
 outs = (torch.empty(ntx * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().numpy().view(TX_HEADER),
         torch.empty(ntx * 32, dtype=torch.uint8).pin_memory().numpy().reshape(ntx, 32),
         torch.empty(ntx, dtype=torch.int32).pin_memory().numpy())
+o = (None,) + outs[1:] if os.environ.get("TXB_NO_HDRS") else outs
 ts = []
-for i in range(30):
+if os.environ.get("TXTL_CLOG"):  # mh_txlog_validate_clog over the pinned log + its cLog
+    from immustore_amd.txlayer import txlog_validate_clog
+    clog = b"".join(struct.pack(">QI", k * rec, rec) for k in range(ntx))
+    for i in range(30):
+        t = time.perf_counter()
+        r = txlog_validate_clog(pin.numpy(), pin.numel(), clog, ctx=ctx, out=o)
+        ts.append(time.perf_counter() - t)
+        assert r[0] == 0 and r[1] == 0 and not o[2].any()
+for i in range(0 if ts else 30):
     t = time.perf_counter()
-    r = m.txlog_validate(pin.numpy(), ctx=ctx, out=(None,) + outs[1:] if os.environ.get("TXB_NO_HDRS") else outs)
+    r = m.txlog_validate(pin.numpy(), ctx=ctx, out=o)
     ts.append(time.perf_counter() - t)
     assert r[0] == 0 and r[1] == ntx and not r[5].any()
 print("ms per call: last 10 median %.3f min %.3f" % (sorted(ts[-10:])[5] * 1e3, min(ts) * 1e3))
