@@ -537,14 +537,17 @@ static TxlShape txl_shape(uint64_t ntx, uint64_t wmax) {
     // MH_TXLOG_LANES=1|2|4|8|16 forces it (read per call, tests)
     int lgl = 0;
     while (lgl < 4 && (ntx << lgl) < 2048ull * 64) lgl++;  // two waves per SIMD (176 VGPRs: at most 2)
-    if (const char *e = getenv("MH_TXLOG_LANES")) {
+    // No LDS cap: from 33 entries a stack of >= 7 slots leaves room for one
+    // workgroup per CU (one wave per SIMD), but more lanes per
+    // record cost more: a lane past a record's last entry idles in its wave,
+    // so the wave-instruction count grows with L unless every record is
+    // exactly P wide.  131 072 records, kernel ms at L = 1 / 2 / 4: 40 entries
+    // 1.05 / 1.51 / 1.55, 56: 1.46 / 1.53 / 1.62, 64: 1.66 / 1.52 / 1.62
+    // (profiles/txlog_wide_r06.txt).
+    if (const char *e = getenv("MH_TXLOG_LANES")) {  // exactly this many (the LDS cap too)
         const int v = atoi(e);
         lgl = v >= 16 ? 4 : v >= 8 ? 3 : v >= 4 ? 2 : v >= 2 ? 1 : 0;
     }
-    // a stack deeper than 5 slots (> 46 KiB of LDS per workgroup) would leave
-    // room for one workgroup per CU, i.e. one wave per SIMD:
-    // more lanes per record instead
-    while (lgl < 4 && sh.lgp - lgl + 1 > 5) lgl++;
     sh.lgl = std::min(lgl, sh.lgp);  // never more lanes than entries
     const int R = 64 >> sh.lgl;
     sh.dep = std::max(1, sh.lgp - sh.lgl + 1);  // stack depth: log2(EP) + 1

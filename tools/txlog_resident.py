@@ -5,7 +5,7 @@ kernel's own time for the scrub / re-validate caller.  Prints one JSON line
 with the call time and the kernel time per call (HIP events); MH_TXLOG_KERNEL
 picks the kernel, MH_TXLOG_PROBE=1 adds the per-phase stamps on stderr.
 
-    python3 tools/txlog_resident.py [records] [calls]
+    python3 tools/txlog_resident.py [records] [calls] [entries per record]
 """
 import json
 import os
@@ -23,7 +23,8 @@ def main():
     ntx = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
     calls = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     ctx = m.Context(0)
-    buf = bw.txlog_records(ntx, 16, 16)
+    ne = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    buf = bw.txlog_records(ntx, ne, 16)
     rec = buf.shape[1]
     raw = buf.reshape(-1)
     _, n, _, _, alh, _ = m.txlog_validate(raw, ctx=ctx)
@@ -31,8 +32,6 @@ def main():
     d = torch.zeros(raw.size + 256, dtype=torch.uint8, device="cuda")
     d[:raw.size].copy_(torch.from_numpy(raw))
     torch.cuda.synchronize()
-    kern = os.environ.get("MH_TXLOG_KERNEL", "wave")
-    name = {"blk": "txlog_blk", "group": "txlog_group", "lanes": "txlog_lanes"}.get(kern, "txlog_wave")
     for _ in range(20):
         r = m.txlog_validate(raw, ctx=ctx, dev=d.data_ptr())
         assert r[0] == 0 and r[1] == ntx and not r[5].any()
@@ -43,17 +42,14 @@ def main():
         m.txlog_validate(raw, ctx=ctx, dev=d.data_ptr())
     t = (time.perf_counter() - t0) / calls
     ctx.set_timing(False)
-    if os.environ.get("MH_TXLOG_FUSED") == "0":  # the six-launch chain: every kernel of the call
-        kms = sum(ctx.timing(k)[0] for k in ("tx_hdr_from_raw", "txe_index", "txe_leaf",
-                                             "small_roots", "seg_level", "tx_alh"))
-        cnt = ctx.timing("txe_leaf")[1]
-        kern = "chain"
-    else:
-        kms, cnt = ctx.timing(name)
-    comps = ntx * (16 * 2 + 2 * 15 + 4)
-    print(json.dumps({"kernel": kern, "records": ntx, "ms_per_call": round(t * 1e3, 4),
+    # the kernel the call picked (lanes by default for one group of >= 16384
+    # records; MH_TXLOG_KERNEL=wave | lanes forces one)
+    kern, (kms, cnt) = max((("lanes", ctx.timing("txlog_lanes")), ("wave", ctx.timing("txlog_wave"))),
+                           key=lambda x: x[1][1])
+    comps = ntx * (ne * 2 + 2 * (ne - 1) + 4)
+    print(json.dumps({"kernel": kern, "records": ntx, "entries": ne, "ms_per_call": round(t * 1e3, 4),
                       "kernel_ms": round(kms / max(cnt, 1), 4),
-                      "sha_frac": round(comps / (kms / max(cnt, 1) * 1e-3) / 1e9 / 30.9, 4)}))
+                      "sha_frac": round(comps / (kms / cnt * 1e-3) / 1e9 / 30.9, 4) if kms else None}))
 
 
 if __name__ == "__main__":
