@@ -614,8 +614,11 @@ int mh_txlog_validate_resident(mh_ctx *ctx, const uint8_t *buf, const uint8_t *d
  * size, cLogEntrySizeV1; 44: + the tx's Alh, cLogEntrySizeV2,
  * immustore.go:122-123) -- the entries after the appendable header, in device
  * or host memory.  dlog: the tx-log data (after its appendable header), len
- * bytes, on the context's device, its allocation extending 256 bytes past it.
- * Record t is parsed where entry t points, on to the end of the log as Go's
+ * bytes, either on the context's device, its allocation extending 256 bytes
+ * past it, or in host memory (pinned -- the cgo shim's arena -- or pageable):
+ * then it is copied up in chunks (5 : 2 : 1 from 16 MiB, as
+ * mh_txlog_validate) and, when the cLog entries are in log order, the records
+ * ending in each chunk are checked as soon as it lands.  Record t is parsed where entry t points, on to the end of the log as Go's
  * reader does; status[t] (each output nullable; device, pinned or pageable
  * memory, capacity ntx):
  *   MH_ERR_TRUNCATED        the record runs past len / reads as an id-0 tail
@@ -630,8 +633,9 @@ int mh_txlog_validate_resident(mh_ctx *ctx, const uint8_t *buf, const uint8_t *d
  * for valid records, zeros for records with a structural error.  *nbad: the
  * number of non-OK records, *first_bad: the first (ntx when none).  Returns
  * MH_OK when the call ran.  Records with metadata not in Go's canonical form
- * or with more than 1024 entries are re-validated from a host copy of that
- * record alone (mh_txlog_validate). */
+ * or with more than 1024 entries (and, for a host log, records whose read runs
+ * past their chunk) are re-validated on the host bytes of that record alone
+ * (mh_txlog_validate). */
 int mh_txlog_validate_clog(mh_ctx *ctx, const uint8_t *dlog, uint64_t len, const uint8_t *clog,
                            uint64_t ntx, uint32_t clog_entry_size, uint32_t max_entries,
                            uint32_t max_key_len, mh_tx_header *hdrs, uint8_t *alh,
