@@ -32,9 +32,8 @@
 #   copyprobe        tools/copy_probe: chunked pinned H2D pipeline costs (host wall time)
 #   workloads        bench_workloads.py: every secondary workload line
 #   ab:<VARIANTS>    tools/ab_env.sh rotation, e.g. ab:base,MH_LPL=1
-#   txab:<VARIANTS>  tools/txlog_bench rotation (ROUNDS x), e.g. txab:base;MH_TXLOG_KERNEL=group
+#   txab:<VARIANTS>  tools/txlog_bench rotation (ROUNDS x), e.g. txab:base;MH_TXLOG_KERNEL=lanes
 #   txtl:<VARIANTS>  a14 kernel + copy timeline of the last call per variant -> txtl.txt
-#   txprobe:<VARS>   MH_TXLOG_PROBE=1 per-phase wave cycles of the a14 launches -> txprobe.txt
 #   workload:<name>  bench_workloads.py --workload <name>
 #   txres:<VARS>     a14 kernel over a resident log (tools/txlog_resident.py) per env variant
 #   fuzz             host-ASan tx-log fuzzer with the device path (FUZZ_ITERS, FUZZ_SEED)
@@ -142,7 +141,7 @@ for s in "$@"; do
     txwl) step txwl 400 python bench_workloads.py --workload txlog --steps ${TXWL_STEPS:-50} --warmup 3 || exit 1 ;;
     copyprobe) step copyprobe 200 ./tools/copy_probe || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;
-    txab:*)  # interleaved A/B of tools/txlog_bench over env variants, e.g. txab:base;MH_TXLOG_KERNEL=group
+    txab:*)  # interleaved A/B of tools/txlog_bench over env variants, e.g. txab:base;MH_TXLOG_KERNEL=lanes
       vs="$(echo "${s#txab:}" | tr ';' ' ')"
       for i in $(seq ${ROUNDS:-3}); do
         for v in $vs; do
@@ -169,13 +168,6 @@ for s in "$@"; do
       rc=$?; rm -rf "$O/corpus"; [ $rc -eq 0 ] || exit 1 ;;
     queue) step queue 300 ./tools/queue_bench 30 2000 16 1024 ${QWAIT:-20} ${QMAXTXS:-64} || exit 1 ;;
     traffic) step traffic 1200 bash tools/gpu_pmc.sh || exit 1 ;;
-    txprobe:*)  # MH_TXLOG_PROBE=1 per-phase wave timings of the a14 launches (last call), per variant
-      vs="$(echo "${s#txprobe:}" | tr ';' ' ')"
-      for v in $vs; do
-        envs=""; [ "$v" != base ] && envs=$(echo "$v" | tr ',' ' ')
-        env MH_TXLOG_PROBE=1 $envs timeout -k 10 200 python3 tools/txlog_timeline.py > "$O/txprobe.out" 2> "$O/txprobe.err" || { tail -5 "$O/txprobe.err"; exit 1; }
-        { echo "# variant $v"; grep txlog_probe "$O/txprobe.err" | tail -4; tail -1 "$O/txprobe.out"; } | tee -a "$O/txprobe.txt"
-      done ;;
     txres:*)  # a14 kernel over a resident log per env variant (tools/txlog_resident.py) -> txres.txt
       vs="$(echo "${s#txres:}" | tr ';' ' ')"
       for v in $vs; do

@@ -3,7 +3,7 @@
 i.e. ONE launch of the a14 kernel over every record after the host hop -- the
 kernel's own time for the scrub / re-validate caller.  Prints one JSON line
 with the call time and the kernel time per call (HIP events); MH_TXLOG_KERNEL
-picks the kernel, MH_TXLOG_PROBE=1 adds the per-phase stamps on stderr.
+picks the kernel (MH_TXLOG_LANES the lanes per record).
 
     python3 tools/txlog_resident.py [records] [calls] [entries per record]
 """
