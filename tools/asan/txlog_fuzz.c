@@ -15,7 +15,12 @@
  * entry digests, trees and Alh rebuilt there, the canonical-metadata side
  * area -- and its status, record count, consumed bytes, Alh values and
  * per-tx statuses must equal the oracle's.  The host code around it still
- * runs under ASan (the device code is built as usual).
+ * runs under ASan (the device code is built as usual).  Each mutant then goes
+ * through mh_txlog_validate_clog too, indexed by the CLEAN log's commit log
+ * (12- or 44-byte entries, some of them mutated: sizes, offsets), with the
+ * mutant in device memory and in host memory (its exact-size malloc: ASan
+ * sees any host over-read of the fallback), against orc_clog below -- the
+ * oracle's readTx restatement (oracle.py txlog_validate_clog) in C.
  *
  * usage: txlog_fuzz <iterations per file> <seed> <log file>...
  * prints one line per file; exit 1 on any mismatch. */
@@ -97,6 +102,117 @@ static uint8_t *mutate(const uint8_t *src, uint64_t len, uint64_t *out_len) {
 
 static mh_ctx *CTX;  /* MH_FUZZ_DEVICE=1: mh_txlog_validate as well */
 
+static uint64_t be_n(const uint8_t *p, int n) {
+    uint64_t v = 0;
+    for (int k = 0; k < n; k++) v = v << 8 | p[k];
+    return v;
+}
+
+/* ImmuStore.readTx (immustore.go:3048-3060) of entry t of the cLog: the record
+ * read at its offset on to the end of the log, plus the open path's cLog
+ * checks (:458-528) -- oracle.py txlog_validate_clog */
+static void orc_clog(const uint8_t *b, uint64_t n, const uint8_t *cl, uint64_t ntx, int es,
+                     uint32_t me, uint32_t mk, uint8_t *alh, int32_t *sts) {
+    for (uint64_t t = 0; t < ntx; t++) {
+        const uint64_t off = be_n(cl + t * es, 8), size = be_n(cl + t * es + 8, 4);
+        memset(alh + 32 * t, 0, 32);
+        if (off > n || n - off < 8) {
+            sts[t] = MH_ERR_TRUNCATED;
+            continue;
+        }
+        uint64_t k = 0, used = 0;
+        uint8_t a[32];
+        int32_t s1 = 0;
+        int st = orc_txlog_validate(b + off, n - off, me, mk, 1, &k, &used, a, &s1);
+        if (st == MH_OK && k == 0) st = MH_ERR_TRUNCATED;
+        if (st == MH_OK && used != size) st = MH_ERR_CORRUPTED_DATA;
+        if (st == MH_OK && es == 44 && memcmp(cl + t * es + 12, b + off + size - 32, 32)) st = MH_ERR_CORRUPTED_DATA;
+        if (st == MH_OK) {
+            sts[t] = s1;
+            memcpy(alh + 32 * t, a, 32);
+        } else {
+            sts[t] = st;
+        }
+    }
+}
+
+/* the clean log's commit log (offset, size, Alh per record), from the scan */
+static uint8_t *CL;
+static uint64_t CL_N;
+static void clean_clog(const uint8_t *src, uint64_t len) {
+    free(CL);
+    CL = NULL;
+    CL_N = 0;
+    const uint64_t cap = len / 90 + 1;
+    uint64_t *ao = malloc(8 * cap), nt = 0, c = 0;
+    mh_txlog_scan(src, len, 1024, 1024, cap, &nt, &c, NULL, ao);
+    CL = malloc(44 * (nt ? nt : 1));
+    for (uint64_t t = 0; t < nt; t++) {
+        const uint64_t s0 = t ? ao[t - 1] + 32 : 0, e = ao[t] + 32;
+        for (int k = 0; k < 8; k++) CL[44 * t + k] = (uint8_t)(s0 >> (56 - 8 * k));
+        for (int k = 0; k < 4; k++) CL[44 * t + 8 + k] = (uint8_t)((e - s0) >> (24 - 8 * k));
+        memcpy(CL + 44 * t + 12, src + e - 32, 32);
+    }
+    CL_N = nt;
+    free(ao);
+}
+
+/* mh_txlog_validate_clog of mutant b (n bytes) vs orc_clog: the clean cLog,
+ * sometimes with mutated entries; the mutant resident and in host memory */
+static int check_clog(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, long *bad) {
+    if (!CL_N) return 1;
+    const uint64_t nt = CL_N;
+    const int es = (rnd() & 1) ? 12 : 44;
+    uint8_t *cl = malloc(es * nt);
+    for (uint64_t t = 0; t < nt; t++) memcpy(cl + es * t, CL + 44 * t, es);
+    if (rnd() & 1) { /* a few entries that disagree with the log */
+        for (int m = 0; m < 3; m++) {
+            uint8_t *e = cl + es * (rnd() % nt);
+            switch (rnd() % 4) {
+            case 0: e[11] ^= (uint8_t)(1 + rnd() % 255); break;        /* size */
+            case 1: e[7] ^= (uint8_t)(1 + rnd() % 255); break;         /* offset, low byte */
+            case 2: e[8] = 0xff; break;                                 /* size past the log */
+            case 3: memcpy(e, cl + es * (rnd() % nt), es); break;       /* another tx's entry */
+            }
+        }
+    }
+    uint8_t *a1 = malloc(32 * nt), *a2 = malloc(32 * nt);
+    int32_t *s1 = malloc(4 * nt), *s2 = malloc(4 * nt);
+    orc_clog(b, n, cl, nt, es, me, mk, a2, s2);
+    uint64_t nb2 = 0, f2 = nt;
+    for (uint64_t t = 0; t < nt; t++)
+        if (s2[t] != MH_OK) {
+            if (!nb2) f2 = t;
+            nb2++;
+        }
+    int ok = 1;
+    for (int mode = 0; mode < 2; mode++) {
+        const uint8_t *src = b;
+        void *d = NULL;
+        if (mode == 0) { /* resident: an allocation 256 bytes longer */
+            if (mh_dev_alloc(CTX, n + 256, &d) != MH_OK) return 0;
+            if (n) mh_memcpy_h2d(CTX, d, b, n);
+            mh_ctx_synchronize(CTX);
+            src = d;
+        }
+        uint64_t nb1 = 0, f1 = 0;
+        memset(s1, 0x55, 4 * nt);
+        const int r = mh_txlog_validate_clog(CTX, n ? src : (mode ? b : src), n, cl, nt, es, me, mk,
+                                             NULL, a1, s1, &nb1, &f1);
+        const int same = r == MH_OK && nb1 == nb2 && f1 == f2 && !memcmp(s1, s2, 4 * nt) &&
+                         !memcmp(a1, a2, 32 * nt);
+        if (!same && (*bad)++ < 5)
+            fprintf(stderr, "clog mismatch (%s, es %d) len %llu: rc %d nbad %llu/%llu first %llu/%llu\n",
+                    mode ? "host" : "resident", es, (unsigned long long)n, r,
+                    (unsigned long long)nb1, (unsigned long long)nb2, (unsigned long long)f1,
+                    (unsigned long long)f2);
+        ok &= same;
+        if (d) mh_dev_free(CTX, d);
+    }
+    free(cl); free(a1); free(a2); free(s1); free(s2);
+    return ok;
+}
+
 static int check_device(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_t cap,
                         int r2, uint64_t n2, uint64_t c2, const uint8_t *alh2,
                         const int32_t *sts2, long *bad) {
@@ -131,6 +247,7 @@ static int check(const uint8_t *b, uint64_t n, uint32_t me, uint32_t mk, uint64_
                 (unsigned long long)n, r1, (unsigned long long)n1, (unsigned long long)c1, r2,
                 (unsigned long long)n2, (unsigned long long)c2);
     if (CTX) ok &= check_device(b, n, me, mk, cap, r2, n2, c2, alh, sts, bad);
+    if (CTX && n) ok &= check_clog(b, n, me, mk, bad);
     free(h); free(ao); free(alh); free(sts);
     return ok;
 }
@@ -153,6 +270,7 @@ int main(int argc, char **argv) {
             return 2;
         }
         long agree = 0, accepted = 0;
+        if (CTX) clean_clog(src, len);
         check(src, len, 1024, 1024, 1ull << 40, &bad);
         /* large logs: fewer mutants (each parse is ~ms) */
         const long it = len > (4u << 20) ? iters / 50 + 1 : iters;
@@ -167,7 +285,7 @@ int main(int argc, char **argv) {
             free(m);
         }
         printf("%s: %ld mutants, %ld agree, %ld parsed >= 1 record%s\n", argv[a], it, agree,
-               accepted, CTX ? " (device validate too)" : "");
+               accepted, CTX ? " (device validate and the cLog call too)" : "");
         fflush(stdout);
         free(src);
     }
