@@ -189,6 +189,7 @@ struct mh_ctx {
     DevBuf s_txlog;       // raw tx-log bytes of mh_txlog_validate
     DevBuf s_txpatch;     // the same + canonical metadata records (rare)
     DevBuf s_clog;        // mh_txlog_validate_clog's per-record arrays
+    uint64_t clog_wmax = 0;  // the widest record of its last resident call (the next launch's guess)
     PinBuf p_tx;          // its pinned staging of the parsed index arrays
     // mh_txlog_validate's groups (one per copy chunk): device arrays and
     // pinned index staging of each, kept across calls

@@ -1785,6 +1785,10 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         ho0.status = k_st;
         ho0.alh = k_alh;
         ho0.hdrs = k_hd;
+        // stats[0]: a lane launch whose shape was too narrow for its records
+        // (the resident form launches on the previous call's widest record
+        // without waiting for this one's: a wider log goes again below)
+        uint64_t *redo = stats;
         // group g's arrays start at its first record
         auto run_group = [&](size_t g, uint64_t wmax, const uint64_t *wmax_dev) -> int {
             const uint64_t t0 = tg[g], n = tg[g + 1] - t0;
@@ -1796,7 +1800,7 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
             MH_HIP(launch_txlog_lanes(st, c->tm(), n, db, ro + t0, ao + t0, nullptr, pre + t0,
                                       hd ? hd + t0 : nullptr, base + b_eh + t0 * 32,
                                       base + b_a + t0 * 32, sts + t0, ho, std::max<uint64_t>(wmax, 1),
-                                      len, wmax_dev));
+                                      len, wmax_dev, wmax_dev ? redo : nullptr));
             return MH_OK;
         };
         uint64_t nhost = 0;
@@ -1804,11 +1808,16 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
             // 1. every record's structure where its cLog entry points
             MH_HIP(launch_txlog_struct(st, c->tm(), ntx, db, len, len, dcl, es, ro, ao, nullptr,
                                        max_entries, max_key_len, pre, gstats));
-            MH_HIP(hipMemcpyAsync((void *)hs, gstats, 2 * 8, hipMemcpyDeviceToHost, st));
-            MH_HIP(hipStreamSynchronize(st));  // the widest record sizes the lane kernel's launch
-            nhost = hs[1];
-            // 2. the accepted records hashed and checked
-            if (int e = run_group(0, hs[0], nullptr)) return e;
+            // 2. the accepted records hashed and checked, the launch shaped by
+            // the previous call's widest record (no wait: 0.264 -> ~0.245 ms
+            // on 65 536 records), by this one's on a first call
+            if (c->clog_wmax) {
+                if (int e = run_group(0, c->clog_wmax, gstats)) return e;
+            } else {
+                MH_HIP(hipMemcpyAsync((void *)hs, gstats, 2 * 8, hipMemcpyDeviceToHost, st));
+                MH_HIP(hipStreamSynchronize(st));
+                if (int e = run_group(0, hs[0], nullptr)) return e;
+            }
         } else {
             for (size_t g = 0; g < ng; g++) {
                 const uint64_t t0 = tg[g], n = tg[g + 1] - t0;
@@ -1831,9 +1840,8 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         // 3. how many records failed, and the first (and, for a host log, how
         // many records the host must re-validate); results down
         MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
-        MH_HIP(hipMemcpyAsync((void *)(hs + 2), stats + 2, 2 * 8, hipMemcpyDeviceToHost, st));
-        if (!log_dev)
-            MH_HIP(hipMemcpyAsync((void *)(hs + 8), gstats, 2 * ng * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync((void *)hs, stats, 4 * 8, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync((void *)(hs + 8), gstats, 2 * ng * 8, hipMemcpyDeviceToHost, st));
         auto results_down = [&]() -> int {
             if (status_out && !k_st) MH_HIP(hipMemcpyAsync(status_out, sts, ntx * 4, hipMemcpyDeviceToHost, st));
             if (alh_out && !k_alh) MH_HIP(hipMemcpyAsync(alh_out, base + b_a, ntx * 32, hipMemcpyDeviceToHost, st));
@@ -1843,10 +1851,20 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         };
         if (int e = results_down()) return e;
         MH_HIP(hipStreamSynchronize(st));
-        if (!log_dev) {
+        if (!log_dev)
             if (hipError_t e = cc.sync()) return -(int)e;  // the caller's log is no longer read
-            for (size_t g = 0; g < ng; g++) nhost += hs[8 + 2 * g + 1];
+        if (hs[0]) {  // a launch too narrow for its records: again, shaped by them
+            MH_HIP(hipMemsetAsync(stats, 0, 4 * 8, st));
+            MH_HIP(hipMemsetAsync(stats + 3, 0xff, 8, st));
+            for (size_t g = 0; g < ng; g++)
+                if (int e = run_group(g, hs[8 + 2 * g], nullptr)) return e;
+            MH_HIP(launch_txlog_status_summary(st, ntx, sts, stats));
+            MH_HIP(hipMemcpyAsync((void *)hs, stats, 4 * 8, hipMemcpyDeviceToHost, st));
+            if (int e = results_down()) return e;
+            MH_HIP(hipStreamSynchronize(st));
         }
+        for (size_t g = 0; g < ng; g++) nhost += hs[8 + 2 * g + 1];
+        if (log_dev) c->clog_wmax = std::max<uint64_t>((uint64_t)hs[8], 1);
         // 4. records for the host hop (rare: a log not written by immudb, or a
         // record that disagrees with its cLog entry)
         if (nhost) {

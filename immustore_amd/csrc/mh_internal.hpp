@@ -288,15 +288,17 @@ hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint
 // every record on 1-16 lanes, each lane's subtree serial (k_txlog_lanes,
 // txlog_lanes.hip), wmax <= kTxlLanesMaxEntries; log_len: the log's length
 // (the checking build's range).  wmax_dev (nullable): the widest record as the
-// structure pass found it on the device; wmax is then an upper bound of it
-// (the launch shape), the kernel takes the entries per lane from wmax_dev.
+// structure pass found it on the device; wmax is then the launch shape (an
+// upper bound of it, or a guess), the kernel takes the entries per lane from
+// wmax_dev -- and if that is wider than the shape, does nothing but set
+// *redo (device, required with wmax_dev) for the caller to launch again.
 constexpr uint64_t kTxlLanesMaxEntries = 1024;
 hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uint8_t *buf,
                               const uint64_t *rec_off, const uint64_t *alh_off,
                               const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
                               uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
                               const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len,
-                              const uint64_t *wmax_dev = nullptr);
+                              const uint64_t *wmax_dev = nullptr, uint64_t *redo = nullptr);
 // The device structure pass over tx-log records (txlog_struct.hip), one lane
 // per record, every check of the host hop (tx.go:419-588) on the device bytes:
 //  * clog != null (mh_txlog_validate_clog): record t at the offset of cLog

@@ -74,7 +74,8 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     const uint64_t *__restrict__ alh_off, const uint64_t *__restrict__ leaf_off,
     const int32_t *__restrict__ pre, MhTxHeader *__restrict__ hdrs, uint8_t *__restrict__ eh_out,
     uint8_t *__restrict__ alh_out, int32_t *__restrict__ status, TxlogHostOut ho, int lgp,
-    int dep, uint64_t blen_, const unsigned long long *__restrict__ wmax_dev) {
+    int dep, uint64_t blen_, const unsigned long long *__restrict__ wmax_dev,
+    unsigned long long *__restrict__ redo) {
     extern __shared__ uint4 lds[];
     constexpr int L = 1 << LGL, R = 64 >> LGL;
     uint32_t *stk = reinterpret_cast<uint32_t *>(lds);  // [dep][256][9]
@@ -82,12 +83,18 @@ __global__ __launch_bounds__(256) void k_txlog_lanes(
     const int r = lane >> LGL, i = lane & (L - 1);
     // entries per lane (>= 1): from the widest record, known on the host, or
     // (wmax_dev) found by the structure pass on the device -- the launch's
-    // lane count and stack depth were then sized from an upper bound of it
+    // lane count and stack depth were then sized for records up to 2^lgp
+    // wide (an upper bound, or the caller's guess): wider ones and the launch
+    // does nothing but raise *redo (uniform: every wave returns at once)
     int lgpk = lgp;
     if (wmax_dev) {
         const uint32_t wm = (uint32_t)*wmax_dev;
         lgpk = 0;
-        while (lgpk < lgp && (1u << lgpk) < wm) lgpk++;  // (never past the launch's shape)
+        while ((1u << lgpk) < wm) lgpk++;
+        if (lgpk > lgp) {
+            if (threadIdx.x == 0) atomicOr(redo, 1ull);
+            return;
+        }
     }
     const int EP = max(1, (1 << lgpk) >> LGL);
     const uint64_t TW = ((uint64_t)blockIdx.x * 4 + wv) * R;  // the wave's first record
@@ -562,8 +569,9 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
                               const uint64_t *leaf_off, const int32_t *pre, MhTxHeader *hdrs,
                               uint8_t *eh_out, uint8_t *alh_out, int32_t *status,
                               const TxlogHostOut &ho, uint64_t wmax, uint64_t log_len,
-                              const uint64_t *wmax_dev) {
+                              const uint64_t *wmax_dev, uint64_t *redo) {
     if (!ntx) return hipSuccess;
+    if (wmax_dev && !redo) return hipErrorInvalidValue;
     if (wmax > kTxlLanesMaxEntries || ((uintptr_t)ho.hdrs & 7) || ((uintptr_t)ho.alh & 3) ||
         ((uintptr_t)ho.status & 3))
         return hipErrorInvalidValue;
@@ -590,7 +598,8 @@ hipError_t launch_txlog_lanes(hipStream_t st, Timer *tm, uint64_t ntx, const uin
 #define MH_TXL(l_)                                                                                 \
     hipLaunchKernelGGL((k_txlog_lanes<l_>), grid, blk, sh.lds, st, ntx, buf, rec_off, alh_off,   \
                        leaf_off, pre, hdrs, eh_out, alh_out, status, ho, sh.lgp, sh.dep, log_len,   \
-                       reinterpret_cast<const unsigned long long *>(wmax_dev))
+                       reinterpret_cast<const unsigned long long *>(wmax_dev),                  \
+                       reinterpret_cast<unsigned long long *>(redo))
     if (sh.lgl == 0) MH_TXL(0);
     else if (sh.lgl == 1) MH_TXL(1);
     else if (sh.lgl == 2) MH_TXL(2);

@@ -276,6 +276,27 @@ def test_clog_host_log_chunk_edges(m, ctx, orc):
         _same_as_oracle(orc, raw, cl, 12, _clog(ctx, raw, d, cl, 12, mode=mode))
 
 
+def test_clog_resident_launch_guess(m, ctx, orc):
+    """The resident form shapes its lane launch by the previous call's widest
+    record (no wait for this call's structure pass): a log wider than the
+    guess is launched again at its own shape (the kernel raises a redo flag
+    and writes nothing), a narrower one runs at the wider shape -- every call
+    equal to the oracle, with host and device outputs."""
+    import torch
+    rng = np.random.default_rng(61)
+    logs = [_synthetic_txlog(rng, 200, orc, max_entries=w) for w in (2, 40, 3, 300, 1, 64)]
+    for raw in logs:
+        spans = record_spans(raw)
+        d = _dev(raw)
+        cl = clog_for(raw, spans, 12)
+        _same_as_oracle(orc, raw, cl, 12, _clog(ctx, raw, d, cl, 12))
+        n = len(spans)
+        da = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        ds = torch.zeros(n, dtype=torch.int32, device="cuda")
+        r = _clog(ctx, raw, d, cl, 12, out=(None, da.data_ptr(), ds.data_ptr()))
+        _same_as_oracle(orc, raw, cl, 12, r[:3] + (None, da.view(n, 32).cpu().numpy(), ds.cpu().numpy()))
+
+
 def test_clog_arguments(m, ctx, orc):
     """A device allocation ending less than 256 bytes past the log, an entry
     size other than 12 / 44: illegal arguments; a host pointer as the log: the
