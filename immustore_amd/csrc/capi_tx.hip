@@ -1742,8 +1742,11 @@ extern "C" int mh_txlog_validate_clog(mh_ctx *c, const uint8_t *dlog, uint64_t l
         std::vector<uint8_t> hcl_copy;
         const uint8_t *hcl = clog_dev ? nullptr : clog;
         if (clog_dev && !log_dev) {
+            // (on this stream, not hipMemcpy's: that one would wait for the
+            // copy streams, i.e. for the whole log to land)
             hcl_copy.resize(ntx * es);
-            MH_HIP(hipMemcpy(hcl_copy.data(), clog, ntx * es, hipMemcpyDeviceToHost));
+            MH_HIP(hipMemcpyAsync(hcl_copy.data(), clog, ntx * es, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipStreamSynchronize(st));
             hcl = hcl_copy.data();
         }
         // group g: records [tg[g], tg[g+1]), read within the first lim[g] bytes
