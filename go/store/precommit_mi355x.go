@@ -263,3 +263,63 @@ func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha25
 	}
 	return alhs[:ntx], errs, uint64(used), mapErr(st)
 }
+
+// ValidateTxLogFromCommitLog is ImmuStore.readTx (immustore.go:3048-3060) for
+// txs 1..n located by the store's commit log, as txOffsetAndSize reads it
+// (:2569-2597): cLog holds n entries of cLogEntrySize bytes (12: BE64 offset
+// || BE32 size; 44: + the tx's Alh, :122-123), txLog the tx log's data.  No
+// host record hop: the device checks every record's structure where its
+// entry points (plus the open path's cLog checks, :458-528), then re-hashes
+// it (tx.go:388-630).  txLog may be a pinned arena or any slice (copied up in
+// chunks, each checked as it lands: from a plain slice this is 1.7x faster
+// than ValidateTxLog, DESIGN.md).  Returns the Alh of every tx (zero where
+// the record is bad), a per-tx error (ErrCorruptedData for an ALH mismatch or
+// a cLog entry that disagrees with its record, ErrCorruptedTxData for a read
+// past the log, readHeader / readEntry's errors otherwise) and the index of
+// the first bad tx (n when none).
+func ValidateTxLogFromCommitLog(txLog, cLog []byte, cLogEntrySize, maxEntries, maxKeyLen int) (
+	alhs [][sha256.Size]byte, errs []error, firstBad int, err error) {
+	if cLogEntrySize != 12 && cLogEntrySize != 44 {
+		return nil, nil, 0, ErrIllegalArguments
+	}
+	n := len(cLog) / cLogEntrySize
+	if n == 0 {
+		return nil, nil, 0, nil
+	}
+	if len(txLog) == 0 {
+		return nil, nil, 0, ErrIllegalArguments
+	}
+	m, e := mi355x.AcquireClique()
+	if e != nil {
+		return nil, nil, 0, e
+	}
+	alhs = make([][sha256.Size]byte, n)
+	status := make([]int32, n)
+	var nbad, first C.uint64_t
+	// one device: the call copies and checks the whole log on it (device 0 of
+	// the clique)
+	st := C.mh_txlog_validate_clog(C.mh_multi_ctx((*C.mh_multi)(m), 0),
+		(*C.uint8_t)(unsafe.Pointer(&txLog[0])), C.uint64_t(len(txLog)),
+		(*C.uint8_t)(unsafe.Pointer(&cLog[0])), C.uint64_t(n), C.uint32_t(cLogEntrySize),
+		C.uint32_t(maxEntries), C.uint32_t(maxKeyLen), nil,
+		(*C.uint8_t)(unsafe.Pointer(&alhs[0][0])), (*C.int32_t)(unsafe.Pointer(&status[0])),
+		&nbad, &first)
+	mi355x.ReleaseClique(m, int(st))
+	if st != C.MH_OK {
+		return nil, nil, 0, mapErr(st)
+	}
+	errs = make([]error, n)
+	for k := range errs {
+		switch status[k] {
+		case 0:
+		case C.MH_ERR_CORRUPTED_DATA:
+			errs[k] = fmt.Errorf("%w: ALH mismatch or commit-log entry disagrees", ErrCorruptedData)
+		case C.MH_ERR_TRUNCATED:
+			// readTx's io.EOF (immustore.go:3054-3056)
+			errs[k] = fmt.Errorf("%w: unexpected EOF while reading tx %d", ErrCorruptedTxData, k+1)
+		default:
+			errs[k] = mapErr(C.int(status[k]))
+		}
+	}
+	return alhs, errs, int(first), nil
+}

@@ -188,6 +188,8 @@ def test_batch_paths_check_cliques_out_of_the_pool():
                             "C.mh_multi_verify_values_batch"),
                            ("store/precommit_mi355x.go", "ValidateTxLog",
                             "C.mh_multi_txlog_validate"),
+                           ("store/precommit_mi355x.go", "ValidateTxLogFromCommitLog",
+                            "C.mh_txlog_validate_clog"),
                            ("ahtree/ahtree_mi355x.go", "appendRun",
                             "C.mh_multi_ahtree_append_batch")):
         b = _func_body(path, fn)
