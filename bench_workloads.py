@@ -1062,6 +1062,12 @@ def run_single(a):
             assert r[0] == 0 and r[1] == ntx
 
         t_pageable = timed(step_pageable, a.steps, a.warmup, sync)
+
+        def step_pageable_po():  # the pageable log, results into the pinned arena
+            r = m.txlog_validate(raw_pageable, ctx=ctx, out=outs)
+            assert r[0] == 0 and r[1] == ntx
+
+        t_pageable_po = timed(step_pageable_po, a.steps, a.warmup, sync)
         prewarm(step, sync, a.prewarm)
         # (the call's ~25 launches would carry ~0.15 ms of timing events)
         t = timed_k(ctx, step, a.steps, a.warmup, sync)
@@ -1191,7 +1197,9 @@ def run_single(a):
                "ms_per_step": round(t * 1e3, 3), "log_bytes": int(raw.size),
                "log_GBps_incl_parse_and_h2d": round(raw.size / t / 1e9, 2),
                "pageable_input": {"ms_per_step": round(t_pageable * 1e3, 3),
-                                  "M_tx_per_s": round(ntx / t_pageable / 1e6, 3)},
+                                  "M_tx_per_s": round(ntx / t_pageable / 1e6, 3),
+                                  "outputs": "fresh pageable arrays per call",
+                                  "pinned_outputs_ms_per_step": round(t_pageable_po * 1e3, 3)},
                "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
                "host_hop_only_ms": round(t_hop * 1e3, 3), "h2d_only_ms": round(t_h2d * 1e3, 3),
                "gcomp_per_s_kernels": round(comps / max(sum(kt.values()) * 1e-3, 1e-12) / 1e9, 2),

@@ -271,8 +271,8 @@ func ValidateTxLog(buf []byte, maxEntries, maxKeyLen, maxTxs int) (alhs [][sha25
 // host record hop: the device checks every record's structure where its
 // entry points (plus the open path's cLog checks, :458-528), then re-hashes
 // it (tx.go:388-630).  txLog may be a pinned arena or any slice (copied up in
-// chunks, each checked as it lands: from a plain slice this is 1.7x faster
-// than ValidateTxLog, DESIGN.md).  Returns the Alh of every tx (zero where
+// chunks, each checked as it lands; as fast as ValidateTxLog from either,
+// with no host record parse, DESIGN.md).  Returns the Alh of every tx (zero where
 // the record is bad), a per-tx error (ErrCorruptedData for an ALH mismatch or
 // a cLog entry that disagrees with its record, ErrCorruptedTxData for a read
 // past the log, readHeader / readEntry's errors otherwise) and the index of

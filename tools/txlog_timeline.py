@@ -38,6 +38,8 @@ outs = (torch.empty(ntx * TX_HEADER.itemsize, dtype=torch.uint8).pin_memory().nu
         torch.empty(ntx * 32, dtype=torch.uint8).pin_memory().numpy().reshape(ntx, 32),
         torch.empty(ntx, dtype=torch.int32).pin_memory().numpy())
 o = (None,) + outs[1:] if os.environ.get("TXB_NO_HDRS") else outs
+if os.environ.get("TXTL_PAGEABLE"):  # the log from pageable memory (a plain numpy copy)
+    pin = torch.from_numpy(pin.numpy().copy())
 ts = []
 if os.environ.get("TXTL_CLOG"):  # mh_txlog_validate_clog over the pinned log + its cLog
     from immustore_amd.txlayer import txlog_validate_clog
