@@ -40,6 +40,29 @@
 
 namespace mh {
 
+// `make WAVE_PROBE=1` (diagnosis only, not in the default library): every
+// wave's lane 0 stamps the 100 MHz real-time counter at its phase boundaries
+// into g_wave_probe[wave][0..7] (read by mh_debug_txlog_wave_probe):
+// 0 start, 1 records staged, 2 entry walk, 3 entry digests + leaves done,
+// 4 tree done, 5 innerHash + Alh done, 6 results staged, 7 stores done
+#ifndef MH_TXLOG_WAVE_PROBE
+#define MH_TXLOG_WAVE_PROBE 0
+#endif
+#if MH_TXLOG_WAVE_PROBE
+constexpr unsigned kWaveProbeWaves = 8192;
+__device__ unsigned long long g_wave_probe[kWaveProbeWaves][8];
+#define TXW_STAMP(k)                                                                        \
+    do {                                                                                    \
+        const unsigned wid_ = blockIdx.x * 4 + (threadIdx.x >> 6);                          \
+        if ((threadIdx.x & 63) == 0 && wid_ < kWaveProbeWaves)                              \
+            g_wave_probe[wid_][k] = __builtin_amdgcn_s_memrealtime();                       \
+    } while (0)
+#else
+#define TXW_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 static inline unsigned grid_for(uint64_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }
@@ -75,6 +98,7 @@ __device__ __forceinline__ void txlog_wave_body(
         }
     }
     txl_wave_sync();
+    TXW_STAMP(2);
     // this lane's entries: digest message start / head length / blocks
     const uint8_t *mp0 = rp, *mp1 = rp;
     uint32_t la0 = 0, la1 = 0, nb0 = 0, nb1 = 0, steps0 = 0;
@@ -107,6 +131,8 @@ __device__ __forceinline__ void txlog_wave_body(
     uint32_t e = 0, b = 0;
 #pragma unroll 1
     for (uint32_t g = 0; g < n0 + n1 + n2; g++) {
+        if (MH_TXLOG_WAVE_PROBE && g == n0) TXW_STAMP(3);
+        if (MH_TXLOG_WAVE_PROBE && g == n0 + n1) TXW_STAMP(4);
         uint32_t wv[16];
         bool on = false, lev = false;
         uint32_t half = 0;
@@ -244,6 +270,7 @@ __device__ __forceinline__ void txlog_wave_body(
             copy8(nd, s.h);
         }
     }
+    TXW_STAMP(5);
     uint32_t a[8];
     copy8(a, s.h);
     int32_t stv = MH_OK;
@@ -285,6 +312,7 @@ __device__ __forceinline__ void txlog_wave_body(
         }
     }
     txl_wave_sync();
+    TXW_STAMP(6);
 }
 
 constexpr int kTxWaves = 4;  // independent waves per workgroup
@@ -312,6 +340,7 @@ __global__ __launch_bounds__(256) void k_txlog_wave(
     uint32_t *eoff = msg + R * kTxMsgWords, *ehb = eoff + 64 * kTxwE;
     const uint64_t T0 = (uint64_t)blockIdx.x * kTxWaves * R;  // the workgroup's first record
     const uint64_t t0 = T0 + (uint64_t)wv * R;                 // the wave's
+    TXW_STAMP(0);
     if (t0 < ntx) {  // wave-uniform
         const uint64_t nmine = min((uint64_t)R, ntx - t0);
         const bool mine = (uint64_t)r < nmine;
@@ -334,6 +363,7 @@ __global__ __launch_bounds__(256) void k_txlog_wave(
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
+            TXW_STAMP(1);
             txlog_wave_body<false>(wl + (rec_g - lo), wl + (alh_off[t] - lo), t, rec_g, w, act,
                                    fail, pst, lgl, r, i, eoff, msg, ehb, eh_out, alh_out, status);
         } else {
@@ -369,6 +399,10 @@ __global__ __launch_bounds__(256) void k_txlog_wave(
     if (ho.status)
         for (uint32_t k = threadIdx.x; k < nb; k += 256)
             ho.status[T0 + k] = m0[(k >> lgr) * wwords + R * 42 + (k & (R - 1))];
+    if (MH_TXLOG_WAVE_PROBE) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        TXW_STAMP(7);
+    }
     // (no system fence: the caller reads the pinned results only after
     // synchronizing the stream, whose end-of-kernel release is system-scope; a
     // fence here held every wave until its PCIe writes completed)
@@ -424,3 +458,17 @@ hipError_t launch_txlog_wave(hipStream_t st, Timer *tm, uint64_t ntx, const uint
 }
 
 }  // namespace mh
+
+#if MH_TXLOG_WAVE_PROBE
+// diagnosis build only: the stamps of waves [0, nwaves) (8 x u64 each); reset
+// with out == NULL
+extern "C" __attribute__((visibility("default"))) int mh_debug_txlog_wave_probe(unsigned long long *out,
+                                                                                unsigned nwaves) {
+    nwaves = std::min(nwaves, mh::kWaveProbeWaves);
+    if (!out) {
+        std::vector<unsigned long long> z(mh::kWaveProbeWaves * 8, 0);
+        return (int)hipMemcpyToSymbol(HIP_SYMBOL(mh::g_wave_probe), z.data(), z.size() * 8);
+    }
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mh::g_wave_probe), (size_t)nwaves * 64);
+}
+#endif

@@ -28,6 +28,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the driver bench
 #   txlog            tools/txlog_bench (a14 through the C ABI)
 #   txclog           tools/txlog_bench with TXB_CLOG=1 (mh_txlog_validate_clog, pinned log + cLog)
+#   waveprobe        k_txlog_wave per-phase stamps of the a14 call's last group (make WAVE_PROBE=1 build)
 #   txwl             bench_workloads.py --workload txlog (a14 + resident / cLog lines) -> txwl.out
 #   copyprobe        tools/copy_probe: chunked pinned H2D pipeline costs (host wall time)
 #   workloads        bench_workloads.py: every secondary workload line
@@ -138,6 +139,8 @@ for s in "$@"; do
       gzip -f "$O/prof/run_kernel_trace.csv" ;;
     txlog) step txlog 300 ./tools/txlog_bench || exit 1 ;;
     txclog) TXB_CLOG=1 step txclog 300 ./tools/txlog_bench ${TXB_ARGS:-200} || exit 1 ;;
+    waveprobe) step waveprobe_build 600 make -s -j16 -C immustore_amd/csrc WAVE_PROBE=1 || exit 1
+      step waveprobe 300 python tools/txlog_wave_probe.py || exit 1 ;;
     txwl) step txwl 400 python bench_workloads.py --workload txlog --steps ${TXWL_STEPS:-50} --warmup 3 || exit 1 ;;
     copyprobe) step copyprobe 200 ./tools/copy_probe || exit 1 ;;
     workloads) step workloads 900 bash tools/bench_all.sh || exit 1 ;;
