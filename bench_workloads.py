@@ -228,6 +228,20 @@ def distributed_main(a):
         torch.cuda.synchronize(dev)
 
     def timed_max(step):
+        # clock pre-warm as the single-GPU lines: chunks of 4 steps until
+        # a.prewarm seconds have passed, every rank deciding after the same
+        # chunk (a step may hold a collective)
+        if a.prewarm > 0:
+            tp = time.perf_counter()
+            while True:
+                for _ in range(4):
+                    step()
+                sync_all()
+                more = torch.tensor([int(time.perf_counter() - tp < a.prewarm)], dtype=torch.int64,
+                                    device=on)
+                dist.all_reduce(more, op=dist.ReduceOp.MAX)
+                if not int(more.item()):
+                    break
         for _ in range(a.warmup):
             step()
         sync_all()
