@@ -104,6 +104,54 @@ int main(int argc, char **argv) {
                       hipLaunchKernelGGL(k_touch, dim3(1), dim3(256), 0, cs, d, len, dout);
                       CK(hipStreamSynchronize(cs));
                   }});
+    // the a14 shape: 5 : 2 : 1 chunks, each kernel behind its chunk's event
+    // (k521kern), and the same with the chunk boundaries overlapped on two copy
+    // streams (k521ov<T>: chunk j+1 starts on the other stream once chunk j has
+    // only its last T MiB left, so the boundary's event and setup run under
+    // that tail instead of leaving the link idle)
+    hipStream_t cs2;
+    CK(hipStreamCreateWithFlags(&cs2, hipStreamNonBlocking));
+    std::vector<hipEvent_t> evp(17);
+    for (auto &e : evp) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+    auto cut521 = [&]() {
+        std::vector<uint64_t> c{0, (uint64_t)((double)len * 5 / 8) & ~4095ull,
+                                (uint64_t)((double)len * 7 / 8) & ~4095ull, len};
+        return c;
+    };
+    vs.push_back({"k521kern", [&] {
+                      auto c = cut521();
+                      for (int j = 0; j < 3; j++) {
+                          CK(hipMemcpyAsync(d + c[j], h + c[j], c[j + 1] - c[j], hipMemcpyHostToDevice, cs));
+                          CK(hipEventRecord(evn[j], cs));
+                      }
+                      for (int j = 0; j < 3; j++) {
+                          CK(hipStreamWaitEvent(ks, evn[j], 0));
+                          hipLaunchKernelGGL(k_touch, dim3(1), dim3(256), 0, ks, d + c[j], c[j + 1] - c[j], dout);
+                      }
+                      CK(hipStreamSynchronize(ks));
+                      CK(hipStreamSynchronize(cs));
+                  }});
+    for (int T : {1, 2, 4})
+        vs.push_back({"k521ov" + std::to_string(T), [&, T] {
+                          auto c = cut521();
+                          const uint64_t tail = (uint64_t)T << 20;
+                          for (int j = 0; j < 3; j++) {
+                              hipStream_t s = (j & 1) ? cs2 : cs;
+                              if (j) CK(hipStreamWaitEvent(s, evp[j - 1], 0));
+                              const uint64_t mid = c[j + 1] - std::min(tail, (c[j + 1] - c[j]) / 2);
+                              CK(hipMemcpyAsync(d + c[j], h + c[j], mid - c[j], hipMemcpyHostToDevice, s));
+                              CK(hipEventRecord(evp[j], s));
+                              CK(hipMemcpyAsync(d + mid, h + mid, c[j + 1] - mid, hipMemcpyHostToDevice, s));
+                              CK(hipEventRecord(evn[j], s));
+                          }
+                          for (int j = 0; j < 3; j++) {
+                              CK(hipStreamWaitEvent(ks, evn[j], 0));
+                              hipLaunchKernelGGL(k_touch, dim3(1), dim3(256), 0, ks, d + c[j], c[j + 1] - c[j], dout);
+                          }
+                          CK(hipStreamSynchronize(ks));
+                          CK(hipStreamSynchronize(cs));
+                          CK(hipStreamSynchronize(cs2));
+                      }});
     for (int K : {2, 3, 4}) {
         const std::string k = "k" + std::to_string(K);
         vs.push_back({k, [&, K] {
