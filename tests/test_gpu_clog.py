@@ -174,11 +174,15 @@ def test_clog_entry_mutations(m, ctx, orc):
     e[13][0:8] = struct.pack(">Q", spans[13][0] + 77)
     e[20] = bytearray(e[21])
     e[30][20] ^= 1  # the cLog's Alh (44-byte form only)
+    e[50][0:8] = struct.pack(">Q", (1 << 64) - 16)  # offset + 8 wraps
+    e[51][8:12] = struct.pack(">I", 0xffffffff)  # offset + size past any log
+    e[52][0:12] = struct.pack(">QI", (1 << 64) - 64, 0xffffffff)  # both, the end wraps
     for es in (12, 44):
         sts = run(e, es)
         assert (sts[3], sts[7], sts[11], sts[12]) == (CORRUPTED, CORRUPTED, TRUNCATED, TRUNCATED)
         assert sts[13] != OK and sts[20] == OK and sts[21] == OK
         assert sts[30] == (CORRUPTED if es == 44 else OK)
+        assert (sts[50], sts[51], sts[52]) == (TRUNCATED, CORRUPTED, TRUNCATED)
     perm = rng.permutation(len(ent))
     for es in (12, 44):
         assert not run([ent[k] for k in perm], es).any()
