@@ -106,8 +106,9 @@ def parse():
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                    help="weak: 2^20 entries per GPU (default); strong: one 2^20-entry tree "
                         "split over the N GPUs (c2 only, N a power of two)")
-    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r03.json"),
-                   help="PMC-derived HBM bytes per launch of the dominant kernel (or missing)")
+    p.add_argument("--traffic-file", default=os.path.join(HERE, "profiles", "traffic_r06.json"),
+                   help="PMC-derived HBM bytes per launch of the dominant kernel (or missing): "
+                        "the round's rocprofv3 --pmc passes (tools/gpu_pmc.sh)")
     return p.parse_args()
 
 
@@ -1150,7 +1151,9 @@ def main():
                    "builds_in_flight": D, "wg_subtree_levels": wgl, "stream_priority": prio},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "k_entries_fixed",
+                     "traffic": traffic,
+                     "traffic_source": os.path.relpath(a.traffic_file, HERE) if traffic else None,
+                     "kernel": "k_entries_fixed",
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
                      "per_step": {"achieved": round(step_achieved, 2),
                                   "frac": round(step_achieved / HBM_PEAK_GBS, 4),
