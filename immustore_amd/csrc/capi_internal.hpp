@@ -337,13 +337,14 @@ struct ChunkCopier {
         started = true;
         const bool idle = hipStreamQuery(c->stream) == hipSuccess;
         (void)hipGetLastError();  // hipErrorNotReady is not an error here
-        if (hipError_t e = hipEventRecord(c->ev_done[0], c->stream)) return e;
         // the copies overwrite device buffers that work queued earlier on the
         // context's stream may still read: the copy streams wait for it, unless
         // that stream is idle already (a cross-queue wait ahead of the first
         // copy delays its start: -20..-50 us per a14 call,
-        // profiles/ab_txlog_wait0_flags_r04.txt)
+        // profiles/ab_txlog_wait0_flags_r04.txt; and the event itself is then
+        // not recorded: ~3 us of host time ahead of the first copy)
         if (!idle) {
+            if (hipError_t e = hipEventRecord(c->ev_done[0], c->stream)) return e;
             if (hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_done[0], 0)) return e;
             if (hipError_t e = hipStreamWaitEvent(c->copy_stream2, c->ev_done[0], 0)) return e;
         }
